@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Headline benchmark (BASELINE.json): checkpoint save/restore GB/s + apply->first-log latency.
+
+Config "Preempt-recover: 100 GB checkpoint pack -> host DRAM -> restore": the 100 GB
+checkpoint (bf16 parameters + fp32 Adam moments of a synthetic transformer, random init) is
+sharded over the N ranks (one per GPU, ``torch.distributed`` over RCCL when N > 1), so the
+total work is fixed: strong scaling.  One step = save (pack + CRC32C tiles -> pinned host
+DRAM over PCIe, side-stream pipeline) + restore (host -> HBM, verify every tile, scatter).
+
+    python bench.py --gpus N --steps K --warmup W
+
+Rank 0 prints one JSON line.  ``value`` = checkpoint bytes moved (save + restore) by all
+ranks per second of wall time (max over ranks of the timed region).  Before the timed
+region rank 0 also measures task apply -> first-log latency of an ``iterative_task`` on the
+node-local runtime (reported as ``first_log_latency_s``; not part of ``value``).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = ("task apply→first-log latency (s) + checkpoint save/restore GB/s, "
+          "1/2/4/8 GPU")
+CONFIG_NAME = ("Preempt-recover: SIGTERM mid-task, 100 GB checkpoint pack→host "
+               "DRAM→restore")
+
+
+def parse_args(argv=None):
+    p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--total-gb", type=float, default=100.0,
+                   help="checkpoint size summed over all ranks (GB, 1e9 bytes)")
+    p.add_argument("--mode", choices=("sdma", "direct"), default="sdma")
+    p.add_argument("--tile-mb", type=float, default=1.0)
+    p.add_argument("--chunk-mb", type=float, default=256.0)
+    p.add_argument("--nbuf", type=int, default=3)
+    p.add_argument("--hidden", type=int, default=8192)
+    p.add_argument("--no-latency", action="store_true", help="skip apply->first-log")
+    p.add_argument("--verify", action="store_true", default=True)
+    return p.parse_args(argv)
+
+
+def synthetic_checkpoint(nbytes: int, hidden: int, device):
+    """bf16 weights + fp32 Adam moments of transformer blocks until ``nbytes`` is reached."""
+    import torch
+
+    h = hidden
+    ffn = int(8 * h / 3 + 255) // 256 * 256
+    block = [("attn.qkv", (3 * h, h)), ("attn.out", (h, h)), ("mlp.up", (2 * ffn, h)),
+             ("mlp.down", (h, ffn)), ("norm1", (h,)), ("norm2", (h,))]
+    tensors, used, layer = {}, 0, 0
+    gen = torch.Generator(device=device).manual_seed(1234)
+    while used < nbytes:
+        for name, shape in block:
+            numel = 1
+            for s in shape:
+                numel *= s
+            for kind, dtype in (("param", torch.bfloat16), ("exp_avg", torch.float32),
+                                ("exp_avg_sq", torch.float32)):
+                esz = torch.empty((), dtype=dtype).element_size()
+                left = nbytes - used
+                if left <= 0:
+                    break
+                n = min(numel, max(left // esz, 1))
+                t = torch.empty(n if n != numel else shape, dtype=dtype, device=device)
+                if dtype == torch.bfloat16:
+                    t.normal_(0, 0.02, generator=gen)
+                else:
+                    t.uniform_(0, 1e-3, generator=gen)
+                tensors["layers.%d.%s.%s" % (layer, name, kind)] = t
+                used += t.numel() * esz
+        layer += 1
+    return tensors
+
+
+def first_log_latency(timeout: float = 60.0):
+    try:
+        from terraform_provider_iterative_amd.bench_latency import measure_first_log_latency
+    except ImportError:
+        return None
+    try:
+        return measure_first_log_latency(timeout=timeout)
+    except Exception as error:  # the headline must not die on the latency probe
+        print("bench: first-log latency probe failed: %s" % error, file=sys.stderr)
+        return None
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print("bench: WORLD_SIZE=%d but --gpus=%d" % (world, args.gpus), file=sys.stderr)
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU (MI355X)")
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def allmax(value: float) -> float:
+        if world == 1:
+            return value
+        t = torch.tensor([value], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    latency = None
+    if rank == 0 and not args.no_latency:
+        latency = first_log_latency()
+
+    from terraform_provider_iterative_amd.checkpoint import Checkpointer
+
+    per_rank = int(args.total_gb * 1e9 / world)
+    t_setup = time.perf_counter()
+    tensors = synthetic_checkpoint(per_rank, args.hidden, device)
+    torch.cuda.synchronize()
+    ck = Checkpointer(tensors, tile_bytes=int(args.tile_mb * (1 << 20)),
+                      chunk_bytes=int(args.chunk_mb * (1 << 20)), nbuf=args.nbuf, mode=args.mode)
+    setup_s = time.perf_counter() - t_setup
+    barrier()
+
+    for _ in range(args.warmup):
+        ck.save({"warmup": True})
+        ck.restore()
+    barrier()
+
+    save_s = restore_s = 0.0
+    t0 = time.perf_counter()
+    for step in range(args.steps):
+        a = time.perf_counter()
+        ck.save({"step": step})
+        b = time.perf_counter()
+        res = ck.restore()
+        c = time.perf_counter()
+        if res.bad_tiles:
+            raise SystemExit("bench: %d corrupt tiles after restore" % res.bad_tiles)
+        save_s += b - a
+        restore_s += c - b
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    verified = None
+    if args.verify:  # outside the timed region: prove the restore really rewrote HBM
+        from terraform_provider_iterative_amd import ops
+
+        names = list(tensors)[:3]
+        before = [ops.shard_hash(tensors[n].view(-1).view(torch.uint8)).cpu() for n in names]
+        for n in names:
+            tensors[n].zero_()
+        ck.restore()
+        torch.cuda.synchronize()
+        after = [ops.shard_hash(tensors[n].view(-1).view(torch.uint8)).cpu() for n in names]
+        verified = all(torch.equal(x, y) for x, y in zip(before, after))
+
+    elapsed = allmax(elapsed)
+    save_max, restore_max = allmax(save_s), allmax(restore_s)
+    total = ck.plan.total * world  # packed bytes per direction per step (all ranks)
+    value = 2 * total * args.steps / elapsed / 1e9
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random-init bf16 params + fp32 Adam moments)",
+            "config": {"model": CONFIG_NAME, "global_batch": 1, "seq_len": None,
+                       "parallelism": "shard%d" % world, "checkpoint_bytes": total,
+                       "tile_bytes": ck.plan.tile_bytes, "chunk_bytes": ck.engine.chunk_bytes,
+                       "mode": args.mode, "tensors_per_rank": len(tensors)},
+            "save_GBps": round(total * args.steps / save_max / 1e9, 3),
+            "restore_GBps": round(total * args.steps / restore_max / 1e9, 3),
+            "per_gpu_save_GBps": round(ck.plan.total * args.steps / save_max / 1e9, 3),
+            "per_gpu_restore_GBps": round(ck.plan.total * args.steps / restore_max / 1e9, 3),
+            "first_log_latency_s": latency,
+            "restore_verified": verified,
+            "setup_s": round(setup_s, 2),
+        }
+        print(json.dumps(out), flush=True)
+    ck.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

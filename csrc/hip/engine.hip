@@ -1,0 +1,495 @@
+// Host side of libtpi_hip.so: per-device engine (streams, staging ring, CRC tables), the
+// save/restore pipelines and NUMA-local pinned host mappings.
+//
+// Save (TPI_MODE_SDMA):  for chunk k (buffer b = k % nbuf)
+//     compute: wait copied[b] (k >= nbuf) -> pack+CRC kernel into staging[b] -> record packed[b]
+//     copy:    wait packed[b] -> hipMemcpyAsync D2H staging[b] -> host + k*chunk -> copied[b]
+//   so packing chunk k+1 overlaps the PCIe transfer of chunk k; the copy engine never idles.
+// Save (TPI_MODE_DIRECT): one pack kernel streams straight into the host-mapped destination.
+// Restore mirrors both (H2D on the copy stream, unpack+verify on the compute stream).
+#include <errno.h>
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../common/crc32c.h"
+#include "tpi_hip.h"
+
+extern "C" hipError_t tpi_launch_stream_crc(int mode, const tpi_seg* segs, int nseg,
+                                            uint64_t stream_base, uint64_t len, void* buf,
+                                            uint64_t tile_bytes, const tpi_crc_tables* tables,
+                                            uint32_t* crcs, uint32_t init_full,
+                                            uint32_t init_last, unsigned long long* bad,
+                                            hipStream_t stream);
+extern "C" hipError_t tpi_launch_shard_hash(const void* data, uint64_t nbytes,
+                                            uint64_t shard_bytes, uint64_t seed, uint64_t* out,
+                                            hipStream_t stream);
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(const std::string& what) {
+  g_err = what;
+  return -1;
+}
+
+#define HIP_OK(expr)                                                                    \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return fail(std::string(#expr) + ": " + hipGetErrorString(e_));                   \
+  } while (0)
+
+const tpi_crc_tables& host_tables() {
+  static tpi_crc_tables t;
+  static std::once_flag once;
+  std::call_once(once, [] { tpi_crc_tables_init(&t); });
+  return t;
+}
+
+// Device copies of the CRC tables, one per device (lazily created, never freed).
+std::mutex g_tab_mu;
+std::vector<tpi_crc_tables*> g_dev_tables;
+
+int device_tables(int dev, tpi_crc_tables** out) {
+  std::lock_guard<std::mutex> lk(g_tab_mu);
+  if ((int)g_dev_tables.size() <= dev) g_dev_tables.resize(dev + 1, nullptr);
+  if (!g_dev_tables[dev]) {
+    tpi_crc_tables* d = nullptr;
+    HIP_OK(hipMalloc(&d, sizeof(tpi_crc_tables)));
+    HIP_OK(hipMemcpy(d, &host_tables(), sizeof(tpi_crc_tables), hipMemcpyHostToDevice));
+    g_dev_tables[dev] = d;
+  }
+  *out = g_dev_tables[dev];
+  return 0;
+}
+
+uint32_t init_for(uint64_t len) {
+  return tpi_multmodp(tpi_x8nmodp(len, host_tables().x2n), 0xFFFFFFFFu);
+}
+
+int check_segments(const tpi_seg* segs, int n, uint64_t total) {
+  if (n <= 0) return fail("no segments");
+  if (segs[0].off != 0) return fail("first segment must start at offset 0");
+  for (int i = 0; i < n; ++i) {
+    if (segs[i].off % 16) return fail("segment offset not 16-byte aligned");
+    if (i && segs[i].off < segs[i - 1].off + segs[i - 1].nbytes)
+      return fail("segments overlap or are unsorted");
+    if (segs[i].off + segs[i].nbytes > total) return fail("segment exceeds stream");
+    if (segs[i].kind == 1 && (segs[i].elem == 0 || segs[i].ndim < 1 ||
+                              segs[i].ndim > TPI_MAX_DIMS))
+      return fail("bad strided segment descriptor");
+  }
+  if (total % 16) return fail("stream length must be a multiple of 16");
+  return 0;
+}
+
+}  // namespace
+
+struct tpi_engine {
+  int device = 0;
+  uint64_t chunk = 0, tile = 0;
+  int nbuf = 0;
+  hipStream_t compute = nullptr, copy = nullptr;
+  std::vector<void*> staging;
+  std::vector<hipEvent_t> ev_a, ev_b;  // save: packed/copied; restore: copied/unpacked
+  hipEvent_t ev_wait = nullptr, ev_done = nullptr;
+  tpi_crc_tables* tables = nullptr;
+  tpi_seg* d_segs = nullptr;
+  size_t seg_cap = 0;
+  uint32_t* d_crcs = nullptr;
+  size_t crc_cap = 0;
+  unsigned long long* d_bad = nullptr;
+  std::mutex mu;
+};
+
+extern "C" {
+
+const char* tpi_last_error(void) { return g_err.c_str(); }
+int tpi_version(void) { return 1; }
+
+int tpi_device_count(int* count) {
+  HIP_OK(hipGetDeviceCount(count));
+  return 0;
+}
+
+int tpi_device_pci_bus_id(int device, char* buf, int len) {
+  HIP_OK(hipDeviceGetPCIBusId(buf, len, device));
+  return 0;
+}
+
+int tpi_device_numa_node(int device, int* node) {
+  char bus[64] = {0};
+  *node = -1;
+  if (tpi_device_pci_bus_id(device, bus, sizeof(bus))) return -1;
+  for (char* p = bus; *p; ++p) *p = (char)tolower(*p);
+  std::string path = std::string("/sys/bus/pci/devices/") + bus + "/numa_node";
+  FILE* f = fopen(path.c_str(), "r");
+  if (!f) return 0;  // unknown topology: no binding
+  if (fscanf(f, "%d", node) != 1) *node = -1;
+  fclose(f);
+  return 0;
+}
+
+tpi_engine* tpi_engine_create(int device, uint64_t chunk_bytes, int nbuf, uint64_t tile_bytes) {
+  if (tile_bytes == 0 || tile_bytes % TPI_ROW_BYTES) {
+    fail("tile_bytes must be a positive multiple of 4096");
+    return nullptr;
+  }
+  if (chunk_bytes < tile_bytes) chunk_bytes = tile_bytes;
+  chunk_bytes -= chunk_bytes % tile_bytes;
+  if (nbuf < 1) nbuf = 1;
+  tpi_engine* e = new tpi_engine();
+  e->device = device;
+  e->chunk = chunk_bytes;
+  e->tile = tile_bytes;
+  e->nbuf = nbuf;
+  auto bail = [&](const char* what, hipError_t err) -> tpi_engine* {
+    fail(std::string(what) + ": " + hipGetErrorString(err));
+    tpi_engine_destroy(e);
+    return nullptr;
+  };
+  hipError_t err;
+  if ((err = hipSetDevice(device)) != hipSuccess) return bail("hipSetDevice", err);
+  if ((err = hipStreamCreateWithFlags(&e->compute, hipStreamNonBlocking)) != hipSuccess)
+    return bail("hipStreamCreate(compute)", err);
+  if ((err = hipStreamCreateWithFlags(&e->copy, hipStreamNonBlocking)) != hipSuccess)
+    return bail("hipStreamCreate(copy)", err);
+  e->staging.assign(nbuf, nullptr);
+  e->ev_a.assign(nbuf, nullptr);
+  e->ev_b.assign(nbuf, nullptr);
+  for (int i = 0; i < nbuf; ++i) {
+    if ((err = hipMalloc(&e->staging[i], chunk_bytes)) != hipSuccess)
+      return bail("hipMalloc(staging)", err);
+    if ((err = hipEventCreateWithFlags(&e->ev_a[i], hipEventDisableTiming)) != hipSuccess)
+      return bail("hipEventCreate", err);
+    if ((err = hipEventCreateWithFlags(&e->ev_b[i], hipEventDisableTiming)) != hipSuccess)
+      return bail("hipEventCreate", err);
+  }
+  if ((err = hipEventCreateWithFlags(&e->ev_wait, hipEventDisableTiming)) != hipSuccess)
+    return bail("hipEventCreate", err);
+  if ((err = hipEventCreateWithFlags(&e->ev_done, hipEventDisableTiming)) != hipSuccess)
+    return bail("hipEventCreate", err);
+  if ((err = hipMalloc(&e->d_bad, 2 * sizeof(unsigned long long))) != hipSuccess)
+    return bail("hipMalloc(bad)", err);
+  if (device_tables(device, &e->tables)) {
+    tpi_engine_destroy(e);
+    return nullptr;
+  }
+  return e;
+}
+
+void tpi_engine_destroy(tpi_engine* e) {
+  if (!e) return;
+  // Teardown is best effort: errors here have nowhere useful to go.
+  (void)hipSetDevice(e->device);
+  if (e->compute) (void)hipStreamSynchronize(e->compute);
+  if (e->copy) (void)hipStreamSynchronize(e->copy);
+  for (void* p : e->staging)
+    if (p) (void)hipFree(p);
+  for (hipEvent_t ev : e->ev_a)
+    if (ev) (void)hipEventDestroy(ev);
+  for (hipEvent_t ev : e->ev_b)
+    if (ev) (void)hipEventDestroy(ev);
+  if (e->ev_wait) (void)hipEventDestroy(e->ev_wait);
+  if (e->ev_done) (void)hipEventDestroy(e->ev_done);
+  if (e->d_segs) (void)hipFree(e->d_segs);
+  if (e->d_crcs) (void)hipFree(e->d_crcs);
+  if (e->d_bad) (void)hipFree(e->d_bad);
+  if (e->compute) (void)hipStreamDestroy(e->compute);
+  if (e->copy) (void)hipStreamDestroy(e->copy);
+  delete e;
+}
+
+uint64_t tpi_engine_tile_bytes(const tpi_engine* e) { return e->tile; }
+uint64_t tpi_engine_chunk_bytes(const tpi_engine* e) { return e->chunk; }
+
+}  // extern "C"
+
+namespace {
+
+int prepare(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total) {
+  if (check_segments(segs, n, total)) return -1;
+  HIP_OK(hipSetDevice(e->device));
+  if ((size_t)n > e->seg_cap) {
+    if (e->d_segs) HIP_OK(hipFree(e->d_segs));
+    e->seg_cap = std::max<size_t>(n, 64);
+    HIP_OK(hipMalloc(&e->d_segs, e->seg_cap * sizeof(tpi_seg)));
+  }
+  const size_t ntiles = (total + e->tile - 1) / e->tile;
+  if (ntiles > e->crc_cap) {
+    if (e->d_crcs) HIP_OK(hipFree(e->d_crcs));
+    e->crc_cap = std::max<size_t>(ntiles, 1024);
+    HIP_OK(hipMalloc(&e->d_crcs, e->crc_cap * sizeof(uint32_t)));
+  }
+  // Descriptors are tiny; a synchronous copy keeps the host array's lifetime simple.
+  HIP_OK(hipMemcpyAsync(e->d_segs, segs, n * sizeof(tpi_seg), hipMemcpyHostToDevice,
+                        e->compute));
+  return 0;
+}
+
+void* device_view(void* host) {
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, host, 0) != hipSuccess) return host;
+  return d;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tpi_save(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* host_dst,
+             uint32_t* crcs_out, int mode, uint64_t wait_stream, tpi_stats* stats) {
+  std::lock_guard<std::mutex> lk(e->mu);
+  auto t0 = std::chrono::steady_clock::now();
+  if (prepare(e, segs, n, total)) return -1;
+  if (wait_stream) {
+    HIP_OK(hipEventRecord(e->ev_wait, (hipStream_t)wait_stream));
+    HIP_OK(hipStreamWaitEvent(e->compute, e->ev_wait, 0));
+  }
+  const uint64_t tile = e->tile;
+  const uint32_t init_full = init_for(tile);
+  const uint32_t init_last = init_for(total % tile ? total % tile : tile);
+  uint64_t nchunks = 0;
+  if (mode == TPI_MODE_DIRECT) {
+    HIP_OK(tpi_launch_stream_crc(0, e->d_segs, n, 0, total, device_view(host_dst), tile,
+                                 e->tables, e->d_crcs, init_full, init_last, nullptr,
+                                 e->compute));
+    nchunks = 1;
+  } else {
+    uint8_t* dst = (uint8_t*)host_dst;
+    for (uint64_t base = 0, k = 0; base < total; base += e->chunk, ++k) {
+      const int b = (int)(k % e->nbuf);
+      const uint64_t len = std::min(e->chunk, total - base);
+      if (k >= (uint64_t)e->nbuf) HIP_OK(hipStreamWaitEvent(e->compute, e->ev_b[b], 0));
+      HIP_OK(tpi_launch_stream_crc(0, e->d_segs, n, base, len, e->staging[b], tile, e->tables,
+                                   e->d_crcs, init_full, init_last, nullptr, e->compute));
+      HIP_OK(hipEventRecord(e->ev_a[b], e->compute));
+      HIP_OK(hipStreamWaitEvent(e->copy, e->ev_a[b], 0));
+      HIP_OK(hipMemcpyAsync(dst + base, e->staging[b], len, hipMemcpyDeviceToHost, e->copy));
+      HIP_OK(hipEventRecord(e->ev_b[b], e->copy));
+      nchunks = k + 1;
+    }
+  }
+  const uint64_t ntiles = (total + tile - 1) / tile;
+  HIP_OK(hipMemcpyAsync(crcs_out, e->d_crcs, ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                        e->compute));
+  HIP_OK(hipStreamSynchronize(e->copy));
+  HIP_OK(hipStreamSynchronize(e->compute));
+  if (stats) {
+    stats->copy_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    stats->pack_ms = 0;
+    stats->bytes = total;
+    stats->chunks = nchunks;
+  }
+  return 0;
+}
+
+int tpi_restore(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, const void* host_src,
+                const uint32_t* crcs, int mode, uint64_t signal_stream, uint64_t* bad_tiles,
+                int64_t* first_bad, tpi_stats* stats) {
+  std::lock_guard<std::mutex> lk(e->mu);
+  auto t0 = std::chrono::steady_clock::now();
+  if (prepare(e, segs, n, total)) return -1;
+  const uint64_t tile = e->tile;
+  const uint64_t ntiles = (total + tile - 1) / tile;
+  const uint32_t init_full = init_for(tile);
+  const uint32_t init_last = init_for(total % tile ? total % tile : tile);
+  unsigned long long bad_init[2] = {0ull, ~0ull};
+  HIP_OK(hipMemcpyAsync(e->d_crcs, crcs, ntiles * sizeof(uint32_t), hipMemcpyHostToDevice,
+                        e->compute));
+  HIP_OK(hipMemcpyAsync(e->d_bad, bad_init, sizeof(bad_init), hipMemcpyHostToDevice,
+                        e->compute));
+  uint64_t nchunks = 0;
+  if (mode == TPI_MODE_DIRECT) {
+    HIP_OK(tpi_launch_stream_crc(1, e->d_segs, n, 0, total, device_view((void*)host_src), tile,
+                                 e->tables, e->d_crcs, init_full, init_last, e->d_bad,
+                                 e->compute));
+    nchunks = 1;
+  } else {
+    // The copy stream must not start before the CRC/bad uploads are ordered on compute.
+    HIP_OK(hipEventRecord(e->ev_wait, e->compute));
+    HIP_OK(hipStreamWaitEvent(e->copy, e->ev_wait, 0));
+    const uint8_t* src = (const uint8_t*)host_src;
+    for (uint64_t base = 0, k = 0; base < total; base += e->chunk, ++k) {
+      const int b = (int)(k % e->nbuf);
+      const uint64_t len = std::min(e->chunk, total - base);
+      if (k >= (uint64_t)e->nbuf) HIP_OK(hipStreamWaitEvent(e->copy, e->ev_b[b], 0));
+      HIP_OK(hipMemcpyAsync(e->staging[b], src + base, len, hipMemcpyHostToDevice, e->copy));
+      HIP_OK(hipEventRecord(e->ev_a[b], e->copy));
+      HIP_OK(hipStreamWaitEvent(e->compute, e->ev_a[b], 0));
+      HIP_OK(tpi_launch_stream_crc(1, e->d_segs, n, base, len, e->staging[b], tile, e->tables,
+                                   e->d_crcs, init_full, init_last, e->d_bad, e->compute));
+      HIP_OK(hipEventRecord(e->ev_b[b], e->compute));
+      nchunks = k + 1;
+    }
+  }
+  unsigned long long bad[2];
+  HIP_OK(hipMemcpyAsync(bad, e->d_bad, sizeof(bad), hipMemcpyDeviceToHost, e->compute));
+  HIP_OK(hipEventRecord(e->ev_done, e->compute));
+  if (signal_stream) HIP_OK(hipStreamWaitEvent((hipStream_t)signal_stream, e->ev_done, 0));
+  HIP_OK(hipStreamSynchronize(e->compute));
+  HIP_OK(hipStreamSynchronize(e->copy));
+  *bad_tiles = bad[0];
+  *first_bad = bad[0] ? (int64_t)bad[1] : -1;
+  if (stats) {
+    stats->copy_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    stats->pack_ms = 0;
+    stats->bytes = total;
+    stats->chunks = nchunks;
+  }
+  return 0;
+}
+
+int tpi_crc32c_tiles(const void* dev_ptr, uint64_t nbytes, uint64_t tile_bytes,
+                     uint32_t* dev_out, uint64_t stream) {
+  if (tile_bytes == 0 || tile_bytes % TPI_ROW_BYTES) return fail("tile must be k*4096");
+  if (nbytes % 16) return fail("length must be a multiple of 16");
+  int dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  tpi_crc_tables* t = nullptr;
+  if (device_tables(dev, &t)) return -1;
+  const uint32_t init_full = init_for(tile_bytes);
+  const uint32_t init_last = init_for(nbytes % tile_bytes ? nbytes % tile_bytes : tile_bytes);
+  HIP_OK(tpi_launch_stream_crc(2, nullptr, 0, 0, nbytes, (void*)dev_ptr, tile_bytes, t, dev_out,
+                               init_full, init_last, nullptr, (hipStream_t)stream));
+  return 0;
+}
+
+int tpi_shard_hash(const void* dev_ptr, uint64_t nbytes, uint64_t shard_bytes, uint64_t seed,
+                   uint64_t* dev_out, uint64_t stream) {
+  if (shard_bytes == 0) return fail("shard_bytes must be positive");
+  if ((uintptr_t)dev_ptr % 16 || shard_bytes % 32) return fail("need 16B-aligned data, 32B shards");
+  HIP_OK(tpi_launch_shard_hash(dev_ptr, nbytes, shard_bytes, seed, dev_out,
+                               (hipStream_t)stream));
+  return 0;
+}
+
+int tpi_pack_device(const tpi_seg* segs, int n, uint64_t total, void* dev_dst,
+                    uint64_t tile_bytes, uint32_t* dev_crcs, uint64_t stream) {
+  // `segs` is a DEVICE array here (the caller owns it); validation happens host-side in the
+  // Python wrapper, which builds it.
+  if (tile_bytes == 0 || tile_bytes % TPI_ROW_BYTES) return fail("tile must be k*4096");
+  int dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  tpi_crc_tables* t = nullptr;
+  if (device_tables(dev, &t)) return -1;
+  HIP_OK(tpi_launch_stream_crc(0, segs, n, 0, total, dev_dst, tile_bytes, t, dev_crcs,
+                               init_for(tile_bytes),
+                               init_for(total % tile_bytes ? total % tile_bytes : tile_bytes),
+                               nullptr, (hipStream_t)stream));
+  return 0;
+}
+
+int tpi_unpack_device(const tpi_seg* segs, int n, uint64_t total, const void* dev_src,
+                      uint64_t tile_bytes, const uint32_t* dev_crcs, uint64_t* dev_bad,
+                      uint64_t stream) {
+  if (tile_bytes == 0 || tile_bytes % TPI_ROW_BYTES) return fail("tile must be k*4096");
+  int dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  tpi_crc_tables* t = nullptr;
+  if (device_tables(dev, &t)) return -1;
+  HIP_OK(tpi_launch_stream_crc(1, segs, n, 0, total, (void*)dev_src, tile_bytes, t,
+                               (uint32_t*)dev_crcs, init_for(tile_bytes),
+                               init_for(total % tile_bytes ? total % tile_bytes : tile_bytes),
+                               (unsigned long long*)dev_bad, (hipStream_t)stream));
+  return 0;
+}
+
+// ---- host memory ---------------------------------------------------------------------------
+
+void* tpi_host_map(const char* path, uint64_t bytes, int numa_node, int populate) {
+  int fd = -1;
+  int flags = MAP_PRIVATE | MAP_ANONYMOUS;
+  if (path && *path) {
+    fd = open(path, O_RDWR | O_CREAT, 0600);
+    if (fd < 0) {
+      fail(std::string("open ") + path + ": " + strerror(errno));
+      return nullptr;
+    }
+    struct stat st;
+    if (fstat(fd, &st) == 0 && (uint64_t)st.st_size < bytes && ftruncate(fd, bytes) != 0) {
+      fail(std::string("ftruncate: ") + strerror(errno));
+      close(fd);
+      return nullptr;
+    }
+    flags = MAP_SHARED;
+  }
+  void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, flags, fd, 0);
+  if (fd >= 0) close(fd);
+  if (p == MAP_FAILED) {
+    fail(std::string("mmap: ") + strerror(errno));
+    return nullptr;
+  }
+  madvise(p, bytes, MADV_HUGEPAGE);
+  if (numa_node >= 0 && numa_node < 1024) {
+    unsigned long mask[1024 / (8 * sizeof(unsigned long))] = {0};
+    mask[numa_node / (8 * sizeof(unsigned long))] |= 1ul << (numa_node % (8 * sizeof(unsigned long)));
+    // MPOL_PREFERRED = 1: fall back to other nodes instead of failing under pressure.
+    syscall(SYS_mbind, p, bytes, 1, mask, 1024, 0);
+  }
+  if (populate) {
+    // Parallel first touch: page faults dominate, one thread per ~1 GiB up to 16.
+    const uint64_t page = 4096;
+    unsigned nth = (unsigned)std::min<uint64_t>(16, std::max<uint64_t>(1, bytes >> 30));
+    std::vector<std::thread> th;
+    const uint64_t per = ((bytes / nth) + page - 1) / page * page;
+    for (unsigned i = 0; i < nth; ++i) {
+      th.emplace_back([=] {
+        uint64_t b = (uint64_t)i * per, e = std::min(bytes, b + per);
+        volatile uint8_t* q = (volatile uint8_t*)p;
+        for (uint64_t o = b; o < e; o += page) q[o] = q[o];
+      });
+    }
+    for (auto& t : th) t.join();
+  }
+  return p;
+}
+
+int tpi_host_unmap(void* ptr, uint64_t bytes) {
+  if (munmap(ptr, bytes)) return fail(std::string("munmap: ") + strerror(errno));
+  return 0;
+}
+
+int tpi_host_register(void* ptr, uint64_t bytes) {
+  HIP_OK(hipHostRegister(ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+  return 0;
+}
+
+int tpi_host_unregister(void* ptr) {
+  HIP_OK(hipHostUnregister(ptr));
+  return 0;
+}
+
+int tpi_h2d(tpi_engine* e, void* dev_dst, const void* host_src, uint64_t bytes) {
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_OK(hipSetDevice(e->device));
+  HIP_OK(hipMemcpyAsync(dev_dst, host_src, bytes, hipMemcpyHostToDevice, e->copy));
+  HIP_OK(hipStreamSynchronize(e->copy));
+  return 0;
+}
+
+int tpi_d2h(tpi_engine* e, void* host_dst, const void* dev_src, uint64_t bytes) {
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_OK(hipSetDevice(e->device));
+  HIP_OK(hipMemcpyAsync(host_dst, dev_src, bytes, hipMemcpyDeviceToHost, e->copy));
+  HIP_OK(hipStreamSynchronize(e->copy));
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,411 @@
+// CDNA4 (gfx950) kernels of the checkpoint / workdir data plane.
+//
+//  k_stream_crc<MODE>  one 256-thread workgroup per tile of the packed stream.
+//     MODE_PACK    gather tensor payloads (contiguous or strided) -> packed buffer
+//     MODE_UNPACK  packed buffer -> scatter into tensors, verify tile CRC
+//     MODE_CRC     CRC only (device buffer integrity digests)
+//   Every lane owns the 16-byte words at row*4096 + lane*16 of its tile, so each row is one
+//   fully coalesced 4 KiB workgroup access (dwordx4 per lane).  The CRC32C of the tile is
+//   computed without serialising lanes: lane l folds its own word stream with Horner's rule
+//   (acc = acc * x^(8*4096) ^ raw16(word)), using slice-by-16 + row-shift tables staged in
+//   LDS, then every lane shifts its accumulator by its distance to the tile end and the
+//   workgroup XOR-reduces (wave64 shuffles + LDS across the 4 waves).
+//
+//  k_shard_hash  one workgroup per shard; lane l runs XXH64 over stripes l, l+256, ... so
+//   every load instruction of the workgroup reads one contiguous 8 KiB span (2 x dwordx4 per
+//   lane, 4 stripes in flight per lane); lanes 0..3 fold the 256 lane digests.
+//
+// Reference hot paths: N2 (machine-script.sh.tpl:118-124 mtime poll),
+// N4 (machine-script.sh.tpl:89,118-124 rclone data sync/restore).
+#include <hip/hip_runtime.h>
+
+#include "../common/crc32c.h"
+#include "../common/xxh64.h"
+#include "tpi_hip.h"
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ static inline uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+
+enum { MODE_PACK = 0, MODE_UNPACK = 1, MODE_CRC = 2 };
+#define WG 256
+#define UNROLL 4
+#define LDS_WORDS (16 * 256 + 4 * 256 + WG)
+
+__device__ static inline uint32_t raw16(const uint32_t* __restrict__ s, u32x4 w) {
+  // s = slice tables [16][256]; byte k of the word goes through table 15-k.
+  uint32_t c;
+  c = s[15 * 256 + (w.x & 0xff)] ^ s[14 * 256 + ((w.x >> 8) & 0xff)] ^
+      s[13 * 256 + ((w.x >> 16) & 0xff)] ^ s[12 * 256 + (w.x >> 24)];
+  c ^= s[11 * 256 + (w.y & 0xff)] ^ s[10 * 256 + ((w.y >> 8) & 0xff)] ^
+       s[9 * 256 + ((w.y >> 16) & 0xff)] ^ s[8 * 256 + (w.y >> 24)];
+  c ^= s[7 * 256 + (w.z & 0xff)] ^ s[6 * 256 + ((w.z >> 8) & 0xff)] ^
+       s[5 * 256 + ((w.z >> 16) & 0xff)] ^ s[4 * 256 + (w.z >> 24)];
+  c ^= s[3 * 256 + (w.w & 0xff)] ^ s[2 * 256 + ((w.w >> 8) & 0xff)] ^
+       s[1 * 256 + ((w.w >> 16) & 0xff)] ^ s[0 * 256 + (w.w >> 24)];
+  return c;
+}
+
+__device__ static inline uint32_t shift_row(const uint32_t* __restrict__ r, uint32_t a) {
+  return r[a & 0xff] ^ r[256 + ((a >> 8) & 0xff)] ^ r[512 + ((a >> 16) & 0xff)] ^
+         r[768 + (a >> 24)];
+}
+
+// ---- segment (tensor) access --------------------------------------------------------------
+
+struct SegCursor {
+  int idx;
+  uint64_t off, nbytes, ptr, next_off;
+  uint32_t kind;
+};
+
+__device__ static inline void seg_load(const tpi_seg* __restrict__ segs, int n, int i,
+                                       SegCursor& c) {
+  c.idx = i;
+  c.off = segs[i].off;
+  c.nbytes = segs[i].nbytes;
+  c.ptr = segs[i].ptr;
+  c.kind = segs[i].kind;
+  c.next_off = (i + 1 < n) ? segs[i + 1].off : ~0ull;
+}
+
+// Largest i with segs[i].off <= pos (segs sorted by off, segs[0].off == 0).
+__device__ static inline int seg_find(const tpi_seg* __restrict__ segs, int n, uint64_t pos) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (segs[mid].off <= pos) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__device__ static inline uint64_t strided_offset(const tpi_seg& s, uint64_t e) {
+  uint64_t off = 0;
+  for (int d = s.ndim - 1; d >= 0; --d) {
+    uint64_t sz = (uint64_t)s.sizes[d];
+    uint64_t idx = e % sz;
+    e /= sz;
+    off += idx * (int64_t)s.strides[d];
+  }
+  return off;
+}
+
+__device__ static inline void bytes_to_word(const uint8_t* b, u32x4& w) {
+  w.x = b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24);
+  w.y = b[4] | (b[5] << 8) | (b[6] << 16) | ((uint32_t)b[7] << 24);
+  w.z = b[8] | (b[9] << 8) | (b[10] << 16) | ((uint32_t)b[11] << 24);
+  w.w = b[12] | (b[13] << 8) | (b[14] << 16) | ((uint32_t)b[15] << 24);
+}
+
+__device__ static inline void word_to_bytes(u32x4 w, uint8_t* b) {
+  uint32_t v[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+  for (int i = 0; i < 16; ++i) b[i] = (v[i >> 2] >> (8 * (i & 3))) & 0xff;
+}
+
+// Slow path: bytes [rel, rel+16) of a segment payload that is misaligned, strided, or ends
+// inside the word (bytes past the payload read as zero = alignment padding).
+__device__ __noinline__ static u32x4 gather_slow(const tpi_seg* __restrict__ segs, int idx,
+                                                  uint64_t rel) {
+  const tpi_seg& s = segs[idx];
+  uint8_t b[16];
+  for (int i = 0; i < 16; ++i) {
+    uint64_t q = rel + i;
+    uint8_t v = 0;
+    if (q < s.nbytes) {
+      if (s.kind == 0) {
+        v = ((const uint8_t*)s.ptr)[q];
+      } else {
+        uint64_t e = q / s.elem;
+        v = ((const uint8_t*)s.ptr)[strided_offset(s, e) * s.elem + (q % s.elem)];
+      }
+    }
+    b[i] = v;
+  }
+  u32x4 w;
+  bytes_to_word(b, w);
+  return w;
+}
+
+__device__ __noinline__ static void scatter_slow(const tpi_seg* __restrict__ segs, int idx,
+                                                 uint64_t rel, u32x4 w) {
+  const tpi_seg& s = segs[idx];
+  uint8_t b[16];
+  word_to_bytes(w, b);
+  for (int i = 0; i < 16; ++i) {
+    uint64_t q = rel + i;
+    if (q >= s.nbytes) break;
+    if (s.kind == 0) {
+      ((uint8_t*)s.ptr)[q] = b[i];
+    } else {
+      uint64_t e = q / s.elem;
+      ((uint8_t*)s.ptr)[strided_offset(s, e) * s.elem + (q % s.elem)] = b[i];
+    }
+  }
+}
+
+__device__ static inline void advance(const tpi_seg* __restrict__ segs, int n, uint64_t pos,
+                                      SegCursor& c) {
+  while (pos >= c.next_off) seg_load(segs, n, c.idx + 1, c);
+}
+
+__device__ static inline u32x4 gather16(const tpi_seg* __restrict__ segs, const SegCursor& c,
+                                        uint64_t pos) {
+  const uint64_t rel = pos - c.off;
+  if (rel >= c.nbytes) return u32x4{0, 0, 0, 0};  // alignment padding
+  const uint64_t addr = c.ptr + rel;
+  if (c.kind == 0 && rel + 16 <= c.nbytes && (addr & 15) == 0)
+    return __builtin_nontemporal_load((const u32x4*)addr);
+  return gather_slow(segs, c.idx, rel);
+}
+
+__device__ static inline void scatter16(const tpi_seg* __restrict__ segs, const SegCursor& c,
+                                        uint64_t pos, u32x4 w) {
+  const uint64_t rel = pos - c.off;
+  if (rel >= c.nbytes) return;
+  const uint64_t addr = c.ptr + rel;
+  if (c.kind == 0 && rel + 16 <= c.nbytes && (addr & 15) == 0) {
+    *(u32x4*)addr = w;
+    return;
+  }
+  scatter_slow(segs, c.idx, rel, w);
+}
+
+// ---- the tile kernel -------------------------------------------------------------------------
+
+struct TileArgs {
+  const tpi_seg* segs;
+  int nseg;
+  uint64_t stream_base;     // packed-stream offset of buf[0]
+  uint64_t len;             // bytes of the stream covered by this launch
+  uint8_t* buf;             // packed bytes of [stream_base, stream_base + len)
+  uint64_t tile_bytes;      // multiple of TPI_ROW_BYTES
+  const tpi_crc_tables* tables;
+  uint32_t* crcs;           // indexed by global tile (stream_base / tile_bytes + blockIdx.x)
+  uint32_t init_full;       // shift(~0, tile_bytes)
+  uint32_t init_last;       // shift(~0, last tile length) for a short final tile
+  unsigned long long* bad;  // [0] mismatching tiles, [1] first bad tile (unpack)
+};
+
+template <int MODE>
+__global__ __launch_bounds__(WG) void k_stream_crc(TileArgs a) {
+  __shared__ uint32_t lds[LDS_WORDS];
+  uint32_t* s_slice = lds;
+  uint32_t* s_row = lds + 16 * 256;
+  uint32_t* s_red = lds + 20 * 256;
+  const int lane = threadIdx.x;
+
+  {  // stage CRC tables (20 KiB) into LDS
+    const u32x4* src = (const u32x4*)a.tables;
+    u32x4* dst = (u32x4*)lds;
+#pragma unroll
+    for (int i = lane; i < 20 * 256 / 4; i += WG) dst[i] = src[i];
+  }
+
+  const uint64_t tile_off = (uint64_t)blockIdx.x * a.tile_bytes;  // within this launch
+  const uint64_t tile_len = umin64(a.tile_bytes, a.len - tile_off);
+  const uint64_t gbase = a.stream_base + tile_off;                // packed-stream offset
+  uint8_t* tbuf = a.buf + tile_off;
+
+  SegCursor cur;
+  if (MODE != MODE_CRC) seg_load(a.segs, a.nseg, seg_find(a.segs, a.nseg, gbase + lane * 16), cur);
+  __syncthreads();
+
+  uint32_t acc = 0;
+  uint64_t last_end = 0;
+  const uint64_t nrows = (tile_len + TPI_ROW_BYTES - 1) / TPI_ROW_BYTES;
+  uint64_t row = 0;
+  // Full groups of UNROLL rows where every lane has a word (no bounds checks).
+  const uint64_t full_rows = tile_len / TPI_ROW_BYTES;
+  for (; row + UNROLL <= full_rows; row += UNROLL) {
+    u32x4 w[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const uint64_t rel = (row + u) * TPI_ROW_BYTES + lane * 16;
+      if (MODE == MODE_PACK) {
+        advance(a.segs, a.nseg, gbase + rel, cur);
+        w[u] = gather16(a.segs, cur, gbase + rel);
+      } else {
+        w[u] = __builtin_nontemporal_load((const u32x4*)(tbuf + rel));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const uint64_t rel = (row + u) * TPI_ROW_BYTES + lane * 16;
+      if (MODE == MODE_PACK) {
+        __builtin_nontemporal_store(w[u], (u32x4*)(tbuf + rel));
+      } else if (MODE == MODE_UNPACK) {
+        advance(a.segs, a.nseg, gbase + rel, cur);
+        scatter16(a.segs, cur, gbase + rel, w[u]);
+      }
+      acc = shift_row(s_row, acc) ^ raw16(s_slice, w[u]);
+    }
+    last_end = (row + UNROLL - 1) * TPI_ROW_BYTES + lane * 16 + 16;
+  }
+  for (; row < nrows; ++row) {  // remainder rows, possibly partial
+    const uint64_t rel = row * TPI_ROW_BYTES + lane * 16;
+    if (rel < tile_len) {
+      u32x4 w;
+      if (MODE == MODE_PACK) {
+        advance(a.segs, a.nseg, gbase + rel, cur);
+        w = gather16(a.segs, cur, gbase + rel);
+        __builtin_nontemporal_store(w, (u32x4*)(tbuf + rel));
+      } else {
+        w = __builtin_nontemporal_load((const u32x4*)(tbuf + rel));
+        if (MODE == MODE_UNPACK) {
+          advance(a.segs, a.nseg, gbase + rel, cur);
+          scatter16(a.segs, cur, gbase + rel, w);
+        }
+      }
+      acc = shift_row(s_row, acc) ^ raw16(s_slice, w);
+      last_end = rel + 16;
+    }
+  }
+
+  // Shift each lane's accumulator to the end of the tile and XOR-reduce.
+  uint32_t contrib = 0;
+  if (last_end) {
+    const uint64_t dist = tile_len - last_end;
+    uint32_t k = (tile_len % TPI_ROW_BYTES == 0) ? a.tables->lane_shift[lane]
+                                                 : tpi_x8nmodp(dist, a.tables->x2n);
+    contrib = tpi_multmodp(k, acc);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) contrib ^= __shfl_xor(contrib, o, 64);
+  if ((lane & 63) == 0) s_red[lane >> 6] = contrib;
+  __syncthreads();
+  if (lane == 0) {
+    uint32_t raw = s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3];
+    const uint32_t init = (tile_len == a.tile_bytes) ? a.init_full : a.init_last;
+    const uint32_t crc = raw ^ init ^ 0xFFFFFFFFu;
+    const uint64_t gtile = a.stream_base / a.tile_bytes + blockIdx.x;
+    if (MODE == MODE_UNPACK) {
+      if (crc != a.crcs[gtile]) {
+        atomicAdd(&a.bad[0], 1ull);
+        atomicMin(&a.bad[1], (unsigned long long)gtile);
+      }
+    } else {
+      a.crcs[gtile] = crc;
+    }
+  }
+}
+
+// ---- striped XXH64 shard hash ----------------------------------------------------------------
+
+__global__ __launch_bounds__(WG) void k_shard_hash(const uint8_t* __restrict__ data,
+                                                   uint64_t nbytes, uint64_t shard_bytes,
+                                                   uint64_t seed, uint64_t* __restrict__ out) {
+  __shared__ uint64_t dig[TPI_HASH_LANES];
+  const int lane = threadIdx.x;
+  const uint64_t base = (uint64_t)blockIdx.x * shard_bytes;
+  const uint64_t len = umin64(shard_bytes, nbytes - base);
+  const uint8_t* d = data + base;
+  const uint64_t full = len / TPI_HASH_STRIPE;
+  const uint32_t rem = (uint32_t)(len % TPI_HASH_STRIPE);
+  const uint64_t nfull = full > (uint64_t)lane ? (full - lane + WG - 1) / WG : 0;
+  const bool owns_tail = rem && (full % WG) == (uint64_t)lane;
+  const uint64_t mylen = nfull * TPI_HASH_STRIPE + (owns_tail ? rem : 0);
+
+  uint64_t h;
+  if (mylen >= 32) {
+    uint64_t v1 = seed + TPI_XXH_P1 + TPI_XXH_P2, v2 = seed + TPI_XXH_P2, v3 = seed,
+             v4 = seed - TPI_XXH_P1;
+    const u32x4* p = (const u32x4*)(d + (uint64_t)lane * TPI_HASH_STRIPE);
+    const uint64_t step = WG * TPI_HASH_STRIPE / 16;  // in u32x4 units
+    uint64_t j = 0;
+    for (; j + 4 <= nfull; j += 4) {
+      u32x4 w[8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        w[2 * u] = __builtin_nontemporal_load(p + (j + u) * step);
+        w[2 * u + 1] = __builtin_nontemporal_load(p + (j + u) * step + 1);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v1 = tpi_xxh_round(v1, ((uint64_t)w[2 * u].y << 32) | w[2 * u].x);
+        v2 = tpi_xxh_round(v2, ((uint64_t)w[2 * u].w << 32) | w[2 * u].z);
+        v3 = tpi_xxh_round(v3, ((uint64_t)w[2 * u + 1].y << 32) | w[2 * u + 1].x);
+        v4 = tpi_xxh_round(v4, ((uint64_t)w[2 * u + 1].w << 32) | w[2 * u + 1].z);
+      }
+    }
+    for (; j < nfull; ++j) {
+      u32x4 a = p[j * step], b = p[j * step + 1];
+      v1 = tpi_xxh_round(v1, ((uint64_t)a.y << 32) | a.x);
+      v2 = tpi_xxh_round(v2, ((uint64_t)a.w << 32) | a.z);
+      v3 = tpi_xxh_round(v3, ((uint64_t)b.y << 32) | b.x);
+      v4 = tpi_xxh_round(v4, ((uint64_t)b.w << 32) | b.z);
+    }
+    h = tpi_xxh_converge(v1, v2, v3, v4);
+  } else {
+    h = seed + TPI_XXH_P5;
+  }
+  h += mylen;
+  uint8_t tail[TPI_HASH_STRIPE];
+  uint32_t nt = 0;
+  if (owns_tail) {
+    for (uint32_t i = 0; i < rem; ++i) tail[i] = d[full * TPI_HASH_STRIPE + i];
+    nt = rem;
+  }
+  dig[lane] = tpi_xxh_finish(h, tail, nt);
+  __syncthreads();
+
+  // XXH64 over the 2048-byte digest array: 64 stripes of 4 words; lane k<4 owns word k.
+  if (lane < 64) {
+    uint64_t v = 0;
+    if (lane < 4) {
+      const uint64_t init[4] = {seed + TPI_XXH_P1 + TPI_XXH_P2, seed + TPI_XXH_P2, seed,
+                                seed - TPI_XXH_P1};
+      v = init[lane];
+      for (int s = 0; s < TPI_HASH_LANES / 4; ++s) v = tpi_xxh_round(v, dig[4 * s + lane]);
+    }
+    const uint64_t v1 = __shfl(v, 0, 64), v2 = __shfl(v, 1, 64), v3 = __shfl(v, 2, 64),
+                   v4 = __shfl(v, 3, 64);
+    if (lane == 0) {
+      uint64_t hh = tpi_xxh_converge(v1, v2, v3, v4) + (uint64_t)(TPI_HASH_LANES * 8);
+      out[blockIdx.x] = tpi_xxh_avalanche(hh);
+    }
+  }
+}
+
+// ---- launch helpers (used by engine.hip) -----------------------------------------------------
+
+extern "C" hipError_t tpi_launch_stream_crc(int mode, const tpi_seg* segs, int nseg,
+                                            uint64_t stream_base, uint64_t len, void* buf,
+                                            uint64_t tile_bytes, const tpi_crc_tables* tables,
+                                            uint32_t* crcs, uint32_t init_full,
+                                            uint32_t init_last, unsigned long long* bad,
+                                            hipStream_t stream) {
+  if (len == 0) return hipSuccess;
+  TileArgs a;
+  a.segs = segs;
+  a.nseg = nseg;
+  a.stream_base = stream_base;
+  a.len = len;
+  a.buf = (uint8_t*)buf;
+  a.tile_bytes = tile_bytes;
+  a.tables = tables;
+  a.crcs = crcs;
+  a.init_full = init_full;
+  a.init_last = init_last;
+  a.bad = bad;
+  const uint64_t ntiles = (len + tile_bytes - 1) / tile_bytes;
+  dim3 grid((unsigned)ntiles), block(WG);
+  switch (mode) {
+    case MODE_PACK: hipLaunchKernelGGL(k_stream_crc<MODE_PACK>, grid, block, 0, stream, a); break;
+    case MODE_UNPACK:
+      hipLaunchKernelGGL(k_stream_crc<MODE_UNPACK>, grid, block, 0, stream, a);
+      break;
+    default: hipLaunchKernelGGL(k_stream_crc<MODE_CRC>, grid, block, 0, stream, a); break;
+  }
+  return hipGetLastError();
+}
+
+extern "C" hipError_t tpi_launch_shard_hash(const void* data, uint64_t nbytes,
+                                            uint64_t shard_bytes, uint64_t seed, uint64_t* out,
+                                            hipStream_t stream) {
+  if (nbytes == 0) return hipSuccess;
+  const uint64_t nshards = (nbytes + shard_bytes - 1) / shard_bytes;
+  hipLaunchKernelGGL(k_shard_hash, dim3((unsigned)nshards), dim3(WG), 0, stream,
+                     (const uint8_t*)data, nbytes, shard_bytes, seed, out);
+  return hipGetLastError();
+}

@@ -1,0 +1,97 @@
+// C ABI of libtpi_hip.so — the MI355X data plane of the task runtime.
+//
+// Hot paths replaced:
+//   N2  workdir/checkpoint change detection  -> tpi_shard_hash   (XXH64-striped per shard)
+//   N4  transparent checkpoint               -> tpi_save/tpi_restore (pack + CRC32C tiles,
+//                                               pinned host spill on a side stream)
+//   N1  workdir staging host -> HBM          -> tpi_h2d_chunks / pinned host mappings
+//
+// Everything here is plain C so the library can be loaded with ctypes after `import torch`
+// (so it binds to the libamdhip64.so.7 torch already mapped) and linked by C++ tools.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TPI_MAX_DIMS 6
+#define TPI_SEG_ALIGN 256  // packed-stream alignment of every tensor payload
+
+// One tensor payload inside the packed checkpoint stream.
+typedef struct tpi_seg {
+  uint64_t ptr;     // device (or host-mapped) address of the tensor's first element
+  uint64_t off;     // byte offset in the packed stream (multiple of TPI_SEG_ALIGN)
+  uint64_t nbytes;  // payload bytes (numel * elem)
+  uint32_t kind;    // 0 = contiguous, 1 = strided gather/scatter
+  uint32_t elem;    // element size in bytes (strided path)
+  int32_t ndim;
+  int32_t pad_;
+  int64_t sizes[TPI_MAX_DIMS];
+  int64_t strides[TPI_MAX_DIMS];  // in elements
+} tpi_seg;
+
+enum { TPI_MODE_SDMA = 0, TPI_MODE_DIRECT = 1 };
+
+typedef struct tpi_engine tpi_engine;
+
+typedef struct tpi_stats {
+  double pack_ms;     // device time of pack/unpack kernels (sum)
+  double copy_ms;     // wall time of the whole pipeline
+  uint64_t bytes;     // packed bytes moved
+  uint64_t chunks;
+} tpi_stats;
+
+// Library / device
+const char* tpi_last_error(void);
+int tpi_version(void);
+int tpi_device_count(int* count);
+int tpi_device_numa_node(int device, int* node);
+int tpi_device_pci_bus_id(int device, char* buf, int len);
+
+// Engine: per-device streams, staging ring, CRC tables.
+tpi_engine* tpi_engine_create(int device, uint64_t chunk_bytes, int nbuf, uint64_t tile_bytes);
+void tpi_engine_destroy(tpi_engine* e);
+uint64_t tpi_engine_tile_bytes(const tpi_engine* e);
+uint64_t tpi_engine_chunk_bytes(const tpi_engine* e);
+
+// Pack `segs` (n entries, sorted by off) into a stream of `total` bytes written to `host_dst`
+// (pinned or host-mapped).  `crcs_out` (host, ceil(total/tile) entries) receives the CRC32C of
+// every tile.  `wait_stream` (may be 0) is a stream whose prior work must finish first.
+int tpi_save(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* host_dst,
+             uint32_t* crcs_out, int mode, uint64_t wait_stream, tpi_stats* stats);
+// Inverse: stream `total` bytes from `host_src`, verify each tile against `crcs`, scatter.
+// Returns 0 and sets *bad_tiles (0 = all verified) / *first_bad (-1 if none).
+int tpi_restore(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total,
+                const void* host_src, const uint32_t* crcs, int mode, uint64_t signal_stream,
+                uint64_t* bad_tiles, int64_t* first_bad, tpi_stats* stats);
+
+// Device-buffer primitives (enqueued on `stream`, asynchronous).
+int tpi_crc32c_tiles(const void* dev_ptr, uint64_t nbytes, uint64_t tile_bytes,
+                     uint32_t* dev_out, uint64_t stream);
+int tpi_shard_hash(const void* dev_ptr, uint64_t nbytes, uint64_t shard_bytes, uint64_t seed,
+                   uint64_t* dev_out, uint64_t stream);
+// Pack/unpack into/out of a device buffer (no host spill); used by tests and by the
+// broadcast path (pack once, RCCL-broadcast the flat buffer, unpack on every rank).
+int tpi_pack_device(const tpi_seg* segs, int n, uint64_t total, void* dev_dst,
+                    uint64_t tile_bytes, uint32_t* dev_crcs, uint64_t stream);
+int tpi_unpack_device(const tpi_seg* segs, int n, uint64_t total, const void* dev_src,
+                      uint64_t tile_bytes, const uint32_t* dev_crcs, uint64_t* dev_bad,
+                      uint64_t stream);
+
+// Host memory: NUMA-bound, populated, registered (pinned) mappings.
+// path == NULL -> anonymous; otherwise a shared file (e.g. /dev/shm/...) that outlives the
+// process (the preemption spill target).  numa_node < 0 -> no binding.
+void* tpi_host_map(const char* path, uint64_t bytes, int numa_node, int populate);
+int tpi_host_unmap(void* ptr, uint64_t bytes);
+int tpi_host_register(void* ptr, uint64_t bytes);
+int tpi_host_unregister(void* ptr);
+
+// Chunked host->device copy through the engine's copy stream (workdir staging).
+int tpi_h2d(tpi_engine* e, void* dev_dst, const void* host_src, uint64_t bytes);
+int tpi_d2h(tpi_engine* e, void* host_dst, const void* dev_src, uint64_t bytes);
+
+#ifdef __cplusplus
+}
+#endif

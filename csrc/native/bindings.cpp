@@ -1,0 +1,134 @@
+// pybind11 module `_tpi_native`: host-side native runtime pieces.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <stdexcept>
+
+#include "filter.h"
+#include "hostops.h"
+#include "transfer.h"
+
+namespace py = pybind11;
+
+namespace {
+
+const tpi_seg* seg_ptr(py::buffer& b, int& n) {
+  py::buffer_info info = b.request();
+  if (info.size * info.itemsize % (py::ssize_t)sizeof(tpi_seg))
+    throw std::invalid_argument("segment buffer size is not a multiple of sizeof(tpi_seg)");
+  n = (int)(info.size * info.itemsize / sizeof(tpi_seg));
+  return (const tpi_seg*)info.ptr;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_tpi_native, m) {
+  m.doc() = "Host-side native runtime of the MI355X task orchestrator";
+  m.attr("SEG_SIZE") = (int)sizeof(tpi_seg);
+
+  py::class_<tpi::Filter>(m, "Filter")
+      .def(py::init<>())
+      .def(py::init([](const std::vector<std::string>& rules) {
+        tpi::Filter f;
+        for (auto& r : rules) f.add_rule(r);
+        return f;
+      }))
+      .def("add_rule", &tpi::Filter::add_rule)
+      .def("add", &tpi::Filter::add)
+      .def("include_file", &tpi::Filter::include_file)
+      .def("include_dir", &tpi::Filter::include_dir)
+      .def("describe", &tpi::Filter::describe);
+
+  m.def("glob_match", [](const std::string& glob, const std::string& path) {
+    return tpi::Glob(glob).match(path);
+  });
+
+  m.def(
+      "walk",
+      [](const std::string& root, const tpi::Filter& f) {
+        std::vector<tpi::Entry> es;
+        {
+          py::gil_scoped_release nogil;
+          es = tpi::walk(root, f);
+        }
+        py::list out;
+        for (auto& e : es)
+          out.append(py::make_tuple(e.rel, e.size, e.mtime_ns, e.mode, e.is_dir));
+        return out;
+      },
+      py::arg("root"), py::arg("filter"));
+
+  m.def(
+      "copy_dir",
+      [](const std::string& src, const std::string& dst, const tpi::Filter& f, int threads,
+         uint64_t piece) {
+        tpi::TransferStats s;
+        {
+          py::gil_scoped_release nogil;
+          s = tpi::copy_dir(src, dst, f, threads, piece);
+        }
+        py::dict d;
+        d["files"] = s.files;
+        d["bytes"] = s.bytes;
+        d["dirs"] = s.dirs;
+        d["skipped"] = s.skipped;
+        d["skipped_bytes"] = s.skipped_bytes;
+        d["seconds"] = s.seconds;
+        return d;
+      },
+      py::arg("src"), py::arg("dst"), py::arg("filter"), py::arg("threads") = 8,
+      py::arg("piece_bytes") = 256ull << 20);
+
+  m.def("remove_tree", [](const std::string& p) {
+    py::gil_scoped_release nogil;
+    return tpi::remove_tree(p);
+  });
+
+  m.def(
+      "crc32c",
+      [](py::buffer b, uint32_t crc) {
+        py::buffer_info i = b.request();
+        py::gil_scoped_release nogil;
+        return tpi::crc32c(i.ptr, (size_t)(i.size * i.itemsize), crc);
+      },
+      py::arg("data"), py::arg("crc") = 0);
+  m.def("crc32c_ptr", [](uintptr_t p, uint64_t n, uint32_t crc) {
+    py::gil_scoped_release nogil;
+    return tpi::crc32c((const void*)p, n, crc);
+  });
+  m.def("crc32c_combine", &tpi::crc32c_combine);
+  m.def("crc32c_combine_tiles_ptr", [](uintptr_t crcs, uint64_t n, uint64_t tile,
+                                       uint64_t total) {
+    return tpi::crc32c_combine_tiles((const uint32_t*)crcs, n, tile, total);
+  });
+  m.def("crc32c_tiles_ptr", [](uintptr_t p, uint64_t n, uint64_t tile, uintptr_t out,
+                               int threads) {
+    py::gil_scoped_release nogil;
+    tpi::crc32c_tiles((const void*)p, n, tile, (uint32_t*)out, threads);
+  });
+  m.def("shard_hash_ptr", [](uintptr_t p, uint64_t n, uint64_t shard, uint64_t seed,
+                             uintptr_t out, int threads) {
+    py::gil_scoped_release nogil;
+    tpi::shard_hash((const void*)p, n, shard, seed, (uint64_t*)out, threads);
+  });
+  m.def("pack_ptr", [](py::buffer segs, uint64_t total, uintptr_t stream, uint64_t tile,
+                       uintptr_t crcs, int threads) {
+    int n = 0;
+    const tpi_seg* s = seg_ptr(segs, n);
+    py::gil_scoped_release nogil;
+    tpi::pack(s, n, total, (void*)stream, tile, (uint32_t*)crcs, threads);
+  });
+  m.def("unpack_ptr", [](py::buffer segs, uint64_t total, uintptr_t stream, uint64_t tile,
+                         uintptr_t crcs, int threads) {
+    int n = 0;
+    const tpi_seg* s = seg_ptr(segs, n);
+    int64_t first = -1;
+    uint64_t bad;
+    {
+      py::gil_scoped_release nogil;
+      bad = tpi::unpack(s, n, total, (const void*)stream, tile, (const uint32_t*)crcs, threads,
+                        &first);
+    }
+    return py::make_tuple(bad, first);
+  });
+}

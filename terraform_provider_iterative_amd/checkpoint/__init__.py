@@ -1,0 +1,8 @@
+"""Tensor checkpoints: pack -> pinned host DRAM -> restore, with preemption handling."""
+from .checkpointer import (CheckpointError, Checkpointer, DeviceEngine, TransferResult,
+                           describe_checkpoint)
+from .host import HostRegion
+from . import preemption
+
+__all__ = ["CheckpointError", "Checkpointer", "DeviceEngine", "TransferResult",
+           "describe_checkpoint", "HostRegion", "preemption"]

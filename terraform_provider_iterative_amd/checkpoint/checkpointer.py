@@ -1,0 +1,294 @@
+"""Checkpoint save/restore of tensor sets through host memory.
+
+This is the MI355X replacement of the reference's "transparent checkpoint" (the workdir
+sync of ``machine-script.sh.tpl:89,118-124``): on preemption (SIGTERM) a rank packs its
+tensors (flatten + CRC32C per tile, ``csrc/hip/kernels.hip``) into pinned host DRAM through
+a double-buffered pipeline on a side stream (``csrc/hip/engine.hip``); its successor restores
+from the same region (or from the persisted file) and verifies every tile.
+
+Region layout (also the persisted file format)::
+
+    0            b"TPICKPT1" | u64 header_len | JSON header (see ``_header``)
+    crc_offset   u32 CRC32C per tile                       (4 KiB aligned)
+    stream_off   packed stream (``ops.packing`` layout)    (4 KiB aligned)
+
+The JSON header carries ``"complete": true`` only after a save finished, and is written last.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import struct
+import time
+from dataclasses import dataclass
+from typing import Any, Dict, Mapping, Optional, Sequence, Union
+
+import numpy as np
+
+from ..ops import hip, native
+from ..ops.packing import PackPlan, TensorEntry, align_up
+from ..ops.packing import pack as host_pack, unpack as host_unpack
+from .host import HostRegion
+
+MAGIC = b"TPICKPT1"
+PREAMBLE = 16
+MODES = {"sdma": 0, "direct": 1}
+
+
+class CheckpointError(RuntimeError):
+    pass
+
+
+class _Stats(ctypes.Structure):
+    _fields_ = [("pack_ms", ctypes.c_double), ("copy_ms", ctypes.c_double),
+                ("bytes", ctypes.c_uint64), ("chunks", ctypes.c_uint64)]
+
+
+@dataclass
+class TransferResult:
+    bytes: int
+    seconds: float
+    chunks: int = 0
+    bad_tiles: int = 0
+    first_bad: int = -1
+    crc: int = 0
+
+    @property
+    def gbps(self) -> float:
+        return self.bytes / self.seconds / 1e9 if self.seconds > 0 else float("inf")
+
+
+class DeviceEngine:
+    """Per-device pipeline: compute + copy streams, ``nbuf`` staging chunks in HBM."""
+
+    def __init__(self, device_index: int, chunk_bytes: int, nbuf: int, tile_bytes: int):
+        self.lib = hip()
+        self.device_index = device_index
+        handle = self.lib.tpi_engine_create(device_index, chunk_bytes, nbuf, tile_bytes)
+        if not handle:
+            raise CheckpointError("engine creation failed: %s" % self.lib.error())
+        self.handle = handle
+        self.chunk_bytes = int(self.lib.tpi_engine_chunk_bytes(handle))
+
+    def save(self, plan: PackPlan, host_addr: int, crcs: np.ndarray, mode: int,
+             wait_stream: int) -> TransferResult:
+        st = _Stats()
+        t0 = time.perf_counter()
+        rc = self.lib.tpi_save(self.handle, plan.segs.ctypes.data, len(plan.entries), plan.total,
+                               ctypes.c_void_p(host_addr), crcs.ctypes.data, mode, wait_stream,
+                               ctypes.byref(st))
+        self.lib.check(rc, "tpi_save")
+        return TransferResult(plan.total, time.perf_counter() - t0, int(st.chunks))
+
+    def restore(self, plan: PackPlan, host_addr: int, crcs: np.ndarray, mode: int,
+                signal_stream: int) -> TransferResult:
+        st = _Stats()
+        bad = ctypes.c_uint64(0)
+        first = ctypes.c_int64(-1)
+        t0 = time.perf_counter()
+        rc = self.lib.tpi_restore(self.handle, plan.segs.ctypes.data, len(plan.entries),
+                                  plan.total, ctypes.c_void_p(host_addr), crcs.ctypes.data, mode,
+                                  signal_stream, ctypes.byref(bad), ctypes.byref(first),
+                                  ctypes.byref(st))
+        self.lib.check(rc, "tpi_restore")
+        return TransferResult(plan.total, time.perf_counter() - t0, int(st.chunks),
+                              int(bad.value), int(first.value))
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.tpi_engine_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _layout(header_len: int, ntiles: int, total: int):
+    crc_offset = align_up(PREAMBLE + header_len, 4096)
+    stream_offset = align_up(crc_offset + 4 * ntiles, 4096)
+    return crc_offset, stream_offset, stream_offset + total
+
+
+class Checkpointer:
+    """Save/restore a fixed set of tensors through one host region.
+
+    ``path=None`` keeps the spill in anonymous host DRAM (lives as long as this object);
+    a path under ``/dev/shm`` survives the process (preemption), a path on disk survives the
+    node.  Device tensors use the HIP pipeline, host tensors the C++ host path.
+    """
+
+    HEADER_RESERVE = 64 * 1024  # room for metadata updates without relayout
+
+    def __init__(self, tensors: Union[Mapping[str, Any], Sequence[Any]],
+                 path: Optional[str] = None, *, tile_bytes: int = 1 << 20,
+                 chunk_bytes: int = 256 << 20, nbuf: int = 3, mode: str = "sdma",
+                 numa: bool = True, populate: bool = True):
+        self.plan = PackPlan.from_tensors(tensors, tile_bytes)
+        self.path = path
+        self.mode = MODES[mode]
+        entries_json = json.dumps([e.to_json() for e in self.plan.entries]).encode()
+        self.header_cap = len(entries_json) + self.HEADER_RESERVE
+        self.crc_offset, self.stream_offset, self.size = _layout(
+            self.header_cap, self.plan.ntiles, self.plan.total)
+        self.engine = None
+        numa_node = -1
+        if self.plan.on_device:
+            import torch
+
+            dev = torch.device(self.plan.device)
+            self.device_index = dev.index if dev.index is not None else torch.cuda.current_device()
+            if numa:
+                node = ctypes.c_int(-1)
+                if hip().tpi_device_numa_node(self.device_index, ctypes.byref(node)) == 0:
+                    numa_node = node.value
+            self.engine = DeviceEngine(self.device_index, chunk_bytes, nbuf, tile_bytes)
+        self.region = HostRegion(self.size, path, device=self.plan.on_device,
+                                 numa_node=numa_node, populate=populate)
+        self.crcs = self.region.array(self.crc_offset, 4 * self.plan.ntiles, np.uint32)
+        self.saves = 0
+        self.last_save: Optional[TransferResult] = None
+        self.last_restore: Optional[TransferResult] = None
+
+    # -- header ------------------------------------------------------------------------------
+    def _header(self, complete: bool, crc: int, metadata: Optional[Dict]) -> Dict:
+        return {"format": 1, "complete": complete, "tile_bytes": self.plan.tile_bytes,
+                "total": self.plan.total, "ntiles": self.plan.ntiles,
+                "crc_offset": self.crc_offset, "stream_offset": self.stream_offset,
+                "crc32c": crc, "saved_at": time.time(), "saves": self.saves,
+                "metadata": metadata or {},
+                "entries": [e.to_json() for e in self.plan.entries]}
+
+    def _write_header(self, header: Dict) -> None:
+        blob = json.dumps(header).encode()
+        if len(blob) > self.header_cap:
+            raise CheckpointError("checkpoint metadata too large (%d bytes)" % len(blob))
+        pre = self.region.array(0, PREAMBLE + len(blob))
+        pre[PREAMBLE:] = np.frombuffer(blob, np.uint8)
+        pre[:PREAMBLE] = np.frombuffer(MAGIC + struct.pack("<Q", len(blob)), np.uint8)
+
+    def _invalidate(self) -> None:
+        self.region.array(0, 8)[:] = 0
+
+    @staticmethod
+    def read_header(buf: np.ndarray) -> Dict:
+        raw = buf[:PREAMBLE].tobytes()
+        if raw[:8] != MAGIC:
+            raise CheckpointError("no checkpoint (bad magic)")
+        (n,) = struct.unpack("<Q", raw[8:16])
+        return json.loads(buf[PREAMBLE:PREAMBLE + n].tobytes())
+
+    def header(self) -> Dict:
+        return self.read_header(self.region.array(0, self.crc_offset))
+
+    # -- operations --------------------------------------------------------------------------
+    def save(self, metadata: Optional[Dict] = None) -> TransferResult:
+        """Pack every tensor into the region; returns bytes/seconds (GB/s via ``.gbps``)."""
+        self._invalidate()
+        if self.engine is not None:
+            import torch
+
+            wait = torch.cuda.current_stream(self.device_index).cuda_stream
+            res = self.engine.save(self.plan, self.region.addr + self.stream_offset, self.crcs,
+                                   self.mode, wait)
+        else:
+            t0 = time.perf_counter()
+            stream = self.region.array(self.stream_offset, self.plan.total)
+            _, crcs = host_pack(self.plan, stream)
+            self.crcs[:] = crcs
+            res = TransferResult(self.plan.total, time.perf_counter() - t0)
+        res.crc = native().crc32c_combine_tiles_ptr(self.crcs.ctypes.data, self.plan.ntiles,
+                                                     self.plan.tile_bytes, self.plan.total)
+        self.saves += 1
+        self._write_header(self._header(True, res.crc, metadata))
+        self.last_save = res
+        return res
+
+    def restore(self, strict: bool = True) -> TransferResult:
+        """Unpack + verify the region into the bound tensors."""
+        header = self.header()
+        if not header.get("complete"):
+            raise CheckpointError("checkpoint incomplete (save was interrupted)")
+        self._check_compatible(header)
+        if self.engine is not None:
+            import torch
+
+            sig = torch.cuda.current_stream(self.device_index).cuda_stream
+            res = self.engine.restore(self.plan, self.region.addr + self.stream_offset,
+                                      self.crcs, self.mode, sig)
+        else:
+            t0 = time.perf_counter()
+            stream = self.region.array(self.stream_offset, self.plan.total)
+            bad, first = host_unpack(self.plan, stream, self.crcs)
+            res = TransferResult(self.plan.total, time.perf_counter() - t0, 0, bad, first)
+        res.crc = int(header.get("crc32c", 0))
+        self.last_restore = res
+        if strict and res.bad_tiles:
+            raise CheckpointError("%d corrupt tile(s), first at %d" % (res.bad_tiles,
+                                                                      res.first_bad))
+        return res
+
+    def _check_compatible(self, header: Dict) -> None:
+        entries = [TensorEntry.from_json(e) for e in header["entries"]]
+        if (header["total"] != self.plan.total or header["tile_bytes"] != self.plan.tile_bytes
+                or entries != self.plan.entries):
+            raise CheckpointError("checkpoint layout does not match the bound tensors")
+
+    def persist(self, path: str) -> str:
+        """Write the region (header, CRCs, stream) to ``path`` atomically."""
+        header = self.header()
+        if not header.get("complete"):
+            raise CheckpointError("nothing saved yet")
+        tmp = path + ".tpi-partial"
+        data = self.region.array(0, self.size)
+        with open(tmp, "wb") as f:
+            f.write(memoryview(data))
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, path)
+        return path
+
+    def load(self, path: str) -> TransferResult:
+        """Read a persisted checkpoint file into the region, then :meth:`restore`."""
+        with open(path, "rb") as f:
+            head = np.frombuffer(f.read(self.crc_offset), np.uint8)
+            header = self.read_header(head)
+            self._check_compatible(header)
+            f.seek(0)
+            dst = self.region.array(0, self.size)
+            view = memoryview(dst)
+            off = 0
+            while off < self.size:
+                n = f.readinto(view[off:off + (64 << 20)])
+                if not n:
+                    break
+                off += n
+        return self.restore()
+
+    def close(self) -> None:
+        if self.engine is not None:
+            self.engine.close()
+            self.engine = None
+        if self.region is not None:
+            self.crcs = None
+            self.region.close()
+            self.region = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def describe_checkpoint(path: str) -> Dict:
+    """Header of a persisted checkpoint file (no tensors needed)."""
+    with open(path, "rb") as f:
+        pre = f.read(PREAMBLE)
+        if pre[:8] != MAGIC:
+            raise CheckpointError("%s is not a checkpoint" % path)
+        (n,) = struct.unpack("<Q", pre[8:16])
+        return json.loads(f.read(n))

@@ -1,0 +1,81 @@
+"""Host memory regions for checkpoint spills.
+
+A region is one mapping holding ``[preamble | tile CRCs | packed stream]``.  Anonymous regions
+model "host DRAM"; file-backed ones (``/dev/shm/...`` or a file in the task's storage root)
+outlive the rank process, which is what lets a preempted rank's successor restore from
+host memory.  For device checkpoints the region is NUMA-bound to the GPU's socket, populated
+with parallel first touch and registered with HIP once (``hipHostRegister``), so every later
+save/restore is a pure DMA pipeline.
+"""
+from __future__ import annotations
+
+import ctypes
+import mmap
+import os
+from typing import Optional
+
+import numpy as np
+
+from ..ops import hip
+
+
+class HostRegion:
+    def __init__(self, size: int, path: Optional[str] = None, *, device: bool = False,
+                 numa_node: int = -1, populate: bool = True):
+        self.size = size
+        self.path = path
+        self.device = device
+        self.registered = False
+        self._mmap = None
+        if device:
+            lib = hip()
+            enc = path.encode() if path else None
+            ptr = lib.tpi_host_map(enc, size, numa_node, 1 if populate else 0)
+            if not ptr:
+                raise MemoryError("tpi_host_map(%d bytes) failed: %s" % (size, lib.error()))
+            self.addr = int(ptr)
+            lib.check(lib.tpi_host_register(ctypes.c_void_p(self.addr), size), "hipHostRegister")
+            self.registered = True
+        else:
+            if path:
+                fd = os.open(path, os.O_RDWR | os.O_CREAT, 0o600)
+                try:
+                    if os.fstat(fd).st_size < size:
+                        os.ftruncate(fd, size)
+                    self._mmap = mmap.mmap(fd, size)
+                finally:
+                    os.close(fd)
+            else:
+                self._mmap = mmap.mmap(-1, size)
+            buf = (ctypes.c_char * size).from_buffer(self._mmap)
+            self.addr = ctypes.addressof(buf)
+            del buf
+
+    def array(self, offset: int = 0, length: Optional[int] = None, dtype=np.uint8) -> np.ndarray:
+        """numpy view of ``[offset, offset + length)``."""
+        length = self.size - offset if length is None else length
+        itemsize = np.dtype(dtype).itemsize
+        buf = (ctypes.c_char * length).from_address(self.addr + offset)
+        arr = np.frombuffer(buf, dtype=np.uint8, count=length)
+        return arr.view(dtype) if itemsize > 1 else arr
+
+    def close(self) -> None:
+        if self.addr is None:
+            return
+        if self.device:
+            lib = hip()
+            if self.registered:
+                lib.tpi_host_unregister(ctypes.c_void_p(self.addr))
+            lib.tpi_host_unmap(ctypes.c_void_p(self.addr), self.size)
+        elif self._mmap is not None:
+            try:
+                self._mmap.close()
+            except BufferError:  # outstanding numpy views; the mapping dies with them
+                pass
+        self.addr = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass

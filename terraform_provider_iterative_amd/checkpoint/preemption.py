@@ -1,0 +1,104 @@
+"""Preemption (SIGTERM) handling for rank processes.
+
+The reference distinguishes preemption from completion on the VM: a machine that is
+shutting down writes no status and gets respawned with the workdir restored from the bucket
+(``machine-script.sh.tpl:10-15,51,89``).  Here the supervisor forwards SIGTERM to the ranks;
+a rank that installed :func:`install` checkpoints its registered tensors to host memory (and
+optionally the storage root) and exits with :data:`PREEMPTED_EXIT_CODE`, and its successor
+calls :func:`resume` to restore them.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import signal
+import sys
+import threading
+import time
+from typing import Callable, Dict, List, Optional
+
+from .checkpointer import Checkpointer, CheckpointError
+
+log = logging.getLogger("tpi.preemption")
+
+PREEMPTED_EXIT_CODE = 143  # 128 + SIGTERM, what an un-handled SIGTERM would report
+
+_registered: List[Checkpointer] = []
+_persist_paths: Dict[int, str] = {}
+_callbacks: List[Callable[[], Optional[Dict]]] = []
+_installed = False
+_fired = threading.Event()
+
+
+def register(checkpointer: Checkpointer, persist_path: Optional[str] = None) -> None:
+    _registered.append(checkpointer)
+    if persist_path:
+        _persist_paths[id(checkpointer)] = persist_path
+
+
+def on_preempt(callback: Callable[[], Optional[Dict]]) -> None:
+    """Callback run before the save; may return metadata (e.g. ``{"step": n}``)."""
+    _callbacks.append(callback)
+
+
+def preempted() -> bool:
+    return _fired.is_set()
+
+
+def checkpoint_all(metadata: Optional[Dict] = None) -> List[float]:
+    """Save every registered checkpointer; returns per-checkpointer GB/s."""
+    meta = dict(metadata or {})
+    for cb in _callbacks:
+        extra = cb()
+        if extra:
+            meta.update(extra)
+    rates = []
+    for ck in _registered:
+        res = ck.save(meta)
+        rates.append(res.gbps)
+        path = _persist_paths.get(id(ck))
+        if path:
+            ck.persist(path)
+    return rates
+
+
+def _handler(signum, frame):  # pragma: no cover - exercised in subprocess tests
+    if _fired.is_set():
+        return
+    _fired.set()
+    t0 = time.perf_counter()
+    try:
+        rates = checkpoint_all({"reason": "preempted", "signal": signum})
+        print("tpi: preemption checkpoint saved in %.3fs (%s GB/s)" % (
+            time.perf_counter() - t0, ", ".join("%.1f" % r for r in rates)), flush=True)
+        code = PREEMPTED_EXIT_CODE
+    except Exception as error:
+        print("tpi: preemption checkpoint FAILED: %s" % error, file=sys.stderr, flush=True)
+        code = 1
+    sys.stdout.flush()
+    os._exit(code)
+
+
+def install(signals=(signal.SIGTERM,)) -> None:
+    global _installed
+    for sig in signals:
+        signal.signal(sig, _handler)
+    _installed = True
+
+
+def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None) -> Optional[Dict]:
+    """Restore from the host region (or ``persist_path``) if a complete checkpoint exists.
+
+    Returns the checkpoint metadata, or ``None`` for a fresh start.
+    """
+    try:
+        header = checkpointer.header()
+        if header.get("complete"):
+            checkpointer.restore()
+            return header.get("metadata", {})
+    except CheckpointError:
+        pass
+    if persist_path and os.path.exists(persist_path):
+        checkpointer.load(persist_path)
+        return checkpointer.header().get("metadata", {})
+    return None

@@ -1,0 +1,92 @@
+"""Checkpointer on CPU tensors (host C++ path): save/restore/persist/load/corruption."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from terraform_provider_iterative_amd.checkpoint import (CheckpointError, Checkpointer,
+                                                         describe_checkpoint)
+
+
+def _model(seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return {
+        "embed": torch.randn(300, 64, generator=g).to(torch.bfloat16),
+        "w1": torch.randn(64, 256, generator=g),
+        "b1": torch.randn(256, generator=g),
+        "step": torch.tensor(17, dtype=torch.int64),
+        "view": torch.randn(40, 30, generator=g).t(),
+    }
+
+
+def test_save_restore_anonymous():
+    src = _model()
+    ref = {k: v.clone() for k, v in src.items()}
+    with Checkpointer(src, tile_bytes=8192) as ck:
+        res = ck.save({"step": 17})
+        assert res.bytes == ck.plan.total and res.crc != 0
+        for v in src.values():
+            v.zero_()
+        out = ck.restore()
+        assert out.bad_tiles == 0
+        assert ck.header()["metadata"] == {"step": 17}
+    for k in ref:
+        assert torch.equal(src[k], ref[k]), k
+
+
+def test_shared_file_survives_object(tmp_path):
+    path = str(tmp_path / "spill.bin")
+    src = _model(1)
+    ref = {k: v.clone() for k, v in src.items()}
+    with Checkpointer(src, path=path, tile_bytes=4096) as ck:
+        ck.save({"epoch": 3})
+    fresh = {k: torch.zeros_like(v) for k, v in ref.items()}
+    fresh["view"] = torch.zeros(40, 30).t()
+    with Checkpointer(fresh, path=path, tile_bytes=4096) as ck2:
+        ck2.restore()
+        assert ck2.header()["metadata"]["epoch"] == 3
+    for k in ref:
+        assert torch.equal(fresh[k], ref[k]), k
+
+
+def test_persist_load_and_corruption(tmp_path):
+    src = _model(2)
+    with Checkpointer(src, tile_bytes=4096) as ck:
+        ck.save()
+        path = ck.persist(str(tmp_path / "ckpt.tpi"))
+    info = describe_checkpoint(path)
+    assert info["complete"] and info["total"] > 0
+    dst = {k: torch.zeros_like(v) for k, v in src.items()}
+    dst["view"] = torch.zeros(40, 30).t()
+    with Checkpointer(dst, tile_bytes=4096) as ck:
+        ck.load(path)
+    assert all(torch.equal(dst[k], src[k]) for k in src)
+    # flip one payload byte on disk -> strict restore refuses
+    with open(path, "r+b") as f:
+        f.seek(info["stream_offset"] + 100)
+        b = f.read(1)
+        f.seek(info["stream_offset"] + 100)
+        f.write(bytes([b[0] ^ 1]))
+    with Checkpointer(dst, tile_bytes=4096) as ck:
+        with pytest.raises(CheckpointError, match="corrupt"):
+            ck.load(path)
+
+
+def test_incomplete_save_is_rejected(tmp_path):
+    src = _model(3)
+    with Checkpointer(src, tile_bytes=4096) as ck:
+        with pytest.raises(CheckpointError):
+            ck.restore()
+
+
+def test_layout_mismatch(tmp_path):
+    path = str(tmp_path / "spill.bin")
+    with Checkpointer(_model(), path=path, tile_bytes=4096) as ck:
+        ck.save()
+    other = {"x": torch.zeros(10)}
+    with Checkpointer(other, path=path, tile_bytes=4096) as ck:
+        with pytest.raises(CheckpointError):
+            ck.restore()
+    assert os.path.getsize(path) > 0
+    assert np.uint32  # keep numpy import used
