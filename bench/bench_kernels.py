@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Device-side throughput of the data-plane kernels (HBM-bound reference: a torch copy).
+
+Reports GB/s of payload processed per kernel (pack/unpack move 2x that over HBM):
+  crc32c_tiles   read-only CRC32C per 1 MiB tile
+  shard_hash     read-only striped XXH64 per 1 MiB shard
+  pack_device    gather tensors -> packed buffer + CRC (read + write)
+  unpack_device  packed buffer -> tensors + CRC verify (read + write)
+  torch_copy     dst.copy_(src) (read + write), the roofline reference
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timeit(fn, iters):
+    import torch
+
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gb", type=float, default=8.0)
+    p.add_argument("--iters", type=int, default=5)
+    args = p.parse_args()
+    import torch
+
+    from terraform_provider_iterative_amd import ops
+    from terraform_provider_iterative_amd.ops.packing import PackPlan, pack, unpack
+
+    n = int(args.gb * 1e9) // 4096 * 4096
+    dev = torch.device("cuda", 0)
+    buf = torch.randint(0, 256, (n,), dtype=torch.uint8, device=dev)
+    out = {}
+    t = timeit(lambda: ops.crc32c_tiles(buf), args.iters)
+    out["crc32c_tiles_GBps"] = n / t / 1e9
+    t = timeit(lambda: ops.shard_hash(buf), args.iters)
+    out["shard_hash_GBps"] = n / t / 1e9
+    # 16 tensors of mixed size (like a model shard) -> one stream
+    sizes = [n // 32] * 8 + [n // 64] * 16
+    views, off = {}, 0
+    for i, s in enumerate(sizes):
+        s = s // 256 * 256
+        views["t%d" % i] = buf[off:off + s]
+        off += s
+    plan = PackPlan.from_tensors(views)
+    stream = torch.empty(plan.total, dtype=torch.uint8, device=dev)
+    crcs = [None]
+
+    def do_pack():
+        crcs[0] = pack(plan, stream)[1]
+
+    t = timeit(do_pack, args.iters)
+    out["pack_GBps"] = plan.total / t / 1e9
+    t = timeit(lambda: unpack(plan, stream, crcs[0]), args.iters)
+    out["unpack_GBps"] = plan.total / t / 1e9
+    dst = torch.empty_like(buf)
+    t = timeit(lambda: dst.copy_(buf), args.iters)
+    out["torch_copy_GBps"] = n / t / 1e9
+    out["bytes"] = n
+    print(json.dumps({k: round(v, 1) if isinstance(v, float) else v for k, v in out.items()}))
+
+
+if __name__ == "__main__":
+    main()

@@ -310,6 +310,12 @@ int tpi_restore(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, const
   const uint32_t init_full = init_for(tile);
   const uint32_t init_last = init_for(total % tile ? total % tile : tile);
   unsigned long long bad_init[2] = {0ull, ~0ull};
+  if (signal_stream) {
+    // The unpack overwrites the caller's tensors: order it after the caller's pending work
+    // on them (e.g. a zero_() still queued on torch's stream).
+    HIP_OK(hipEventRecord(e->ev_wait, (hipStream_t)signal_stream));
+    HIP_OK(hipStreamWaitEvent(e->compute, e->ev_wait, 0));
+  }
   HIP_OK(hipMemcpyAsync(e->d_crcs, crcs, ntiles * sizeof(uint32_t), hipMemcpyHostToDevice,
                         e->compute));
   HIP_OK(hipMemcpyAsync(e->d_bad, bad_init, sizeof(bad_init), hipMemcpyHostToDevice,

@@ -340,22 +340,18 @@ __global__ __launch_bounds__(WG) void k_shard_hash(const uint8_t* __restrict__ d
     h = seed + TPI_XXH_P5;
   }
   h += mylen;
-  uint8_t tail[TPI_HASH_STRIPE];
-  uint32_t nt = 0;
-  if (owns_tail) {
-    for (uint32_t i = 0; i < rem; ++i) tail[i] = d[full * TPI_HASH_STRIPE + i];
-    nt = rem;
-  }
-  dig[lane] = tpi_xxh_finish(h, tail, nt);
+  // The tail (< 32 bytes, one lane per shard) is read straight from global memory.
+  dig[lane] = tpi_xxh_finish(h, d + full * TPI_HASH_STRIPE, owns_tail ? rem : 0);
   __syncthreads();
 
   // XXH64 over the 2048-byte digest array: 64 stripes of 4 words; lane k<4 owns word k.
   if (lane < 64) {
     uint64_t v = 0;
     if (lane < 4) {
-      const uint64_t init[4] = {seed + TPI_XXH_P1 + TPI_XXH_P2, seed + TPI_XXH_P2, seed,
-                                seed - TPI_XXH_P1};
-      v = init[lane];
+      v = lane == 0 ? seed + TPI_XXH_P1 + TPI_XXH_P2
+        : lane == 1 ? seed + TPI_XXH_P2
+        : lane == 2 ? seed
+                    : seed - TPI_XXH_P1;
       for (int s = 0; s < TPI_HASH_LANES / 4; ++s) v = tpi_xxh_round(v, dig[4 * s + lane]);
     }
     const uint64_t v1 = __shfl(v, 0, 64), v2 = __shfl(v, 1, 64), v3 = __shfl(v, 2, 64),

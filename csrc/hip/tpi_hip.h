@@ -62,6 +62,8 @@ uint64_t tpi_engine_chunk_bytes(const tpi_engine* e);
 int tpi_save(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* host_dst,
              uint32_t* crcs_out, int mode, uint64_t wait_stream, tpi_stats* stats);
 // Inverse: stream `total` bytes from `host_src`, verify each tile against `crcs`, scatter.
+// `signal_stream` (may be 0): the unpack starts after that stream's pending work and the
+// stream waits for the unpack before its later work.
 // Returns 0 and sets *bad_tiles (0 = all verified) / *first_bad (-1 if none).
 int tpi_restore(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total,
                 const void* host_src, const uint32_t* crcs, int mode, uint64_t signal_stream,

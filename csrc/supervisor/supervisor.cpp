@@ -1,0 +1,742 @@
+// tpi-supervisor: the on-node runtime of a task (one process per task).
+//
+// It replaces the reference's per-VM machinery -- the cloud scaling group that keeps
+// `parallelism` machines alive and the systemd unit + bash sync loops of
+// task/common/machine/machine-script.sh.tpl -- with one event loop on this node:
+//
+//  * spawns `parallelism` rank processes (own process group, cwd = task workdir, env from
+//    the spec plus RANK/WORLD_SIZE/LOCAL_RANK/MASTER_* and HIP_VISIBLE_DEVICES for the GPUs
+//    placed for that rank); PR_SET_PDEATHSIG ties them to the supervisor;
+//  * streams every stdout/stderr line straight into reports/task-<machine uuid> as
+//    "YYYY-MM-DDTHH:MM:SSZ line" the moment it arrives (the reference polls journald every
+//    5 s, tpl:108-116; this is the first-log-latency floor);
+//  * writes reports/status-<uuid> = {"result","code","status"} when a rank exits on its own
+//    (systemd ExecStop semantics, tpl:51) and nothing when it was preempted or stopped;
+//  * enforces the absolute deadline (RuntimeMaxSec, tpl:36-41): SIGTERM, grace, SIGKILL,
+//    status result "timeout";
+//  * preemption: SIGUSR1 to the supervisor, or a rank dying of SIGTERM / exiting 143 (the
+//    code the checkpoint handler uses after spilling to host DRAM), respawns the rank(s)
+//    with a new machine identity -- gang-wide when ranks are coupled by RCCL -- like the
+//    scaling group replacing a reclaimed spot VM (tpl:89, resource_auto_scaling_group.go);
+//  * SIGTERM/SIGINT/SIGHUP = stop (`leo stop`, scale to 0): ranks terminated, no status;
+//  * exits when no rank is left to run ("no waste" auto-cleanup, tpl:10-15), removing its
+//    GPU lease files.
+//
+// State for readers: supervisor/state.json (atomically replaced) and an append-only
+// supervisor/events.jsonl journal.
+#include <errno.h>
+#include <fcntl.h>
+#include <poll.h>
+#include <signal.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/prctl.h>
+#include <sys/signalfd.h>
+#include <sys/stat.h>
+#include <sys/time.h>
+#include <sys/types.h>
+#include <sys/wait.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "json.h"
+
+using tpi::json::quote;
+using tpi::json::Value;
+
+namespace {
+
+double now() {
+  struct timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+std::string read_file(const std::string& path) {
+  std::ifstream in(path, std::ios::binary);
+  if (!in) throw std::runtime_error("cannot read " + path);
+  std::stringstream ss;
+  ss << in.rdbuf();
+  return ss.str();
+}
+
+void write_all(int fd, const std::string& s) {
+  const char* p = s.data();
+  size_t left = s.size();
+  while (left) {
+    ssize_t n = write(fd, p, left);
+    if (n < 0) {
+      if (errno == EINTR) continue;
+      return;
+    }
+    p += n;
+    left -= (size_t)n;
+  }
+}
+
+bool atomic_write(const std::string& path, const std::string& data) {
+  std::string tmp = path + ".tmp";
+  int fd = open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+  if (fd < 0) return false;
+  write_all(fd, data);
+  close(fd);
+  return rename(tmp.c_str(), path.c_str()) == 0;
+}
+
+std::string uuid4() {
+  unsigned char b[16];
+  int fd = open("/dev/urandom", O_RDONLY | O_CLOEXEC);
+  if (fd < 0 || read(fd, b, 16) != 16) {
+    for (int i = 0; i < 16; ++i) b[i] = (unsigned char)(rand() & 0xff);
+  }
+  if (fd >= 0) close(fd);
+  b[6] = (b[6] & 0x0f) | 0x40;
+  b[8] = (b[8] & 0x3f) | 0x80;
+  char out[37];
+  snprintf(out, sizeof(out),
+           "%02x%02x%02x%02x-%02x%02x-%02x%02x-%02x%02x-%02x%02x%02x%02x%02x%02x", b[0], b[1],
+           b[2], b[3], b[4], b[5], b[6], b[7], b[8], b[9], b[10], b[11], b[12], b[13], b[14],
+           b[15]);
+  return out;
+}
+
+std::string utc_stamp(double t) {
+  time_t s = (time_t)t;
+  struct tm tm;
+  gmtime_r(&s, &tm);
+  char buf[32];
+  strftime(buf, sizeof(buf), "%Y-%m-%dT%H:%M:%SZ", &tm);
+  return buf;
+}
+
+const char* signame(int sig) {
+  switch (sig) {
+    case SIGTERM: return "TERM";
+    case SIGKILL: return "KILL";
+    case SIGINT: return "INT";
+    case SIGHUP: return "HUP";
+    case SIGSEGV: return "SEGV";
+    case SIGABRT: return "ABRT";
+    case SIGBUS: return "BUS";
+    case SIGFPE: return "FPE";
+    case SIGILL: return "ILL";
+    case SIGPIPE: return "PIPE";
+    case SIGQUIT: return "QUIT";
+    case SIGUSR1: return "USR1";
+    case SIGUSR2: return "USR2";
+    default: return "UNKNOWN";
+  }
+}
+
+enum class TermReason { NONE, STOP, PREEMPT, TIMEOUT, FAILFAST };
+
+// --daemon: the launching parent blocks on this pipe until the ranks are spawned and the
+// first state.json is on disk, so "create returned" implies "supervisor visible".
+int g_ready_fd = -1;
+
+void signal_ready() {
+  if (g_ready_fd >= 0) {
+    write_all(g_ready_fd, "1");
+    close(g_ready_fd);
+    g_ready_fd = -1;
+  }
+}
+
+struct Rank {
+  int index = 0;
+  std::string gpus;
+  pid_t pid = -1;
+  int fd = -1;
+  int logfd = -1;
+  std::string uuid;
+  std::string partial;
+  enum State { PENDING, RUNNING, DONE, PREEMPTED } state = PENDING;
+  int restarts = 0;
+  TermReason reason = TermReason::NONE;
+  double term_at = 0;
+  bool killed = false;
+  int exit_code = -1, exit_signal = 0;
+  double started = 0;
+};
+
+struct Spec {
+  std::string task_id, task_dir, workdir, script, shell = "/bin/bash";
+  std::vector<std::pair<std::string, std::string>> env;
+  double deadline = 0;
+  int parallelism = 1;
+  std::vector<std::string> rank_gpus;        // HIP_VISIBLE_DEVICES (the task's GPU set)
+  std::vector<std::string> rank_local_gpus;  // the rank's own GPUs, task-visible numbering
+  std::string master_addr = "127.0.0.1";
+  int master_port = 29500;
+  bool gang = true, fail_fast = true, respawn_on_sigterm = true, login_shell = false;
+  int max_restarts = -1;
+  double grace = 30, respawn_delay = 0;
+  std::string reports_dir, state_path, events_path;
+  std::vector<std::string> leases;
+};
+
+Spec load_spec(const std::string& path) {
+  Value v = tpi::json::parse(read_file(path));
+  Spec s;
+  s.task_id = v["task_id"].str();
+  s.task_dir = v["task_dir"].str();
+  s.workdir = v["workdir"].str();
+  s.script = v["script"].str();
+  s.shell = v["shell"].str("/bin/bash");
+  for (auto& kv : v["env"].o) s.env.emplace_back(kv.first, kv.second.str());
+  s.deadline = v["deadline"].num(0);
+  s.parallelism = std::max(1, (int)v["parallelism"].num(1));
+  for (auto& r : v["ranks"].a) {
+    s.rank_gpus.push_back(r["gpus"].str());
+    s.rank_local_gpus.push_back(r["rank_gpus"].str());
+  }
+  s.rank_gpus.resize(s.parallelism);
+  s.rank_local_gpus.resize(s.parallelism);
+  s.master_addr = v["master_addr"].str("127.0.0.1");
+  s.master_port = (int)v["master_port"].num(29500);
+  s.gang = v["gang"].boolean(true);
+  s.fail_fast = v["fail_fast"].boolean(s.parallelism > 1);
+  s.respawn_on_sigterm = v["respawn_on_sigterm"].boolean(true);
+  s.login_shell = v["login_shell"].boolean(false);
+  s.max_restarts = (int)v["max_restarts"].num(-1);
+  s.grace = v["grace_seconds"].num(30);
+  s.respawn_delay = v["respawn_delay"].num(0);
+  s.reports_dir = v["reports_dir"].str(s.task_dir + "/reports");
+  s.state_path = v["state_path"].str(s.task_dir + "/supervisor/state.json");
+  s.events_path = v["events_path"].str(s.task_dir + "/supervisor/events.jsonl");
+  for (auto& l : v["leases"].a) s.leases.push_back(l.str());
+  if (s.workdir.empty() || s.script.empty()) throw std::runtime_error("spec needs workdir+script");
+  return s;
+}
+
+class Supervisor {
+ public:
+  explicit Supervisor(Spec spec) : s_(std::move(spec)) {
+    ranks_.resize(s_.parallelism);
+    for (int i = 0; i < s_.parallelism; ++i) {
+      ranks_[i].index = i;
+      ranks_[i].gpus = s_.rank_gpus[i];
+    }
+  }
+
+  int run() {
+    sigset_t mask;
+    sigemptyset(&mask);
+    for (int sig : {SIGCHLD, SIGTERM, SIGINT, SIGHUP, SIGUSR1, SIGUSR2}) sigaddset(&mask, sig);
+    sigprocmask(SIG_BLOCK, &mask, nullptr);
+    sfd_ = signalfd(-1, &mask, SFD_CLOEXEC | SFD_NONBLOCK);
+    signal(SIGPIPE, SIG_IGN);
+    started_ = now();
+    event("supervisor-start", {"pid " + std::to_string(getpid()),
+                               "parallelism " + std::to_string(s_.parallelism)});
+    if (s_.deadline > 0 && now() >= s_.deadline) {
+      // Past the deadline before running (tpl:38-41): nothing may run any more.
+      for (auto& r : ranks_) {
+        r.uuid = uuid4();
+        write_status(r, "timeout", "", "killed");
+        r.state = Rank::DONE;
+      }
+      event("deadline", {"deadline passed before start"});
+      return finish();
+    }
+    for (auto& r : ranks_) spawn(r);
+    write_state();
+    signal_ready();
+    double last_state = now();
+    while (true) {
+      double t = now();
+      check_deadline(t);
+      check_grace(t);
+      check_respawn(t);
+      if (all_finished()) break;
+      double timeout = 2.0;
+      if (s_.deadline > 0 && !timed_out_) timeout = std::min(timeout, s_.deadline - t);
+      for (auto& r : ranks_)
+        if (r.pid > 0 && r.term_at > 0 && !r.killed)
+          timeout = std::min(timeout, r.term_at + s_.grace - t);
+      if (respawn_at_ > 0) timeout = std::min(timeout, respawn_at_ - t);
+      timeout = std::max(timeout, 0.0);
+      std::vector<struct pollfd> pfds;
+      pfds.push_back({sfd_, POLLIN, 0});
+      std::vector<Rank*> owners;
+      for (auto& r : ranks_)
+        if (r.fd >= 0) {
+          pfds.push_back({r.fd, POLLIN, 0});
+          owners.push_back(&r);
+        }
+      int rc = poll(pfds.data(), pfds.size(), (int)(timeout * 1000) + 1);
+      if (rc < 0 && errno != EINTR) break;
+      for (size_t i = 1; i < pfds.size(); ++i)
+        if (pfds[i].revents & (POLLIN | POLLHUP | POLLERR)) pump(*owners[i - 1]);
+      if (pfds[0].revents & POLLIN) handle_signals();
+      if (dirty_ || now() - last_state > 5) {
+        write_state();
+        last_state = now();
+        dirty_ = false;
+      }
+    }
+    return finish();
+  }
+
+ private:
+  Spec s_;
+  std::vector<Rank> ranks_;
+  int sfd_ = -1;
+  double started_ = 0, respawn_at_ = 0;
+  bool stop_ = false, timed_out_ = false, dirty_ = true;
+  int total_restarts_ = 0;
+
+  void event(const std::string& code, const std::vector<std::string>& desc) {
+    std::string line = "{\"time\": " + std::to_string(now()) + ", \"code\": " + quote(code) +
+                       ", \"description\": [";
+    for (size_t i = 0; i < desc.size(); ++i) line += (i ? ", " : "") + quote(desc[i]);
+    line += "]}\n";
+    int fd = open(s_.events_path.c_str(), O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
+    if (fd >= 0) {
+      write_all(fd, line);
+      close(fd);
+    }
+    dirty_ = true;
+  }
+
+  static const char* state_name(Rank::State st) {
+    switch (st) {
+      case Rank::PENDING: return "pending";
+      case Rank::RUNNING: return "running";
+      case Rank::DONE: return "done";
+      default: return "preempted";
+    }
+  }
+
+  int running() const {
+    int n = 0;
+    for (auto& r : ranks_) n += r.state == Rank::RUNNING;
+    return n;
+  }
+
+  void write_state(const char* phase = nullptr) {
+    std::string p = phase ? phase
+                    : stop_ ? "stopping"
+                    : timed_out_ ? "timing-out"
+                    : respawn_at_ > 0 ? "respawning"
+                                      : "running";
+    std::string out = "{\"pid\": " + std::to_string(getpid()) +
+                      ", \"task_id\": " + quote(s_.task_id) + ", \"phase\": " + quote(p) +
+                      ", \"started_at\": " + std::to_string(started_) +
+                      ", \"heartbeat\": " + std::to_string(now()) +
+                      ", \"running\": " + std::to_string(running()) +
+                      ", \"restarts\": " + std::to_string(total_restarts_) + ", \"ranks\": [";
+    for (size_t i = 0; i < ranks_.size(); ++i) {
+      auto& r = ranks_[i];
+      out += std::string(i ? ", " : "") + "{\"rank\": " + std::to_string(r.index) +
+             ", \"pid\": " + std::to_string(r.pid) + ", \"uuid\": " + quote(r.uuid) +
+             ", \"gpus\": " + quote(r.gpus) + ", \"state\": " + quote(state_name(r.state)) +
+             ", \"restarts\": " + std::to_string(r.restarts) +
+             ", \"exit_code\": " + std::to_string(r.exit_code) +
+             ", \"exit_signal\": " + std::to_string(r.exit_signal) + "}";
+    }
+    out += "]}\n";
+    atomic_write(s_.state_path, out);
+  }
+
+  void write_status(Rank& r, const std::string& result, const std::string& code,
+                    const std::string& status) {
+    std::string body = "{\"result\": " + quote(result) + ", \"code\": " + quote(code) +
+                       ", \"status\": " + quote(status) + "}";
+    std::string path = s_.reports_dir + "/status-" + r.uuid;
+    std::string tmp = s_.reports_dir + "/.status-" + r.uuid + ".tmp";
+    int fd = open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    if (fd >= 0) {
+      write_all(fd, body);
+      close(fd);
+      rename(tmp.c_str(), path.c_str());
+    }
+  }
+
+  std::vector<std::string> rank_env(const Rank& r) {
+    std::vector<std::string> env;
+    bool has_path = false;
+    for (auto& kv : s_.env) {
+      if (kv.first == "PATH") has_path = true;
+      env.push_back(kv.first + "=" + kv.second);
+    }
+    if (!has_path) env.push_back("PATH=/usr/local/sbin:/usr/local/bin:/usr/sbin:/usr/bin:/sbin:/bin");
+    auto add = [&](const std::string& k, const std::string& v) { env.push_back(k + "=" + v); };
+    add("TPI_MACHINE_IDENTITY", r.uuid);
+    add("TPI_LOG_DIRECTORY", s_.reports_dir);
+    add("TPI_DATA_DIRECTORY", s_.workdir);
+    add("TPI_TASK_IDENTIFIER", s_.task_id);
+    add("TPI_TASK_DIRECTORY", s_.task_dir);
+    add("TPI_RESTART_COUNT", std::to_string(r.restarts));
+    if (s_.deadline > 0) {
+      add("TPI_DEADLINE", std::to_string((long long)s_.deadline));
+      add("TPI_REMAINING_RUN_TIME", std::to_string((long long)(s_.deadline - now())));
+    }
+    add("RANK", std::to_string(r.index));
+    add("LOCAL_RANK", std::to_string(r.index));
+    add("WORLD_SIZE", std::to_string(s_.parallelism));
+    add("LOCAL_WORLD_SIZE", std::to_string(s_.parallelism));
+    add("GROUP_RANK", "0");
+    add("MASTER_ADDR", s_.master_addr);
+    add("MASTER_PORT", std::to_string(s_.master_port));
+    add("JOB_COMPLETION_INDEX", std::to_string(r.index));  // k8s Indexed Job parity
+    if (!r.gpus.empty()) {
+      add("HIP_VISIBLE_DEVICES", r.gpus);
+      add("TPI_GPUS", r.gpus);
+      add("TPI_RANK_GPUS", s_.rank_local_gpus[r.index]);
+    }
+    return env;
+  }
+
+  void spawn(Rank& r) {
+    r.uuid = uuid4();
+    r.partial.clear();
+    r.reason = TermReason::NONE;
+    r.term_at = 0;
+    r.killed = false;
+    r.exit_code = -1;
+    r.exit_signal = 0;
+    std::string logpath = s_.reports_dir + "/task-" + r.uuid;
+    r.logfd = open(logpath.c_str(), O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
+    int p[2];
+    if (pipe2(p, O_CLOEXEC)) {
+      event("rank-spawn-failed", {"rank " + std::to_string(r.index), strerror(errno)});
+      r.state = Rank::DONE;
+      write_status(r, "resources", "", "exited");
+      return;
+    }
+    std::vector<std::string> env = rank_env(r);
+    std::vector<char*> envp;
+    for (auto& e : env) envp.push_back(const_cast<char*>(e.c_str()));
+    envp.push_back(nullptr);
+    bool shebang = false;
+    {
+      int sf = open(s_.script.c_str(), O_RDONLY | O_CLOEXEC);
+      char hb[2] = {0, 0};
+      if (sf >= 0) {
+        shebang = read(sf, hb, 2) == 2 && hb[0] == '#' && hb[1] == '!';
+        close(sf);
+      }
+    }
+    std::string exec_cmd = "exec \"$0\"";
+    pid_t parent = getpid();
+    pid_t pid = fork();
+    if (pid == 0) {
+      setpgid(0, 0);
+      prctl(PR_SET_PDEATHSIG, SIGTERM);
+      if (getppid() != parent) _exit(127);
+      sigset_t none;
+      sigemptyset(&none);
+      sigprocmask(SIG_SETMASK, &none, nullptr);
+      for (int sig : {SIGCHLD, SIGTERM, SIGINT, SIGHUP, SIGUSR1, SIGUSR2, SIGPIPE})
+        signal(sig, SIG_DFL);
+      int devnull = open("/dev/null", O_RDONLY);
+      if (devnull >= 0) dup2(devnull, 0);
+      dup2(p[1], 1);
+      dup2(p[1], 2);
+      if (chdir(s_.workdir.c_str())) {
+        dprintf(2, "tpi-supervisor: chdir %s: %s\n", s_.workdir.c_str(), strerror(errno));
+        _exit(126);
+      }
+      if (s_.login_shell) {
+        const char* argv[] = {s_.shell.c_str(), "-lc", exec_cmd.c_str(), s_.script.c_str(), nullptr};
+        execve(s_.shell.c_str(), const_cast<char**>(argv), envp.data());
+      } else if (shebang) {
+        const char* argv[] = {s_.script.c_str(), nullptr};
+        execve(s_.script.c_str(), const_cast<char**>(argv), envp.data());
+      } else {
+        const char* argv[] = {"/bin/sh", s_.script.c_str(), nullptr};
+        execve("/bin/sh", const_cast<char**>(argv), envp.data());
+      }
+      dprintf(2, "tpi-supervisor: exec %s: %s\n", s_.script.c_str(), strerror(errno));
+      _exit(127);
+    }
+    close(p[1]);
+    if (pid < 0) {
+      close(p[0]);
+      event("rank-spawn-failed", {"rank " + std::to_string(r.index), strerror(errno)});
+      r.state = Rank::DONE;
+      write_status(r, "resources", "", "exited");
+      return;
+    }
+    setpgid(pid, pid);
+    fcntl(p[0], F_SETFL, fcntl(p[0], F_GETFL) | O_NONBLOCK);
+    r.pid = pid;
+    r.fd = p[0];
+    r.state = Rank::RUNNING;
+    r.started = now();
+    event("rank-start", {"rank " + std::to_string(r.index), "pid " + std::to_string(pid),
+                         "machine " + r.uuid, "gpus " + (r.gpus.empty() ? "-" : r.gpus),
+                         "restart " + std::to_string(r.restarts)});
+  }
+
+  void emit_line(Rank& r, const std::string& line) {
+    if (r.logfd < 0) return;
+    write_all(r.logfd, utc_stamp(now()) + " " + line + "\n");
+  }
+
+  void pump(Rank& r) {
+    char buf[65536];
+    for (;;) {
+      ssize_t n = read(r.fd, buf, sizeof(buf));
+      if (n > 0) {
+        r.partial.append(buf, (size_t)n);
+        size_t start = 0, nl;
+        while ((nl = r.partial.find('\n', start)) != std::string::npos) {
+          emit_line(r, r.partial.substr(start, nl - start));
+          start = nl + 1;
+        }
+        r.partial.erase(0, start);
+        if (r.partial.size() > (1 << 20)) {
+          emit_line(r, r.partial);
+          r.partial.clear();
+        }
+        continue;
+      }
+      if (n == 0) {  // EOF: every writer (rank and its children) closed the pipe
+        if (!r.partial.empty()) emit_line(r, r.partial);
+        r.partial.clear();
+        close(r.fd);
+        r.fd = -1;
+        if (r.pid < 0) close_log(r);
+        return;
+      }
+      if (errno == EINTR) continue;
+      return;  // EAGAIN
+    }
+  }
+
+  void close_log(Rank& r) {
+    if (r.logfd >= 0) {
+      close(r.logfd);
+      r.logfd = -1;
+    }
+  }
+
+  void terminate(Rank& r, TermReason why) {
+    if (r.pid <= 0 || r.state != Rank::RUNNING) return;
+    if (r.reason == TermReason::NONE || why == TermReason::STOP) r.reason = why;
+    if (r.term_at == 0) {
+      r.term_at = now();
+      kill(-r.pid, SIGTERM);
+      kill(r.pid, SIGTERM);
+    }
+  }
+
+  void check_grace(double t) {
+    for (auto& r : ranks_)
+      if (r.pid > 0 && r.term_at > 0 && !r.killed && t >= r.term_at + s_.grace) {
+        kill(-r.pid, SIGKILL);
+        kill(r.pid, SIGKILL);
+        r.killed = true;
+        event("rank-killed", {"rank " + std::to_string(r.index), "grace period expired"});
+      }
+  }
+
+  void check_deadline(double t) {
+    if (s_.deadline <= 0 || timed_out_ || t < s_.deadline) return;
+    timed_out_ = true;
+    respawn_at_ = 0;
+    event("deadline", {"timeout reached"});
+    for (auto& r : ranks_) {
+      if (r.state == Rank::RUNNING) {
+        terminate(r, TermReason::TIMEOUT);
+      } else if (r.state == Rank::PREEMPTED || r.state == Rank::PENDING) {
+        write_status(r, "timeout", "", "killed");
+        r.state = Rank::DONE;
+      }
+    }
+  }
+
+  void check_respawn(double t) {
+    if (respawn_at_ <= 0 || t < respawn_at_ || stop_ || timed_out_) return;
+    if (s_.gang && running() > 0) return;  // wait for the whole gang to go down
+    respawn_at_ = 0;
+    for (auto& r : ranks_)
+      if (r.state == Rank::PREEMPTED) {
+        if (s_.max_restarts >= 0 && r.restarts >= s_.max_restarts) {
+          write_status(r, "start-limit-hit", "", "exited");
+          r.state = Rank::DONE;
+          event("rank-restart-limit", {"rank " + std::to_string(r.index)});
+          continue;
+        }
+        r.restarts++;
+        total_restarts_++;
+        event("respawn", {"rank " + std::to_string(r.index),
+                          "restart " + std::to_string(r.restarts)});
+        spawn(r);
+      }
+  }
+
+  void handle_signals() {
+    struct signalfd_siginfo si;
+    while (read(sfd_, &si, sizeof(si)) == sizeof(si)) {
+      switch (si.ssi_signo) {
+        case SIGCHLD: reap(); break;
+        case SIGTERM:
+        case SIGINT:
+        case SIGHUP:
+          if (!stop_) {
+            stop_ = true;
+            respawn_at_ = 0;
+            event("stop-requested", {std::string("signal ") + signame(si.ssi_signo)});
+            for (auto& r : ranks_) {
+              if (r.state == Rank::RUNNING) terminate(r, TermReason::STOP);
+              else if (r.state != Rank::DONE) r.state = Rank::DONE;
+            }
+          }
+          break;
+        case SIGUSR1:
+          if (!stop_ && !timed_out_) {
+            event("preempt-requested", {"all ranks"});
+            for (auto& r : ranks_) terminate(r, TermReason::PREEMPT);
+          }
+          break;
+        default: break;
+      }
+    }
+    reap();
+  }
+
+  void reap() {
+    for (;;) {
+      int st = 0;
+      pid_t pid = waitpid(-1, &st, WNOHANG);
+      if (pid <= 0) return;
+      for (auto& r : ranks_)
+        if (r.pid == pid) on_exit(r, st);
+    }
+  }
+
+  void on_exit(Rank& r, int st) {
+    if (r.fd >= 0) pump(r);  // drain what is already buffered
+    r.pid = -1;
+    if (r.fd < 0) close_log(r);
+    bool signaled = WIFSIGNALED(st);
+    int sig = signaled ? WTERMSIG(st) : 0;
+    int code = WIFEXITED(st) ? WEXITSTATUS(st) : -1;
+    r.exit_code = code;
+    r.exit_signal = sig;
+    std::string code_s = signaled ? signame(sig) : std::to_string(code);
+    std::string status_s = signaled ? (WCOREDUMP(st) ? "dumped" : "killed") : "exited";
+    std::vector<std::string> desc = {"rank " + std::to_string(r.index), "machine " + r.uuid,
+                                     (signaled ? "signal " : "code ") + code_s};
+    if (r.reason == TermReason::STOP || stop_) {
+      r.state = Rank::DONE;  // scaled to zero: no status (the machine was "shut down")
+      event("rank-stopped", desc);
+      return;
+    }
+    if (r.reason == TermReason::TIMEOUT) {
+      r.state = Rank::DONE;
+      write_status(r, "timeout", code_s, status_s);
+      event("rank-timeout", desc);
+      return;
+    }
+    bool preempted = r.reason == TermReason::PREEMPT ||
+                     (s_.respawn_on_sigterm && r.reason == TermReason::NONE &&
+                      ((signaled && sig == SIGTERM) || code == 143));
+    if (preempted && !timed_out_) {
+      r.state = Rank::PREEMPTED;
+      event("rank-preempted", desc);
+      if (s_.gang)
+        for (auto& o : ranks_)
+          if (o.state == Rank::RUNNING) terminate(o, TermReason::PREEMPT);
+      respawn_at_ = now() + s_.respawn_delay;
+      return;
+    }
+    r.state = Rank::DONE;
+    std::string result = signaled ? "signal" : (code == 0 ? "success" : "exit-code");
+    if (r.reason == TermReason::FAILFAST) result = "signal";
+    write_status(r, result, code_s, status_s);
+    event("rank-exit", desc);
+    if (!signaled && code != 0 && s_.fail_fast)
+      for (auto& o : ranks_)
+        if (o.state == Rank::RUNNING) terminate(o, TermReason::FAILFAST);
+  }
+
+  bool all_finished() {
+    for (auto& r : ranks_)
+      if (r.state != Rank::DONE || r.pid > 0) return false;
+    return true;
+  }
+
+  int finish() {
+    // Ranks are gone; give lingering writers (daemonized children) a moment, then close.
+    double until = now() + 0.5;
+    while (now() < until) {
+      bool open_fd = false;
+      std::vector<struct pollfd> pfds;
+      std::vector<Rank*> owners;
+      for (auto& r : ranks_)
+        if (r.fd >= 0) {
+          open_fd = true;
+          pfds.push_back({r.fd, POLLIN, 0});
+          owners.push_back(&r);
+        }
+      if (!open_fd) break;
+      poll(pfds.data(), pfds.size(), 50);
+      for (size_t i = 0; i < pfds.size(); ++i)
+        if (pfds[i].revents) pump(*owners[i]);
+    }
+    for (auto& r : ranks_) {
+      if (r.fd >= 0) {
+        if (!r.partial.empty()) emit_line(r, r.partial);
+        close(r.fd);
+        r.fd = -1;
+      }
+      close_log(r);
+    }
+    for (auto& l : s_.leases) unlink(l.c_str());
+    event("supervisor-exit", {stop_ ? "stopped" : "all ranks finished"});
+    write_state("stopped");
+    signal_ready();
+    return 0;
+  }
+};
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  bool daemonize = argc >= 3 && std::string(argv[1]) == "--daemon";
+  const char* spec_path = daemonize ? argv[2] : (argc >= 2 ? argv[1] : nullptr);
+  if (!spec_path) {
+    fprintf(stderr, "usage: %s [--daemon] <spec.json>\n", argv[0]);
+    return 2;
+  }
+  try {
+    Spec spec = load_spec(spec_path);
+    if (daemonize) {
+      int p[2];
+      if (pipe2(p, O_CLOEXEC)) throw std::runtime_error("pipe2 failed");
+      pid_t pid = fork();
+      if (pid < 0) throw std::runtime_error("fork failed");
+      if (pid > 0) {  // launcher: report the daemon's pid once it is ready
+        close(p[1]);
+        char c;
+        ssize_t n;
+        do {
+          n = read(p[0], &c, 1);
+        } while (n < 0 && errno == EINTR);
+        printf("%d\n", (int)pid);
+        fflush(stdout);
+        _exit(n == 1 ? 0 : 1);
+      }
+      close(p[0]);
+      g_ready_fd = p[1];
+      setsid();
+      dup2(2, 1);  // stdout -> the supervisor log the launcher gave us as stderr
+    }
+    Supervisor sup(std::move(spec));
+    return sup.run();
+  } catch (const std::exception& e) {
+    fprintf(stderr, "tpi-supervisor: %s\n", e.what());
+    return 1;
+  }
+}

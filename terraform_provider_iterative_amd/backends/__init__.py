@@ -1,0 +1,48 @@
+"""Task factory (reference: ``task/task.go:17-45``)."""
+from __future__ import annotations
+
+import os
+from dataclasses import replace
+from typing import List
+
+from ..models.cloud import (ALL_PROVIDERS, NODE_PROVIDERS, REMOTE_PROVIDERS, Cloud)
+from ..models.values import Task as TaskSpec
+from ..utils.identifier import Identifier
+from .base import Resource, Task
+from .node import NodeTask, list_tasks as _node_list
+from .remote import RemoteProviderUnavailable, RemoteTask, list_tasks as _remote_list
+
+
+class UnknownProviderError(ValueError):
+    def __init__(self, provider: str):
+        super().__init__("unknown provider: %r (expected one of %s)"
+                         % (provider, ", ".join(ALL_PROVIDERS)))
+
+
+def _retarget(cloud: Cloud) -> Cloud:
+    target = os.environ.get("TPI_REMOTE_AS")
+    if cloud.provider in REMOTE_PROVIDERS and target in NODE_PROVIDERS:
+        return replace(cloud, provider=target)
+    return cloud
+
+
+def new(cloud: Cloud, identifier: Identifier, task: TaskSpec) -> Task:
+    cloud = _retarget(cloud)
+    if cloud.provider in NODE_PROVIDERS:
+        return NodeTask(cloud, identifier, task)
+    if cloud.provider in REMOTE_PROVIDERS:
+        return RemoteTask(cloud, identifier, task)
+    raise UnknownProviderError(cloud.provider)
+
+
+def list_tasks(cloud: Cloud) -> List[Identifier]:
+    cloud = _retarget(cloud)
+    if cloud.provider in NODE_PROVIDERS:
+        return _node_list(cloud)
+    if cloud.provider in REMOTE_PROVIDERS:
+        return _remote_list(cloud)
+    raise UnknownProviderError(cloud.provider)
+
+
+__all__ = ["new", "list_tasks", "Task", "Resource", "NodeTask", "RemoteTask",
+           "RemoteProviderUnavailable", "UnknownProviderError"]
