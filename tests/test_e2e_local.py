@@ -1,0 +1,187 @@
+"""Config 1 end to end on CPU: main.tf -> tpi apply -> script -> logs/status -> destroy,
+and the reference smoke-test flow (task/task_smoke_test.go:63-237) through leo."""
+import json
+import os
+import subprocess
+import sys
+import time
+import uuid
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TPI = [sys.executable, os.path.join(ROOT, "bin", "tpi")]
+LEO = [sys.executable, os.path.join(ROOT, "bin", "leo")]
+
+
+@pytest.fixture()
+def env(tmp_path):
+    e = dict(os.environ)
+    e["TPI_STATE_ROOT"] = str(tmp_path / "state")
+    e.pop("TF_LOG_PROVIDER", None)
+    for k in list(e):
+        if k.startswith("TASK_"):
+            e.pop(k)
+    return e
+
+
+def run(cmd, cwd, env, check=True, timeout=120):
+    r = subprocess.run(cmd, cwd=cwd, env=env, capture_output=True, text=True, timeout=timeout)
+    if check and r.returncode != 0:
+        raise AssertionError("%s failed (%d):\n%s\n%s" % (cmd, r.returncode, r.stdout, r.stderr))
+    return r
+
+
+HELLO = '''
+terraform {
+  required_providers { iterative = { source = "iterative/iterative" } }
+}
+provider "iterative" {}
+
+resource "iterative_task" "hello" {
+  name    = "hello-%(suffix)s"
+  cloud   = "local"
+  machine = "s"
+  environment = { GREETING = "hello", INHERITED = "" }
+  storage {
+    workdir = "."
+    output  = "results"
+  }
+  script = <<-END
+    #!/bin/bash
+    mkdir -p results
+    echo "$GREETING from rank $RANK of $WORLD_SIZE ($TPI_TASK)"
+    echo "inherited=$INHERITED"
+    cat input.txt
+    echo done > results/out.txt
+  END
+}
+
+output "status" { value = iterative_task.hello.status }
+'''
+
+
+def _wait_state(workdir, env, predicate, timeout=30):
+    deadline = time.time() + timeout
+    state = None
+    while time.time() < deadline:
+        run(TPI + ["refresh"], workdir, env)
+        with open(os.path.join(workdir, "terraform.tfstate")) as f:
+            state = json.load(f)
+        attrs = state["resources"][0]["instances"][0]["attributes"]
+        if predicate(attrs):
+            return attrs
+        time.sleep(0.2)
+    raise AssertionError("timed out; last state %s" % state)
+
+
+def test_apply_refresh_destroy(tmp_path, env):
+    work = tmp_path / "project"
+    work.mkdir()
+    (work / "main.tf").write_text(HELLO % {"suffix": uuid.uuid4().hex[:6]})
+    (work / "input.txt").write_text("payload-from-workdir\n")
+    env["INHERITED"] = "from-parent"
+    run(TPI + ["init"], str(work), env)
+    run(TPI + ["validate"], str(work), env)
+    plan = run(TPI + ["plan"], str(work), env)
+    assert "iterative_task.hello will be created" in plan.stdout
+    assert "Plan: 1 to add, 0 to change, 0 to destroy." in plan.stdout
+    out = run(TPI + ["apply", "-auto-approve"], str(work), env)
+    assert "Apply complete! Resources: 1 added" in out.stdout
+    state = json.loads((work / "terraform.tfstate").read_text())
+    assert state["version"] == 4
+    res = state["resources"][0]
+    assert res["type"] == "iterative_task" and res["provider"].endswith('iterative/iterative"]')
+    attrs = res["instances"][0]["attributes"]
+    assert attrs["id"].startswith("tpi-hello-")
+    attrs = _wait_state(str(work), env, lambda a: (a["status"] or {}).get("succeeded") == 1)
+    log = attrs["logs"][0]
+    assert "hello from rank 0 of 1 (true)" in log
+    assert "inherited=from-parent" in log
+    assert "payload-from-workdir" in log
+    assert log.split(" ")[0].endswith("Z")  # 2022-01-01T00:00:00Z line prefix
+    assert any("rank-exit" in e for e in attrs["events"])
+    # second apply is a no-op
+    assert "No changes" in run(TPI + ["apply", "-auto-approve"], str(work), env).stdout
+    outputs = json.loads(run(TPI + ["output", "-json"], str(work), env).stdout)
+    assert outputs["status"]["value"]["succeeded"] == 1
+    # destroy pulls storage.output into the workdir and removes the task
+    out = run(TPI + ["destroy", "-auto-approve"], str(work), env)
+    assert "Destroy complete! Resources: 1 destroyed." in out.stdout
+    assert (work / "results" / "out.txt").read_text() == "done\n"
+    state = json.loads((work / "terraform.tfstate").read_text())
+    assert state["resources"] == []
+    assert not os.listdir(os.path.join(env["TPI_STATE_ROOT"], "local"))
+
+
+def test_replace_on_force_new_and_in_place_update(tmp_path, env):
+    work = tmp_path / "p2"
+    work.mkdir()
+    base = HELLO % {"suffix": "x"}
+    (work / "main.tf").write_text(base)
+    (work / "input.txt").write_text("x\n")
+    run(TPI + ["apply", "-auto-approve"], str(work), env)
+    (work / "main.tf").write_text(base.replace('output  = "results"', 'output  = "other"'))
+    plan = run(TPI + ["plan"], str(work), env)
+    assert "will be updated in-place" in plan.stdout
+    run(TPI + ["apply", "-auto-approve"], str(work), env)
+    (work / "main.tf").write_text(base.replace('machine = "s"', 'machine = "m"'))
+    plan = run(TPI + ["plan"], str(work), env)
+    assert "must be replaced" in plan.stdout and "forces replacement: machine" in plan.stdout
+    run(TPI + ["destroy", "-auto-approve"], str(work), env)
+
+
+def test_invalid_config_reports_error(tmp_path, env):
+    work = tmp_path / "bad"
+    work.mkdir()
+    (work / "main.tf").write_text('resource "iterative_task" "t" {\n  cloud = "local"\n}\n')
+    r = run(TPI + ["plan"], str(work), env, check=False)
+    assert r.returncode == 1 and "script" in r.stderr
+
+
+def test_leo_create_read_follow_delete(tmp_path, env):
+    """task_smoke_test.go flow: old data in workdir, create twice, wait for logs with both
+    uuids, wait for success, delete twice, output pulled and cache not pulled."""
+    work = tmp_path / "w"
+    (work / "cache").mkdir(parents=True)
+    old, new = str(uuid.uuid4()), str(uuid.uuid4())
+    (work / "cache" / "old").write_text(old)
+    script = ("#!/bin/sh\ncat cache/old\necho $NEW_UUID\nmkdir -p output\n"
+              "echo $NEW_UUID > output/new\necho changed > cache/old\n")
+    name = "smoke-%s" % uuid.uuid4().hex[:8]
+    base = LEO + ["--cloud", "local"]
+    r = run(base + ["create", "--name", name, "--workdir", str(work), "--output", "output",
+                    "--environment", "NEW_UUID=%s" % new, "--script", script], str(tmp_path), env)
+    ident = r.stdout.strip().splitlines()[-1]
+    assert ident.startswith("tpi-" + name)
+    # idempotent create (same deterministic name)
+    run(base + ["create", "--name", ident, "--workdir", str(work), "--output", "output",
+                "--environment", "NEW_UUID=%s" % new, "--script", script], str(tmp_path), env)
+    follow = run(base + ["read", "--follow", ident], str(tmp_path), env, timeout=60)
+    assert old in follow.stdout and new in follow.stdout
+    assert ident in run(base + ["list"], str(tmp_path), env).stdout
+    run(base + ["delete", "--workdir", str(work), "--output", "output", ident], str(tmp_path), env)
+    run(base + ["delete", "--workdir", str(work), "--output", "output", ident], str(tmp_path), env)
+    assert (work / "output" / "new").read_text().strip() == new
+    assert (work / "cache" / "old").read_text() == old  # cache not downloaded
+
+
+def test_leo_read_exit_code_on_failure(tmp_path, env):
+    base = LEO + ["--cloud", "local"]
+    r = run(base + ["create", "--workdir", str(tmp_path), "--", "sh", "-c", "echo boom; exit 3"],
+            str(tmp_path), env)
+    ident = r.stdout.strip().splitlines()[-1]
+    follow = run(base + ["read", "--follow", "--timestamps", ident], str(tmp_path), env,
+                 check=False, timeout=60)
+    assert follow.returncode == 1
+    assert "boom" in follow.stdout and follow.stdout.split()[0].endswith("Z")
+    run(base + ["delete", ident], str(tmp_path), env)
+
+
+def test_leo_reads_main_tf_defaults(tmp_path, env):
+    from terraform_provider_iterative_amd.cli.leo import config_defaults
+
+    (tmp_path / "main.tf").write_text(HELLO % {"suffix": "d"})
+    d = config_defaults(str(tmp_path), environ={"TASK_MACHINE": "l"})
+    assert d["cloud"] == "local" and d["machine"] == "l" and d["output"] == "results"
+    assert d["environment"]["GREETING"] == "hello"
