@@ -79,6 +79,32 @@ PYBIND11_MODULE(_tpi_native, m) {
       py::arg("src"), py::arg("dst"), py::arg("filter"), py::arg("threads") = 8,
       py::arg("piece_bytes") = 256ull << 20);
 
+  auto pieces_of = [](const py::list& items) {
+    std::vector<tpi::ReadPiece> pieces;
+    for (auto item : items) {
+      auto t = item.cast<py::tuple>();
+      pieces.push_back({t[0].cast<std::string>(), t[1].cast<uint64_t>(), t[2].cast<uint64_t>(),
+                        t[3].cast<uint64_t>()});
+    }
+    return pieces;
+  };
+  m.def(
+      "read_pieces",
+      [pieces_of](const py::list& items, uintptr_t dst, int threads) {
+        auto pieces = pieces_of(items);
+        py::gil_scoped_release nogil;
+        return tpi::read_pieces(pieces, (uint8_t*)dst, threads);
+      },
+      "read [(path, file_off, len, dst_off)] into the buffer at dst");
+  m.def(
+      "write_pieces",
+      [pieces_of](const py::list& items, uintptr_t src, int threads) {
+        auto pieces = pieces_of(items);
+        py::gil_scoped_release nogil;
+        return tpi::write_pieces(pieces, (const uint8_t*)src, threads);
+      },
+      "write buffer ranges [(path, file_off, len, src_off)] into files");
+
   m.def("remove_tree", [](const std::string& p) {
     py::gil_scoped_release nogil;
     return tpi::remove_tree(p);

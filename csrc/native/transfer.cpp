@@ -250,6 +250,85 @@ TransferStats copy_dir(const std::string& src, const std::string& dst, const Fil
   return stats;
 }
 
+namespace {
+
+template <class F>
+uint64_t pool_over(size_t n, int threads, F&& f) {
+  std::atomic<size_t> next{0};
+  std::atomic<uint64_t> done{0};
+  std::string first_error;
+  std::mutex mu;
+  auto worker = [&] {
+    for (;;) {
+      size_t i = next.fetch_add(1);
+      if (i >= n) return;
+      std::string err;
+      uint64_t got = f(i, err);
+      if (!err.empty()) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (first_error.empty()) first_error = err;
+      }
+      done += got;
+    }
+  };
+  int nth = std::max(1, std::min<int>(threads, (int)n));
+  std::vector<std::thread> pool;
+  for (int i = 0; i < nth - 1; ++i) pool.emplace_back(worker);
+  worker();
+  for (auto& t : pool) t.join();
+  if (!first_error.empty()) throw std::runtime_error(first_error);
+  return done;
+}
+
+}  // namespace
+
+uint64_t read_pieces(const std::vector<ReadPiece>& pieces, uint8_t* dst, int threads) {
+  return pool_over(pieces.size(), threads, [&](size_t i, std::string& err) -> uint64_t {
+    const ReadPiece& p = pieces[i];
+    int fd = open(p.path.c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0) {
+      err = "open " + p.path + ": " + strerror(errno);
+      return 0;
+    }
+    posix_fadvise(fd, (off_t)p.file_off, (off_t)p.len, POSIX_FADV_SEQUENTIAL);
+    uint64_t got = 0;
+    while (got < p.len) {
+      ssize_t n = pread(fd, dst + p.dst_off + got, p.len - got, (off_t)(p.file_off + got));
+      if (n < 0 && errno == EINTR) continue;
+      if (n <= 0) {
+        err = "read " + p.path + ": " + (n < 0 ? strerror(errno) : "short file");
+        break;
+      }
+      got += (uint64_t)n;
+    }
+    close(fd);
+    return got;
+  });
+}
+
+uint64_t write_pieces(const std::vector<ReadPiece>& pieces, const uint8_t* src, int threads) {
+  return pool_over(pieces.size(), threads, [&](size_t i, std::string& err) -> uint64_t {
+    const ReadPiece& p = pieces[i];
+    int fd = open(p.path.c_str(), O_WRONLY | O_CREAT | O_CLOEXEC, 0644);
+    if (fd < 0) {
+      err = "open " + p.path + ": " + strerror(errno);
+      return 0;
+    }
+    uint64_t put = 0;
+    while (put < p.len) {
+      ssize_t n = pwrite(fd, src + p.dst_off + put, p.len - put, (off_t)(p.file_off + put));
+      if (n < 0 && errno == EINTR) continue;
+      if (n <= 0) {
+        err = "write " + p.path + ": " + strerror(errno);
+        break;
+      }
+      put += (uint64_t)n;
+    }
+    close(fd);
+    return put;
+  });
+}
+
 uint64_t remove_tree(const std::string& path) {
   struct stat st;
   if (lstat(path.c_str(), &st)) return 0;

@@ -36,4 +36,14 @@ TransferStats copy_dir(const std::string& src, const std::string& dst, const Fil
 // rm -rf; returns number of entries removed.  Missing path -> 0.
 uint64_t remove_tree(const std::string& path);
 
+// Staging reads: read pieces of files into a caller buffer (typically pinned host memory the
+// GPU DMA engine reads from) with a thread pool of pread()s.
+struct ReadPiece {
+  std::string path;
+  uint64_t file_off, len, dst_off;
+};
+uint64_t read_pieces(const std::vector<ReadPiece>& pieces, uint8_t* dst, int threads);
+// Inverse for spills: write buffer ranges into files (created/truncated to `size`).
+uint64_t write_pieces(const std::vector<ReadPiece>& pieces, const uint8_t* src, int threads);
+
 }  // namespace tpi

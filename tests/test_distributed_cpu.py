@@ -1,0 +1,74 @@
+"""Workdir fan-out over torch.distributed with gloo (world 2 and 4) on CPU."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, root, results, method):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from terraform_provider_iterative_amd.parallel.broadcast import broadcast_buffer
+        from terraform_provider_iterative_amd.runtime.workdir import stage_workdir
+
+        n = 100003
+        buf = torch.arange(n, dtype=torch.int64).to(torch.uint8) if rank == 0 else \
+            torch.zeros(n, dtype=torch.uint8)
+        broadcast_buffer(buf, src=0, method=method)
+        ok_buf = bool(torch.equal(buf, torch.arange(n, dtype=torch.int64).to(torch.uint8)))
+        staged = stage_workdir(root, device=torch.device("cpu"), method=method,
+                               exclude=["skip.bin"])
+        names = sorted(f.path for f in staged.files)
+        a = bytes(staged.tensor("a.txt").tolist())
+        big = staged.tensor("sub/big.bin")
+        expect = torch.from_numpy(
+            __import__("numpy").frombuffer(open(os.path.join(root, "sub/big.bin"), "rb").read(),
+                                           dtype="uint8").copy())
+        results[rank] = (ok_buf, names, a, bool(torch.equal(big, expect)),
+                         staged.stats.get("verified"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,method", [(2, "broadcast"), (4, "scatter_allgather"),
+                                          (3, "auto")])
+def test_stage_and_broadcast(tmp_path, world, method):
+    root = tmp_path / "wd"
+    (root / "sub").mkdir(parents=True)
+    (root / "a.txt").write_bytes(b"hello workdir")
+    (root / "sub" / "big.bin").write_bytes(os.urandom(300001))
+    (root / "skip.bin").write_bytes(b"x" * 10)
+    (root / "main.tf").write_text("# excluded by default")
+    manager = mp.Manager()
+    results = manager.dict()
+    mp.spawn(_worker, args=(world, _free_port(), str(root), results, method), nprocs=world)
+    assert len(results) == world
+    for rank in range(world):
+        ok_buf, names, a, big_ok, verified = results[rank]
+        assert ok_buf, rank
+        assert names == ["a.txt", "sub/big.bin"]
+        assert a == b"hello workdir" and big_ok
+        assert verified in (True, None)
+
+
+def test_write_back(tmp_path):
+    from terraform_provider_iterative_amd.runtime.workdir import stage_workdir
+
+    root = tmp_path / "src"
+    root.mkdir()
+    (root / "x.bin").write_bytes(b"abc" * 1000)
+    staged = stage_workdir(str(root), device=torch.device("cpu"))
+    staged.tensor("x.bin")[:3] = torch.tensor([120, 121, 122], dtype=torch.uint8)
+    out = tmp_path / "out"
+    staged.write_back(str(out))
+    assert (out / "x.bin").read_bytes()[:6] == b"xyzabc"

@@ -1,0 +1,131 @@
+"""mi355x provider on a fake 8-GPU inventory (CPU-only scripts): placement, rank env,
+concurrency (config 5: 4 concurrent 2-GPU tasks), auto-cleanup of leases, stop/start."""
+import json
+import os
+import time
+
+import pytest
+
+from terraform_provider_iterative_amd import backends
+from terraform_provider_iterative_amd.models.cloud import Cloud, Credentials, NodeCredentials
+from terraform_provider_iterative_amd.models.machine_types import (MachineTypeError,
+                                                                   parse_node_machine)
+from terraform_provider_iterative_amd.models.values import Environment, Size, Task, Variables
+from terraform_provider_iterative_amd.parallel.placement import (GPU, Placement,
+                                                                 PlacementError, discover)
+from terraform_provider_iterative_amd.utils.identifier import new_deterministic_identifier
+
+
+@pytest.fixture()
+def cloud(tmp_path, monkeypatch):
+    monkeypatch.setenv("TPI_MI355X_GPUS", "0,1,2,3,4,5,6,7")
+    return Cloud(provider="mi355x",
+                 credentials=Credentials(node=NodeCredentials(state_root=str(tmp_path / "st"))))
+
+
+def _task(cloud, name, script, machine="m+mi355x", parallelism=1, timeout=60):
+    spec = Task(size=Size(machine=machine), parallelism=parallelism,
+                environment=Environment(script=script, variables=Variables({"TPI_TASK": "true"}),
+                                        timeout=timeout))
+    return backends.new(cloud, new_deterministic_identifier(name), spec)
+
+
+ENV_SCRIPT = "#!/bin/sh\necho \"rank=$RANK world=$WORLD_SIZE hip=$HIP_VISIBLE_DEVICES mine=$TPI_RANK_GPUS port=$MASTER_PORT\"\n"
+
+
+def test_machine_types():
+    assert parse_node_machine("m").gpus == 0
+    assert parse_node_machine("m+mi355x").gpus == 1
+    assert parse_node_machine("l+mi355x").gpus == 4
+    assert parse_node_machine("xl+mi355x").gpus == 8
+    assert parse_node_machine("xl+v100").gpus == 8
+    mt = parse_node_machine("16-64000+mi355x*2")
+    assert (mt.cpus, mt.memory_mb, mt.gpus) == (16, 64000, 2)
+    with pytest.raises(MachineTypeError):
+        parse_node_machine("64-1000+mi355x*9")
+    with pytest.raises(MachineTypeError):
+        parse_node_machine("bogus")
+
+
+def test_rank_env_and_gpu_assignment(cloud):
+    task = _task(cloud, "envtest", ENV_SCRIPT, machine="m+mi355x", parallelism=2)
+    task.create()
+    status = task.wait(20)
+    assert status["succeeded"] == 2
+    logs = sorted(l.split(" ", 1)[1].strip() for l in task.logs())
+    gpus = task.gpus()
+    assert len(gpus) == 2
+    visible = ",".join(str(g) for g in gpus)
+    assert logs[0].startswith("rank=0 world=2 hip=%s mine=0 " % visible)
+    assert logs[1].startswith("rank=1 world=2 hip=%s mine=1 " % visible)
+    # supervisor exited -> leases released
+    assert Placement(cloud.state_root()).free() and len(Placement(cloud.state_root()).free()) == 8
+    task.delete()
+
+
+def test_four_concurrent_two_gpu_tasks(cloud):
+    tasks = [_task(cloud, "conc-%d" % i, "#!/bin/sh\nsleep 2\necho done\n",
+                   machine="16-64000+mi355x*2") for i in range(4)]
+    for t in tasks:
+        t.create()
+    sets = [set(t.gpus()) for t in tasks]
+    assert all(len(s) == 2 for s in sets)
+    assert len(set().union(*sets)) == 8  # disjoint
+    extra = _task(cloud, "conc-extra", "#!/bin/sh\necho hi\n", machine="m+mi355x")
+    with pytest.raises(PlacementError):
+        extra.create()
+    extra.delete()
+    for t in tasks:
+        assert t.wait(30)["succeeded"] == 1
+    # auto-cleanup: all GPUs free again, a new task fits
+    again = _task(cloud, "after", "#!/bin/sh\necho ok\n", machine="xl+mi355x")
+    again.create()
+    assert sorted(again.gpus()) == list(range(8))
+    assert again.wait(20)["succeeded"] == 1
+    for t in tasks + [again]:
+        t.delete()
+
+
+def test_stop_and_start(cloud):
+    task = _task(cloud, "stopstart", "#!/bin/sh\necho started\nsleep 30\n")
+    task.create()
+    deadline = time.time() + 10
+    while not task.logs() and time.time() < deadline:
+        time.sleep(0.05)
+    assert task.status()["running"] == 1
+    task.stop()
+    st = task.status()
+    assert st["running"] == 0 and st["succeeded"] == 0 and st["failed"] == 0  # no status
+    assert len(Placement(cloud.state_root()).free()) == 8
+    codes = [e.code for e in task.events()]
+    assert "stop-requested" in codes and "rank-stopped" in codes
+    task.delete()
+
+
+def test_deadline_marks_failed(cloud, monkeypatch):
+    monkeypatch.setenv("TPI_GRACE_SECONDS", "1")
+    task = _task(cloud, "deadline", "#!/bin/sh\necho start\nsleep 30\n", timeout=1)
+    task.create()
+    st = task.wait(15)
+    assert st["failed"] == 1
+    status_files = [n for n in os.listdir(os.path.join(task.root, "reports"))
+                    if n.startswith("status-")]
+    report = json.load(open(os.path.join(task.root, "reports", status_files[0])))
+    assert report["result"] == "timeout"
+    task.delete()
+
+
+def test_discover_kfd_does_not_crash(monkeypatch):
+    monkeypatch.delenv("TPI_MI355X_GPUS", raising=False)
+    assert isinstance(discover(), list)
+
+
+def test_numa_preference(tmp_path):
+    gpus = [GPU(i, numa_node=0 if i < 4 else 1) for i in range(8)]
+    p = Placement(str(tmp_path), gpus)
+    a = p.allocate("t1", 3)
+    assert {g.numa_node for g in a} == {0}
+    b = p.allocate("t2", 4)
+    assert {g.numa_node for g in b} == {1}
+    assert p.allocate("t1", 3) == a  # idempotent
+    assert p.release("t1") == 3

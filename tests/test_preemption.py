@@ -1,0 +1,85 @@
+"""Preempt-recover on the node runtime (config 4 control flow, CPU tensors):
+SIGTERM mid-task -> rank checkpoints (pack -> host region) -> supervisor respawns it with a
+new machine identity -> successor restores and finishes.  The reference's equivalent is spot
+recovery with the workdir restored from the bucket (machine-script.sh.tpl:89,118-124)."""
+import os
+import sys
+import time
+
+import pytest
+
+from terraform_provider_iterative_amd import backends
+from terraform_provider_iterative_amd.models.cloud import Cloud, Credentials, NodeCredentials
+from terraform_provider_iterative_amd.models.values import Environment, Task, Variables
+from terraform_provider_iterative_amd.utils.identifier import new_deterministic_identifier
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+TRAIN = r'''#!%(python)s
+import os, sys, time
+sys.path.insert(0, %(root)r)
+import torch
+from terraform_provider_iterative_amd.checkpoint import Checkpointer, preemption
+
+state = {"w": torch.zeros(4096), "step": torch.zeros((), dtype=torch.int64),
+         "m": torch.randn(64, 32).t()}
+spill = os.path.join(os.environ["TPI_DATA_DIRECTORY"], ".spill")  # survives the rank
+ck = Checkpointer(state, path=spill, tile_bytes=4096)
+meta = preemption.resume(ck)
+start = int(state["step"])
+print(("resumed %%d %%s" %% (start, meta.get("reason"))) if meta else "fresh", flush=True)
+preemption.register(ck)
+preemption.on_preempt(lambda: {"step": int(state["step"])})
+preemption.install()
+for step in range(start, %(steps)d):
+    state["w"].fill_(step + 1)
+    state["step"].fill_(step + 1)
+    print("step", step + 1, flush=True)
+    time.sleep(0.05)
+print("final", int(state["w"][0].item()), int(state["step"]), flush=True)
+'''
+
+
+@pytest.fixture()
+def cloud(tmp_path):
+    return Cloud(provider="local",
+                 credentials=Credentials(node=NodeCredentials(state_root=str(tmp_path / "st"))))
+
+
+def _wait_for(task, text, timeout=60):
+    deadline = time.time() + timeout
+    while time.time() < deadline:
+        if any(text in log for log in task.logs()):
+            return True
+        time.sleep(0.05)
+    raise AssertionError("%r never appeared in logs: %s" % (text, task.logs()))
+
+
+@pytest.mark.parametrize("how", ["supervisor", "rank-sigterm"])
+def test_preempt_checkpoint_respawn_resume(cloud, how):
+    script = TRAIN % {"python": sys.executable, "root": ROOT, "steps": 40}
+    spec = Task(environment=Environment(script=script, timeout=300,
+                                        variables=Variables({"TPI_TASK": "true"})))
+    task = backends.new(cloud, new_deterministic_identifier("preempt-" + how), spec)
+    task.create()
+    _wait_for(task, "step 5")
+    if how == "supervisor":
+        task.preempt()  # leo preempt: SIGUSR1 -> supervisor SIGTERMs the ranks
+    else:  # an external agent SIGTERMs the rank process directly
+        import json
+        import signal
+
+        state = json.load(open(os.path.join(task.root, "supervisor", "state.json")))
+        os.kill(state["ranks"][0]["pid"], signal.SIGTERM)
+    status = task.wait(90)
+    logs = task.logs()
+    assert status["succeeded"] == 1 and status["failed"] == 0, (status, logs)
+    assert len(logs) == 2, logs  # one log per machine identity, like the reference
+    assert "preemption checkpoint saved" in logs[0]
+    assert "resumed" in logs[1] and "preempted" in logs[1]
+    resumed_at = int(logs[1].split("resumed ")[1].split()[0])
+    assert resumed_at >= 5
+    assert "final 40 40" in logs[1]
+    codes = [e.code for e in task.events()]
+    assert "rank-preempted" in codes and "respawn" in codes
+    task.delete()
