@@ -44,6 +44,8 @@ def parse_args(argv=None):
     p.add_argument("--nbuf", type=int, default=3)
     p.add_argument("--hidden", type=int, default=8192)
     p.add_argument("--no-latency", action="store_true", help="skip apply->first-log")
+    p.add_argument("--broadcast-gb", type=float, default=10.0,
+                   help="N>1: also measure the RCCL workdir fan-out of this many GB")
     p.add_argument("--verify", action="store_true", default=True)
     return p.parse_args(argv)
 
@@ -170,6 +172,17 @@ def main(argv=None):
         after = [ops.shard_hash(tensors[n].view(-1).view(torch.uint8)).cpu() for n in names]
         verified = all(torch.equal(x, y) for x, y in zip(before, after))
 
+    broadcast = None
+    if world > 1 and args.broadcast_gb > 0:  # config 3: workdir fan-out over xGMI (untimed)
+        try:
+            from terraform_provider_iterative_amd.parallel.broadcast import measure
+
+            nbytes = int(args.broadcast_gb * 1e9)
+            broadcast = {m: measure(nbytes, method=m, iters=3, warmup=1, device=device)
+                         for m in ("broadcast", "scatter_allgather")}
+        except Exception as error:  # never lose the headline to the side measurement
+            broadcast = {"error": repr(error)}
+
     elapsed = allmax(elapsed)
     save_max, restore_max = allmax(save_s), allmax(restore_s)
     total = ck.plan.total * world  # packed bytes per direction per step (all ranks)
@@ -196,7 +209,9 @@ def main(argv=None):
             "restore_GBps": round(total * args.steps / restore_max / 1e9, 3),
             "per_gpu_save_GBps": round(ck.plan.total * args.steps / save_max / 1e9, 3),
             "per_gpu_restore_GBps": round(ck.plan.total * args.steps / restore_max / 1e9, 3),
-            "first_log_latency_s": latency,
+            "first_log_latency_s": (latency or {}).get("cli_s"),
+            "first_log_latency": latency,
+            "workdir_broadcast": broadcast,
             "restore_verified": verified,
             "setup_s": round(setup_s, 2),
         }

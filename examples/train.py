@@ -1,0 +1,132 @@
+#!/usr/bin/env python3
+"""Example rank workload for ``iterative_task`` on ``cloud = "mi355x"``.
+
+* stages the task workdir into HBM (rank 0 reads, RCCL fans out to the other ranks),
+* trains a small random-init transformer-style MLP in bf16 on synthetic tokens (DDP over
+  RCCL when ``WORLD_SIZE > 1``),
+* checkpoints model + optimizer state to host DRAM on SIGTERM (preemption) and resumes from
+  it when respawned, persisting to the task's storage at the end.
+
+Environment (set by the supervisor): RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT,
+HIP_VISIBLE_DEVICES, TPI_DATA_DIRECTORY, TPI_MACHINE_IDENTITY.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.environ.get("TPI_FRAMEWORK_ROOT") or os.path.dirname(os.path.dirname(
+    os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def log(*parts):
+    print(*parts, flush=True)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--hidden", type=int, default=2048)
+    p.add_argument("--layers", type=int, default=4)
+    p.add_argument("--batch", type=int, default=16)
+    p.add_argument("--seq", type=int, default=512)
+    p.add_argument("--stage", action="store_true", help="stage the workdir into HBM first")
+    p.add_argument("--sleep", type=float, default=0.0, help="sleep per step (tests)")
+    args = p.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from terraform_provider_iterative_amd.checkpoint import Checkpointer, preemption
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    device = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+    if device.type == "cuda":
+        torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("nccl" if device.type == "cuda" else "gloo",
+                                **({"device_id": device} if device.type == "cuda" else {}))
+    log("rank %d/%d on %s (machine %s)" % (rank, world, device,
+                                          os.environ.get("TPI_MACHINE_IDENTITY", "-")))
+    stats = {}
+    if args.stage:
+        from terraform_provider_iterative_amd.runtime.workdir import stage_workdir
+
+        t0 = time.perf_counter()
+        staged = stage_workdir(device=device, exclude=[".ckpt*", "checkpoints"])
+        dt = time.perf_counter() - t0
+        stats["stage_GBps"] = staged.stats["bytes"] / dt / 1e9 if dt else None
+        stats.update({k: v for k, v in staged.stats.items() if isinstance(v, (int, float, bool, str))})
+        log("staged %d files, %.2f GB into HBM in %.3fs (%s)" % (
+            len(staged.files), staged.stats["bytes"] / 1e9, dt, json.dumps(stats)))
+
+    torch.manual_seed(1234)
+    h = args.hidden
+    layers = []
+    for _ in range(args.layers):
+        layers += [torch.nn.LayerNorm(h), torch.nn.Linear(h, 4 * h), torch.nn.GELU(),
+                   torch.nn.Linear(4 * h, h)]
+    model = torch.nn.Sequential(*layers).to(device=device, dtype=torch.bfloat16)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-4)
+    if world > 1:
+        model = torch.nn.parallel.DistributedDataParallel(model)
+    step_t = torch.zeros((), dtype=torch.int64, device=device)
+
+    # Optimizer state must exist before it can be checkpointed: one warm step on zeros.
+    x = torch.zeros(args.batch, args.seq, h, device=device, dtype=torch.bfloat16)
+    model(x).float().pow(2).mean().backward()
+    opt.step()
+    opt.zero_grad(set_to_none=False)
+    tensors = {"step": step_t}
+    for name, t in (model.module if world > 1 else model).state_dict().items():
+        tensors["model." + name] = t
+    params = [p for group in opt.param_groups for p in group["params"]]
+    for i, param in enumerate(params):
+        for k, v in opt.state[param].items():
+            if torch.is_tensor(v) and v.device == device:
+                tensors["opt.%d.%s" % (i, k)] = v
+    data_dir = os.environ.get("TPI_DATA_DIRECTORY", ".")
+    spill = os.path.join(data_dir, ".ckpt-rank%d" % rank)
+    ck = Checkpointer(tensors, path=spill)
+    meta = preemption.resume(ck)
+    start = int(step_t.item())
+    log("resumed from step %d" % start if meta else "fresh start")
+    preemption.register(ck)
+    preemption.install()
+
+    gen = torch.Generator(device=device).manual_seed(rank + 7)
+    t_steps = []
+    for step in range(start, args.steps):
+        t0 = time.perf_counter()
+        x = torch.randn(args.batch, args.seq, h, device=device, dtype=torch.bfloat16,
+                        generator=gen)
+        loss = (model(x).float() - x.float()).pow(2).mean()
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=False)
+        step_t.fill_(step + 1)
+        if device.type == "cuda":
+            torch.cuda.synchronize()
+        t_steps.append(time.perf_counter() - t0)
+        if rank == 0 and (step % 10 == 0 or step + 1 == args.steps):
+            log("step %d loss %.5f" % (step + 1, loss.item()))
+        if args.sleep:
+            time.sleep(args.sleep)
+    res = ck.save({"step": int(step_t.item()), "final": True})
+    if t_steps:
+        stats["step_ms"] = 1e3 * sorted(t_steps)[len(t_steps) // 2]
+    stats["final_save_GBps"] = res.gbps
+    log("done %s" % json.dumps(stats))
+    ck.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

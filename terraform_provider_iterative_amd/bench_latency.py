@@ -1,0 +1,132 @@
+"""apply -> first-log latency of an ``iterative_task`` on the node runtime (BASELINE metric).
+
+Two measurements, both from a fresh state root and a hello-world ``main.tf``:
+
+* ``cli``: wall time from launching ``tpi apply -auto-approve`` (a new Python process, as a
+  user would) until the first line of the task's log is on disk;
+* ``api``: the same from calling the resource's Create in-process.
+
+The reference's floor for the same metric is VM provisioning + tool downloads + the 5 s log
+tick (machine-script.sh.tpl:108-116) + the 3 s ``leo read`` poll (read.go:124).
+"""
+from __future__ import annotations
+
+import glob
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+from typing import Dict, Optional
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+MAIN_TF = '''
+resource "iterative_task" "latency" {
+  name    = "latency-%(tag)s"
+  cloud   = "%(cloud)s"
+  machine = "%(machine)s"
+  storage {
+    workdir = "."
+  }
+  script = <<-END
+    #!/bin/sh
+    echo "first log line"
+  END
+}
+'''
+
+
+def _first_log(state_root: str, timeout: float, t0: float, poll: float = 0.0005) -> Optional[float]:
+    pattern = os.path.join(state_root, "*", "*", "reports", "task-*")
+    deadline = t0 + timeout
+    while time.perf_counter() < deadline:
+        for path in glob.glob(pattern):
+            try:
+                if os.path.getsize(path) > 0:
+                    return time.perf_counter() - t0
+            except OSError:
+                pass
+        time.sleep(poll)
+    return None
+
+
+def _cleanup(workdir: str, env: Dict[str, str]) -> None:
+    subprocess.run([sys.executable, os.path.join(ROOT, "bin", "tpi"), "destroy", "-auto-approve"],
+                   cwd=workdir, env=env, capture_output=True, timeout=120)
+
+
+def measure_first_log_latency(timeout: float = 60.0, cloud: Optional[str] = None,
+                              repeats: int = 3) -> Dict[str, float]:
+    """Returns ``{"cli_s": .., "api_s": .., "cloud": ..}`` (medians over ``repeats``)."""
+    gpu = False
+    try:
+        import torch
+
+        gpu = torch.cuda.is_available()
+    except ImportError:  # pragma: no cover
+        pass
+    cloud = cloud or ("mi355x" if gpu else "local")
+    machine = "m+mi355x" if cloud == "mi355x" else "s"
+    cli, api = [], []
+    for i in range(repeats):
+        base = tempfile.mkdtemp(prefix="tpi-latency-")
+        try:
+            work = os.path.join(base, "work")
+            os.makedirs(work)
+            with open(os.path.join(work, "main.tf"), "w") as handle:
+                handle.write(MAIN_TF % {"tag": "%d%d" % (os.getpid(), i), "cloud": cloud,
+                                        "machine": machine})
+            env = dict(os.environ)
+            env["TPI_STATE_ROOT"] = os.path.join(base, "state")
+            env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+            t0 = time.perf_counter()
+            proc = subprocess.Popen([sys.executable, os.path.join(ROOT, "bin", "tpi"), "apply",
+                                     "-auto-approve"], cwd=work, env=env,
+                                    stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+            latency = _first_log(env["TPI_STATE_ROOT"], timeout, t0)
+            proc.wait(timeout=timeout)
+            if latency is not None:
+                cli.append(latency)
+            _cleanup(work, env)
+            # in-process API path
+            from .provider import resources
+            from .models.schema import normalize
+
+            old = os.environ.get("TPI_STATE_ROOT")
+            os.environ["TPI_STATE_ROOT"] = os.path.join(base, "state-api")
+            cwd = os.getcwd()
+            os.chdir(work)
+            try:
+                data = normalize("iterative_task", {
+                    "name": "latency-api-%d%d" % (os.getpid(), i), "cloud": cloud,
+                    "machine": machine, "storage": [{"workdir": "."}],
+                    "script": "#!/bin/sh\necho first log line\n"})
+                t1 = time.perf_counter()
+                result = resources.task_create(data)
+                lat = _first_log(os.environ["TPI_STATE_ROOT"], timeout, t1)
+                if lat is not None:
+                    api.append(lat)
+                if result.id:
+                    data["id"] = result.id
+                    resources.task_delete(data)
+            finally:
+                os.chdir(cwd)
+                if old is None:
+                    os.environ.pop("TPI_STATE_ROOT", None)
+                else:
+                    os.environ["TPI_STATE_ROOT"] = old
+        finally:
+            shutil.rmtree(base, ignore_errors=True)
+
+    def median(xs):
+        xs = sorted(xs)
+        return round(xs[len(xs) // 2], 4) if xs else None
+
+    return {"cli_s": median(cli), "api_s": median(api), "cloud": cloud, "samples": len(cli)}
+
+
+if __name__ == "__main__":
+    print(json.dumps(measure_first_log_latency()))

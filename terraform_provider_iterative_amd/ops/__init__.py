@@ -4,14 +4,28 @@ Every operator dispatches on where the data lives: device tensors go to the hand
 CDNA4 kernels in ``libtpi_hip.so`` (``csrc/hip/kernels.hip``); host tensors / buffers to the
 C++ implementations in ``_tpi_native`` (``csrc/native/hostops.cpp``), which define the same
 formats bit for bit.
+
+Attributes are resolved lazily so control-plane tools (``leo``/``tpi``) that only need the
+native loader do not pay for importing numpy/torch.
 """
 from ._loader import HipError, gpu_visible, hip, native
-from .hashing import (DEFAULT_SHARD_BYTES, DEFAULT_TILE_BYTES, crc32c, crc32c_combine,
-                      crc32c_tiles, dirty_shards, shard_hash)
-from .packing import SEG_DTYPE, PackPlan, TensorEntry, pack, unpack
 
-__all__ = [
-    "HipError", "gpu_visible", "hip", "native", "DEFAULT_SHARD_BYTES", "DEFAULT_TILE_BYTES",
-    "crc32c", "crc32c_combine", "crc32c_tiles", "dirty_shards", "shard_hash", "SEG_DTYPE",
-    "PackPlan", "TensorEntry", "pack", "unpack",
-]
+_LAZY = {
+    "DEFAULT_SHARD_BYTES": "hashing", "DEFAULT_TILE_BYTES": "hashing", "crc32c": "hashing",
+    "crc32c_combine": "hashing", "crc32c_tiles": "hashing", "dirty_shards": "hashing",
+    "shard_hash": "hashing", "SEG_DTYPE": "packing", "PackPlan": "packing",
+    "TensorEntry": "packing", "pack": "packing", "unpack": "packing",
+}
+
+__all__ = ["HipError", "gpu_visible", "hip", "native"] + sorted(_LAZY)
+
+
+def __getattr__(name):
+    module = _LAZY.get(name)
+    if module is None:
+        raise AttributeError(name)
+    import importlib
+
+    value = getattr(importlib.import_module("." + module, __name__), name)
+    globals()[name] = value
+    return value

@@ -91,9 +91,12 @@ def discover(environ=None) -> List[GPU]:
         version = int(props.get("gfx_target_version", "0") or 0)
         if not version:
             continue
+        minor = props.get("drm_render_minor")
+        if minor and os.path.exists("/dev/dri") and \
+                not os.access("/dev/dri/renderD%s" % minor, os.R_OK | os.W_OK):
+            continue  # not ours (container/cgroup); ROCr would not enumerate it either
         gpu = GPU(index=len(gpus), gfx=_gfx_name(version),
                   cus=int(props.get("simd_count", "0") or 0) // 4)
-        minor = props.get("drm_render_minor")
         if minor:
             dev = "/sys/class/drm/renderD%s/device" % minor
             numa = _read(os.path.join(dev, "numa_node")).strip()

@@ -1,0 +1,95 @@
+"""Runtime on a real MI355X (``pytest -m gpu``): HBM workdir staging, the mi355x provider
+placing a rank on the GPU, and preempt/resume of a bf16 training job with device tensors."""
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from terraform_provider_iterative_amd import backends, ops
+from terraform_provider_iterative_amd.models.cloud import Cloud, Credentials, NodeCredentials
+from terraform_provider_iterative_amd.models.values import Environment, Size, Task, Variables
+from terraform_provider_iterative_amd.utils.identifier import new_deterministic_identifier
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU visible")
+    ops.hip(required=True)
+
+
+def test_stage_workdir_on_device(tmp_path):
+    from terraform_provider_iterative_amd.runtime.workdir import ALIGN, stage_workdir
+
+    rng = np.random.default_rng(0)
+    sizes = {"a.bin": 5000, "sub/b.bin": (3 << 20) + 17, "c.txt": 1}
+    for rel, n in sizes.items():
+        p = tmp_path / rel
+        p.parent.mkdir(parents=True, exist_ok=True)
+        p.write_bytes(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+    staged = stage_workdir(str(tmp_path), device=torch.device("cuda", 0), chunk_bytes=1 << 20)
+    assert staged.buffer.device.type == "cuda"
+    for rel, n in sizes.items():
+        got = staged.tensor(rel).cpu().numpy().tobytes()
+        assert got == (tmp_path / rel).read_bytes(), rel
+    # digest on device == host shard hash of the same layout (gaps zero)
+    host = np.zeros(staged.buffer.numel(), dtype=np.uint8)
+    for f in staged.files:
+        host[f.offset:f.offset + f.size] = np.frombuffer((tmp_path / f.path).read_bytes(), np.uint8)
+    assert all(f.offset % ALIGN == 0 for f in staged.files)
+    assert staged.digest().cpu().numpy().view(np.uint64).tolist() == \
+        ops.shard_hash(host).tolist()
+
+
+@pytest.fixture()
+def cloud(tmp_path, monkeypatch):
+    monkeypatch.delenv("TPI_MI355X_GPUS", raising=False)
+    return Cloud(provider="mi355x",
+                 credentials=Credentials(node=NodeCredentials(state_root=str(tmp_path / "st"))))
+
+
+def test_mi355x_task_sees_its_gpu(cloud):
+    script = ("#!%s\nimport os, torch\nprint('visible', os.environ.get('HIP_VISIBLE_DEVICES'), "
+              "torch.cuda.device_count(), torch.cuda.get_device_properties(0).gcnArchName, "
+              "flush=True)\n" % sys.executable)
+    spec = Task(size=Size(machine="m+mi355x"),
+                environment=Environment(script=script, timeout=600,
+                                        variables=Variables({"TPI_TASK": "true"})))
+    task = backends.new(cloud, new_deterministic_identifier("gpu-visible"), spec)
+    task.create()
+    assert len(task.gpus()) == 1
+    status = task.wait(300)
+    logs = "".join(task.logs())
+    assert status["succeeded"] == 1, logs
+    assert "visible %d 1 gfx950" % task.gpus()[0] in logs
+    task.delete()
+
+
+def test_preempt_resume_training_on_gpu(cloud, tmp_path):
+    env = {"TPI_FRAMEWORK_ROOT": ROOT, "TPI_TASK": "true"}
+    script = ("#!/bin/sh\nexec %s %s/examples/train.py --steps 60 --hidden 256 --layers 2 "
+              "--batch 4 --seq 64 --sleep 0.05\n" % (sys.executable, ROOT))
+    spec = Task(size=Size(machine="m+mi355x"),
+                environment=Environment(script=script, timeout=600, variables=Variables(env)))
+    task = backends.new(cloud, new_deterministic_identifier("gpu-preempt"), spec)
+    task.create()
+    deadline = time.time() + 300
+    while time.time() < deadline and not any("step 11" in l for l in task.logs()):
+        time.sleep(0.1)
+    assert any("step 11" in l for l in task.logs()), task.logs()
+    task.preempt()
+    status = task.wait(300)
+    logs = task.logs()
+    assert status["succeeded"] == 1, logs
+    assert len(logs) == 2 and "preemption checkpoint saved" in logs[0]
+    resumed = [l for l in logs[1].splitlines() if "resumed from step" in l]
+    assert resumed and int(resumed[0].rsplit(" ", 1)[1]) >= 11
+    assert "done" in logs[1]
+    task.delete()
