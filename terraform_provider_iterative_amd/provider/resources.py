@@ -67,7 +67,7 @@ def _timeouts(resource_type: str, overrides: Optional[Dict[str, float]] = None) 
 
 def _split_container(cloud: str, container: str) -> Tuple[str, str]:
     """rclone ``bucket.Split`` for remote clouds; node providers take a directory path."""
-    if cloud in (PROVIDER_LOCAL, PROVIDER_MI355X) or container.startswith((".", "/", ":")):
+    if cloud in (PROVIDER_LOCAL, PROVIDER_MI355X) or container.startswith(":"):
         return container, ""
     container = container.lstrip("/")
     bucket, _, path = container.partition("/")
