@@ -36,6 +36,19 @@ extern "C" hipError_t tpi_launch_stream_crc(int mode, const tpi_seg* segs, int n
 extern "C" hipError_t tpi_launch_shard_hash(const void* data, uint64_t nbytes,
                                             uint64_t shard_bytes, uint64_t seed, uint64_t* out,
                                             hipStream_t stream);
+extern "C" hipError_t tpi_launch_pack_list(const tpi_seg* segs, int nseg, uint64_t total,
+                                           const uint32_t* list, uint32_t n, void* buf,
+                                           uint64_t tile_bytes, const tpi_crc_tables* tables,
+                                           uint32_t* crcs, uint32_t init_full,
+                                           uint32_t init_last, hipStream_t stream);
+extern "C" hipError_t tpi_launch_stream_hash(const tpi_seg* segs, int nseg, uint64_t total,
+                                             uint64_t tile_bytes, uint64_t seed, uint64_t* out,
+                                             hipStream_t stream);
+extern "C" hipError_t tpi_launch_dirty_tiles(const uint64_t* hash, uint64_t* prev, uint64_t n,
+                                             int all, uint32_t* idx, unsigned int* count,
+                                             hipStream_t stream);
+
+#define TPI_SYNC_SEED 0x7470692d73796e63ull  // "tpi-sync"
 
 namespace {
 
@@ -113,6 +126,15 @@ struct tpi_engine {
   uint32_t* d_crcs = nullptr;
   size_t crc_cap = 0;
   unsigned long long* d_bad = nullptr;
+  // incremental sync state: digests of the last synced content (valid only until a full
+  // save/restore rewrites one side)
+  uint64_t* d_hash = nullptr;
+  uint64_t* d_prev = nullptr;
+  uint32_t* d_idx = nullptr;
+  unsigned int* d_count = nullptr;
+  size_t hash_cap = 0;
+  uint64_t hash_ntiles = 0;
+  bool hash_valid = false;
   std::mutex mu;
 };
 
@@ -209,6 +231,10 @@ void tpi_engine_destroy(tpi_engine* e) {
   if (e->d_segs) (void)hipFree(e->d_segs);
   if (e->d_crcs) (void)hipFree(e->d_crcs);
   if (e->d_bad) (void)hipFree(e->d_bad);
+  if (e->d_hash) (void)hipFree(e->d_hash);
+  if (e->d_prev) (void)hipFree(e->d_prev);
+  if (e->d_idx) (void)hipFree(e->d_idx);
+  if (e->d_count) (void)hipFree(e->d_count);
   if (e->compute) (void)hipStreamDestroy(e->compute);
   if (e->copy) (void)hipStreamDestroy(e->copy);
   delete e;
@@ -256,6 +282,7 @@ int tpi_save(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* ho
   std::lock_guard<std::mutex> lk(e->mu);
   auto t0 = std::chrono::steady_clock::now();
   if (prepare(e, segs, n, total)) return -1;
+  e->hash_valid = false;  // host content no longer matches the last sync's digests
   if (wait_stream) {
     HIP_OK(hipEventRecord(e->ev_wait, (hipStream_t)wait_stream));
     HIP_OK(hipStreamWaitEvent(e->compute, e->ev_wait, 0));
@@ -305,6 +332,7 @@ int tpi_restore(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, const
   std::lock_guard<std::mutex> lk(e->mu);
   auto t0 = std::chrono::steady_clock::now();
   if (prepare(e, segs, n, total)) return -1;
+  e->hash_valid = false;  // tensors are overwritten: digests of the last sync are stale
   const uint64_t tile = e->tile;
   const uint64_t ntiles = (total + tile - 1) / tile;
   const uint32_t init_full = init_for(tile);
@@ -359,6 +387,99 @@ int tpi_restore(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, const
     stats->bytes = total;
     stats->chunks = nchunks;
   }
+  return 0;
+}
+
+int tpi_sync(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* host_dst,
+             uint32_t* crcs_inout, int full, uint64_t wait_stream, uint64_t* dirty_tiles,
+             tpi_stats* stats) {
+  std::lock_guard<std::mutex> lk(e->mu);
+  auto t0 = std::chrono::steady_clock::now();
+  if (prepare(e, segs, n, total)) return -1;
+  const uint64_t tile = e->tile;
+  const uint64_t ntiles = (total + tile - 1) / tile;
+  if (ntiles > e->hash_cap) {
+    for (void* p : {(void*)e->d_hash, (void*)e->d_prev, (void*)e->d_idx})
+      if (p) HIP_OK(hipFree(p));
+    e->hash_cap = std::max<size_t>(ntiles, 1024);
+    HIP_OK(hipMalloc(&e->d_hash, e->hash_cap * sizeof(uint64_t)));
+    HIP_OK(hipMalloc(&e->d_prev, e->hash_cap * sizeof(uint64_t)));
+    HIP_OK(hipMalloc(&e->d_idx, e->hash_cap * sizeof(uint32_t)));
+    e->hash_valid = false;
+  }
+  if (!e->d_count) HIP_OK(hipMalloc(&e->d_count, sizeof(unsigned int)));
+  if (e->hash_ntiles != ntiles) e->hash_valid = false;
+  const int all = full || !e->hash_valid;
+  if (wait_stream) {
+    HIP_OK(hipEventRecord(e->ev_wait, (hipStream_t)wait_stream));
+    HIP_OK(hipStreamWaitEvent(e->compute, e->ev_wait, 0));
+  }
+  // 1. digests of the current tensors, 2. dirty list (and new digests remembered)
+  HIP_OK(tpi_launch_stream_hash(e->d_segs, n, total, tile, TPI_SYNC_SEED, e->d_hash,
+                                e->compute));
+  HIP_OK(hipMemsetAsync(e->d_count, 0, sizeof(unsigned int), e->compute));
+  HIP_OK(tpi_launch_dirty_tiles(e->d_hash, e->d_prev, ntiles, all, e->d_idx, e->d_count,
+                                e->compute));
+  unsigned int count = 0;
+  HIP_OK(hipMemcpyAsync(&count, e->d_count, sizeof(count), hipMemcpyDeviceToHost, e->compute));
+  HIP_OK(hipStreamSynchronize(e->compute));
+  std::vector<uint32_t> idx(count);
+  if (count) {
+    HIP_OK(hipMemcpy(idx.data(), e->d_idx, count * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    std::sort(idx.begin(), idx.end());  // ascending: consecutive tiles coalesce into one DMA
+    HIP_OK(hipMemcpy(e->d_idx, idx.data(), count * sizeof(uint32_t), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpyAsync(e->d_crcs, crcs_inout, ntiles * sizeof(uint32_t),
+                          hipMemcpyHostToDevice, e->compute));
+  }
+  // 3. pack the dirty tiles compactly, 4. DMA each run of consecutive tiles to its place
+  const uint32_t init_full = init_for(tile);
+  const uint32_t init_last = init_for(total % tile ? total % tile : tile);
+  const uint64_t per_buf = e->chunk / tile;
+  uint8_t* dst = (uint8_t*)host_dst;
+  uint64_t batches = 0;
+  for (uint64_t first = 0, k = 0; first < count; first += per_buf, ++k) {
+    const int b = (int)(k % e->nbuf);
+    const uint32_t m = (uint32_t)std::min<uint64_t>(per_buf, count - first);
+    if (k >= (uint64_t)e->nbuf) HIP_OK(hipStreamWaitEvent(e->compute, e->ev_b[b], 0));
+    HIP_OK(tpi_launch_pack_list(e->d_segs, n, total, e->d_idx + first, m, e->staging[b], tile,
+                                e->tables, e->d_crcs, init_full, init_last, e->compute));
+    HIP_OK(hipEventRecord(e->ev_a[b], e->compute));
+    HIP_OK(hipStreamWaitEvent(e->copy, e->ev_a[b], 0));
+    for (uint32_t j = 0; j < m;) {
+      uint32_t r = j + 1;
+      while (r < m && idx[first + r] == idx[first + r - 1] + 1) ++r;
+      const uint64_t start = (uint64_t)idx[first + j] * tile;
+      const uint64_t end = std::min<uint64_t>(total, (uint64_t)(idx[first + r - 1] + 1) * tile);
+      HIP_OK(hipMemcpyAsync(dst + start, (uint8_t*)e->staging[b] + (uint64_t)j * tile,
+                            end - start, hipMemcpyDeviceToHost, e->copy));
+      j = r;
+    }
+    HIP_OK(hipEventRecord(e->ev_b[b], e->copy));
+    batches = k + 1;
+  }
+  if (count)
+    HIP_OK(hipMemcpyAsync(crcs_inout, e->d_crcs, ntiles * sizeof(uint32_t),
+                          hipMemcpyDeviceToHost, e->compute));
+  HIP_OK(hipStreamSynchronize(e->copy));
+  HIP_OK(hipStreamSynchronize(e->compute));
+  e->hash_valid = true;
+  e->hash_ntiles = ntiles;
+  *dirty_tiles = count;
+  if (stats) {
+    stats->copy_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    stats->pack_ms = 0;
+    stats->bytes = std::min<uint64_t>(total, (uint64_t)count * tile);
+    stats->chunks = batches;
+  }
+  return 0;
+}
+
+int tpi_stream_hash(const tpi_seg* dev_segs, int n, uint64_t total, uint64_t tile_bytes,
+                    uint64_t seed, uint64_t* dev_out, uint64_t stream) {
+  if (tile_bytes == 0 || tile_bytes % TPI_ROW_BYTES) return fail("tile must be k*4096");
+  HIP_OK(tpi_launch_stream_hash(dev_segs, n, total, tile_bytes, seed, dev_out,
+                                (hipStream_t)stream));
   return 0;
 }
 

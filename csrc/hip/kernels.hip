@@ -185,7 +185,32 @@ struct TileArgs {
   uint32_t init_full;       // shift(~0, tile_bytes)
   uint32_t init_last;       // shift(~0, last tile length) for a short final tile
   unsigned long long* bad;  // [0] mismatching tiles, [1] first bad tile (unpack)
+  const uint32_t* list;     // optional: workgroup i handles stream tile list[i] (sparse pack)
+  uint64_t total;           // stream length (needed with `list`)
 };
+
+// Stream geometry of this workgroup's tile: (global tile, stream offset, length, buffer).
+struct TileGeom {
+  uint64_t gtile, gbase, len;
+  uint8_t* buf;
+};
+
+__device__ static inline TileGeom tile_geom(const TileArgs& a) {
+  TileGeom g;
+  if (a.list) {  // sparse: compact buffer, tiles scattered over the stream
+    g.gtile = a.list[blockIdx.x];
+    g.gbase = g.gtile * a.tile_bytes;
+    g.len = umin64(a.tile_bytes, a.total - g.gbase);
+    g.buf = a.buf + (uint64_t)blockIdx.x * a.tile_bytes;
+  } else {
+    const uint64_t off = (uint64_t)blockIdx.x * a.tile_bytes;
+    g.gtile = a.stream_base / a.tile_bytes + blockIdx.x;
+    g.gbase = a.stream_base + off;
+    g.len = umin64(a.tile_bytes, a.len - off);
+    g.buf = a.buf + off;
+  }
+  return g;
+}
 
 template <int MODE>
 __global__ __launch_bounds__(WG) void k_stream_crc(TileArgs a) {
@@ -202,10 +227,10 @@ __global__ __launch_bounds__(WG) void k_stream_crc(TileArgs a) {
     for (int i = lane; i < 20 * 256 / 4; i += WG) dst[i] = src[i];
   }
 
-  const uint64_t tile_off = (uint64_t)blockIdx.x * a.tile_bytes;  // within this launch
-  const uint64_t tile_len = umin64(a.tile_bytes, a.len - tile_off);
-  const uint64_t gbase = a.stream_base + tile_off;                // packed-stream offset
-  uint8_t* tbuf = a.buf + tile_off;
+  const TileGeom geom = tile_geom(a);
+  const uint64_t tile_len = geom.len;
+  const uint64_t gbase = geom.gbase;  // packed-stream offset
+  uint8_t* tbuf = geom.buf;
 
   SegCursor cur;
   if (MODE != MODE_CRC) seg_load(a.segs, a.nseg, seg_find(a.segs, a.nseg, gbase + lane * 16), cur);
@@ -278,7 +303,7 @@ __global__ __launch_bounds__(WG) void k_stream_crc(TileArgs a) {
     uint32_t raw = s_red[0] ^ s_red[1] ^ s_red[2] ^ s_red[3];
     const uint32_t init = (tile_len == a.tile_bytes) ? a.init_full : a.init_last;
     const uint32_t crc = raw ^ init ^ 0xFFFFFFFFu;
-    const uint64_t gtile = a.stream_base / a.tile_bytes + blockIdx.x;
+    const uint64_t gtile = geom.gtile;
     if (MODE == MODE_UNPACK) {
       if (crc != a.crcs[gtile]) {
         atomicAdd(&a.bad[0], 1ull);
@@ -363,6 +388,72 @@ __global__ __launch_bounds__(WG) void k_shard_hash(const uint8_t* __restrict__ d
   }
 }
 
+// ---- incremental checkpoints: per-tile digests gathered from the tensors -----------------------
+//
+// 64-bit change-detection digest of every tile of the *virtual* packed stream, read straight
+// from the tensors (nothing is written).  Lane l folds its words (row*4096 + 16l, the same
+// coalesced layout as the tile kernel) with XXH64 rounds from a lane-distinct seed; the tile
+// digest is the XOR of the avalanched lane states, mixed with the tile length.  It is a
+// private format (only compared with itself), so it needs no host reference beyond tests.
+
+__global__ __launch_bounds__(WG) void k_stream_hash(const tpi_seg* __restrict__ segs, int nseg,
+                                                    uint64_t total, uint64_t tile_bytes,
+                                                    uint64_t seed, uint64_t* __restrict__ out) {
+  __shared__ uint64_t red[WG / 64];
+  const int lane = threadIdx.x;
+  const uint64_t gtile = blockIdx.x;
+  const uint64_t gbase = gtile * tile_bytes;
+  const uint64_t len = umin64(tile_bytes, total - gbase);
+  SegCursor cur;
+  seg_load(segs, nseg, seg_find(segs, nseg, gbase + lane * 16), cur);
+  uint64_t v = seed + (uint64_t)(lane + 1) * TPI_XXH_P1;
+  uint64_t nwords = 0;
+  const uint64_t full_rows = len / TPI_ROW_BYTES;
+  uint64_t row = 0;
+  for (; row + UNROLL <= full_rows; row += UNROLL) {
+    u32x4 w[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const uint64_t pos = gbase + (row + u) * TPI_ROW_BYTES + lane * 16;
+      advance(segs, nseg, pos, cur);
+      w[u] = gather16(segs, cur, pos);
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      v = tpi_xxh_round(v, ((uint64_t)w[u].y << 32) | w[u].x);
+      v = tpi_xxh_round(v, ((uint64_t)w[u].w << 32) | w[u].z);
+    }
+    nwords += UNROLL;
+  }
+  for (uint64_t rel = row * TPI_ROW_BYTES + lane * 16; rel < len; rel += TPI_ROW_BYTES) {
+    advance(segs, nseg, gbase + rel, cur);
+    const u32x4 w = gather16(segs, cur, gbase + rel);
+    v = tpi_xxh_round(v, ((uint64_t)w.y << 32) | w.x);
+    v = tpi_xxh_round(v, ((uint64_t)w.w << 32) | w.z);
+    ++nwords;
+  }
+  uint64_t h = tpi_xxh_avalanche(v + nwords * 16);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) h ^= __shfl_xor(h, o, 64);
+  if ((lane & 63) == 0) red[lane >> 6] = h;
+  __syncthreads();
+  if (lane == 0) out[gtile] = tpi_xxh_avalanche(red[0] ^ red[1] ^ red[2] ^ red[3] ^ len);
+}
+
+// Compare digests with the previous sync, append dirty tile indices, remember the new ones.
+__global__ __launch_bounds__(256) void k_dirty_tiles(const uint64_t* __restrict__ hash,
+                                                     uint64_t* __restrict__ prev, uint64_t n,
+                                                     int all, uint32_t* __restrict__ idx,
+                                                     unsigned int* __restrict__ count) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t h = hash[i];
+  if (all || h != prev[i]) {
+    idx[atomicAdd(count, 1u)] = (uint32_t)i;
+    prev[i] = h;
+  }
+}
+
 // ---- launch helpers (used by engine.hip) -----------------------------------------------------
 
 extern "C" hipError_t tpi_launch_stream_crc(int mode, const tpi_seg* segs, int nseg,
@@ -384,6 +475,8 @@ extern "C" hipError_t tpi_launch_stream_crc(int mode, const tpi_seg* segs, int n
   a.init_full = init_full;
   a.init_last = init_last;
   a.bad = bad;
+  a.list = nullptr;
+  a.total = 0;
   const uint64_t ntiles = (len + tile_bytes - 1) / tile_bytes;
   dim3 grid((unsigned)ntiles), block(WG);
   switch (mode) {
@@ -403,5 +496,50 @@ extern "C" hipError_t tpi_launch_shard_hash(const void* data, uint64_t nbytes,
   const uint64_t nshards = (nbytes + shard_bytes - 1) / shard_bytes;
   hipLaunchKernelGGL(k_shard_hash, dim3((unsigned)nshards), dim3(WG), 0, stream,
                      (const uint8_t*)data, nbytes, shard_bytes, seed, out);
+  return hipGetLastError();
+}
+
+// Pack only the stream tiles listed in `list` (device, n entries) into `buf` compactly
+// (entry i -> buf + i * tile_bytes), writing their CRCs at crcs[list[i]].
+extern "C" hipError_t tpi_launch_pack_list(const tpi_seg* segs, int nseg, uint64_t total,
+                                           const uint32_t* list, uint32_t n, void* buf,
+                                           uint64_t tile_bytes, const tpi_crc_tables* tables,
+                                           uint32_t* crcs, uint32_t init_full,
+                                           uint32_t init_last, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  TileArgs a;
+  a.segs = segs;
+  a.nseg = nseg;
+  a.stream_base = 0;
+  a.len = total;
+  a.buf = (uint8_t*)buf;
+  a.tile_bytes = tile_bytes;
+  a.tables = tables;
+  a.crcs = crcs;
+  a.init_full = init_full;
+  a.init_last = init_last;
+  a.bad = nullptr;
+  a.list = list;
+  a.total = total;
+  hipLaunchKernelGGL(k_stream_crc<MODE_PACK>, dim3(n), dim3(WG), 0, stream, a);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t tpi_launch_stream_hash(const tpi_seg* segs, int nseg, uint64_t total,
+                                             uint64_t tile_bytes, uint64_t seed, uint64_t* out,
+                                             hipStream_t stream) {
+  if (total == 0) return hipSuccess;
+  const uint64_t ntiles = (total + tile_bytes - 1) / tile_bytes;
+  hipLaunchKernelGGL(k_stream_hash, dim3((unsigned)ntiles), dim3(WG), 0, stream, segs, nseg,
+                     total, tile_bytes, seed, out);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t tpi_launch_dirty_tiles(const uint64_t* hash, uint64_t* prev, uint64_t n,
+                                             int all, uint32_t* idx, unsigned int* count,
+                                             hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_dirty_tiles, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                     hash, prev, n, all, idx, count);
   return hipGetLastError();
 }

@@ -69,6 +69,17 @@ int tpi_restore(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total,
                 const void* host_src, const uint32_t* crcs, int mode, uint64_t signal_stream,
                 uint64_t* bad_tiles, int64_t* first_bad, tpi_stats* stats);
 
+// Incremental save: hash every tile of the packed stream straight from the tensors, compare
+// with the digests of the previous sync (kept in the engine), and pack + spill only the tiles
+// that changed into `host_dst` (stream offsets), updating their CRCs in `crcs_inout` (host,
+// full array).  `full` forces every tile (first sync).  *dirty_tiles receives the count.
+int tpi_sync(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* host_dst,
+             uint32_t* crcs_inout, int full, uint64_t wait_stream, uint64_t* dirty_tiles,
+             tpi_stats* stats);
+// Digest of every tile (device output, ntiles u64); exposed for tests.
+int tpi_stream_hash(const tpi_seg* dev_segs, int n, uint64_t total, uint64_t tile_bytes,
+                    uint64_t seed, uint64_t* dev_out, uint64_t stream);
+
 // Device-buffer primitives (enqueued on `stream`, asynchronous).
 int tpi_crc32c_tiles(const void* dev_ptr, uint64_t nbytes, uint64_t tile_bytes,
                      uint32_t* dev_out, uint64_t stream);

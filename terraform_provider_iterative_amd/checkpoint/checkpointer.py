@@ -53,6 +53,7 @@ class TransferResult:
     bad_tiles: int = 0
     first_bad: int = -1
     crc: int = 0
+    dirty_tiles: int = -1  # incremental sync: tiles that changed since the previous sync
 
     @property
     def gbps(self) -> float:
@@ -94,6 +95,19 @@ class DeviceEngine:
         self.lib.check(rc, "tpi_restore")
         return TransferResult(plan.total, time.perf_counter() - t0, int(st.chunks),
                               int(bad.value), int(first.value))
+
+    def sync(self, plan: PackPlan, host_addr: int, crcs: np.ndarray, full: bool,
+             wait_stream: int) -> TransferResult:
+        st = _Stats()
+        dirty = ctypes.c_uint64(0)
+        t0 = time.perf_counter()
+        rc = self.lib.tpi_sync(self.handle, plan.segs.ctypes.data, len(plan.entries), plan.total,
+                               ctypes.c_void_p(host_addr), crcs.ctypes.data, 1 if full else 0,
+                               wait_stream, ctypes.byref(dirty), ctypes.byref(st))
+        self.lib.check(rc, "tpi_sync")
+        res = TransferResult(int(st.bytes), time.perf_counter() - t0, int(st.chunks))
+        res.dirty_tiles = int(dirty.value)
+        return res
 
     def close(self) -> None:
         if self.handle:
@@ -150,6 +164,7 @@ class Checkpointer:
                                  numa_node=numa_node, populate=populate)
         self.crcs = self.region.array(self.crc_offset, 4 * self.plan.ntiles, np.uint32)
         self.saves = 0
+        self._synced = False
         self.last_save: Optional[TransferResult] = None
         self.last_restore: Optional[TransferResult] = None
 
@@ -203,6 +218,33 @@ class Checkpointer:
         res.crc = native().crc32c_combine_tiles_ptr(self.crcs.ctypes.data, self.plan.ntiles,
                                                      self.plan.tile_bytes, self.plan.total)
         self.saves += 1
+        self._write_header(self._header(True, res.crc, metadata))
+        self.last_save = res
+        return res
+
+    def sync(self, metadata: Optional[Dict] = None) -> TransferResult:
+        """Incremental save: only tiles whose content changed since the previous ``sync`` are
+        packed and spilled (the device-side replacement of the reference's 10-second
+        newest-mtime poll + ``rclone sync``, machine-script.sh.tpl:118-124).
+
+        The first sync (and any sync after ``save``/``restore``) moves every tile.  Host
+        tensors fall back to a full :meth:`save`.
+        """
+        if self.engine is None:
+            res = self.save(metadata)
+            res.dirty_tiles = self.plan.ntiles
+            return res
+        import torch
+
+        full = not self._synced
+        self._invalidate()
+        wait = torch.cuda.current_stream(self.device_index).cuda_stream
+        res = self.engine.sync(self.plan, self.region.addr + self.stream_offset, self.crcs,
+                               full, wait)
+        res.crc = native().crc32c_combine_tiles_ptr(self.crcs.ctypes.data, self.plan.ntiles,
+                                                     self.plan.tile_bytes, self.plan.total)
+        self.saves += 1
+        self._synced = True
         self._write_header(self._header(True, res.crc, metadata))
         self.last_save = res
         return res

@@ -73,6 +73,14 @@ def test_persist_load_and_corruption(tmp_path):
             ck.load(path)
 
 
+def test_sync_on_host_is_full_save():
+    src = _model(4)
+    with Checkpointer(src, tile_bytes=4096) as ck:
+        res = ck.sync({"k": 1})
+        assert res.dirty_tiles == ck.plan.ntiles
+        assert ck.header()["complete"] and ck.header()["metadata"] == {"k": 1}
+
+
 def test_incomplete_save_is_rejected(tmp_path):
     src = _model(3)
     with Checkpointer(src, tile_bytes=4096) as ck:

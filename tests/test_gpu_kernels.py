@@ -100,6 +100,41 @@ def test_unpack_device_roundtrip_and_corruption():
     assert bad == 1 and first == 1
 
 
+def test_incremental_sync_moves_only_dirty_tiles():
+    from terraform_provider_iterative_amd.checkpoint import Checkpointer
+
+    src = _tensors("cuda")
+    tile = 1 << 20
+    with Checkpointer(src, tile_bytes=tile, chunk_bytes=2 << 20, nbuf=2) as ck:
+        first = ck.sync({"n": 1})
+        assert first.dirty_tiles == ck.plan.ntiles
+        again = ck.sync({"n": 2})
+        assert again.dirty_tiles == 0 and again.bytes == 0
+        # touch one element of "big" (3 MiB) -> exactly the tile holding it is dirty
+        big = [e for e in ck.plan.entries if e.name == "big"][0]
+        src["big"][100000] += 1.0
+        touched_tile = (big.offset + 100000 * 4) // tile
+        third = ck.sync({"n": 3})
+        assert third.dirty_tiles == 1
+        # the host region now equals a full pack of the current tensors
+        hplan = PackPlan.from_tensors({k: v.cpu() for k, v in src.items()}, tile_bytes=tile)
+        hs, hc = pack(hplan)
+        assert np.array_equal(ck.region.array(ck.stream_offset, ck.plan.total), hs)
+        assert ck.crcs.tolist() == hc.tolist()
+        assert 0 <= touched_tile < ck.plan.ntiles
+        # strided tensor change is detected too
+        src["sliced"][0, 0, 0] = 42.0
+        assert ck.sync().dirty_tiles == 1
+        # restore round trip after syncs, then a save invalidates digests -> next sync full
+        ref = {k: v.clone() for k, v in src.items()}
+        for v in src.values():
+            v.zero_()
+        ck.restore()
+        torch.cuda.synchronize()
+        assert all(torch.equal(src[k], ref[k]) for k in ref)
+        assert ck.sync().dirty_tiles == ck.plan.ntiles
+
+
 @pytest.mark.parametrize("mode", ["sdma", "direct"])
 def test_checkpointer_device_roundtrip(mode, tmp_path):
     from terraform_provider_iterative_amd.checkpoint import Checkpointer
