@@ -4,8 +4,14 @@
 Config "Preempt-recover: 100 GB checkpoint pack -> host DRAM -> restore": the 100 GB
 checkpoint (bf16 parameters + fp32 Adam moments of a synthetic transformer, random init) is
 sharded over the N ranks (one per GPU, ``torch.distributed`` over RCCL when N > 1), so the
-total work is fixed: strong scaling.  One step = save (pack + CRC32C tiles -> pinned host
-DRAM over PCIe, side-stream pipeline) + restore (host -> HBM, verify every tile, scatter).
+total work is fixed: strong scaling.  One step = save (pack + CRC32C tiles [+ TPZ1 byte-plane
+encode] -> pinned host DRAM over PCIe, side-stream pipeline) + restore (host -> HBM [decode],
+verify every tile's CRC32C, scatter).  The codec is lossless; ``value`` counts checkpoint
+(tensor) bytes, the JSON also reports the compressed bytes that crossed PCIe.
+
+Synthetic state (random, no dataset/checkpoint available): bf16 parameters ~ N(0, 0.02),
+fp32 exp_avg ~ N(0, 1e-3), fp32 exp_avg_sq ~ N(0, 1e-3)^2 -- value distributions of a
+trained AdamW state (an untrained one would be all-zero moments, which compress ~1000x).
 
     python bench.py --gpus N --steps K --warmup W
 
@@ -39,6 +45,7 @@ def parse_args(argv=None):
     p.add_argument("--total-gb", type=float, default=100.0,
                    help="checkpoint size summed over all ranks (GB, 1e9 bytes)")
     p.add_argument("--mode", choices=("sdma", "direct"), default="sdma")
+    p.add_argument("--codec", choices=("none", "tpz1"), default="tpz1")
     p.add_argument("--tile-mb", type=float, default=1.0)
     p.add_argument("--chunk-mb", type=float, default=256.0)
     p.add_argument("--nbuf", type=int, default=3)
@@ -51,7 +58,7 @@ def parse_args(argv=None):
 
 
 def synthetic_checkpoint(nbytes: int, hidden: int, device):
-    """bf16 weights + fp32 Adam moments of transformer blocks until ``nbytes`` is reached."""
+    """bf16 weights + fp32 AdamW moments of transformer blocks until ``nbytes`` is reached."""
     import torch
 
     h = hidden
@@ -73,10 +80,13 @@ def synthetic_checkpoint(nbytes: int, hidden: int, device):
                     break
                 n = min(numel, max(left // esz, 1))
                 t = torch.empty(n if n != numel else shape, dtype=dtype, device=device)
-                if dtype == torch.bfloat16:
+                if kind == "param":
                     t.normal_(0, 0.02, generator=gen)
+                elif kind == "exp_avg":
+                    t.normal_(0, 1e-3, generator=gen)
                 else:
-                    t.uniform_(0, 1e-3, generator=gen)
+                    t.normal_(0, 1e-3, generator=gen)
+                    t.mul_(t)
                 tensors["layers.%d.%s.%s" % (layer, name, kind)] = t
                 used += t.numel() * esz
         layer += 1
@@ -135,7 +145,8 @@ def main(argv=None):
     tensors = synthetic_checkpoint(per_rank, args.hidden, device)
     torch.cuda.synchronize()
     ck = Checkpointer(tensors, tile_bytes=int(args.tile_mb * (1 << 20)),
-                      chunk_bytes=int(args.chunk_mb * (1 << 20)), nbuf=args.nbuf, mode=args.mode)
+                      chunk_bytes=int(args.chunk_mb * (1 << 20)), nbuf=args.nbuf, mode=args.mode,
+                      codec=args.codec)
     setup_s = time.perf_counter() - t_setup
     barrier()
 
@@ -145,10 +156,11 @@ def main(argv=None):
     barrier()
 
     save_s = restore_s = 0.0
+    wire = 0
     t0 = time.perf_counter()
     for step in range(args.steps):
         a = time.perf_counter()
-        ck.save({"step": step})
+        wire = ck.save({"step": step}).wire_bytes
         b = time.perf_counter()
         res = ck.restore()
         c = time.perf_counter()
@@ -186,6 +198,7 @@ def main(argv=None):
     elapsed = allmax(elapsed)
     save_max, restore_max = allmax(save_s), allmax(restore_s)
     total = ck.plan.total * world  # packed bytes per direction per step (all ranks)
+    wire_total = int(allmax(float(wire))) * world  # (upper bound: max rank x N)
     value = 2 * total * args.steps / elapsed / 1e9
     if rank == 0:
         out = {
@@ -200,15 +213,20 @@ def main(argv=None):
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic (random-init bf16 params + fp32 Adam moments)",
+            "data": ("synthetic random AdamW state: bf16 params N(0,0.02), fp32 exp_avg "
+                     "N(0,1e-3), fp32 exp_avg_sq N(0,1e-3)^2"),
             "config": {"model": CONFIG_NAME, "global_batch": 1, "seq_len": None,
                        "parallelism": "shard%d" % world, "checkpoint_bytes": total,
                        "tile_bytes": ck.plan.tile_bytes, "chunk_bytes": ck.engine.chunk_bytes,
-                       "mode": args.mode, "tensors_per_rank": len(tensors)},
+                       "mode": args.mode, "codec": args.codec,
+                       "tensors_per_rank": len(tensors)},
             "save_GBps": round(total * args.steps / save_max / 1e9, 3),
             "restore_GBps": round(total * args.steps / restore_max / 1e9, 3),
             "per_gpu_save_GBps": round(ck.plan.total * args.steps / save_max / 1e9, 3),
             "per_gpu_restore_GBps": round(ck.plan.total * args.steps / restore_max / 1e9, 3),
+            "wire_bytes_per_step": wire_total,
+            "compression_ratio": round(wire_total / total, 4),
+            "save_wire_GBps": round(wire_total * args.steps / save_max / 1e9, 3),
             "first_log_latency_s": (latency or {}).get("cli_s"),
             "first_log_latency": latency,
             "workdir_broadcast": broadcast,

@@ -7,6 +7,8 @@ Reports GB/s of payload processed per kernel (pack/unpack move 2x that over HBM)
   pack_device    gather tensors -> packed buffer + CRC (read + write)
   unpack_device  packed buffer -> tensors + CRC verify (read + write)
   torch_copy     dst.copy_(src) (read + write), the roofline reference
+  sync_unchanged incremental-checkpoint digest pass when nothing changed
+  tpz_encode / tpz_decode  TPZ1 byte-plane codec on an AdamW-like state (GB/s of raw bytes)
 """
 from __future__ import annotations
 
@@ -78,8 +80,33 @@ def main():
     t = timeit(lambda: ck.sync(), args.iters)
     out["sync_unchanged_GBps"] = plan.total / t / 1e9
     ck.close()
+    # TPZ1 codec on AdamW-like state (bf16 N(0,.02) + fp32 N(0,1e-3) + fp32 N(0,1e-3)^2)
+    from terraform_provider_iterative_amd.ops import codec
+
+    q = n // 10 // 16 * 16
+    state = torch.empty(10 * q, dtype=torch.uint8, device=dev)
+    state[:2 * q].view(torch.bfloat16).normal_(0, 0.02)
+    state[2 * q:6 * q].view(torch.float32).normal_(0, 1e-3)
+    sq = state[6 * q:].view(torch.float32)
+    sq.normal_(0, 1e-3)
+    sq.mul_(sq)
+    enc = [None]
+
+    def do_encode():
+        enc[0] = codec.encode(state)
+
+    t = timeit(do_encode, args.iters)
+    out["tpz_encode_GBps"] = state.numel() / t / 1e9
+    blobs, sizes = enc[0]
+    out["tpz_ratio"] = blobs.numel() / state.numel()
+    t = timeit(lambda: codec.decode(blobs, sizes, state.numel()), args.iters)
+    out["tpz_decode_GBps"] = state.numel() / t / 1e9
+    back, _ = codec.decode(blobs, sizes, state.numel())
+    out["tpz_roundtrip_ok"] = bool(torch.equal(back, state))
+    del state, back, blobs
     out["bytes"] = n
-    print(json.dumps({k: round(v, 1) if isinstance(v, float) else v for k, v in out.items()}))
+    print(json.dumps({k: round(v, 4 if k == "tpz_ratio" else 1) if isinstance(v, float) else v
+                      for k, v in out.items()}))
 
 
 if __name__ == "__main__":

@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "../common/crc32c.h"
+#include "../common/tpz.h"
 #include "tpi_hip.h"
 
 extern "C" hipError_t tpi_launch_stream_crc(int mode, const tpi_seg* segs, int nseg,
@@ -47,6 +48,13 @@ extern "C" hipError_t tpi_launch_stream_hash(const tpi_seg* segs, int nseg, uint
 extern "C" hipError_t tpi_launch_dirty_tiles(const uint64_t* hash, uint64_t* prev, uint64_t n,
                                              int all, uint32_t* idx, unsigned int* count,
                                              hipStream_t stream);
+
+extern "C" hipError_t tpi_launch_tpz_encode(const void* raw, uint64_t len, uint64_t tile,
+                                            void* meta, uint32_t* csize, void* out,
+                                            hipStream_t stream);
+extern "C" hipError_t tpi_launch_tpz_decode(const void* comp, const uint64_t* coff,
+                                            uint64_t comp_base, uint64_t len, uint64_t tile,
+                                            void* raw, hipStream_t stream);
 
 #define TPI_SYNC_SEED 0x7470692d73796e63ull  // "tpi-sync"
 
@@ -135,6 +143,13 @@ struct tpi_engine {
   size_t hash_cap = 0;
   uint64_t hash_ntiles = 0;
   bool hash_valid = false;
+  // TPZ1 codec: raw pack scratch (one chunk), per-tile headers of the chunk in flight,
+  // blob sizes / offsets of the whole stream
+  void* zraw = nullptr;
+  void* d_meta = nullptr;
+  uint32_t* d_csize = nullptr;
+  uint64_t* d_coff = nullptr;
+  size_t z_cap = 0;
   std::mutex mu;
 };
 
@@ -190,11 +205,13 @@ tpi_engine* tpi_engine_create(int device, uint64_t chunk_bytes, int nbuf, uint64
     return bail("hipStreamCreate(compute)", err);
   if ((err = hipStreamCreateWithFlags(&e->copy, hipStreamNonBlocking)) != hipSuccess)
     return bail("hipStreamCreate(copy)", err);
+  // staging chunks also hold TPZ1 blobs: worst case tpz_bound() per tile
+  const uint64_t staging_bytes = chunk_bytes + (chunk_bytes / tile_bytes) * (TPZ_HDR + 128);
   e->staging.assign(nbuf, nullptr);
   e->ev_a.assign(nbuf, nullptr);
   e->ev_b.assign(nbuf, nullptr);
   for (int i = 0; i < nbuf; ++i) {
-    if ((err = hipMalloc(&e->staging[i], chunk_bytes)) != hipSuccess)
+    if ((err = hipMalloc(&e->staging[i], staging_bytes)) != hipSuccess)
       return bail("hipMalloc(staging)", err);
     if ((err = hipEventCreateWithFlags(&e->ev_a[i], hipEventDisableTiming)) != hipSuccess)
       return bail("hipEventCreate", err);
@@ -235,6 +252,8 @@ void tpi_engine_destroy(tpi_engine* e) {
   if (e->d_prev) (void)hipFree(e->d_prev);
   if (e->d_idx) (void)hipFree(e->d_idx);
   if (e->d_count) (void)hipFree(e->d_count);
+  for (void* p : {e->zraw, e->d_meta, (void*)e->d_csize, (void*)e->d_coff})
+    if (p) (void)hipFree(p);
   if (e->compute) (void)hipStreamDestroy(e->compute);
   if (e->copy) (void)hipStreamDestroy(e->copy);
   delete e;
@@ -472,6 +491,177 @@ int tpi_sync(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* ho
     stats->bytes = std::min<uint64_t>(total, (uint64_t)count * tile);
     stats->chunks = batches;
   }
+  return 0;
+}
+
+}  // extern "C"
+
+namespace {
+
+int prepare_codec(tpi_engine* e, uint64_t ntiles) {
+  const uint64_t per_chunk = e->chunk / e->tile;
+  if (!e->zraw) {
+    HIP_OK(hipMalloc(&e->zraw, e->chunk));
+    HIP_OK(hipMalloc(&e->d_meta, per_chunk * 4 * sizeof(tpz_plane)));
+  }
+  if (ntiles + 1 > e->z_cap) {
+    if (e->d_csize) HIP_OK(hipFree(e->d_csize));
+    if (e->d_coff) HIP_OK(hipFree(e->d_coff));
+    e->z_cap = std::max<size_t>(ntiles + 1, 1024);
+    HIP_OK(hipMalloc(&e->d_csize, e->z_cap * sizeof(uint32_t)));
+    HIP_OK(hipMalloc(&e->d_coff, e->z_cap * sizeof(uint64_t)));
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Compressed save: per chunk  pack+CRC -> zraw, analyze+encode -> staging[b] (TPZ1 blobs,
+// contiguous), blob sizes -> csizes_out (host);  the host learns the chunk's compressed length
+// from those sizes and only then queues its D2H, so PCIe carries the compressed bytes only.
+// The host waits on each chunk's (short) compute while the copy stream is still draining the
+// previous chunks, so the link stays busy.
+int tpi_save_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* host_dst,
+               uint32_t* crcs_out, uint32_t* csizes_out, uint64_t wait_stream,
+               uint64_t* stream_bytes, tpi_stats* stats) {
+  std::lock_guard<std::mutex> lk(e->mu);
+  auto t0 = std::chrono::steady_clock::now();
+  if (prepare(e, segs, n, total)) return -1;
+  const uint64_t tile = e->tile;
+  const uint64_t ntiles = (total + tile - 1) / tile;
+  if (prepare_codec(e, ntiles)) return -1;
+  e->hash_valid = false;
+  if (wait_stream) {
+    HIP_OK(hipEventRecord(e->ev_wait, (hipStream_t)wait_stream));
+    HIP_OK(hipStreamWaitEvent(e->compute, e->ev_wait, 0));
+  }
+  const uint32_t init_full = init_for(tile);
+  const uint32_t init_last = init_for(total % tile ? total % tile : tile);
+  uint8_t* dst = (uint8_t*)host_dst;
+  uint64_t out = 0, nchunks = 0;
+  for (uint64_t base = 0, k = 0; base < total; base += e->chunk, ++k) {
+    const int b = (int)(k % e->nbuf);
+    const uint64_t len = std::min(e->chunk, total - base);
+    const uint64_t t0i = base / tile, nt = (len + tile - 1) / tile;
+    if (k >= (uint64_t)e->nbuf) HIP_OK(hipStreamWaitEvent(e->compute, e->ev_b[b], 0));
+    HIP_OK(tpi_launch_stream_crc(0, e->d_segs, n, base, len, e->zraw, tile, e->tables,
+                                 e->d_crcs, init_full, init_last, nullptr, e->compute));
+    HIP_OK(tpi_launch_tpz_encode(e->zraw, len, tile, e->d_meta, e->d_csize + t0i,
+                                 e->staging[b], e->compute));
+    HIP_OK(hipMemcpyAsync(csizes_out + t0i, e->d_csize + t0i, nt * sizeof(uint32_t),
+                          hipMemcpyDeviceToHost, e->compute));
+    HIP_OK(hipEventRecord(e->ev_a[b], e->compute));
+    HIP_OK(hipEventSynchronize(e->ev_a[b]));
+    uint64_t clen = 0;
+    for (uint64_t i = 0; i < nt; ++i) clen += csizes_out[t0i + i];
+    HIP_OK(hipStreamWaitEvent(e->copy, e->ev_a[b], 0));
+    HIP_OK(hipMemcpyAsync(dst + out, e->staging[b], clen, hipMemcpyDeviceToHost, e->copy));
+    HIP_OK(hipEventRecord(e->ev_b[b], e->copy));
+    out += clen;
+    nchunks = k + 1;
+  }
+  HIP_OK(hipMemcpyAsync(crcs_out, e->d_crcs, ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                        e->compute));
+  HIP_OK(hipStreamSynchronize(e->copy));
+  HIP_OK(hipStreamSynchronize(e->compute));
+  *stream_bytes = out;
+  if (stats) {
+    stats->copy_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    stats->pack_ms = 0;
+    stats->bytes = out;
+    stats->chunks = nchunks;
+  }
+  return 0;
+}
+
+// Compressed restore: H2D of each chunk's blobs -> staging[b], decode -> zraw, unpack+verify.
+int tpi_restore_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total,
+                  const void* host_src, const uint32_t* crcs, const uint32_t* csizes,
+                  uint64_t signal_stream, uint64_t* bad_tiles, int64_t* first_bad,
+                  tpi_stats* stats) {
+  std::lock_guard<std::mutex> lk(e->mu);
+  auto t0 = std::chrono::steady_clock::now();
+  if (prepare(e, segs, n, total)) return -1;
+  const uint64_t tile = e->tile;
+  const uint64_t ntiles = (total + tile - 1) / tile;
+  if (prepare_codec(e, ntiles)) return -1;
+  e->hash_valid = false;
+  // Blob offsets; a size that cannot come from the encoder means a corrupt index.
+  std::vector<uint64_t> coff(ntiles + 1, 0);
+  for (uint64_t i = 0; i < ntiles; ++i) {
+    const uint64_t tl = std::min(tile, total - i * tile);
+    if (csizes[i] < TPZ_HDR || csizes[i] > tpz_bound(tl) || csizes[i] % 16)
+      return fail("corrupt compressed index at tile " + std::to_string(i));
+    coff[i + 1] = coff[i] + csizes[i];
+  }
+  const uint32_t init_full = init_for(tile);
+  const uint32_t init_last = init_for(total % tile ? total % tile : tile);
+  unsigned long long bad_init[2] = {0ull, ~0ull};
+  if (signal_stream) {
+    HIP_OK(hipEventRecord(e->ev_wait, (hipStream_t)signal_stream));
+    HIP_OK(hipStreamWaitEvent(e->compute, e->ev_wait, 0));
+  }
+  HIP_OK(hipMemcpyAsync(e->d_crcs, crcs, ntiles * sizeof(uint32_t), hipMemcpyHostToDevice,
+                        e->compute));
+  HIP_OK(hipMemcpyAsync(e->d_coff, coff.data(), (ntiles + 1) * sizeof(uint64_t),
+                        hipMemcpyHostToDevice, e->compute));
+  HIP_OK(hipMemcpyAsync(e->d_bad, bad_init, sizeof(bad_init), hipMemcpyHostToDevice,
+                        e->compute));
+  HIP_OK(hipEventRecord(e->ev_wait, e->compute));
+  HIP_OK(hipStreamWaitEvent(e->copy, e->ev_wait, 0));
+  const uint8_t* src = (const uint8_t*)host_src;
+  uint64_t nchunks = 0;
+  for (uint64_t base = 0, k = 0; base < total; base += e->chunk, ++k) {
+    const int b = (int)(k % e->nbuf);
+    const uint64_t len = std::min(e->chunk, total - base);
+    const uint64_t t0i = base / tile, nt = (len + tile - 1) / tile;
+    const uint64_t cbeg = coff[t0i], cend = coff[t0i + nt];
+    if (k >= (uint64_t)e->nbuf) HIP_OK(hipStreamWaitEvent(e->copy, e->ev_b[b], 0));
+    HIP_OK(hipMemcpyAsync(e->staging[b], src + cbeg, cend - cbeg, hipMemcpyHostToDevice,
+                          e->copy));
+    HIP_OK(hipEventRecord(e->ev_a[b], e->copy));
+    HIP_OK(hipStreamWaitEvent(e->compute, e->ev_a[b], 0));
+    HIP_OK(tpi_launch_tpz_decode(e->staging[b], e->d_coff + t0i, cbeg, len, tile, e->zraw,
+                                 e->compute));
+    HIP_OK(hipEventRecord(e->ev_b[b], e->compute));
+    HIP_OK(tpi_launch_stream_crc(1, e->d_segs, n, base, len, e->zraw, tile, e->tables,
+                                 e->d_crcs, init_full, init_last, e->d_bad, e->compute));
+    nchunks = k + 1;
+  }
+  unsigned long long bad[2];
+  HIP_OK(hipMemcpyAsync(bad, e->d_bad, sizeof(bad), hipMemcpyDeviceToHost, e->compute));
+  HIP_OK(hipEventRecord(e->ev_done, e->compute));
+  if (signal_stream) HIP_OK(hipStreamWaitEvent((hipStream_t)signal_stream, e->ev_done, 0));
+  HIP_OK(hipStreamSynchronize(e->compute));
+  HIP_OK(hipStreamSynchronize(e->copy));
+  *bad_tiles = bad[0];
+  *first_bad = bad[0] ? (int64_t)bad[1] : -1;
+  if (stats) {
+    stats->copy_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    stats->pack_ms = 0;
+    stats->bytes = coff[ntiles];
+    stats->chunks = nchunks;
+  }
+  return 0;
+}
+
+int tpi_tpz_encode_device(const void* raw, uint64_t len, uint64_t tile, void* meta_scratch,
+                          uint32_t* csize, void* out, uint64_t stream) {
+  if (tile == 0 || tile % TPI_ROW_BYTES) return fail("tile must be k*4096");
+  if (len % 16) return fail("length must be a multiple of 16");
+  HIP_OK(tpi_launch_tpz_encode(raw, len, tile, meta_scratch, csize, out, (hipStream_t)stream));
+  return 0;
+}
+
+int tpi_tpz_decode_device(const void* comp, const uint64_t* coff, uint64_t len, uint64_t tile,
+                          void* raw, uint64_t stream) {
+  if (tile == 0 || tile % TPI_ROW_BYTES) return fail("tile must be k*4096");
+  if (len % 16) return fail("length must be a multiple of 16");
+  HIP_OK(tpi_launch_tpz_decode(comp, coff, 0, len, tile, raw, (hipStream_t)stream));
   return 0;
 }
 

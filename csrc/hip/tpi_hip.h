@@ -69,6 +69,24 @@ int tpi_restore(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total,
                 const void* host_src, const uint32_t* crcs, int mode, uint64_t signal_stream,
                 uint64_t* bad_tiles, int64_t* first_bad, tpi_stats* stats);
 
+// Compressed (TPZ1, csrc/common/tpz.h) variants: the stream at `host_dst` is the concatenation
+// of per-tile blobs whose sizes go to `csizes_out` (host, one u32 per tile; host_dst needs
+// room for sum(tpz_bound(tile))).  *stream_bytes = bytes written.  CRCs cover the raw tiles.
+int tpi_save_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* host_dst,
+               uint32_t* crcs_out, uint32_t* csizes_out, uint64_t wait_stream,
+               uint64_t* stream_bytes, tpi_stats* stats);
+int tpi_restore_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total,
+                  const void* host_src, const uint32_t* crcs, const uint32_t* csizes,
+                  uint64_t signal_stream, uint64_t* bad_tiles, int64_t* first_bad,
+                  tpi_stats* stats);
+// Device-buffer codec (tests / tools): encode `len` bytes of `raw` into contiguous blobs
+// (`meta_scratch`: ntiles*96 bytes, `csize`: ntiles u32), decode with blob offsets `coff`
+// (ntiles+1 u64, device).
+int tpi_tpz_encode_device(const void* raw, uint64_t len, uint64_t tile, void* meta_scratch,
+                          uint32_t* csize, void* out, uint64_t stream);
+int tpi_tpz_decode_device(const void* comp, const uint64_t* coff, uint64_t len, uint64_t tile,
+                          void* raw, uint64_t stream);
+
 // Incremental save: hash every tile of the packed stream straight from the tensors, compare
 // with the digests of the previous sync (kept in the engine), and pack + spill only the tiles
 // that changed into `host_dst` (stream offsets), updating their CRCs in `crcs_inout` (host,

@@ -5,6 +5,7 @@
 #include <stdexcept>
 
 #include "filter.h"
+#include "../common/tpz.h"
 #include "hostops.h"
 #include "transfer.h"
 
@@ -156,5 +157,18 @@ PYBIND11_MODULE(_tpi_native, m) {
                         &first);
     }
     return py::make_tuple(bad, first);
+  });
+  m.def("tpz_bound", [](uint64_t len) { return tpz_bound(len); });
+  m.def("tpz_encode_ptr", [](uintptr_t src, uint64_t total, uint64_t tile, uintptr_t dst,
+                             uintptr_t csizes, int threads) {
+    py::gil_scoped_release nogil;
+    return tpi::tpz_encode_stream((const void*)src, total, tile, (void*)dst,
+                                  (uint32_t*)csizes, threads);
+  });
+  m.def("tpz_decode_ptr", [](uintptr_t src, uintptr_t csizes, uint64_t total, uint64_t tile,
+                             uintptr_t dst, int threads) {
+    py::gil_scoped_release nogil;
+    return tpi::tpz_decode_stream((const void*)src, (const uint32_t*)csizes, total, tile,
+                                  (void*)dst, threads);
   });
 }

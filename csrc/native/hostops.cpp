@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../common/crc32c.h"
+#include "../common/tpz.h"
 #include "../common/xxh64.h"
 
 namespace tpi {
@@ -205,6 +206,44 @@ uint64_t unpack(const tpi_seg* segs, int n, uint64_t total, const void* stream, 
   });
   *first_bad = bad ? first.load() : -1;
   return bad;
+}
+
+uint64_t tpz_encode_stream(const void* src, uint64_t total, uint64_t tile, void* dst,
+                           uint32_t* csizes, int threads) {
+  // Tiles encode independently into worst-case slots, then slide down to be contiguous.
+  const uint64_t ntiles = (total + tile - 1) / tile;
+  std::vector<uint8_t> slots(ntiles * tpz_bound(tile));
+  const uint8_t* s = (const uint8_t*)src;
+  parallel_for(ntiles, threads, [&](uint64_t t) {
+    const uint64_t lo = t * tile;
+    csizes[t] = (uint32_t)tpz_encode_tile(s + lo, std::min(tile, total - lo),
+                                          slots.data() + t * tpz_bound(tile));
+  });
+  uint64_t off = 0;
+  for (uint64_t t = 0; t < ntiles; ++t) {
+    memcpy((uint8_t*)dst + off, slots.data() + t * tpz_bound(tile), csizes[t]);
+    off += csizes[t];
+  }
+  return off;
+}
+
+int64_t tpz_decode_stream(const void* src, const uint32_t* csizes, uint64_t total, uint64_t tile,
+                          void* dst, int threads) {
+  const uint64_t ntiles = (total + tile - 1) / tile;
+  std::vector<uint64_t> off(ntiles + 1, 0);
+  for (uint64_t t = 0; t < ntiles; ++t) off[t + 1] = off[t] + csizes[t];
+  std::atomic<int64_t> first{INT64_MAX};
+  parallel_for(ntiles, threads, [&](uint64_t t) {
+    const uint64_t lo = t * tile, len = std::min(tile, total - lo);
+    if (tpz_decode_tile((const uint8_t*)src + off[t], csizes[t], len, (uint8_t*)dst + lo) !=
+        csizes[t]) {
+      memset((uint8_t*)dst + lo, 0, len);
+      int64_t cur = first.load();
+      while ((int64_t)t < cur && !first.compare_exchange_weak(cur, (int64_t)t)) {
+      }
+    }
+  });
+  return first.load() == INT64_MAX ? -1 : first.load();
 }
 
 }  // namespace tpi

@@ -19,4 +19,12 @@ void pack(const tpi_seg* segs, int n, uint64_t total, void* stream, uint64_t til
 uint64_t unpack(const tpi_seg* segs, int n, uint64_t total, const void* stream, uint64_t tile,
                 const uint32_t* crcs, int threads, int64_t* first_bad);
 
+// TPZ1 codec (csrc/common/tpz.h) over a stream of tiles: blobs are written back to back,
+// sizes to `csizes`; returns the compressed length.  Decode returns -1, or the first tile
+// whose blob is malformed (that tile is zero-filled).
+uint64_t tpz_encode_stream(const void* src, uint64_t total, uint64_t tile, void* dst,
+                           uint32_t* csizes, int threads);
+int64_t tpz_decode_stream(const void* src, const uint32_t* csizes, uint64_t total, uint64_t tile,
+                          void* dst, int threads);
+
 }  // namespace tpi

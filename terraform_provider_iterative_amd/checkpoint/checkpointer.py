@@ -8,11 +8,16 @@ from the same region (or from the persisted file) and verifies every tile.
 
 Region layout (also the persisted file format)::
 
-    0            b"TPICKPT1" | u64 header_len | JSON header (see ``_header``)
-    crc_offset   u32 CRC32C per tile                       (4 KiB aligned)
-    stream_off   packed stream (``ops.packing`` layout)    (4 KiB aligned)
+    0              b"TPICKPT1" | u64 header_len | JSON header (see ``_header``)
+    crc_offset     u32 CRC32C per (raw) tile                  (4 KiB aligned)
+    csize_offset   u32 encoded blob size per tile (codec "tpz1" only)
+    stream_offset  packed stream (``ops.packing`` layout), or with ``codec="tpz1"`` the
+                   concatenated TPZ1 tile blobs (``ops.codec``)   (4 KiB aligned)
 
-The JSON header carries ``"complete": true`` only after a save finished, and is written last.
+The JSON header carries ``"complete": true`` only after a save finished, and is written last;
+``"codec"`` / ``"stream_bytes"`` say how the stream section is encoded and how long it is.
+The layout does not depend on the codec, so any reader bound to the same tensors loads
+either encoding.
 """
 from __future__ import annotations
 
@@ -26,6 +31,7 @@ from typing import Any, Dict, Mapping, Optional, Sequence, Union
 
 import numpy as np
 
+from ..ops import codec as tpz
 from ..ops import hip, native
 from ..ops.packing import PackPlan, TensorEntry, align_up
 from ..ops.packing import pack as host_pack, unpack as host_unpack
@@ -34,6 +40,7 @@ from .host import HostRegion
 MAGIC = b"TPICKPT1"
 PREAMBLE = 16
 MODES = {"sdma": 0, "direct": 1}
+CODECS = ("none", "tpz1")
 
 
 class CheckpointError(RuntimeError):
@@ -54,6 +61,11 @@ class TransferResult:
     first_bad: int = -1
     crc: int = 0
     dirty_tiles: int = -1  # incremental sync: tiles that changed since the previous sync
+    wire_bytes: int = -1   # bytes that crossed the link / landed in the region (codec)
+
+    def __post_init__(self):
+        if self.wire_bytes < 0:
+            self.wire_bytes = self.bytes
 
     @property
     def gbps(self) -> float:
@@ -96,6 +108,33 @@ class DeviceEngine:
         return TransferResult(plan.total, time.perf_counter() - t0, int(st.chunks),
                               int(bad.value), int(first.value))
 
+    def save_z(self, plan: PackPlan, host_addr: int, crcs: np.ndarray, csizes: np.ndarray,
+               wait_stream: int) -> TransferResult:
+        st = _Stats()
+        wire = ctypes.c_uint64(0)
+        t0 = time.perf_counter()
+        rc = self.lib.tpi_save_z(self.handle, plan.segs.ctypes.data, len(plan.entries),
+                                 plan.total, ctypes.c_void_p(host_addr), crcs.ctypes.data,
+                                 csizes.ctypes.data, wait_stream, ctypes.byref(wire),
+                                 ctypes.byref(st))
+        self.lib.check(rc, "tpi_save_z")
+        return TransferResult(plan.total, time.perf_counter() - t0, int(st.chunks),
+                              wire_bytes=int(wire.value))
+
+    def restore_z(self, plan: PackPlan, host_addr: int, crcs: np.ndarray, csizes: np.ndarray,
+                  signal_stream: int) -> TransferResult:
+        st = _Stats()
+        bad = ctypes.c_uint64(0)
+        first = ctypes.c_int64(-1)
+        t0 = time.perf_counter()
+        rc = self.lib.tpi_restore_z(self.handle, plan.segs.ctypes.data, len(plan.entries),
+                                    plan.total, ctypes.c_void_p(host_addr), crcs.ctypes.data,
+                                    csizes.ctypes.data, signal_stream, ctypes.byref(bad),
+                                    ctypes.byref(first), ctypes.byref(st))
+        self.lib.check(rc, "tpi_restore_z")
+        return TransferResult(plan.total, time.perf_counter() - t0, int(st.chunks),
+                              int(bad.value), int(first.value), wire_bytes=int(st.bytes))
+
     def sync(self, plan: PackPlan, host_addr: int, crcs: np.ndarray, full: bool,
              wait_stream: int) -> TransferResult:
         st = _Stats()
@@ -121,10 +160,12 @@ class DeviceEngine:
             pass
 
 
-def _layout(header_len: int, ntiles: int, total: int):
+def _layout(header_len: int, ntiles: int, total: int, tile_bytes: int):
     crc_offset = align_up(PREAMBLE + header_len, 4096)
-    stream_offset = align_up(crc_offset + 4 * ntiles, 4096)
-    return crc_offset, stream_offset, stream_offset + total
+    csize_offset = crc_offset + 4 * ntiles
+    stream_offset = align_up(csize_offset + 4 * ntiles, 4096)
+    capacity = max(total, tpz.bound(total, tile_bytes))
+    return crc_offset, csize_offset, stream_offset, stream_offset + capacity
 
 
 class Checkpointer:
@@ -133,6 +174,10 @@ class Checkpointer:
     ``path=None`` keeps the spill in anonymous host DRAM (lives as long as this object);
     a path under ``/dev/shm`` survives the process (preemption), a path on disk survives the
     node.  Device tensors use the HIP pipeline, host tensors the C++ host path.
+
+    ``codec="tpz1"`` encodes every tile with the lossless byte-plane codec before it leaves
+    the GPU (``csrc/hip/codec.hip``): the PCIe-bound spill then moves fewer bytes, which is
+    what bounds save/restore throughput.  CRCs always cover the raw tiles.
     """
 
     HEADER_RESERVE = 64 * 1024  # room for metadata updates without relayout
@@ -140,14 +185,19 @@ class Checkpointer:
     def __init__(self, tensors: Union[Mapping[str, Any], Sequence[Any]],
                  path: Optional[str] = None, *, tile_bytes: int = 1 << 20,
                  chunk_bytes: int = 256 << 20, nbuf: int = 3, mode: str = "sdma",
-                 numa: bool = True, populate: bool = True):
+                 numa: bool = True, populate: bool = True, codec: str = "none"):
         self.plan = PackPlan.from_tensors(tensors, tile_bytes)
         self.path = path
         self.mode = MODES[mode]
+        if codec not in CODECS:
+            raise ValueError("codec must be one of %s" % (CODECS,))
+        if codec != "none" and self.mode != MODES["sdma"]:
+            raise ValueError("the codec needs the staged (sdma) pipeline")
+        self.codec = codec
         entries_json = json.dumps([e.to_json() for e in self.plan.entries]).encode()
         self.header_cap = len(entries_json) + self.HEADER_RESERVE
-        self.crc_offset, self.stream_offset, self.size = _layout(
-            self.header_cap, self.plan.ntiles, self.plan.total)
+        self.crc_offset, self.csize_offset, self.stream_offset, self.size = _layout(
+            self.header_cap, self.plan.ntiles, self.plan.total, self.plan.tile_bytes)
         self.engine = None
         numa_node = -1
         if self.plan.on_device:
@@ -163,16 +213,20 @@ class Checkpointer:
         self.region = HostRegion(self.size, path, device=self.plan.on_device,
                                  numa_node=numa_node, populate=populate)
         self.crcs = self.region.array(self.crc_offset, 4 * self.plan.ntiles, np.uint32)
+        self.csizes = self.region.array(self.csize_offset, 4 * self.plan.ntiles, np.uint32)
         self.saves = 0
         self._synced = False
         self.last_save: Optional[TransferResult] = None
         self.last_restore: Optional[TransferResult] = None
 
     # -- header ------------------------------------------------------------------------------
-    def _header(self, complete: bool, crc: int, metadata: Optional[Dict]) -> Dict:
-        return {"format": 1, "complete": complete, "tile_bytes": self.plan.tile_bytes,
+    def _header(self, complete: bool, crc: int, metadata: Optional[Dict], codec: str = "none",
+                stream_bytes: Optional[int] = None) -> Dict:
+        return {"format": 2, "complete": complete, "tile_bytes": self.plan.tile_bytes,
                 "total": self.plan.total, "ntiles": self.plan.ntiles,
-                "crc_offset": self.crc_offset, "stream_offset": self.stream_offset,
+                "crc_offset": self.crc_offset, "csize_offset": self.csize_offset,
+                "stream_offset": self.stream_offset, "codec": codec,
+                "stream_bytes": self.plan.total if stream_bytes is None else stream_bytes,
                 "crc32c": crc, "saved_at": time.time(), "saves": self.saves,
                 "metadata": metadata or {},
                 "entries": [e.to_json() for e in self.plan.entries]}
@@ -203,22 +257,34 @@ class Checkpointer:
     def save(self, metadata: Optional[Dict] = None) -> TransferResult:
         """Pack every tensor into the region; returns bytes/seconds (GB/s via ``.gbps``)."""
         self._invalidate()
+        zipped = self.codec == "tpz1"
+        dst = self.region.addr + self.stream_offset
         if self.engine is not None:
             import torch
 
             wait = torch.cuda.current_stream(self.device_index).cuda_stream
-            res = self.engine.save(self.plan, self.region.addr + self.stream_offset, self.crcs,
-                                   self.mode, wait)
+            if zipped:
+                res = self.engine.save_z(self.plan, dst, self.crcs, self.csizes, wait)
+            else:
+                res = self.engine.save(self.plan, dst, self.crcs, self.mode, wait)
         else:
             t0 = time.perf_counter()
-            stream = self.region.array(self.stream_offset, self.plan.total)
-            _, crcs = host_pack(self.plan, stream)
+            if zipped:
+                raw, crcs = host_pack(self.plan)
+                blobs, sizes = tpz.encode(raw, self.plan.tile_bytes)
+                self.region.array(self.stream_offset, len(blobs))[:] = blobs
+                self.csizes[:] = sizes
+                wire = len(blobs)
+            else:
+                stream = self.region.array(self.stream_offset, self.plan.total)
+                _, crcs = host_pack(self.plan, stream)
+                wire = self.plan.total
             self.crcs[:] = crcs
-            res = TransferResult(self.plan.total, time.perf_counter() - t0)
+            res = TransferResult(self.plan.total, time.perf_counter() - t0, wire_bytes=wire)
         res.crc = native().crc32c_combine_tiles_ptr(self.crcs.ctypes.data, self.plan.ntiles,
                                                      self.plan.tile_bytes, self.plan.total)
         self.saves += 1
-        self._write_header(self._header(True, res.crc, metadata))
+        self._write_header(self._header(True, res.crc, metadata, self.codec, res.wire_bytes))
         self.last_save = res
         return res
 
@@ -255,17 +321,28 @@ class Checkpointer:
         if not header.get("complete"):
             raise CheckpointError("checkpoint incomplete (save was interrupted)")
         self._check_compatible(header)
+        zipped = header.get("codec", "none") == "tpz1"
+        src = self.region.addr + self.stream_offset
         if self.engine is not None:
             import torch
 
             sig = torch.cuda.current_stream(self.device_index).cuda_stream
-            res = self.engine.restore(self.plan, self.region.addr + self.stream_offset,
-                                      self.crcs, self.mode, sig)
+            if zipped:
+                res = self.engine.restore_z(self.plan, src, self.crcs, self.csizes, sig)
+            else:
+                res = self.engine.restore(self.plan, src, self.crcs, self.mode, sig)
         else:
             t0 = time.perf_counter()
-            stream = self.region.array(self.stream_offset, self.plan.total)
+            if zipped:
+                nbytes = int(header["stream_bytes"])
+                stream, _ = tpz.decode(self.region.array(self.stream_offset, nbytes),
+                                       self.csizes, self.plan.total, self.plan.tile_bytes)
+            else:
+                nbytes = self.plan.total
+                stream = self.region.array(self.stream_offset, self.plan.total)
             bad, first = host_unpack(self.plan, stream, self.crcs)
-            res = TransferResult(self.plan.total, time.perf_counter() - t0, 0, bad, first)
+            res = TransferResult(self.plan.total, time.perf_counter() - t0, 0, bad, first,
+                                 wire_bytes=nbytes)
         res.crc = int(header.get("crc32c", 0))
         self.last_restore = res
         if strict and res.bad_tiles:
@@ -276,6 +353,8 @@ class Checkpointer:
     def _check_compatible(self, header: Dict) -> None:
         entries = [TensorEntry.from_json(e) for e in header["entries"]]
         if (header["total"] != self.plan.total or header["tile_bytes"] != self.plan.tile_bytes
+                or header.get("stream_offset") != self.stream_offset
+                or header.get("crc_offset") != self.crc_offset
                 or entries != self.plan.entries):
             raise CheckpointError("checkpoint layout does not match the bound tensors")
 
@@ -285,7 +364,7 @@ class Checkpointer:
         if not header.get("complete"):
             raise CheckpointError("nothing saved yet")
         tmp = path + ".tpi-partial"
-        data = self.region.array(0, self.size)
+        data = self.region.array(0, self.stream_offset + int(header["stream_bytes"]))
         with open(tmp, "wb") as f:
             f.write(memoryview(data))
             f.flush()
@@ -300,10 +379,11 @@ class Checkpointer:
             header = self.read_header(head)
             self._check_compatible(header)
             f.seek(0)
-            dst = self.region.array(0, self.size)
+            end = self.stream_offset + int(header["stream_bytes"])
+            dst = self.region.array(0, end)
             view = memoryview(dst)
             off = 0
-            while off < self.size:
+            while off < end:
                 n = f.readinto(view[off:off + (64 << 20)])
                 if not n:
                     break

@@ -14,7 +14,7 @@ _LAZY = {
     "DEFAULT_SHARD_BYTES": "hashing", "DEFAULT_TILE_BYTES": "hashing", "crc32c": "hashing",
     "crc32c_combine": "hashing", "crc32c_tiles": "hashing", "dirty_shards": "hashing",
     "shard_hash": "hashing", "SEG_DTYPE": "packing", "PackPlan": "packing",
-    "TensorEntry": "packing", "pack": "packing", "unpack": "packing",
+    "TensorEntry": "packing", "pack": "packing", "unpack": "packing", "codec": None,
 }
 
 __all__ = ["HipError", "gpu_visible", "hip", "native"] + sorted(_LAZY)
@@ -22,10 +22,13 @@ __all__ = ["HipError", "gpu_visible", "hip", "native"] + sorted(_LAZY)
 
 def __getattr__(name):
     module = _LAZY.get(name)
-    if module is None:
-        raise AttributeError(name)
     import importlib
 
-    value = getattr(importlib.import_module("." + module, __name__), name)
+    if name not in _LAZY:
+        raise AttributeError(name)
+    if module is None:  # a submodule
+        value = importlib.import_module("." + name, __name__)
+    else:
+        value = getattr(importlib.import_module("." + module, __name__), name)
     globals()[name] = value
     return value

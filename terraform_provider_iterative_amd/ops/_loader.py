@@ -69,6 +69,11 @@ class HipLib:
             "tpi_restore": (i32, [vp, vp, i32, u64, vp, vp, i32, u64, c.POINTER(u64),
                                   c.POINTER(i64), vp]),
             "tpi_sync": (i32, [vp, vp, i32, u64, vp, vp, i32, u64, c.POINTER(u64), vp]),
+            "tpi_save_z": (i32, [vp, vp, i32, u64, vp, vp, vp, u64, c.POINTER(u64), vp]),
+            "tpi_restore_z": (i32, [vp, vp, i32, u64, vp, vp, vp, u64, c.POINTER(u64),
+                                    c.POINTER(i64), vp]),
+            "tpi_tpz_encode_device": (i32, [vp, u64, u64, vp, vp, vp, u64]),
+            "tpi_tpz_decode_device": (i32, [vp, vp, u64, u64, vp, u64]),
             "tpi_stream_hash": (i32, [vp, i32, u64, u64, u64, vp, u64]),
             "tpi_crc32c_tiles": (i32, [vp, u64, u64, vp, u64]),
             "tpi_shard_hash": (i32, [vp, u64, u64, u64, vp, u64]),

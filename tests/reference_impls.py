@@ -39,3 +39,38 @@ def shard_hash_py(data: bytes, shard_bytes: int = 1 << 20, seed: int = 0):
             digests.append(xxhash.xxh64(msg, seed=seed).intdigest())
         out.append(xxhash.xxh64(struct.pack("<256Q", *digests), seed=seed).intdigest())
     return np.array(out, dtype=np.uint64)
+
+
+def _a16(x: int) -> int:
+    return (x + 15) & ~15
+
+
+def tpz_decode_tile_py(blob: bytes, length: int) -> np.ndarray:
+    """Independent numpy decoder of one TPZ1 tile blob (spec: csrc/common/tpz.h)."""
+    n = length // 4
+    ngroups = (n + 31) // 32
+    out = np.zeros(length, np.uint8)
+    off = 96
+    for p in range(4):
+        k, m, _, _, nesc = struct.unpack_from("<BBBBI", blob, 24 * p)
+        dictionary = np.frombuffer(blob, np.uint8, 16, 24 * p + 8)
+        if k == 8:  # raw plane
+            out[p::4] = np.frombuffer(blob, np.uint8, n, off)
+            off += ngroups * 32
+            continue
+        if k == 0:  # constant plane
+            out[p::4] = dictionary[0]
+            continue
+        esc_code = (1 << k) - 1
+        words = np.frombuffer(blob, np.uint32, ngroups * k, off)
+        bits = np.unpackbits(words.view(np.uint8), bitorder="little")
+        codes = bits[:ngroups * 32 * k].reshape(-1, k).astype(np.uint32)
+        codes = (codes << np.arange(k, dtype=np.uint32)).sum(axis=1)[:n]
+        escapes = np.frombuffer(blob, np.uint8, nesc, off + _a16(ngroups * 4 * k))
+        vals = dictionary[np.minimum(codes, m - 1)].copy()
+        is_esc = codes == esc_code
+        assert int(is_esc.sum()) == nesc
+        vals[is_esc] = escapes
+        out[p::4] = vals
+        off += _a16(ngroups * 4 * k) + _a16(nesc)
+    return out

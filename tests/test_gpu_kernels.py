@@ -163,3 +163,87 @@ def test_checkpointer_device_roundtrip(mode, tmp_path):
         torch.cuda.synchronize()
     for k in ref:
         assert torch.equal(dst[k], ref[k]), k
+
+
+def _codec_inputs():
+    g = torch.Generator().manual_seed(7)
+    parts = [
+        torch.randn(1 << 19, generator=g).mul(0.02).to(torch.bfloat16).view(torch.uint8),
+        torch.randn(1 << 18, generator=g).mul(1e-3).view(torch.uint8),
+        torch.randn(1 << 18, generator=g).mul(1e-3).pow(2).view(torch.uint8),
+        torch.zeros(200000, dtype=torch.uint8),
+        torch.randint(0, 256, (300016,), dtype=torch.uint8, generator=g),
+        torch.randint(0, 5, (100000,), dtype=torch.int32, generator=g).view(torch.uint8),
+    ]
+    raw = torch.cat([p.reshape(-1) for p in parts])
+    return raw[:raw.numel() // 16 * 16 - 48]  # short final tile, length % 128 != 0
+
+
+@pytest.mark.parametrize("tile", [4096, 65536, 1 << 20])
+def test_tpz_device_encoder_is_bit_identical_to_host(tile):
+    from terraform_provider_iterative_amd.ops import codec
+
+    raw = _codec_inputs()
+    host_blobs, host_sizes = codec.encode(raw.numpy(), tile)
+    dev_blobs, dev_sizes = codec.encode(raw.cuda(), tile)
+    assert dev_sizes.cpu().numpy().astype(np.uint32).tolist() == host_sizes.tolist()
+    assert np.array_equal(dev_blobs.cpu().numpy(), host_blobs)
+    # device decode of host blobs (and so of its own) restores the raw stream
+    out, _ = codec.decode(torch.from_numpy(host_blobs).cuda(), host_sizes, raw.numel(), tile)
+    assert torch.equal(out.cpu(), raw)
+
+
+def test_tpz_device_decode_corrupt_blob_fails_crc():
+    from terraform_provider_iterative_amd.ops import codec
+
+    raw = _codec_inputs()[:1 << 20]
+    blobs, sizes = codec.encode(raw.numpy(), 65536)
+    bad = blobs.copy()
+    bad[int(codec.offsets(sizes)[3])] = 9  # invalid plane mode in tile 3
+    out, _ = codec.decode(torch.from_numpy(bad).cuda(), sizes, raw.numel(), 65536)
+    got = crc_array(ops.crc32c_tiles(out, tile_bytes=65536)).tolist()
+    want = ops.crc32c_tiles(raw.numpy(), tile_bytes=65536).tolist()
+    assert [i for i, (a, b) in enumerate(zip(got, want)) if a != b] == [3]
+
+
+def test_checkpointer_codec_device_roundtrip(tmp_path):
+    from terraform_provider_iterative_amd.checkpoint import Checkpointer
+
+    g = torch.Generator().manual_seed(3)
+    src = {
+        "w": torch.randn(3000, 1000, generator=g).mul(0.02).to(torch.bfloat16).cuda(),
+        "m": torch.randn(1500, 1000, generator=g).mul(1e-3).cuda(),
+        "v": torch.randn(1500, 1000, generator=g).mul(1e-3).pow(2).cuda(),
+        "sliced": torch.randn(64, 96, generator=g).cuda()[:, 5:77:3],
+        "odd": torch.randint(0, 255, (100001,), dtype=torch.uint8, generator=g).cuda(),
+    }
+    ref = {k: v.clone() for k, v in src.items()}
+    with Checkpointer(src, tile_bytes=1 << 20, chunk_bytes=4 << 20, nbuf=2, codec="tpz1") as ck:
+        res = ck.save({"step": 9})
+        assert res.wire_bytes < 0.9 * res.bytes
+        # host view of the region = host encoding of a host pack of the same tensors
+        hplan = PackPlan.from_tensors({k: v.cpu() for k, v in ref.items()}, tile_bytes=1 << 20)
+        hs, hc = pack(hplan)
+        assert ck.crcs.tolist() == hc.tolist()
+        from terraform_provider_iterative_amd.ops import codec
+
+        hb, hsz = codec.encode(hs, 1 << 20)
+        assert ck.csizes.tolist() == hsz.tolist()
+        assert np.array_equal(ck.region.array(ck.stream_offset, len(hb)), hb)
+        for v in src.values():
+            v.zero_()
+        out = ck.restore()
+        torch.cuda.synchronize()
+        assert out.bad_tiles == 0 and out.wire_bytes == res.wire_bytes
+        assert all(torch.equal(src[k], ref[k]) for k in ref)
+        path = ck.persist(str(tmp_path / "z.tpi"))
+        # corrupt one escape/code byte in the region -> strict restore refuses
+        ck.region.array(ck.stream_offset + 5000, 1)[0] ^= 0x5A
+        with pytest.raises(Exception, match="corrupt"):
+            ck.restore()
+    dst = {k: torch.zeros_like(v) for k, v in ref.items()}
+    dst["sliced"] = torch.zeros(64, 96, device="cuda")[:, 5:77:3]
+    with Checkpointer(dst, tile_bytes=1 << 20, chunk_bytes=4 << 20) as ck2:  # codec-agnostic
+        ck2.load(path)
+        torch.cuda.synchronize()
+    assert all(torch.equal(dst[k], ref[k]) for k in ref)
