@@ -306,8 +306,9 @@ class NodeTask(Task):
         spec = self._spec_json()
         spec_path = os.path.join(self.sup_dir, "spec.json")
         _write_json(spec_path, spec)
-        binary = _build.SUPERVISOR
-        if not os.path.exists(binary):
+        # TPI_SUPERVISOR_BIN: an alternative build (e.g. the ASan/UBSan one of the tests)
+        binary = os.environ.get("TPI_SUPERVISOR_BIN") or _build.SUPERVISOR
+        if binary == _build.SUPERVISOR and not os.path.exists(binary):
             _build.build_supervisor()
         logfile = open(os.path.join(self.sup_dir, "supervisor.log"), "ab")
         try:

@@ -1,0 +1,75 @@
+"""ASan/UBSan builds of the host C++: the native data-plane sources plus a
+self-checking harness (tests/native/sanitize_main.cpp), and the rank supervisor driving a
+real two-rank task through the node backend."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+from terraform_provider_iterative_amd import _build
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SAN = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer",
+       "-g", "-O1"]
+ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:halt_on_error=1",
+           UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+
+pytestmark = pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+
+
+def _compile(out, sources, extra=()):
+    cmd = ["g++", "-std=c++17", "-msse4.2", "-pthread", *SAN, *extra, *sources, "-o", out]
+    res = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if res.returncode != 0 and "sanitizer" in res.stdout and "cannot find" in res.stdout:
+        pytest.skip("sanitizer runtime not installed")
+    assert res.returncode == 0, res.stdout
+
+
+def test_native_sources_under_asan_ubsan(tmp_path):
+    exe = str(tmp_path / "sanitize_main")
+    srcs = [os.path.join(ROOT, "csrc", "native", f) for f in
+            ("filter.cpp", "transfer.cpp", "hostops.cpp")]
+    _compile(exe, srcs + [os.path.join(ROOT, "tests", "native", "sanitize_main.cpp")])
+    scratch = tmp_path / "scratch"
+    scratch.mkdir()
+    res = subprocess.run([exe, str(scratch)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                         text=True, env=ENV, timeout=300)
+    assert res.returncode == 0, res.stdout[-4000:]
+    assert "sanitize harness ok" in res.stdout
+
+
+def test_supervisor_under_asan_ubsan(tmp_path, monkeypatch):
+    exe = str(tmp_path / "tpi-supervisor-asan")
+    _compile(exe, [os.path.join(ROOT, "csrc", "supervisor", "supervisor.cpp")])
+    monkeypatch.setenv("TPI_SUPERVISOR_BIN", exe)
+    monkeypatch.setenv("TPI_MI355X_GPUS", "0,1,2,3")
+    monkeypatch.setenv("ASAN_OPTIONS", ENV["ASAN_OPTIONS"])
+    from terraform_provider_iterative_amd import backends
+    from terraform_provider_iterative_amd.models.cloud import Cloud, Credentials, NodeCredentials
+    from terraform_provider_iterative_amd.models.values import Environment, Size, Task
+    from terraform_provider_iterative_amd.utils.identifier import new_deterministic_identifier
+
+    state = tmp_path / "state"
+    cloud = Cloud(provider="mi355x",
+                  credentials=Credentials(node=NodeCredentials(state_root=str(state))))
+    spec = Task(size=Size(machine="m+mi355x"), parallelism=2,
+                environment=Environment(script="#!/bin/sh\necho rank $RANK of $WORLD_SIZE\n"
+                                               "seq 1 2000\n", timeout=60))
+    task = backends.new(cloud, new_deterministic_identifier("asan-sup"), spec)
+    task.create()
+    try:
+        status = task.wait(60)
+        assert status["succeeded"] == 2, status
+        logs = task.logs()
+        assert len(logs) == 2 and all("rank" in log and "2000" in log for log in logs)
+        reports = []
+        for dirpath, _, files in os.walk(str(state)):
+            reports += [os.path.join(dirpath, f) for f in files if f == "supervisor.log"]
+        assert reports
+        for path in reports:
+            text = open(path, errors="replace").read()
+            for marker in ("AddressSanitizer", "LeakSanitizer", "runtime error"):
+                assert marker not in text, text[-2000:]
+    finally:
+        task.delete()
