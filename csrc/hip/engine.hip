@@ -7,9 +7,13 @@
 //   so packing chunk k+1 overlaps the PCIe transfer of chunk k; the copy engine never idles.
 // Save (TPI_MODE_DIRECT): one pack kernel streams straight into the host-mapped destination.
 // Restore mirrors both (H2D on the copy stream, unpack+verify on the compute stream).
+// Save/restore with the TPZ1 codec (tpi_save_z / tpi_restore_z): pack+CRC into a raw scratch
+// chunk, byte-plane encode into staging[b], D2H only the compressed bytes (and the inverse).
+// Incremental sync (tpi_sync): per-tile digests from the tensors, pack + D2H of dirty tiles.
 #include <errno.h>
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include <stdio.h>
 #include <string.h>
 #include <sys/mman.h>
@@ -61,6 +65,13 @@ extern "C" hipError_t tpi_launch_tpz_decode(const void* comp, const uint64_t* co
 namespace {
 
 thread_local std::string g_err;
+
+// roctx range around each pipeline call: `rocprofv3 --marker-trace` shows save/restore/sync
+// phases next to the kernels and copies they issued (no cost when no tool is attached).
+struct Range {
+  explicit Range(const char* name) { roctxRangePushA(name); }
+  ~Range() { roctxRangePop(); }
+};
 
 int fail(const std::string& what) {
   g_err = what;
@@ -298,6 +309,7 @@ extern "C" {
 
 int tpi_save(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* host_dst,
              uint32_t* crcs_out, int mode, uint64_t wait_stream, tpi_stats* stats) {
+  Range range("tpi_save");
   std::lock_guard<std::mutex> lk(e->mu);
   auto t0 = std::chrono::steady_clock::now();
   if (prepare(e, segs, n, total)) return -1;
@@ -348,6 +360,7 @@ int tpi_save(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* ho
 int tpi_restore(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, const void* host_src,
                 const uint32_t* crcs, int mode, uint64_t signal_stream, uint64_t* bad_tiles,
                 int64_t* first_bad, tpi_stats* stats) {
+  Range range("tpi_restore");
   std::lock_guard<std::mutex> lk(e->mu);
   auto t0 = std::chrono::steady_clock::now();
   if (prepare(e, segs, n, total)) return -1;
@@ -412,6 +425,7 @@ int tpi_restore(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, const
 int tpi_sync(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* host_dst,
              uint32_t* crcs_inout, int full, uint64_t wait_stream, uint64_t* dirty_tiles,
              tpi_stats* stats) {
+  Range range("tpi_sync");
   std::lock_guard<std::mutex> lk(e->mu);
   auto t0 = std::chrono::steady_clock::now();
   if (prepare(e, segs, n, total)) return -1;
@@ -526,6 +540,7 @@ extern "C" {
 int tpi_save_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* host_dst,
                uint32_t* crcs_out, uint32_t* csizes_out, uint64_t wait_stream,
                uint64_t* stream_bytes, tpi_stats* stats) {
+  Range range("tpi_save_z");
   std::lock_guard<std::mutex> lk(e->mu);
   auto t0 = std::chrono::steady_clock::now();
   if (prepare(e, segs, n, total)) return -1;
@@ -582,6 +597,7 @@ int tpi_restore_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total,
                   const void* host_src, const uint32_t* crcs, const uint32_t* csizes,
                   uint64_t signal_stream, uint64_t* bad_tiles, int64_t* first_bad,
                   tpi_stats* stats) {
+  Range range("tpi_restore_z");
   std::lock_guard<std::mutex> lk(e->mu);
   auto t0 = std::chrono::steady_clock::now();
   if (prepare(e, segs, n, total)) return -1;

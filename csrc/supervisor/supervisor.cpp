@@ -164,6 +164,7 @@ struct Rank {
   bool killed = false;
   int exit_code = -1, exit_signal = 0;
   double started = 0;
+  bool first_output = false;  // phase journal: first line of this incarnation seen
 };
 
 struct Spec {
@@ -375,6 +376,7 @@ class Supervisor {
     add("TPI_TASK_IDENTIFIER", s_.task_id);
     add("TPI_TASK_DIRECTORY", s_.task_dir);
     add("TPI_RESTART_COUNT", std::to_string(r.restarts));
+    add("TPI_EVENTS_FILE", s_.events_path);  // ranks journal checkpoint phases here
     if (s_.deadline > 0) {
       add("TPI_DEADLINE", std::to_string((long long)s_.deadline));
       add("TPI_REMAINING_RUN_TIME", std::to_string((long long)(s_.deadline - now())));
@@ -472,6 +474,7 @@ class Supervisor {
     r.fd = p[0];
     r.state = Rank::RUNNING;
     r.started = now();
+    r.first_output = false;
     event("rank-start", {"rank " + std::to_string(r.index), "pid " + std::to_string(pid),
                          "machine " + r.uuid, "gpus " + (r.gpus.empty() ? "-" : r.gpus),
                          "restart " + std::to_string(r.restarts)});
@@ -479,7 +482,14 @@ class Supervisor {
 
   void emit_line(Rank& r, const std::string& line) {
     if (r.logfd < 0) return;
-    write_all(r.logfd, utc_stamp(now()) + " " + line + "\n");
+    const double t = now();
+    write_all(r.logfd, utc_stamp(t) + " " + line + "\n");
+    if (!r.first_output) {  // phase journal: start -> first log line of this incarnation
+      r.first_output = true;
+      char ms[32];
+      snprintf(ms, sizeof(ms), "%.1f ms", (t - r.started) * 1e3);
+      event("rank-first-output", {"rank " + std::to_string(r.index), ms});
+    }
   }
 
   void pump(Rank& r) {

@@ -23,6 +23,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(ROOT, "csrc")
 LIB = os.path.join(PKG, "_lib")
+ROCM_LIB = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0] or "gfx950"
 
 NATIVE_SO = os.path.join(LIB, "_tpi_native" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
@@ -97,7 +98,8 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
         tmp = _atomic_output(HIP_SO)
         _run([hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
               "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics",
-              *srcs, "-L" + tl, "-Wl,-rpath," + tl, "-o", tmp], verbose)
+              *srcs, "-L" + tl, "-Wl,-rpath," + tl, "-L" + ROCM_LIB, "-Wl,-rpath," + ROCM_LIB,
+              "-lrocprofiler-sdk-roctx", "-o", tmp], verbose)
         os.replace(tmp, HIP_SO)
     return HIP_SO
 

@@ -9,6 +9,7 @@ calls :func:`resume` to restore them.
 """
 from __future__ import annotations
 
+import json
 import logging
 import os
 import signal
@@ -45,6 +46,31 @@ def preempted() -> bool:
     return _fired.is_set()
 
 
+def journal(code: str, *description: str) -> None:
+    """Append a phase event to the task's event journal (``TPI_EVENTS_FILE``, set by the
+    supervisor), shown in ``iterative_task.events`` next to placement/start/exit events.
+    One ``O_APPEND`` write per line, so concurrent ranks do not interleave."""
+    path = os.environ.get("TPI_EVENTS_FILE")
+    if not path:
+        return
+    rank = os.environ.get("RANK", "0")
+    line = json.dumps({"time": time.time(), "code": code,
+                       "description": ["rank " + rank] + list(description)}) + "\n"
+    try:
+        fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_APPEND, 0o644)
+        try:
+            os.write(fd, line.encode())
+        finally:
+            os.close(fd)
+    except OSError:
+        pass
+
+
+def _describe(res) -> List[str]:
+    return ["%d bytes" % res.bytes, "%d on the wire" % res.wire_bytes,
+            "%.3f s" % res.seconds, "%.1f GB/s" % res.gbps]
+
+
 def checkpoint_all(metadata: Optional[Dict] = None) -> List[float]:
     """Save every registered checkpointer; returns per-checkpointer GB/s."""
     meta = dict(metadata or {})
@@ -56,9 +82,12 @@ def checkpoint_all(metadata: Optional[Dict] = None) -> List[float]:
     for ck in _registered:
         res = ck.save(meta)
         rates.append(res.gbps)
+        journal("checkpoint-saved", *_describe(res))
         path = _persist_paths.get(id(ck))
         if path:
+            t0 = time.perf_counter()
             ck.persist(path)
+            journal("checkpoint-persisted", path, "%.3f s" % (time.perf_counter() - t0))
     return rates
 
 
@@ -66,6 +95,7 @@ def _handler(signum, frame):  # pragma: no cover - exercised in subprocess tests
     if _fired.is_set():
         return
     _fired.set()
+    journal("preempt-signal", "signal %d" % signum)
     t0 = time.perf_counter()
     try:
         rates = checkpoint_all({"reason": "preempted", "signal": signum})
@@ -94,11 +124,13 @@ def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None) -> Op
     try:
         header = checkpointer.header()
         if header.get("complete"):
-            checkpointer.restore()
+            res = checkpointer.restore()
+            journal("checkpoint-restored", "host region", *_describe(res))
             return header.get("metadata", {})
     except CheckpointError:
         pass
     if persist_path and os.path.exists(persist_path):
-        checkpointer.load(persist_path)
+        res = checkpointer.load(persist_path)
+        journal("checkpoint-restored", persist_path, *_describe(res))
         return checkpointer.header().get("metadata", {})
     return None

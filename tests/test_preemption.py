@@ -82,4 +82,12 @@ def test_preempt_checkpoint_respawn_resume(cloud, how):
     assert "final 40 40" in logs[1]
     codes = [e.code for e in task.events()]
     assert "rank-preempted" in codes and "respawn" in codes
+    # phase journal: start -> first output -> preempt -> saved -> respawn -> restored
+    for phase in ("rank-start", "rank-first-output", "preempt-signal", "checkpoint-saved",
+                  "checkpoint-restored"):
+        assert phase in codes, (phase, codes)
+    assert codes.index("checkpoint-saved") < codes.index("respawn") < \
+        codes.index("checkpoint-restored")
+    saved = [e for e in task.events() if e.code == "checkpoint-saved"][0]
+    assert saved.description[0] == "rank 0" and saved.description[-1].endswith("GB/s")
     task.delete()
