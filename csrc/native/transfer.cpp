@@ -280,9 +280,26 @@ uint64_t pool_over(size_t n, int threads, F&& f) {
   return done;
 }
 
+// Large pieces are cut into <= kSplit sub-pieces so one big file still spreads over the
+// whole thread pool (page-cache -> pinned memcpy is per-thread bound at a few GB/s).
+constexpr uint64_t kSplit = 8ull << 20;
+
+std::vector<ReadPiece> split_pieces(const std::vector<ReadPiece>& pieces) {
+  std::vector<ReadPiece> out;
+  out.reserve(pieces.size());
+  for (const ReadPiece& p : pieces) {
+    for (uint64_t o = 0; o < p.len || (o == 0 && p.len == 0); o += kSplit) {
+      out.push_back({p.path, p.file_off + o, std::min(kSplit, p.len - o), p.dst_off + o});
+      if (p.len == 0) break;
+    }
+  }
+  return out;
+}
+
 }  // namespace
 
-uint64_t read_pieces(const std::vector<ReadPiece>& pieces, uint8_t* dst, int threads) {
+uint64_t read_pieces(const std::vector<ReadPiece>& in, uint8_t* dst, int threads) {
+  const std::vector<ReadPiece> pieces = split_pieces(in);
   return pool_over(pieces.size(), threads, [&](size_t i, std::string& err) -> uint64_t {
     const ReadPiece& p = pieces[i];
     int fd = open(p.path.c_str(), O_RDONLY | O_CLOEXEC);
@@ -306,7 +323,8 @@ uint64_t read_pieces(const std::vector<ReadPiece>& pieces, uint8_t* dst, int thr
   });
 }
 
-uint64_t write_pieces(const std::vector<ReadPiece>& pieces, const uint8_t* src, int threads) {
+uint64_t write_pieces(const std::vector<ReadPiece>& in, const uint8_t* src, int threads) {
+  const std::vector<ReadPiece> pieces = split_pieces(in);
   return pool_over(pieces.size(), threads, [&](size_t i, std::string& err) -> uint64_t {
     const ReadPiece& p = pieces[i];
     int fd = open(p.path.c_str(), O_WRONLY | O_CREAT | O_CLOEXEC, 0644);

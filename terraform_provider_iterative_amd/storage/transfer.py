@@ -74,7 +74,7 @@ def _local_path(remote: str) -> str:
 
 
 def transfer(source: str, destination: str, exclude: Optional[Iterable[str]] = None,
-             rules: Optional[List[str]] = None, threads: int = 8) -> Dict:
+             rules: Optional[List[str]] = None, threads: int = 0) -> Dict:
     """Copy ``source`` -> ``destination`` with filter rules (``storage.go:123-159``).
 
     ``rules`` (already in rclone form) overrides the default-exclude construction, which is
@@ -86,7 +86,8 @@ def transfer(source: str, destination: str, exclude: Optional[Iterable[str]] = N
     entries = native().walk(src, flt)
     files = [e for e in entries if not e[4]]
     log.info("Transferring %s (%d files)...", human_size(sum(e[1] for e in files)), len(files))
-    stats = native().copy_dir(src, dst, flt, threads)
+    threads = threads or min(16, os.cpu_count() or 1)
+    stats = native().copy_dir(src, dst, flt, threads, 64 << 20)
     log.debug("transfer %s -> %s: %s", src, dst, stats)
     return stats
 
