@@ -108,6 +108,9 @@ def load_into(root: str, files: List[FileEntry], total: int, buffer,
             read_s += time.perf_counter() - t
         return {"seconds": time.perf_counter() - t0, "read_s": read_s, "bytes": total}
     stream = torch.cuda.Stream(buffer.device)
+    # the copies must land after whatever the caller queued on ``buffer`` (its allocation /
+    # fill on the current stream)
+    stream.wait_stream(torch.cuda.current_stream(buffer.device))
     hosts = [torch.empty(min(chunk_bytes, max(total, 1)), dtype=torch.uint8, pin_memory=True)
              for _ in range(2)]
     events = [None, None]
@@ -165,7 +168,10 @@ def stage_workdir(root: Optional[str] = None, device=None, exclude: Optional[Lis
         dist.broadcast_object_list(meta, src=src, group=group)
     files = [FileEntry(*m) for m in meta[0]]
     total = int(meta[1])
-    buffer = torch.zeros(total, dtype=torch.uint8, device=device)
+    # on the device the source rank's load writes every byte (gaps included) and receivers
+    # get the broadcast; the host path reads straight into the buffer, so gaps start zeroed
+    alloc = torch.empty if torch.device(device).type == "cuda" else torch.zeros
+    buffer = alloc(total, dtype=torch.uint8, device=device)
     stats: Dict[str, float] = {"bytes": total, "files": len(files)}
     if rank == src:
         load = load_into(root, files, total, buffer, chunk_bytes, threads)
