@@ -86,8 +86,9 @@ def transfer(source: str, destination: str, exclude: Optional[Iterable[str]] = N
     entries = native().walk(src, flt)
     files = [e for e in entries if not e[4]]
     log.info("Transferring %s (%d files)...", human_size(sum(e[1] for e in files)), len(files))
-    threads = threads or min(16, os.cpu_count() or 1)
-    stats = native().copy_dir(src, dst, flt, threads, 64 << 20)
+    # 8 threads x 256 MiB copy_file_range pieces measured best on the MI355X box (23 GB/s for
+    # a 10 GB workdir; 16 x 64 MiB: 15.6 GB/s, inode-lock contention within files)
+    stats = native().copy_dir(src, dst, flt, threads or 8, 256 << 20)
     log.debug("transfer %s -> %s: %s", src, dst, stats)
     return stats
 
