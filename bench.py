@@ -117,10 +117,17 @@ def main(argv=None):
         print("bench: WORLD_SIZE=%d but --gpus=%d" % (world, args.gpus), file=sys.stderr)
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (MI355X)")
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    # TPI_BENCH_BACKEND=gloo rehearses the multi-rank flow on a box with fewer GPUs than ranks
+    # (ranks then share devices); the real runs use RCCL ("nccl"), one rank per GPU.
+    backend = os.environ.get("TPI_BENCH_BACKEND", "nccl")
+    index = local_rank % torch.cuda.device_count()
+    torch.cuda.set_device(index)
+    device = torch.device("cuda", index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
 
     def barrier():
         if world > 1:
@@ -130,7 +137,8 @@ def main(argv=None):
     def allmax(value: float) -> float:
         if world == 1:
             return value
-        t = torch.tensor([value], dtype=torch.float64, device=device)
+        t = torch.tensor([value], dtype=torch.float64,
+                         device=device if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 

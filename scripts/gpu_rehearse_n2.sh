@@ -1,0 +1,6 @@
+# Multi-rank rehearsal of bench.py on a 1-GPU box: 2 ranks share cuda:0, gloo for the
+# control collectives (RCCL cannot put two ranks on one GPU).  Not a performance number.
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+TPI_BENCH_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29633 bench.py --gpus 2 --total-gb 8 --steps 2 --warmup 1 --broadcast-gb 0 > gpurun_out/rehearse_n2.log 2>&1 && echo N2_OK
