@@ -109,12 +109,11 @@ static inline uint32_t tpz_word(const uint8_t* t, uint64_t len, uint64_t w) {
   return x;
 }
 
-// Encode one tile (`len` % 16 == 0, len > 0) into `out` (>= tpz_bound(len) bytes).
-// Returns the blob size.
-static inline uint64_t tpz_encode_tile(const uint8_t* t, uint64_t len, uint8_t* out) {
+// Pass 1 (= k_tpz_analyze): dictionaries, exact hit counts and the mode of every plane.
+// Fills hdr[4] and returns the blob size.
+static inline uint64_t tpz_analyze_tile(const uint8_t* t, uint64_t len, tpz_plane hdr[4]) {
   const uint64_t n = len / 4, ngroups = tpz_ngroups(len);
-  tpz_plane hdr[4];
-  memset(hdr, 0, sizeof(hdr));
+  memset(hdr, 0, 4 * sizeof(tpz_plane));
   uint8_t rank[4][256];
   {
     uint32_t hist[4][256];
@@ -131,13 +130,23 @@ static inline uint64_t tpz_encode_tile(const uint8_t* t, uint64_t len, uint8_t* 
       for (int r = 0; r < hdr[p].m; ++r) rank[p][hdr[p].dict[r]] = (uint8_t)r;
     }
   }
-  static const int thr[4] = {1, 3, 7, 15};
+  // hits[p][r] = bytes of plane p with rank r (r = 15: not in the dictionary)
+  uint64_t cnt[4][16];
+  memset(cnt, 0, sizeof(cnt));
+  for (uint64_t i = 0; i < n; ++i) {
+    uint32_t w;
+    memcpy(&w, t + 4 * i, 4);
+    cnt[0][rank[0][w & 0xff]]++;
+    cnt[1][rank[1][(w >> 8) & 0xff]]++;
+    cnt[2][rank[2][(w >> 16) & 0xff]]++;
+    cnt[3][rank[3][w >> 24]]++;
+  }
+  uint64_t size = TPZ_HDR;
   for (int p = 0; p < 4; ++p) {
     uint64_t hits[4] = {0, 0, 0, 0};
-    for (uint64_t i = 0; i < n; ++i) {
-      const int r = rank[p][t[4 * i + p]];
-      for (int q = 0; q < 4; ++q) hits[q] += r < thr[q];
-    }
+    static const int thr[4] = {1, 3, 7, 15};
+    for (int q = 0; q < 4; ++q)
+      for (int r = 0; r < thr[q]; ++r) hits[q] += cnt[p][r];
     uint64_t nesc = 0;
     const int k = tpz_choose(n, ngroups, hdr[p].m, hits, &nesc);
     hdr[p].k = (uint8_t)k;
@@ -150,45 +159,70 @@ static inline uint64_t tpz_encode_tile(const uint8_t* t, uint64_t len, uint8_t* 
       for (int r = used; r < 16; ++r) hdr[p].dict[r] = 0;
       hdr[p].m = (uint8_t)used;
     }
+    size += tpz_plane_bytes(k, ngroups, nesc);
   }
+  return size;
+}
+
+// Pass 2 (= k_tpz_encode): write the blob described by `hdr` (>= its size bytes at `out`).
+static inline uint64_t tpz_emit_tile(const uint8_t* t, uint64_t len, const tpz_plane hdr[4],
+                                     uint8_t* out) {
+  const uint64_t n = len / 4, ngroups = tpz_ngroups(len);
   memcpy(out, hdr, TPZ_HDR);
   uint64_t off = TPZ_HDR;
   for (int p = 0; p < 4; ++p) {
     const int k = hdr[p].k;
     uint8_t* sec = out + off;
     const uint64_t bytes = tpz_plane_bytes(k, ngroups, hdr[p].nesc);
-    memset(sec, 0, bytes);
     if (k == TPZ_RAW) {
       for (uint64_t i = 0; i < n; ++i) sec[i] = t[4 * i + p];
+      memset(sec + n, 0, bytes - n);
     } else if (k > 0) {
+      memset(sec, 0, bytes);
+      uint8_t rank[256];
+      memset(rank, 15, sizeof(rank));
+      for (int r = 0; r < hdr[p].m; ++r) rank[hdr[p].dict[r]] = (uint8_t)r;
       const uint32_t E = (1u << k) - 1;
       uint8_t* esc = sec + tpz_align16(ngroups * 4 * (uint64_t)k);
       uint64_t ne = 0;
       for (uint64_t g = 0; g < ngroups; ++g) {
-        uint32_t words[4] = {0, 0, 0, 0};
+        uint64_t acc = 0;  // k <= 4: 32 codes fit in 128 bits, emitted 64 bits at a time
+        int nbits = 0;
+        uint8_t* dst = sec + g * 4 * k;
         for (int j = 0; j < 32; ++j) {
           const uint64_t i = g * 32 + j;
           uint32_t c = 0;
           if (i < n) {
             const uint8_t v = t[4 * i + p];
-            const uint32_t r = rank[p][v];
-            if (r < E && r < hdr[p].m) {
-              c = r;
-            } else {
+            c = rank[v];
+            if (c >= E) {
               c = E;
               esc[ne++] = v;
             }
           }
-          const int bit = j * k;
-          words[bit >> 5] |= c << (bit & 31);
-          if ((bit & 31) + k > 32) words[(bit >> 5) + 1] |= c >> (32 - (bit & 31));
+          acc |= (uint64_t)c << nbits;
+          nbits += k;
+          if (nbits >= 64) {
+            memcpy(dst, &acc, 8);
+            dst += 8;
+            nbits -= 64;
+            acc = nbits ? (uint64_t)c >> (k - nbits) : 0;
+          }
         }
-        memcpy(sec + g * 4 * k, words, 4 * k);
+        if (nbits) memcpy(dst, &acc, (size_t)(nbits + 7) / 8);
       }
     }
     off += bytes;
   }
   return off;
+}
+
+// Encode one tile (`len` % 16 == 0, len > 0) into `out` (>= tpz_bound(len) bytes).
+// Returns the blob size.
+static inline uint64_t tpz_encode_tile(const uint8_t* t, uint64_t len, uint8_t* out) {
+  tpz_plane hdr[4];
+  tpz_analyze_tile(t, len, hdr);
+  return tpz_emit_tile(t, len, hdr, out);
 }
 
 // Decode a blob of `avail` bytes into `len` tile bytes.  Returns the blob size consumed, or

@@ -210,21 +210,21 @@ uint64_t unpack(const tpi_seg* segs, int n, uint64_t total, const void* stream, 
 
 uint64_t tpz_encode_stream(const void* src, uint64_t total, uint64_t tile, void* dst,
                            uint32_t* csizes, int threads) {
-  // Tiles encode independently into worst-case slots, then slide down to be contiguous.
+  // Same two passes as the GPU: headers + sizes, then blobs written at their offsets.
   const uint64_t ntiles = (total + tile - 1) / tile;
-  std::vector<uint8_t> slots(ntiles * tpz_bound(tile));
   const uint8_t* s = (const uint8_t*)src;
+  std::vector<tpz_plane> hdr(ntiles * 4);
   parallel_for(ntiles, threads, [&](uint64_t t) {
     const uint64_t lo = t * tile;
-    csizes[t] = (uint32_t)tpz_encode_tile(s + lo, std::min(tile, total - lo),
-                                          slots.data() + t * tpz_bound(tile));
+    csizes[t] = (uint32_t)tpz_analyze_tile(s + lo, std::min(tile, total - lo), &hdr[t * 4]);
   });
-  uint64_t off = 0;
-  for (uint64_t t = 0; t < ntiles; ++t) {
-    memcpy((uint8_t*)dst + off, slots.data() + t * tpz_bound(tile), csizes[t]);
-    off += csizes[t];
-  }
-  return off;
+  std::vector<uint64_t> off(ntiles + 1, 0);
+  for (uint64_t t = 0; t < ntiles; ++t) off[t + 1] = off[t] + csizes[t];
+  parallel_for(ntiles, threads, [&](uint64_t t) {
+    const uint64_t lo = t * tile;
+    tpz_emit_tile(s + lo, std::min(tile, total - lo), &hdr[t * 4], (uint8_t*)dst + off[t]);
+  });
+  return off[ntiles];
 }
 
 int64_t tpz_decode_stream(const void* src, const uint32_t* csizes, uint64_t total, uint64_t tile,
