@@ -41,7 +41,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from terraform_provider_iterative_amd.checkpoint import Checkpointer, preemption
+    from terraform_provider_iterative_amd.checkpoint import TrainingState
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -83,22 +83,16 @@ def main():
     model(x).float().pow(2).mean().backward()
     opt.step()
     opt.zero_grad(set_to_none=False)
-    tensors = {"step": step_t}
-    for name, t in (model.module if world > 1 else model).state_dict().items():
-        tensors["model." + name] = t
-    params = [p for group in opt.param_groups for p in group["params"]]
-    for i, param in enumerate(params):
-        for k, v in opt.state[param].items():
-            if torch.is_tensor(v) and v.device == device:
-                tensors["opt.%d.%s" % (i, k)] = v
     data_dir = os.environ.get("TPI_DATA_DIRECTORY", ".")
     spill = os.path.join(data_dir, ".ckpt-rank%d" % rank)
-    ck = Checkpointer(tensors, path=spill)
-    meta = preemption.resume(ck)
+    # model + optimizer device state by reference; CPU-side Adam step counters ride in the
+    # checkpoint header (bias correction needs them after a resume)
+    state = TrainingState(model, opt, extra={"step": step_t}, path=spill)
+    ck = state.checkpointer
+    meta = state.resume()
     start = int(step_t.item())
     log("resumed from step %d" % start if meta else "fresh start")
-    preemption.register(ck)
-    preemption.install()
+    state.install()
 
     gen = torch.Generator(device=device).manual_seed(rank + 7)
     t_steps = []
@@ -118,7 +112,7 @@ def main():
             log("step %d loss %.5f" % (step + 1, loss.item()))
         if args.sleep:
             time.sleep(args.sleep)
-    res = ck.save({"step": int(step_t.item()), "final": True})
+    res = state.save({"step": int(step_t.item()), "final": True})
     if t_steps:
         stats["step_ms"] = 1e3 * sorted(t_steps)[len(t_steps) // 2]
     stats["final_save_GBps"] = res.gbps

@@ -3,6 +3,7 @@ from .checkpointer import (CheckpointError, Checkpointer, DeviceEngine, Transfer
                            describe_checkpoint)
 from .host import HostRegion
 from . import preemption
+from .training import TrainingState, collect
 
 __all__ = ["CheckpointError", "Checkpointer", "DeviceEngine", "TransferResult",
-           "describe_checkpoint", "HostRegion", "preemption"]
+           "describe_checkpoint", "HostRegion", "TrainingState", "collect", "preemption"]

@@ -180,7 +180,7 @@ class Checkpointer:
     what bounds save/restore throughput.  CRCs always cover the raw tiles.
     """
 
-    HEADER_RESERVE = 64 * 1024  # room for metadata updates without relayout
+    HEADER_RESERVE = 1 << 20  # room for metadata (e.g. host-side optimizer scalars)
 
     def __init__(self, tensors: Union[Mapping[str, Any], Sequence[Any]],
                  path: Optional[str] = None, *, tile_bytes: int = 1 << 20,

@@ -1,0 +1,123 @@
+"""Preemption-safe training state: a model's parameters/buffers + its optimizer's state.
+
+``TrainingState(model, optimizer)`` binds every device tensor of ``model.state_dict()`` and
+of the optimizer's per-parameter state into one :class:`Checkpointer` (by reference, no
+copies), and carries the small host-side tensors that optimizers keep on the CPU (e.g. the
+per-parameter ``step`` counters of non-capturable Adam/AdamW, which bias correction depends
+on) in the checkpoint header.  ``resume()`` restores both; ``install()`` arms the SIGTERM
+handler of :mod:`.preemption`.
+
+This is the tensor-level counterpart of the reference's workdir sync: there the user script
+had to re-read its own files after a spot respawn (README.md:93-101).
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, Optional, Tuple
+
+from . import preemption
+from .checkpointer import Checkpointer
+
+HOST_NUMEL_LIMIT = 4096  # per host tensor carried in the JSON header
+
+
+def collect(model, optimizer=None, extra: Optional[Dict[str, Any]] = None,
+            device=None) -> Tuple[Dict[str, Any], Dict[str, Any]]:
+    """(tensors on ``device``, small tensors elsewhere) of a model/optimizer pair.
+
+    ``device`` defaults to the device of the model's first parameter.  Optimizer state needs
+    to exist (take one step first: PyTorch creates it lazily).
+    """
+    import torch
+
+    module = getattr(model, "module", model)  # DDP / FSDP-style wrappers
+    state = module.state_dict(keep_vars=False)
+    if device is None:
+        first = next(iter(module.parameters()), None)
+        device = first.device if first is not None else torch.device("cpu")
+    device = torch.device(device)
+    main, host = {}, {}
+
+    def put(name, t):
+        if not torch.is_tensor(t):
+            return
+        if t.device == device:
+            main[name] = t
+        else:
+            if t.numel() > HOST_NUMEL_LIMIT:
+                raise ValueError("%s: %d elements on %s (checkpoint device %s); move it to the "
+                                 "device or checkpoint it separately" % (name, t.numel(),
+                                                                        t.device, device))
+            host[name] = t
+
+    for name, t in state.items():
+        put("model." + name, t)
+    if optimizer is not None:
+        params = [p for group in optimizer.param_groups for p in group["params"]]
+        for i, param in enumerate(params):
+            for key, value in optimizer.state.get(param, {}).items():
+                put("optim.%d.%s" % (i, key), value)
+    for name, t in (extra or {}).items():
+        put("extra." + name, t)
+    return main, host
+
+
+def _encode(t) -> Dict[str, Any]:
+    return {"dtype": str(t.dtype).replace("torch.", ""), "shape": list(t.shape),
+            "data": t.detach().reshape(-1).cpu().tolist()}
+
+
+def _decode_into(t, blob: Dict[str, Any]) -> None:
+    import torch
+
+    src = torch.tensor(blob["data"], dtype=getattr(torch, blob["dtype"])).reshape(blob["shape"])
+    with torch.no_grad():
+        t.copy_(src.to(t.device))
+
+
+class TrainingState:
+    """Checkpointer over a model + optimizer (see module docstring)."""
+
+    def __init__(self, model, optimizer=None, extra: Optional[Dict[str, Any]] = None,
+                 path: Optional[str] = None, device=None, **checkpointer_kwargs):
+        tensors, self.host = collect(model, optimizer, extra, device)
+        if not tensors:
+            raise ValueError("nothing to checkpoint on the model's device")
+        self.checkpointer = Checkpointer(tensors, path=path, **checkpointer_kwargs)
+        self.path = path
+
+    def host_metadata(self) -> Dict[str, Any]:
+        return {"host_tensors": {k: _encode(t) for k, t in self.host.items()}}
+
+    def save(self, metadata: Optional[Dict] = None):
+        return self.checkpointer.save({**(metadata or {}), **self.host_metadata()})
+
+    def restore_host(self, metadata: Dict) -> None:
+        blobs = metadata.get("host_tensors", {})
+        missing = sorted(set(self.host) - set(blobs))
+        if missing:
+            raise ValueError("checkpoint lacks host tensors %s" % missing[:5])
+        for name, t in self.host.items():
+            _decode_into(t, blobs[name])
+
+    def resume(self, persist_path: Optional[str] = None) -> Optional[Dict]:
+        """Restore device tensors (host region, else ``persist_path``) and host tensors;
+        returns the saved metadata or ``None`` for a fresh start."""
+        meta = preemption.resume(self.checkpointer, persist_path)
+        if meta is not None:
+            self.restore_host(meta)
+        return meta
+
+    def install(self, persist_path: Optional[str] = None) -> None:
+        """Checkpoint on SIGTERM (then exit 143 so the supervisor respawns the rank)."""
+        preemption.register(self.checkpointer, persist_path)
+        preemption.on_preempt(self.host_metadata)
+        preemption.install()
+
+    def close(self) -> None:
+        self.checkpointer.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
