@@ -93,3 +93,32 @@ def test_preempt_resume_training_on_gpu(cloud, tmp_path):
     assert resumed and int(resumed[0].rsplit(" ", 1)[1]) >= 11
     assert "done" in logs[1]
     task.delete()
+
+
+def test_training_state_on_device_carries_cpu_step_counters(tmp_path):
+    from terraform_provider_iterative_amd.checkpoint import TrainingState, collect
+
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(64, 128), torch.nn.GELU(),
+                                torch.nn.Linear(128, 64)).cuda().to(torch.bfloat16)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
+
+    def train(n):
+        for _ in range(n):
+            model(torch.randn(4, 64, device="cuda", dtype=torch.bfloat16)).float().pow(2) \
+                .mean().backward()
+            opt.step()
+            opt.zero_grad()
+
+    train(3)
+    tensors, host = collect(model, opt)
+    assert host and all(k.endswith(".step") for k in host)  # AdamW keeps step on the CPU
+    want = {k: v.clone() for k, v in {**tensors, **host}.items()}
+    with TrainingState(model, opt, path=str(tmp_path / "spill"), codec="tpz1") as state:
+        state.save({"iteration": 3})
+        train(2)
+        assert state.resume()["iteration"] == 3
+        torch.cuda.synchronize()
+    tensors2, host2 = collect(model, opt)
+    for k, v in {**tensors2, **host2}.items():
+        assert torch.equal(v, want[k]), k
