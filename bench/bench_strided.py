@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""Pack/unpack throughput of non-contiguous tensor views (GB/s of payload):
+transposed 2-D (fp32 / bf16), row-sliced 2-D, channels-last 4-D, every-other-element."""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import torch
+
+    from terraform_provider_iterative_amd.ops.packing import PackPlan, pack, unpack
+
+    dev = torch.device("cuda", 0)
+    cases = {
+        "transpose_fp32": torch.randn(8192, 8192, device=dev).t(),
+        "transpose_bf16": torch.randn(8192, 8192, device=dev).to(torch.bfloat16).t(),
+        "row_slice_fp32": torch.randn(8192, 8192, device=dev)[:, 100:8000],
+        "channels_last_bf16": torch.randn(64, 256, 32, 32, device=dev).to(torch.bfloat16)
+        .contiguous(memory_format=torch.channels_last),
+        "stride2_fp32": torch.randn(1 << 26, device=dev)[::2],
+    }
+    out = {}
+    for name, t in cases.items():
+        plan = PackPlan.from_tensors({name: t})
+        stream, crcs = pack(plan)
+        torch.cuda.synchronize()
+        iters = 3
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            pack(plan, stream)
+        torch.cuda.synchronize()
+        tp = (time.perf_counter() - t0) / iters
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            bad, _ = unpack(plan, stream, crcs)
+        torch.cuda.synchronize()
+        tu = (time.perf_counter() - t0) / iters
+        nbytes = t.numel() * t.element_size()
+        out[name] = {"pack_GBps": round(nbytes / tp / 1e9, 1),
+                     "unpack_GBps": round(nbytes / tu / 1e9, 1), "bad": int(bad)}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

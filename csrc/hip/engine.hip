@@ -37,6 +37,9 @@ extern "C" hipError_t tpi_launch_stream_crc(int mode, const tpi_seg* segs, int n
                                             uint64_t tile_bytes, const tpi_crc_tables* tables,
                                             uint32_t* crcs, uint32_t init_full,
                                             uint32_t init_last, unsigned long long* bad,
+                                            int staged, hipStream_t stream);
+extern "C" hipError_t tpi_launch_transposes(const tpi_seg* host_segs, int nseg, uint64_t base,
+                                            uint64_t len, void* buf, int dir,
                                             hipStream_t stream);
 extern "C" hipError_t tpi_launch_shard_hash(const void* data, uint64_t nbytes,
                                             uint64_t shard_bytes, uint64_t seed, uint64_t* out,
@@ -121,9 +124,15 @@ int check_segments(const tpi_seg* segs, int n, uint64_t total) {
     if (i && segs[i].off < segs[i - 1].off + segs[i - 1].nbytes)
       return fail("segments overlap or are unsorted");
     if (segs[i].off + segs[i].nbytes > total) return fail("segment exceeds stream");
-    if (segs[i].kind == 1 && (segs[i].elem == 0 || segs[i].ndim < 1 ||
-                              segs[i].ndim > TPI_MAX_DIMS))
+    if (segs[i].kind > TPI_SEG_TRANSPOSE) return fail("unknown segment kind");
+    if (segs[i].kind != TPI_SEG_CONTIG && (segs[i].elem == 0 || segs[i].ndim < 1 ||
+                                           segs[i].ndim > TPI_MAX_DIMS))
       return fail("bad strided segment descriptor");
+    if (segs[i].kind == TPI_SEG_TRANSPOSE &&
+        (segs[i].ndim < 2 || segs[i].ndim > 3 || segs[i].elem > 8 ||
+         (segs[i].elem & (segs[i].elem - 1)) || segs[i].ptr % segs[i].elem ||
+         segs[i].strides[segs[i].ndim - 2] != 1))
+      return fail("bad transpose segment descriptor");
   }
   if (total % 16) return fail("stream length must be a multiple of 16");
   return 0;
@@ -324,7 +333,7 @@ int tpi_save(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* ho
   uint64_t nchunks = 0;
   if (mode == TPI_MODE_DIRECT) {
     HIP_OK(tpi_launch_stream_crc(0, e->d_segs, n, 0, total, device_view(host_dst), tile,
-                                 e->tables, e->d_crcs, init_full, init_last, nullptr,
+                                 e->tables, e->d_crcs, init_full, init_last, nullptr, 0,
                                  e->compute));
     nchunks = 1;
   } else {
@@ -333,8 +342,9 @@ int tpi_save(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* ho
       const int b = (int)(k % e->nbuf);
       const uint64_t len = std::min(e->chunk, total - base);
       if (k >= (uint64_t)e->nbuf) HIP_OK(hipStreamWaitEvent(e->compute, e->ev_b[b], 0));
+      HIP_OK(tpi_launch_transposes(segs, n, base, len, e->staging[b], 0, e->compute));
       HIP_OK(tpi_launch_stream_crc(0, e->d_segs, n, base, len, e->staging[b], tile, e->tables,
-                                   e->d_crcs, init_full, init_last, nullptr, e->compute));
+                                   e->d_crcs, init_full, init_last, nullptr, 1, e->compute));
       HIP_OK(hipEventRecord(e->ev_a[b], e->compute));
       HIP_OK(hipStreamWaitEvent(e->copy, e->ev_a[b], 0));
       HIP_OK(hipMemcpyAsync(dst + base, e->staging[b], len, hipMemcpyDeviceToHost, e->copy));
@@ -383,7 +393,7 @@ int tpi_restore(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, const
   uint64_t nchunks = 0;
   if (mode == TPI_MODE_DIRECT) {
     HIP_OK(tpi_launch_stream_crc(1, e->d_segs, n, 0, total, device_view((void*)host_src), tile,
-                                 e->tables, e->d_crcs, init_full, init_last, e->d_bad,
+                                 e->tables, e->d_crcs, init_full, init_last, e->d_bad, 0,
                                  e->compute));
     nchunks = 1;
   } else {
@@ -399,7 +409,8 @@ int tpi_restore(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, const
       HIP_OK(hipEventRecord(e->ev_a[b], e->copy));
       HIP_OK(hipStreamWaitEvent(e->compute, e->ev_a[b], 0));
       HIP_OK(tpi_launch_stream_crc(1, e->d_segs, n, base, len, e->staging[b], tile, e->tables,
-                                   e->d_crcs, init_full, init_last, e->d_bad, e->compute));
+                                   e->d_crcs, init_full, init_last, e->d_bad, 1, e->compute));
+      HIP_OK(tpi_launch_transposes(segs, n, base, len, e->staging[b], 1, e->compute));
       HIP_OK(hipEventRecord(e->ev_b[b], e->compute));
       nchunks = k + 1;
     }
@@ -561,8 +572,9 @@ int tpi_save_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* 
     const uint64_t len = std::min(e->chunk, total - base);
     const uint64_t t0i = base / tile, nt = (len + tile - 1) / tile;
     if (k >= (uint64_t)e->nbuf) HIP_OK(hipStreamWaitEvent(e->compute, e->ev_b[b], 0));
+    HIP_OK(tpi_launch_transposes(segs, n, base, len, e->zraw, 0, e->compute));
     HIP_OK(tpi_launch_stream_crc(0, e->d_segs, n, base, len, e->zraw, tile, e->tables,
-                                 e->d_crcs, init_full, init_last, nullptr, e->compute));
+                                 e->d_crcs, init_full, init_last, nullptr, 1, e->compute));
     HIP_OK(tpi_launch_tpz_encode(e->zraw, len, tile, e->d_meta, e->d_csize + t0i,
                                  e->staging[b], e->compute));
     HIP_OK(hipMemcpyAsync(csizes_out + t0i, e->d_csize + t0i, nt * sizeof(uint32_t),
@@ -644,7 +656,8 @@ int tpi_restore_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total,
                                  e->compute));
     HIP_OK(hipEventRecord(e->ev_b[b], e->compute));
     HIP_OK(tpi_launch_stream_crc(1, e->d_segs, n, base, len, e->zraw, tile, e->tables,
-                                 e->d_crcs, init_full, init_last, e->d_bad, e->compute));
+                                 e->d_crcs, init_full, init_last, e->d_bad, 1, e->compute));
+    HIP_OK(tpi_launch_transposes(segs, n, base, len, e->zraw, 1, e->compute));
     nchunks = k + 1;
   }
   unsigned long long bad[2];
@@ -700,7 +713,7 @@ int tpi_crc32c_tiles(const void* dev_ptr, uint64_t nbytes, uint64_t tile_bytes,
   const uint32_t init_full = init_for(tile_bytes);
   const uint32_t init_last = init_for(nbytes % tile_bytes ? nbytes % tile_bytes : tile_bytes);
   HIP_OK(tpi_launch_stream_crc(2, nullptr, 0, 0, nbytes, (void*)dev_ptr, tile_bytes, t, dev_out,
-                               init_full, init_last, nullptr, (hipStream_t)stream));
+                               init_full, init_last, nullptr, 0, (hipStream_t)stream));
   return 0;
 }
 
@@ -713,8 +726,8 @@ int tpi_shard_hash(const void* dev_ptr, uint64_t nbytes, uint64_t shard_bytes, u
   return 0;
 }
 
-int tpi_pack_device(const tpi_seg* segs, int n, uint64_t total, void* dev_dst,
-                    uint64_t tile_bytes, uint32_t* dev_crcs, uint64_t stream) {
+int tpi_pack_device(const tpi_seg* segs, const tpi_seg* host_segs, int n, uint64_t total,
+                    void* dev_dst, uint64_t tile_bytes, uint32_t* dev_crcs, uint64_t stream) {
   // `segs` is a DEVICE array here (the caller owns it); validation happens host-side in the
   // Python wrapper, which builds it.
   if (tile_bytes == 0 || tile_bytes % TPI_ROW_BYTES) return fail("tile must be k*4096");
@@ -722,25 +735,28 @@ int tpi_pack_device(const tpi_seg* segs, int n, uint64_t total, void* dev_dst,
   HIP_OK(hipGetDevice(&dev));
   tpi_crc_tables* t = nullptr;
   if (device_tables(dev, &t)) return -1;
+  HIP_OK(tpi_launch_transposes(host_segs, n, 0, total, dev_dst, 0, (hipStream_t)stream));
   HIP_OK(tpi_launch_stream_crc(0, segs, n, 0, total, dev_dst, tile_bytes, t, dev_crcs,
                                init_for(tile_bytes),
                                init_for(total % tile_bytes ? total % tile_bytes : tile_bytes),
-                               nullptr, (hipStream_t)stream));
+                               nullptr, host_segs ? 1 : 0, (hipStream_t)stream));
   return 0;
 }
 
-int tpi_unpack_device(const tpi_seg* segs, int n, uint64_t total, const void* dev_src,
-                      uint64_t tile_bytes, const uint32_t* dev_crcs, uint64_t* dev_bad,
-                      uint64_t stream) {
+int tpi_unpack_device(const tpi_seg* segs, const tpi_seg* host_segs, int n, uint64_t total,
+                      void* dev_src, uint64_t tile_bytes, const uint32_t* dev_crcs,
+                      uint64_t* dev_bad, uint64_t stream) {
   if (tile_bytes == 0 || tile_bytes % TPI_ROW_BYTES) return fail("tile must be k*4096");
   int dev = 0;
   HIP_OK(hipGetDevice(&dev));
   tpi_crc_tables* t = nullptr;
   if (device_tables(dev, &t)) return -1;
-  HIP_OK(tpi_launch_stream_crc(1, segs, n, 0, total, (void*)dev_src, tile_bytes, t,
+  HIP_OK(tpi_launch_stream_crc(1, segs, n, 0, total, dev_src, tile_bytes, t,
                                (uint32_t*)dev_crcs, init_for(tile_bytes),
                                init_for(total % tile_bytes ? total % tile_bytes : tile_bytes),
-                               (unsigned long long*)dev_bad, (hipStream_t)stream));
+                               (unsigned long long*)dev_bad, host_segs ? 1 : 0,
+                               (hipStream_t)stream));
+  HIP_OK(tpi_launch_transposes(host_segs, n, 0, total, dev_src, 1, (hipStream_t)stream));
   return 0;
 }
 

@@ -52,6 +52,14 @@ __device__ static inline uint32_t shift_row(const uint32_t* __restrict__ r, uint
 }
 
 // ---- segment (tensor) access --------------------------------------------------------------
+//
+// The packed stream is read/written in 16-byte words.  Per segment kind:
+//   CONTIG     one dwordx4 load/store per word (nontemporal)
+//   ROWS       row = rel / row_bytes; the row's base comes from the outer dims; one dwordx4
+//              per word while the word stays inside an aligned row
+//   TRANSPOSE  with `staged`, the bytes were already moved between tensor and stream buffer
+//              by k_transpose (LDS tiles); the tile kernel only reads/keeps them there
+//   otherwise  element-wise: 16/elem typed loads/stores at the view's strided offsets
 
 struct SegCursor {
   int idx;
@@ -90,57 +98,77 @@ __device__ static inline uint64_t strided_offset(const tpi_seg& s, uint64_t e) {
   return off;
 }
 
-__device__ static inline void bytes_to_word(const uint8_t* b, u32x4& w) {
-  w.x = b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24);
-  w.y = b[4] | (b[5] << 8) | (b[6] << 16) | ((uint32_t)b[7] << 24);
-  w.z = b[8] | (b[9] << 8) | (b[10] << 16) | ((uint32_t)b[11] << 24);
-  w.w = b[12] | (b[13] << 8) | (b[14] << 16) | ((uint32_t)b[15] << 24);
+// Element-wise path: the word holds 16/E whole elements (E divides 16, words 16-aligned).
+// Component arithmetic with compile-time indices only (no private arrays -> no scratch).
+template <int E>
+__device__ static inline uint32_t elem_bits(const uint8_t* src) {
+  if (E == 1) return *src;
+  if (E == 2) return *(const uint16_t*)src;
+  return *(const uint32_t*)src;
 }
 
-__device__ static inline void word_to_bytes(u32x4 w, uint8_t* b) {
-  uint32_t v[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-  for (int i = 0; i < 16; ++i) b[i] = (v[i >> 2] >> (8 * (i & 3))) & 0xff;
-}
-
-// Slow path: bytes [rel, rel+16) of a segment payload that is misaligned, strided, or ends
-// inside the word (bytes past the payload read as zero = alignment padding).
-__device__ __noinline__ static u32x4 gather_slow(const tpi_seg* __restrict__ segs, int idx,
+template <int E>
+__device__ static inline u32x4 gather_elems(const tpi_seg* __restrict__ segs, int idx,
                                                   uint64_t rel) {
   const tpi_seg& s = segs[idx];
-  uint8_t b[16];
-  for (int i = 0; i < 16; ++i) {
-    uint64_t q = rel + i;
-    uint8_t v = 0;
-    if (q < s.nbytes) {
-      if (s.kind == 0) {
-        v = ((const uint8_t*)s.ptr)[q];
-      } else {
-        uint64_t e = q / s.elem;
-        v = ((const uint8_t*)s.ptr)[strided_offset(s, e) * s.elem + (q % s.elem)];
-      }
-    }
-    b[i] = v;
+  const uint8_t* base = (const uint8_t*)s.ptr;
+  uint32_t u0 = 0, u1 = 0, u2 = 0, u3 = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k += (E < 4 ? E : 4)) {
+    const uint64_t q = rel + k;
+    if (q >= s.nbytes) break;
+    const int sub = E > 4 ? k % E : 0;  // 8/16-byte elements move as dwords
+    const uint64_t off = (s.kind == TPI_SEG_CONTIG ? q - sub : strided_offset(s, q / E) * E) + sub;
+    const uint32_t v = elem_bits < (E < 4 ? E : 4) > (base + off) << (8 * (k & 3));
+    if (k < 4) u0 |= v; else if (k < 8) u1 |= v; else if (k < 12) u2 |= v; else u3 |= v;
   }
-  u32x4 w;
-  bytes_to_word(b, w);
-  return w;
+  return u32x4{u0, u1, u2, u3};
 }
 
-__device__ __noinline__ static void scatter_slow(const tpi_seg* __restrict__ segs, int idx,
-                                                 uint64_t rel, u32x4 w) {
+template <int E>
+__device__ static inline void scatter_elems(const tpi_seg* __restrict__ segs, int idx,
+                                                  uint64_t rel, u32x4 w) {
   const tpi_seg& s = segs[idx];
-  uint8_t b[16];
-  word_to_bytes(w, b);
-  for (int i = 0; i < 16; ++i) {
-    uint64_t q = rel + i;
+  uint8_t* base = (uint8_t*)s.ptr;
+#pragma unroll
+  for (int k = 0; k < 16; k += (E < 4 ? E : 4)) {
+    const uint64_t q = rel + k;
     if (q >= s.nbytes) break;
-    if (s.kind == 0) {
-      ((uint8_t*)s.ptr)[q] = b[i];
-    } else {
-      uint64_t e = q / s.elem;
-      ((uint8_t*)s.ptr)[strided_offset(s, e) * s.elem + (q % s.elem)] = b[i];
-    }
+    const int sub = E > 4 ? k % E : 0;
+    const uint64_t off = (s.kind == TPI_SEG_CONTIG ? q - sub : strided_offset(s, q / E) * E) + sub;
+    const uint32_t comp = k < 4 ? w.x : k < 8 ? w.y : k < 12 ? w.z : w.w;
+    const uint32_t v = comp >> (8 * (k & 3));
+    if (E == 1) base[off] = (uint8_t)v;
+    else if (E == 2) *(uint16_t*)(base + off) = (uint16_t)v;
+    else *(uint32_t*)(base + off) = v;
+  }
+}
+
+// Element size as the access width; odd sizes (and unaligned bases) go byte by byte.
+__device__ static inline int access_width(const tpi_seg& s) {
+  const uint32_t e = s.elem;
+  if (e == 0 || e > 16 || (e & (e - 1)) || (s.ptr % e)) return 1;
+  return (int)e;
+}
+
+__device__ static u32x4 gather_any(const tpi_seg* __restrict__ segs, int idx, uint64_t rel) {
+  switch (access_width(segs[idx])) {
+    case 2: return gather_elems<2>(segs, idx, rel);
+    case 4: return gather_elems<4>(segs, idx, rel);
+    case 8: return gather_elems<8>(segs, idx, rel);
+    case 16: return gather_elems<16>(segs, idx, rel);
+    default: return gather_elems<1>(segs, idx, rel);
+  }
+}
+
+__device__ static void scatter_any(const tpi_seg* __restrict__ segs, int idx, uint64_t rel,
+                                   u32x4 w) {
+  switch (access_width(segs[idx])) {
+    case 2: scatter_elems<2>(segs, idx, rel, w); break;
+    case 4: scatter_elems<4>(segs, idx, rel, w); break;
+    case 8: scatter_elems<8>(segs, idx, rel, w); break;
+    case 16: scatter_elems<16>(segs, idx, rel, w); break;
+    default: scatter_elems<1>(segs, idx, rel, w); break;
   }
 }
 
@@ -149,26 +177,140 @@ __device__ static inline void advance(const tpi_seg* __restrict__ segs, int n, u
   while (pos >= c.next_off) seg_load(segs, n, c.idx + 1, c);
 }
 
+// Address of a word of a ROWS segment if it can be moved as one aligned dwordx4, else 0.
+__device__ static inline uint64_t rows_addr(const tpi_seg& s, uint64_t rel) {
+  const uint64_t row_elems = (uint64_t)s.sizes[s.ndim - 1], row_bytes = row_elems * s.elem;
+  const uint64_t row = rel / row_bytes, within = rel - row * row_bytes;
+  if (within + 16 > row_bytes) return 0;
+  const uint64_t addr = s.ptr + strided_offset(s, row * row_elems) * s.elem + within;
+  return (addr & 15) ? 0 : addr;
+}
+
+// Non-contiguous words (ROWS vectors, staged TRANSPOSE words, element-wise fallback).
+__device__ static inline u32x4 gather_other(const tpi_seg* __restrict__ segs, int idx,
+                                                  uint64_t rel, const uint8_t* sbuf,
+                                                  bool staged) {
+  const tpi_seg& s = segs[idx];
+  if (s.kind == TPI_SEG_ROWS) {
+    const uint64_t addr = rows_addr(s, rel);
+    if (addr) return *(const u32x4*)addr;
+  } else if (s.kind == TPI_SEG_TRANSPOSE && staged) {
+    u32x4 w = *(const u32x4*)sbuf;
+    if (rel + 16 > s.nbytes) {  // the tail word: bytes past the payload are padding (zero)
+      const uint64_t keep = s.nbytes - rel;  // 1..15
+      auto m = [&](int j) -> uint32_t {
+        const int64_t n = (int64_t)keep - 4 * j;
+        return n >= 4 ? 0xffffffffu : n <= 0 ? 0u : (1u << (8 * n)) - 1;
+      };
+      w.x &= m(0);
+      w.y &= m(1);
+      w.z &= m(2);
+      w.w &= m(3);
+    }
+    return w;
+  }
+  return gather_any(segs, idx, rel);
+}
+
+__device__ static inline void scatter_other(const tpi_seg* __restrict__ segs, int idx,
+                                                  uint64_t rel, u32x4 w, bool staged) {
+  const tpi_seg& s = segs[idx];
+  if (s.kind == TPI_SEG_ROWS) {
+    const uint64_t addr = rows_addr(s, rel);
+    if (addr) {
+      *(u32x4*)addr = w;
+      return;
+    }
+  } else if (s.kind == TPI_SEG_TRANSPOSE && staged) {
+    return;  // k_transpose scatters this segment from the stream buffer afterwards
+  }
+  scatter_any(segs, idx, rel, w);
+}
+
+// `staged`: the word's bytes for TRANSPOSE segments are already at `sbuf` (stream buffer).
 __device__ static inline u32x4 gather16(const tpi_seg* __restrict__ segs, const SegCursor& c,
-                                        uint64_t pos) {
+                                        uint64_t pos, const uint8_t* sbuf, bool staged) {
   const uint64_t rel = pos - c.off;
   if (rel >= c.nbytes) return u32x4{0, 0, 0, 0};  // alignment padding
   const uint64_t addr = c.ptr + rel;
-  if (c.kind == 0 && rel + 16 <= c.nbytes && (addr & 15) == 0)
+  if (c.kind == TPI_SEG_CONTIG && rel + 16 <= c.nbytes && (addr & 15) == 0)
     return __builtin_nontemporal_load((const u32x4*)addr);
-  return gather_slow(segs, c.idx, rel);
+  return gather_other(segs, c.idx, rel, sbuf, staged);
 }
 
 __device__ static inline void scatter16(const tpi_seg* __restrict__ segs, const SegCursor& c,
-                                        uint64_t pos, u32x4 w) {
+                                        uint64_t pos, u32x4 w, bool staged) {
   const uint64_t rel = pos - c.off;
   if (rel >= c.nbytes) return;
   const uint64_t addr = c.ptr + rel;
-  if (c.kind == 0 && rel + 16 <= c.nbytes && (addr & 15) == 0) {
+  if (c.kind == TPI_SEG_CONTIG && rel + 16 <= c.nbytes && (addr & 15) == 0) {
     *(u32x4*)addr = w;
     return;
   }
-  scatter_slow(segs, c.idx, rel, w);
+  scatter_other(segs, c.idx, rel, w, staged);
+}
+
+// ---- LDS-tiled transpose for TRANSPOSE segments ------------------------------------------------
+//
+// A TRANSPOSE view is (B, R, C) in logical (row-major) order with memory strides (sB, 1, sC):
+// memory-contiguous along R, while the stream is contiguous along C.  One 256-thread
+// workgroup moves a 64(R) x 64(C) element tile through LDS: reads are 64 consecutive R
+// elements per C column (coalesced), writes are 64 consecutive C elements per R row
+// (coalesced); the +1 column of padding keeps the LDS transpose free of bank conflicts.
+// DIR 0: tensor -> stream buffer (before the pack kernel), DIR 1: stream buffer -> tensor
+// (after the unpack kernel has verified the CRCs).  Only logical elements in [e_lo, e_hi)
+// (the part of the segment inside the current chunk) are touched.
+
+struct TransposeArgs {
+  uint64_t ptr;      // tensor base
+  uint64_t sbuf;     // address of logical element 0 of the segment in the stream buffer
+  int64_t B, R, C, sB, sC;
+  uint64_t e_lo, e_hi;
+  uint64_t t_lo;     // first (b, r-tile) pair: b * RT + rt
+  uint32_t ct;       // number of C tiles
+  uint32_t rt;       // number of R tiles per batch
+};
+
+template <typename T, int DIR>
+__global__ __launch_bounds__(256) void k_transpose(TransposeArgs a) {
+  __shared__ T tile[64][65];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const uint64_t pair = a.t_lo + blockIdx.x / a.ct;
+  const int64_t b = (int64_t)(pair / a.rt);
+  const int64_t r0 = (int64_t)(pair % a.rt) * 64;
+  const int64_t c0 = (int64_t)(blockIdx.x % a.ct) * 64;
+  T* tensor = (T*)a.ptr;
+  T* stream = (T*)a.sbuf;
+  const uint64_t row0 = (uint64_t)(b * a.R) * (uint64_t)a.C;  // logical index of (b, 0, 0)
+  if (DIR == 0) {
+#pragma unroll 4
+    for (int j = ty; j < 64; j += 4) {  // column c0+j, rows r0+tx: contiguous in memory
+      const int64_t r = r0 + tx, c = c0 + j;
+      if (r < a.R && c < a.C) tile[j][tx] = tensor[b * a.sB + r + c * a.sC];
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int j = ty; j < 64; j += 4) {  // row r0+j, columns c0+tx: contiguous in the stream
+      const int64_t r = r0 + j, c = c0 + tx;
+      const uint64_t e = row0 + (uint64_t)r * a.C + c;
+      if (r < a.R && c < a.C && e >= a.e_lo && e < a.e_hi) stream[e] = tile[tx][j];
+    }
+  } else {
+#pragma unroll 4
+    for (int j = ty; j < 64; j += 4) {
+      const int64_t r = r0 + j, c = c0 + tx;
+      const uint64_t e = row0 + (uint64_t)r * a.C + c;
+      if (r < a.R && c < a.C && e >= a.e_lo && e < a.e_hi) tile[tx][j] = stream[e];
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int j = ty; j < 64; j += 4) {
+      const int64_t r = r0 + tx, c = c0 + j;
+      const uint64_t e = row0 + (uint64_t)r * a.C + c;
+      if (r < a.R && c < a.C && e >= a.e_lo && e < a.e_hi)
+        tensor[b * a.sB + r + c * a.sC] = tile[j][tx];
+    }
+  }
 }
 
 // ---- the tile kernel -------------------------------------------------------------------------
@@ -187,6 +329,7 @@ struct TileArgs {
   unsigned long long* bad;  // [0] mismatching tiles, [1] first bad tile (unpack)
   const uint32_t* list;     // optional: workgroup i handles stream tile list[i] (sparse pack)
   uint64_t total;           // stream length (needed with `list`)
+  int staged;               // TRANSPOSE segments are moved by k_transpose (see gather16)
 };
 
 // Stream geometry of this workgroup's tile: (global tile, stream offset, length, buffer).
@@ -249,7 +392,7 @@ __global__ __launch_bounds__(WG) void k_stream_crc(TileArgs a) {
       const uint64_t rel = (row + u) * TPI_ROW_BYTES + lane * 16;
       if (MODE == MODE_PACK) {
         advance(a.segs, a.nseg, gbase + rel, cur);
-        w[u] = gather16(a.segs, cur, gbase + rel);
+        w[u] = gather16(a.segs, cur, gbase + rel, tbuf + rel, a.staged);
       } else {
         w[u] = __builtin_nontemporal_load((const u32x4*)(tbuf + rel));
       }
@@ -261,7 +404,7 @@ __global__ __launch_bounds__(WG) void k_stream_crc(TileArgs a) {
         __builtin_nontemporal_store(w[u], (u32x4*)(tbuf + rel));
       } else if (MODE == MODE_UNPACK) {
         advance(a.segs, a.nseg, gbase + rel, cur);
-        scatter16(a.segs, cur, gbase + rel, w[u]);
+        scatter16(a.segs, cur, gbase + rel, w[u], a.staged);
       }
       acc = shift_row(s_row, acc) ^ raw16(s_slice, w[u]);
     }
@@ -273,13 +416,13 @@ __global__ __launch_bounds__(WG) void k_stream_crc(TileArgs a) {
       u32x4 w;
       if (MODE == MODE_PACK) {
         advance(a.segs, a.nseg, gbase + rel, cur);
-        w = gather16(a.segs, cur, gbase + rel);
+        w = gather16(a.segs, cur, gbase + rel, tbuf + rel, a.staged);
         __builtin_nontemporal_store(w, (u32x4*)(tbuf + rel));
       } else {
         w = __builtin_nontemporal_load((const u32x4*)(tbuf + rel));
         if (MODE == MODE_UNPACK) {
           advance(a.segs, a.nseg, gbase + rel, cur);
-          scatter16(a.segs, cur, gbase + rel, w);
+          scatter16(a.segs, cur, gbase + rel, w, a.staged);
         }
       }
       acc = shift_row(s_row, acc) ^ raw16(s_slice, w);
@@ -416,7 +559,7 @@ __global__ __launch_bounds__(WG) void k_stream_hash(const tpi_seg* __restrict__ 
     for (int u = 0; u < UNROLL; ++u) {
       const uint64_t pos = gbase + (row + u) * TPI_ROW_BYTES + lane * 16;
       advance(segs, nseg, pos, cur);
-      w[u] = gather16(segs, cur, pos);
+      w[u] = gather16(segs, cur, pos, nullptr, false);
     }
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
@@ -427,7 +570,7 @@ __global__ __launch_bounds__(WG) void k_stream_hash(const tpi_seg* __restrict__ 
   }
   for (uint64_t rel = row * TPI_ROW_BYTES + lane * 16; rel < len; rel += TPI_ROW_BYTES) {
     advance(segs, nseg, gbase + rel, cur);
-    const u32x4 w = gather16(segs, cur, gbase + rel);
+    const u32x4 w = gather16(segs, cur, gbase + rel, nullptr, false);
     v = tpi_xxh_round(v, ((uint64_t)w.y << 32) | w.x);
     v = tpi_xxh_round(v, ((uint64_t)w.w << 32) | w.z);
     ++nwords;
@@ -461,7 +604,7 @@ extern "C" hipError_t tpi_launch_stream_crc(int mode, const tpi_seg* segs, int n
                                             uint64_t tile_bytes, const tpi_crc_tables* tables,
                                             uint32_t* crcs, uint32_t init_full,
                                             uint32_t init_last, unsigned long long* bad,
-                                            hipStream_t stream) {
+                                            int staged, hipStream_t stream) {
   if (len == 0) return hipSuccess;
   TileArgs a;
   a.segs = segs;
@@ -477,6 +620,7 @@ extern "C" hipError_t tpi_launch_stream_crc(int mode, const tpi_seg* segs, int n
   a.bad = bad;
   a.list = nullptr;
   a.total = 0;
+  a.staged = staged;
   const uint64_t ntiles = (len + tile_bytes - 1) / tile_bytes;
   dim3 grid((unsigned)ntiles), block(WG);
   switch (mode) {
@@ -521,6 +665,7 @@ extern "C" hipError_t tpi_launch_pack_list(const tpi_seg* segs, int nseg, uint64
   a.bad = nullptr;
   a.list = list;
   a.total = total;
+  a.staged = 0;
   hipLaunchKernelGGL(k_stream_crc<MODE_PACK>, dim3(n), dim3(WG), 0, stream, a);
   return hipGetLastError();
 }
@@ -542,4 +687,53 @@ extern "C" hipError_t tpi_launch_dirty_tiles(const uint64_t* hash, uint64_t* pre
   hipLaunchKernelGGL(k_dirty_tiles, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
                      hash, prev, n, all, idx, count);
   return hipGetLastError();
+}
+
+// Transposes of the TRANSPOSE segments (host descriptors) overlapping the stream window
+// [base, base + len) whose bytes live at `buf` (buf[0] = stream byte `base`).
+extern "C" hipError_t tpi_launch_transposes(const tpi_seg* host_segs, int nseg, uint64_t base,
+                                            uint64_t len, void* buf, int dir,
+                                            hipStream_t stream) {
+  if (!host_segs) return hipSuccess;
+  for (int i = 0; i < nseg; ++i) {
+    const tpi_seg& s = host_segs[i];
+    if (s.kind != TPI_SEG_TRANSPOSE) continue;
+    const uint64_t lo = s.off > base ? s.off : base;
+    const uint64_t hi = s.off + s.nbytes < base + len ? s.off + s.nbytes : base + len;
+    if (lo >= hi) continue;
+    TransposeArgs a;
+    a.ptr = s.ptr;
+    a.sbuf = (uint64_t)buf + s.off - base;  // may point before buf: only [e_lo, e_hi) is used
+    if (s.ndim == 3) {
+      a.B = s.sizes[0]; a.sB = s.strides[0]; a.R = s.sizes[1]; a.C = s.sizes[2];
+      a.sC = s.strides[2];
+    } else {
+      a.B = 1; a.sB = 0; a.R = s.sizes[0]; a.C = s.sizes[1]; a.sC = s.strides[1];
+    }
+    a.e_lo = (lo - s.off) / s.elem;
+    a.e_hi = (hi - s.off + s.elem - 1) / s.elem;
+    a.ct = (uint32_t)((a.C + 63) / 64);
+    a.rt = (uint32_t)((a.R + 63) / 64);
+    const uint64_t lr_lo = a.e_lo / a.C, lr_hi = (a.e_hi - 1) / a.C;  // logical rows b*R + r
+    const uint64_t b_lo = lr_lo / a.R, b_hi = lr_hi / a.R;
+    a.t_lo = b_lo * a.rt + (lr_lo - b_lo * a.R) / 64;
+    const uint64_t t_hi = b_hi * a.rt + (lr_hi - b_hi * a.R) / 64;
+    const uint64_t blocks = (t_hi - a.t_lo + 1) * a.ct;
+    if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)blocks), block(256);
+    switch (s.elem * 2 + (dir ? 1 : 0)) {
+      case 2: hipLaunchKernelGGL((k_transpose<uint8_t, 0>), grid, block, 0, stream, a); break;
+      case 3: hipLaunchKernelGGL((k_transpose<uint8_t, 1>), grid, block, 0, stream, a); break;
+      case 4: hipLaunchKernelGGL((k_transpose<uint16_t, 0>), grid, block, 0, stream, a); break;
+      case 5: hipLaunchKernelGGL((k_transpose<uint16_t, 1>), grid, block, 0, stream, a); break;
+      case 8: hipLaunchKernelGGL((k_transpose<uint32_t, 0>), grid, block, 0, stream, a); break;
+      case 9: hipLaunchKernelGGL((k_transpose<uint32_t, 1>), grid, block, 0, stream, a); break;
+      case 16: hipLaunchKernelGGL((k_transpose<uint64_t, 0>), grid, block, 0, stream, a); break;
+      case 17: hipLaunchKernelGGL((k_transpose<uint64_t, 1>), grid, block, 0, stream, a); break;
+      default: return hipErrorInvalidValue;  // the host only emits TRANSPOSE for 1/2/4/8
+    }
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return err;
+  }
+  return hipSuccess;
 }

@@ -19,12 +19,21 @@ extern "C" {
 #define TPI_MAX_DIMS 6
 #define TPI_SEG_ALIGN 256  // packed-stream alignment of every tensor payload
 
+// Segment kinds.  sizes/strides always describe the view (canonicalised: size-1 dims
+// dropped, mergeable dims merged), so any kind may fall back to the element-wise path.
+enum {
+  TPI_SEG_CONTIG = 0,     // one contiguous run
+  TPI_SEG_STRIDED = 1,    // general view: element gather/scatter
+  TPI_SEG_ROWS = 2,       // last dim contiguous (sliced rows): 16-byte vector path
+  TPI_SEG_TRANSPOSE = 3,  // (B,) R, C with R unit-stride: LDS-tiled transpose pre/post pass
+};
+
 // One tensor payload inside the packed checkpoint stream.
 typedef struct tpi_seg {
   uint64_t ptr;     // device (or host-mapped) address of the tensor's first element
   uint64_t off;     // byte offset in the packed stream (multiple of TPI_SEG_ALIGN)
   uint64_t nbytes;  // payload bytes (numel * elem)
-  uint32_t kind;    // 0 = contiguous, 1 = strided gather/scatter
+  uint32_t kind;    // TPI_SEG_*
   uint32_t elem;    // element size in bytes (strided path)
   int32_t ndim;
   int32_t pad_;
@@ -105,11 +114,13 @@ int tpi_shard_hash(const void* dev_ptr, uint64_t nbytes, uint64_t shard_bytes, u
                    uint64_t* dev_out, uint64_t stream);
 // Pack/unpack into/out of a device buffer (no host spill); used by tests and by the
 // broadcast path (pack once, RCCL-broadcast the flat buffer, unpack on every rank).
-int tpi_pack_device(const tpi_seg* segs, int n, uint64_t total, void* dev_dst,
-                    uint64_t tile_bytes, uint32_t* dev_crcs, uint64_t stream);
-int tpi_unpack_device(const tpi_seg* segs, int n, uint64_t total, const void* dev_src,
-                      uint64_t tile_bytes, const uint32_t* dev_crcs, uint64_t* dev_bad,
-                      uint64_t stream);
+// `host_segs` (may be NULL) is a host copy of the same descriptors: with it, transposed
+// views go through the LDS-tiled transpose kernels instead of element gathers.
+int tpi_pack_device(const tpi_seg* segs, const tpi_seg* host_segs, int n, uint64_t total,
+                    void* dev_dst, uint64_t tile_bytes, uint32_t* dev_crcs, uint64_t stream);
+int tpi_unpack_device(const tpi_seg* segs, const tpi_seg* host_segs, int n, uint64_t total,
+                      void* dev_src, uint64_t tile_bytes, const uint32_t* dev_crcs,
+                      uint64_t* dev_bad, uint64_t stream);
 
 // Host memory: NUMA-bound, populated, registered (pinned) mappings.
 // path == NULL -> anonymous; otherwise a shared file (e.g. /dev/shm/...) that outlives the

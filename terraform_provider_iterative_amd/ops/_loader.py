@@ -77,8 +77,8 @@ class HipLib:
             "tpi_stream_hash": (i32, [vp, i32, u64, u64, u64, vp, u64]),
             "tpi_crc32c_tiles": (i32, [vp, u64, u64, vp, u64]),
             "tpi_shard_hash": (i32, [vp, u64, u64, u64, vp, u64]),
-            "tpi_pack_device": (i32, [vp, i32, u64, vp, u64, vp, u64]),
-            "tpi_unpack_device": (i32, [vp, i32, u64, vp, u64, vp, vp, u64]),
+            "tpi_pack_device": (i32, [vp, vp, i32, u64, vp, u64, vp, u64]),
+            "tpi_unpack_device": (i32, [vp, vp, i32, u64, vp, u64, vp, vp, u64]),
             "tpi_host_map": (vp, [c.c_char_p, u64, i32, i32]),
             "tpi_host_unmap": (i32, [vp, u64]),
             "tpi_host_register": (i32, [vp, u64]),

@@ -3,7 +3,10 @@
 Stream layout: tensor payloads in plan order, each starting at a multiple of
 :data:`SEG_ALIGN` bytes, gaps zero-filled; tile ``t`` covers bytes ``[t*tile, (t+1)*tile)``
 and carries the standard CRC32C of those bytes.  Non-contiguous tensors (<= 6 dims) are
-gathered/scattered element-wise by the kernels, so no temporary contiguous copy is made.
+moved straight from/to their storage, no temporary contiguous copy: the view is first
+canonicalised (size-1 dims dropped, mergeable dims merged) and classified for the kernels
+(``csrc/hip/kernels.hip``): sliced rows move as 16-byte vectors, transposed matrices through
+LDS-tiled transposes, anything else element by element.
 """
 from __future__ import annotations
 
@@ -17,6 +20,7 @@ from .hashing import DEFAULT_TILE_BYTES, _is_device_tensor, _stream
 
 SEG_ALIGN = 256
 MAX_DIMS = 6
+SEG_CONTIG, SEG_STRIDED, SEG_ROWS, SEG_TRANSPOSE = 0, 1, 2, 3  # csrc/hip/tpi_hip.h
 SEG_DTYPE = np.dtype([
     ("ptr", "<u8"), ("off", "<u8"), ("nbytes", "<u8"), ("kind", "<u4"), ("elem", "<u4"),
     ("ndim", "<i4"), ("pad", "<i4"), ("sizes", "<i8", (MAX_DIMS,)),
@@ -27,6 +31,36 @@ assert SEG_DTYPE.itemsize == 136
 
 def align_up(value: int, alignment: int = SEG_ALIGN) -> int:
     return (value + alignment - 1) // alignment * alignment
+
+
+def canonical_view(shape, stride) -> List[Tuple[int, int]]:
+    """(size, stride) dims of a view with size-1 dims dropped and mergeable dims merged
+    (outer dim d folds into inner dim d+1 when stride[d] == stride[d+1] * size[d+1])."""
+    merged: List[Tuple[int, int]] = []
+    for size, st in zip(shape, stride):
+        size, st = int(size), int(st)
+        if size == 1:
+            continue
+        if merged and merged[-1][1] == st * size:
+            merged[-1] = (merged[-1][0] * size, st)
+        else:
+            merged.append((size, st))
+    return merged or [(1, 1)]
+
+
+def classify_view(dims: List[Tuple[int, int]], elem: int) -> int:
+    """Kernel path for a canonical view (see ``tpi_hip.h``)."""
+    strides = [st for _, st in dims]
+    if len(dims) == 1 and strides[0] == 1:
+        return SEG_CONTIG
+    if any(st <= 0 for st in strides):  # expanded (stride 0) views: element path
+        return SEG_STRIDED
+    if strides[-1] == 1:
+        return SEG_ROWS
+    if elem in (1, 2, 4, 8) and ((len(dims) == 2 and strides[0] == 1) or
+                                 (len(dims) == 3 and strides[1] == 1)):
+        return SEG_TRANSPOSE
+    return SEG_STRIDED
 
 
 @dataclass
@@ -110,17 +144,20 @@ class PackPlan:
             s["off"] = e.offset
             s["nbytes"] = e.nbytes
             s["elem"] = t.element_size()
-            if t.is_contiguous() or t.numel() <= 1:
-                s["kind"], s["ndim"] = 0, 0
+            dims = [(1, 1)] if t.is_contiguous() or t.numel() <= 1 else \
+                canonical_view(t.shape, t.stride())
+            kind = classify_view(dims, t.element_size())
+            if kind == SEG_CONTIG:
+                s["kind"], s["ndim"] = SEG_CONTIG, 0
             else:
-                if t.dim() > MAX_DIMS:
-                    raise ValueError("non-contiguous tensors with more than %d dims are not "
-                                     "supported (%r)" % (MAX_DIMS, name))
-                s["kind"], s["ndim"] = 1, t.dim()
+                if len(dims) > MAX_DIMS:
+                    raise ValueError("non-contiguous tensors with more than %d (merged) dims "
+                                     "are not supported (%r)" % (MAX_DIMS, name))
+                s["kind"], s["ndim"] = kind, len(dims)
                 s["sizes"][:] = 1
                 s["strides"][:] = 0
-                s["sizes"][:t.dim()] = t.shape
-                s["strides"][:t.dim()] = t.stride()
+                s["sizes"][:len(dims)] = [d[0] for d in dims]
+                s["strides"][:len(dims)] = [d[1] for d in dims]
         if len(devices) != 1:
             raise ValueError("all tensors of a plan must live on one device, got %s" % devices)
         self.device = devices.pop()
@@ -159,9 +196,10 @@ def pack(plan: PackPlan, out=None, threads: int = 8):
         segs = plan.device_segments()
         lib = hip()
         with torch.cuda.device(dev):
-            lib.check(lib.tpi_pack_device(segs.data_ptr(), len(plan.entries), plan.total,
-                                          out.data_ptr(), plan.tile_bytes, crcs.data_ptr(),
-                                          _stream(out)), "pack")
+            lib.check(lib.tpi_pack_device(segs.data_ptr(), plan.segs.ctypes.data,
+                                          len(plan.entries), plan.total, out.data_ptr(),
+                                          plan.tile_bytes, crcs.data_ptr(), _stream(out)),
+                      "pack")
         return out, crcs
     if out is None:
         out = np.empty(plan.total, dtype=np.uint8)
@@ -193,10 +231,10 @@ def unpack(plan: PackPlan, stream, crcs, threads: int = 8) -> Tuple[int, int]:
         segs = plan.device_segments()
         lib = hip()
         with torch.cuda.device(dev):
-            lib.check(lib.tpi_unpack_device(segs.data_ptr(), len(plan.entries), plan.total,
-                                            stream.data_ptr(), plan.tile_bytes,
-                                            crc_t.data_ptr(), bad.data_ptr(), _stream(stream)),
-                      "unpack")
+            lib.check(lib.tpi_unpack_device(segs.data_ptr(), plan.segs.ctypes.data,
+                                            len(plan.entries), plan.total, stream.data_ptr(),
+                                            plan.tile_bytes, crc_t.data_ptr(), bad.data_ptr(),
+                                            _stream(stream)), "unpack")
         count, first = (int(v) for v in bad.cpu().tolist())
         return count, (first if count else -1)
     from .hashing import host_buffer

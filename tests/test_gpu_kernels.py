@@ -247,3 +247,71 @@ def test_checkpointer_codec_device_roundtrip(tmp_path):
         ck2.load(path)
         torch.cuda.synchronize()
     assert all(torch.equal(dst[k], ref[k]) for k in ref)
+
+
+def _views(device):
+    """Non-contiguous views of every kernel path (kind in the comment)."""
+    g = torch.Generator().manual_seed(11)
+
+    def r(*shape, dtype=torch.float32):
+        return torch.randn(*shape, generator=g).to(dtype).to(device)
+
+    return {
+        "t_f32": r(300, 257).t(),                                   # TRANSPOSE 2-D
+        "t_bf16": r(129, 1000, dtype=torch.bfloat16).t(),           # TRANSPOSE 2-D
+        "t_u8": torch.randint(0, 255, (77, 333), dtype=torch.uint8, generator=g).to(device).t(),
+        "t_f64": r(65, 70, dtype=torch.float64).t(),                # TRANSPOSE 2-D, 8-byte
+        "batched": r(5, 40, 70).transpose(1, 2),                    # TRANSPOSE 3-D
+        "channels_last": r(4, 16, 9, 9, dtype=torch.bfloat16)
+        .contiguous(memory_format=torch.channels_last),             # TRANSPOSE 3-D (merged)
+        "rows": r(100, 300)[:, 7:290],                              # ROWS, unaligned rows
+        "rows_aligned": r(64, 512)[:, 64:448],                      # ROWS, vector path
+        "stride2": r(100001)[::2],                                  # STRIDED
+        "expanded": r(1, 50).expand(30, 50),                        # STRIDED (stride 0)
+        "contig": r(1000),
+    }
+
+
+@pytest.mark.parametrize("tile", [4096, 1 << 20])
+def test_view_kinds_pack_unpack_match_host(tile):
+    dev = _views("cuda")
+    host = {k: v.cpu() for k, v in dev.items()}
+    pd = PackPlan.from_tensors(dev, tile_bytes=tile)
+    ph = PackPlan.from_tensors(host, tile_bytes=tile)
+    sd, cd = pack(pd)
+    sh, ch = pack(ph)
+    assert np.array_equal(sd.cpu().numpy(), sh)
+    assert crc_array(cd).tolist() == ch.tolist()
+    dst = {k: torch.zeros_like(v) for k, v in dev.items()}  # zeros_like keeps the strides
+    assert all(dst[k].stride() == dev[k].stride() for k in dev if k != "expanded")
+    pd.bind(dst)
+    assert unpack(pd, sd, cd) == (0, -1)
+    torch.cuda.synchronize()
+    for k in dev:
+        assert torch.equal(dst[k], dev[k]), k
+
+
+@pytest.mark.parametrize("codec,mode", [("none", "sdma"), ("tpz1", "sdma"), ("none", "direct")])
+def test_view_kinds_through_checkpointer_chunks(codec, mode):
+    """Small chunks split the transposed views over many chunk windows (partial ranges)."""
+    from terraform_provider_iterative_amd.checkpoint import Checkpointer
+
+    src = _views("cuda")
+    ref = {k: v.clone() for k, v in src.items()}
+    with Checkpointer(src, tile_bytes=4096, chunk_bytes=16384, nbuf=2, mode=mode,
+                      codec=codec) as ck:
+        ck.save()
+        hplan = PackPlan.from_tensors({k: v.cpu() for k, v in ref.items()}, tile_bytes=4096)
+        hs, hc = pack(hplan)
+        assert ck.crcs.tolist() == hc.tolist()
+        for v in src.values():
+            v.zero_()
+        assert ck.restore().bad_tiles == 0
+        torch.cuda.synchronize()
+        for k in ref:
+            assert torch.equal(src[k], ref[k]), k
+        # incremental sync reads the views through the element path (no staging)
+        src["t_f32"][3, 5] += 1
+        assert ck.sync().dirty_tiles == ck.plan.ntiles
+        src["batched"][1, 2, 3] += 1
+        assert ck.sync().dirty_tiles == 1
