@@ -87,8 +87,20 @@ __device__ static inline int seg_find(const tpi_seg* __restrict__ segs, int n, u
   return lo;
 }
 
+// Element offset (in elements) of logical element e of a strided view.  32-bit div/mod when
+// the index fits (64-bit division is a long instruction sequence on CDNA).
 __device__ static inline uint64_t strided_offset(const tpi_seg& s, uint64_t e) {
   uint64_t off = 0;
+  if ((e >> 32) == 0) {
+    uint32_t e32 = (uint32_t)e;
+    for (int d = s.ndim - 1; d >= 0; --d) {
+      const uint32_t sz = (uint32_t)s.sizes[d];  // <= e's range whenever e fits 32 bits
+      const uint32_t q = e32 / sz;
+      off += (uint64_t)(e32 - q * sz) * (int64_t)s.strides[d];
+      e32 = q;
+    }
+    return off;
+  }
   for (int d = s.ndim - 1; d >= 0; --d) {
     uint64_t sz = (uint64_t)s.sizes[d];
     uint64_t idx = e % sz;
@@ -180,7 +192,10 @@ __device__ static inline void advance(const tpi_seg* __restrict__ segs, int n, u
 // Address of a word of a ROWS segment if it can be moved as one aligned dwordx4, else 0.
 __device__ static inline uint64_t rows_addr(const tpi_seg& s, uint64_t rel) {
   const uint64_t row_elems = (uint64_t)s.sizes[s.ndim - 1], row_bytes = row_elems * s.elem;
-  const uint64_t row = rel / row_bytes, within = rel - row * row_bytes;
+  uint64_t row;
+  if (((rel | row_bytes) >> 32) == 0) row = (uint32_t)rel / (uint32_t)row_bytes;
+  else row = rel / row_bytes;
+  const uint64_t within = rel - row * row_bytes;
   if (within + 16 > row_bytes) return 0;
   const uint64_t addr = s.ptr + strided_offset(s, row * row_elems) * s.elem + within;
   return (addr & 15) ? 0 : addr;
@@ -254,61 +269,64 @@ __device__ static inline void scatter16(const tpi_seg* __restrict__ segs, const 
 //
 // A TRANSPOSE view is (B, R, C) in logical (row-major) order with memory strides (sB, 1, sC):
 // memory-contiguous along R, while the stream is contiguous along C.  One 256-thread
-// workgroup moves a 64(R) x 64(C) element tile through LDS: reads are 64 consecutive R
-// elements per C column (coalesced), writes are 64 consecutive C elements per R row
-// (coalesced); the +1 column of padding keeps the LDS transpose free of bank conflicts.
+// workgroup moves a TR(R) x TC(C) element tile (TR * TC = 4096) through LDS: the load walks
+// the tile column by column with consecutive lanes on consecutive R (coalesced tensor
+// reads), the store walks it row by row with consecutive lanes on consecutive C (coalesced
+// stream writes).  When C <= 64 the tile spans whole logical rows (TC = C, TR = 4096 / C),
+// so its stream bytes are one contiguous run -- small-C views such as channels-last conv
+// weights (C = kh*kw) keep full tiles.  The +1 element of padding per LDS column keeps the
+// transpose free of bank conflicts.
 // DIR 0: tensor -> stream buffer (before the pack kernel), DIR 1: stream buffer -> tensor
 // (after the unpack kernel has verified the CRCs).  Only logical elements in [e_lo, e_hi)
 // (the part of the segment inside the current chunk) are touched.
+
+#define TP_ELEMS 4096
 
 struct TransposeArgs {
   uint64_t ptr;      // tensor base
   uint64_t sbuf;     // address of logical element 0 of the segment in the stream buffer
   int64_t B, R, C, sB, sC;
   uint64_t e_lo, e_hi;
-  uint64_t t_lo;     // first (b, r-tile) pair: b * RT + rt
+  uint64_t t_lo;     // first (b, r-tile) pair: b * rt + r-tile
   uint32_t ct;       // number of C tiles
   uint32_t rt;       // number of R tiles per batch
+  uint32_t tr, tc;   // tile shape (tr * tc == TP_ELEMS)
 };
 
 template <typename T, int DIR>
 __global__ __launch_bounds__(256) void k_transpose(TransposeArgs a) {
-  __shared__ T tile[64][65];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  __shared__ T tile[TP_ELEMS + 64];  // [tc][tr + 1]
+  const uint32_t tr = a.tr, tc = a.tc, ld = tr + 1;
   const uint64_t pair = a.t_lo + blockIdx.x / a.ct;
   const int64_t b = (int64_t)(pair / a.rt);
-  const int64_t r0 = (int64_t)(pair % a.rt) * 64;
-  const int64_t c0 = (int64_t)(blockIdx.x % a.ct) * 64;
-  T* tensor = (T*)a.ptr;
+  const int64_t r0 = (int64_t)(pair % a.rt) * tr;
+  const int64_t c0 = (int64_t)(blockIdx.x % a.ct) * tc;
+  T* tensor = (T*)a.ptr + b * a.sB;
   T* stream = (T*)a.sbuf;
   const uint64_t row0 = (uint64_t)(b * a.R) * (uint64_t)a.C;  // logical index of (b, 0, 0)
   if (DIR == 0) {
-#pragma unroll 4
-    for (int j = ty; j < 64; j += 4) {  // column c0+j, rows r0+tx: contiguous in memory
-      const int64_t r = r0 + tx, c = c0 + j;
-      if (r < a.R && c < a.C) tile[j][tx] = tensor[b * a.sB + r + c * a.sC];
+    for (uint32_t f = threadIdx.x; f < TP_ELEMS; f += 256) {  // column-major: lanes along R
+      const uint32_t c = f / tr, r = f - c * tr;
+      if (r0 + r < a.R && c0 + c < a.C) tile[c * ld + r] = tensor[r0 + r + (c0 + c) * a.sC];
     }
     __syncthreads();
-#pragma unroll 4
-    for (int j = ty; j < 64; j += 4) {  // row r0+j, columns c0+tx: contiguous in the stream
-      const int64_t r = r0 + j, c = c0 + tx;
-      const uint64_t e = row0 + (uint64_t)r * a.C + c;
-      if (r < a.R && c < a.C && e >= a.e_lo && e < a.e_hi) stream[e] = tile[tx][j];
+    for (uint32_t f = threadIdx.x; f < TP_ELEMS; f += 256) {  // row-major: lanes along C
+      const uint32_t r = f / tc, c = f - r * tc;
+      const uint64_t e = row0 + (uint64_t)(r0 + r) * a.C + (c0 + c);
+      if (r0 + r < a.R && c0 + c < a.C && e >= a.e_lo && e < a.e_hi) stream[e] = tile[c * ld + r];
     }
   } else {
-#pragma unroll 4
-    for (int j = ty; j < 64; j += 4) {
-      const int64_t r = r0 + j, c = c0 + tx;
-      const uint64_t e = row0 + (uint64_t)r * a.C + c;
-      if (r < a.R && c < a.C && e >= a.e_lo && e < a.e_hi) tile[tx][j] = stream[e];
+    for (uint32_t f = threadIdx.x; f < TP_ELEMS; f += 256) {
+      const uint32_t r = f / tc, c = f - r * tc;
+      const uint64_t e = row0 + (uint64_t)(r0 + r) * a.C + (c0 + c);
+      if (r0 + r < a.R && c0 + c < a.C && e >= a.e_lo && e < a.e_hi) tile[c * ld + r] = stream[e];
     }
     __syncthreads();
-#pragma unroll 4
-    for (int j = ty; j < 64; j += 4) {
-      const int64_t r = r0 + tx, c = c0 + j;
-      const uint64_t e = row0 + (uint64_t)r * a.C + c;
-      if (r < a.R && c < a.C && e >= a.e_lo && e < a.e_hi)
-        tensor[b * a.sB + r + c * a.sC] = tile[j][tx];
+    for (uint32_t f = threadIdx.x; f < TP_ELEMS; f += 256) {
+      const uint32_t c = f / tr, r = f - c * tr;
+      const uint64_t e = row0 + (uint64_t)(r0 + r) * a.C + (c0 + c);
+      if (r0 + r < a.R && c0 + c < a.C && e >= a.e_lo && e < a.e_hi)
+        tensor[r0 + r + (c0 + c) * a.sC] = tile[c * ld + r];
     }
   }
 }
@@ -387,12 +405,16 @@ __global__ __launch_bounds__(WG) void k_stream_crc(TileArgs a) {
   const uint64_t full_rows = tile_len / TPI_ROW_BYTES;
   for (; row + UNROLL <= full_rows; row += UNROLL) {
     u32x4 w[UNROLL];
+    uint32_t kept = 0;  // bit u: word u is a staged TRANSPOSE word already in place
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       const uint64_t rel = (row + u) * TPI_ROW_BYTES + lane * 16;
       if (MODE == MODE_PACK) {
         advance(a.segs, a.nseg, gbase + rel, cur);
         w[u] = gather16(a.segs, cur, gbase + rel, tbuf + rel, a.staged);
+        kept |= (cur.kind == TPI_SEG_TRANSPOSE && gbase + rel + 16 <= cur.off + cur.nbytes ? 1u
+                                                                                      : 0u)
+                << u;
       } else {
         w[u] = __builtin_nontemporal_load((const u32x4*)(tbuf + rel));
       }
@@ -401,7 +423,9 @@ __global__ __launch_bounds__(WG) void k_stream_crc(TileArgs a) {
     for (int u = 0; u < UNROLL; ++u) {
       const uint64_t rel = (row + u) * TPI_ROW_BYTES + lane * 16;
       if (MODE == MODE_PACK) {
-        __builtin_nontemporal_store(w[u], (u32x4*)(tbuf + rel));
+        // staged TRANSPOSE words are already in place (except a tail word's padding)
+        if (!(a.staged && ((kept >> u) & 1u)))
+          __builtin_nontemporal_store(w[u], (u32x4*)(tbuf + rel));
       } else if (MODE == MODE_UNPACK) {
         advance(a.segs, a.nseg, gbase + rel, cur);
         scatter16(a.segs, cur, gbase + rel, w[u], a.staged);
@@ -712,12 +736,15 @@ extern "C" hipError_t tpi_launch_transposes(const tpi_seg* host_segs, int nseg, 
     }
     a.e_lo = (lo - s.off) / s.elem;
     a.e_hi = (hi - s.off + s.elem - 1) / s.elem;
-    a.ct = (uint32_t)((a.C + 63) / 64);
-    a.rt = (uint32_t)((a.R + 63) / 64);
+    // tile shape: whole rows when C is small (TC = C), else 64 x 64
+    a.tc = a.C <= 64 ? (uint32_t)a.C : 64u;
+    a.tr = TP_ELEMS / a.tc;
+    a.ct = (uint32_t)((a.C + a.tc - 1) / a.tc);
+    a.rt = (uint32_t)((a.R + a.tr - 1) / a.tr);
     const uint64_t lr_lo = a.e_lo / a.C, lr_hi = (a.e_hi - 1) / a.C;  // logical rows b*R + r
     const uint64_t b_lo = lr_lo / a.R, b_hi = lr_hi / a.R;
-    a.t_lo = b_lo * a.rt + (lr_lo - b_lo * a.R) / 64;
-    const uint64_t t_hi = b_hi * a.rt + (lr_hi - b_hi * a.R) / 64;
+    a.t_lo = b_lo * a.rt + (lr_lo - b_lo * a.R) / a.tr;
+    const uint64_t t_hi = b_hi * a.rt + (lr_hi - b_hi * a.R) / a.tr;
     const uint64_t blocks = (t_hi - a.t_lo + 1) * a.ct;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
     const dim3 grid((unsigned)blocks), block(256);
