@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Pack/unpack throughput of non-contiguous tensor views (GB/s of payload):
-transposed 2-D (fp32 / bf16), row-sliced 2-D, channels-last 4-D, every-other-element."""
+transposed 2-D (fp32 / bf16), row-sliced 2-D, channels-last 4-D activations and conv weights
+(small C = kh*kw), every-other-element.  Each view is >= 150 MB so the pack kernel has a
+full grid (one workgroup per 1 MiB tile), as inside a checkpoint chunk."""
 from __future__ import annotations
 
 import json
@@ -19,14 +21,16 @@ def main():
     dev = torch.device("cuda", 0)
     cases = {
         "transpose_fp32": torch.randn(8192, 8192, device=dev).t(),
-        "transpose_bf16": torch.randn(8192, 8192, device=dev).to(torch.bfloat16).t(),
+        "transpose_bf16": torch.randn(16384, 8192, device=dev).to(torch.bfloat16).t(),
         "row_slice_fp32": torch.randn(8192, 8192, device=dev)[:, 100:8000],
-        "channels_last_bf16": torch.randn(64, 256, 32, 32, device=dev).to(torch.bfloat16)
+        "channels_last_bf16": torch.randn(256, 256, 32, 32, device=dev).to(torch.bfloat16)
         .contiguous(memory_format=torch.channels_last),
-        "stride2_fp32": torch.randn(1 << 26, device=dev)[::2],
+        "conv_weight_cl_bf16": torch.randn(16384, 512, 3, 3, device=dev).to(torch.bfloat16)
+        .contiguous(memory_format=torch.channels_last),
+        "stride2_fp32": torch.randn(1 << 27, device=dev)[::2],
     }
     out = {}
-    for name, t in cases.items():
+    for name, t in list(cases.items()):
         plan = PackPlan.from_tensors({name: t})
         stream, crcs = pack(plan)
         torch.cuda.synchronize()
@@ -43,7 +47,10 @@ def main():
         tu = (time.perf_counter() - t0) / iters
         nbytes = t.numel() * t.element_size()
         out[name] = {"pack_GBps": round(nbytes / tp / 1e9, 1),
-                     "unpack_GBps": round(nbytes / tu / 1e9, 1), "bad": int(bad)}
+                     "unpack_GBps": round(nbytes / tu / 1e9, 1), "bad": int(bad),
+                     "MB": round(nbytes / 1e6)}
+        del cases[name], plan, stream, crcs, t
+        torch.cuda.empty_cache()
     print(json.dumps(out))
 
 

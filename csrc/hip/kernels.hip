@@ -293,10 +293,14 @@ struct TransposeArgs {
   uint32_t tr, tc;   // tile shape (tr * tc == TP_ELEMS)
 };
 
-template <typename T, int DIR>
+// FULLROWS = false: 64 x 64 tiles (compile-time shape, shifts only).  FULLROWS = true: the
+// tile is tr whole logical rows of C (< 64) elements, so its stream bytes are contiguous.
+template <typename T, int DIR, bool FULLROWS>
 __global__ __launch_bounds__(256) void k_transpose(TransposeArgs a) {
   __shared__ T tile[TP_ELEMS + 64];  // [tc][tr + 1]
-  const uint32_t tr = a.tr, tc = a.tc, ld = tr + 1;
+  const uint32_t tr = FULLROWS ? a.tr : 64u, tc = FULLROWS ? a.tc : 64u, ld = tr + 1;
+  const uint32_t n = FULLROWS ? tr * tc : (uint32_t)TP_ELEMS;
+  const uint32_t trs = FULLROWS ? (uint32_t)__ffs(tr) - 1 : 6u;  // tr is a power of two
   const uint64_t pair = a.t_lo + blockIdx.x / a.ct;
   const int64_t b = (int64_t)(pair / a.rt);
   const int64_t r0 = (int64_t)(pair % a.rt) * tr;
@@ -305,29 +309,45 @@ __global__ __launch_bounds__(256) void k_transpose(TransposeArgs a) {
   T* stream = (T*)a.sbuf;
   const uint64_t row0 = (uint64_t)(b * a.R) * (uint64_t)a.C;  // logical index of (b, 0, 0)
   if (DIR == 0) {
-    for (uint32_t f = threadIdx.x; f < TP_ELEMS; f += 256) {  // column-major: lanes along R
-      const uint32_t c = f / tr, r = f - c * tr;
+#pragma unroll 4
+    for (uint32_t f = threadIdx.x; f < n; f += 256) {  // column-major: lanes along R
+      const uint32_t c = f >> trs, r = f & (tr - 1);
       if (r0 + r < a.R && c0 + c < a.C) tile[c * ld + r] = tensor[r0 + r + (c0 + c) * a.sC];
     }
     __syncthreads();
-    for (uint32_t f = threadIdx.x; f < TP_ELEMS; f += 256) {  // row-major: lanes along C
+#pragma unroll 4
+    for (uint32_t f = threadIdx.x; f < n; f += 256) {  // row-major: lanes along C
       const uint32_t r = f / tc, c = f - r * tc;
       const uint64_t e = row0 + (uint64_t)(r0 + r) * a.C + (c0 + c);
       if (r0 + r < a.R && c0 + c < a.C && e >= a.e_lo && e < a.e_hi) stream[e] = tile[c * ld + r];
     }
   } else {
-    for (uint32_t f = threadIdx.x; f < TP_ELEMS; f += 256) {
+#pragma unroll 4
+    for (uint32_t f = threadIdx.x; f < n; f += 256) {
       const uint32_t r = f / tc, c = f - r * tc;
       const uint64_t e = row0 + (uint64_t)(r0 + r) * a.C + (c0 + c);
       if (r0 + r < a.R && c0 + c < a.C && e >= a.e_lo && e < a.e_hi) tile[c * ld + r] = stream[e];
     }
     __syncthreads();
-    for (uint32_t f = threadIdx.x; f < TP_ELEMS; f += 256) {
-      const uint32_t c = f / tr, r = f - c * tr;
+#pragma unroll 4
+    for (uint32_t f = threadIdx.x; f < n; f += 256) {
+      const uint32_t c = f >> trs, r = f & (tr - 1);
       const uint64_t e = row0 + (uint64_t)(r0 + r) * a.C + (c0 + c);
       if (r0 + r < a.R && c0 + c < a.C && e >= a.e_lo && e < a.e_hi)
         tensor[r0 + r + (c0 + c) * a.sC] = tile[c * ld + r];
     }
+  }
+}
+
+template <typename T>
+static void launch_transpose(const TransposeArgs& a, int dir, dim3 grid, hipStream_t stream) {
+  const bool full = a.tc != 64;
+  if (dir == 0) {
+    if (full) hipLaunchKernelGGL((k_transpose<T, 0, true>), grid, dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((k_transpose<T, 0, false>), grid, dim3(256), 0, stream, a);
+  } else {
+    if (full) hipLaunchKernelGGL((k_transpose<T, 1, true>), grid, dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((k_transpose<T, 1, false>), grid, dim3(256), 0, stream, a);
   }
 }
 
@@ -736,9 +756,11 @@ extern "C" hipError_t tpi_launch_transposes(const tpi_seg* host_segs, int nseg, 
     }
     a.e_lo = (lo - s.off) / s.elem;
     a.e_hi = (hi - s.off + s.elem - 1) / s.elem;
-    // tile shape: whole rows when C is small (TC = C), else 64 x 64
-    a.tc = a.C <= 64 ? (uint32_t)a.C : 64u;
-    a.tr = TP_ELEMS / a.tc;
+    // tile shape: whole rows when C < 64 (TC = C, TR = largest power of two with
+    // TR * C <= 4096), else 64 x 64
+    a.tc = a.C < 64 ? (uint32_t)a.C : 64u;
+    a.tr = 64;
+    while (a.tc < 64 && a.tr * 2 * a.tc <= TP_ELEMS) a.tr *= 2;
     a.ct = (uint32_t)((a.C + a.tc - 1) / a.tc);
     a.rt = (uint32_t)((a.R + a.tr - 1) / a.tr);
     const uint64_t lr_lo = a.e_lo / a.C, lr_hi = (a.e_hi - 1) / a.C;  // logical rows b*R + r
@@ -747,16 +769,12 @@ extern "C" hipError_t tpi_launch_transposes(const tpi_seg* host_segs, int nseg, 
     const uint64_t t_hi = b_hi * a.rt + (lr_hi - b_hi * a.R) / a.tr;
     const uint64_t blocks = (t_hi - a.t_lo + 1) * a.ct;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    const dim3 grid((unsigned)blocks), block(256);
-    switch (s.elem * 2 + (dir ? 1 : 0)) {
-      case 2: hipLaunchKernelGGL((k_transpose<uint8_t, 0>), grid, block, 0, stream, a); break;
-      case 3: hipLaunchKernelGGL((k_transpose<uint8_t, 1>), grid, block, 0, stream, a); break;
-      case 4: hipLaunchKernelGGL((k_transpose<uint16_t, 0>), grid, block, 0, stream, a); break;
-      case 5: hipLaunchKernelGGL((k_transpose<uint16_t, 1>), grid, block, 0, stream, a); break;
-      case 8: hipLaunchKernelGGL((k_transpose<uint32_t, 0>), grid, block, 0, stream, a); break;
-      case 9: hipLaunchKernelGGL((k_transpose<uint32_t, 1>), grid, block, 0, stream, a); break;
-      case 16: hipLaunchKernelGGL((k_transpose<uint64_t, 0>), grid, block, 0, stream, a); break;
-      case 17: hipLaunchKernelGGL((k_transpose<uint64_t, 1>), grid, block, 0, stream, a); break;
+    const dim3 grid((unsigned)blocks);
+    switch (s.elem) {
+      case 1: launch_transpose<uint8_t>(a, dir, grid, stream); break;
+      case 2: launch_transpose<uint16_t>(a, dir, grid, stream); break;
+      case 4: launch_transpose<uint32_t>(a, dir, grid, stream); break;
+      case 8: launch_transpose<uint64_t>(a, dir, grid, stream); break;
       default: return hipErrorInvalidValue;  // the host only emits TRANSPOSE for 1/2/4/8
     }
     const hipError_t err = hipGetLastError();
