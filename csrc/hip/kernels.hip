@@ -197,7 +197,9 @@ __device__ static inline uint64_t rows_addr(const tpi_seg& s, uint64_t rel) {
   else row = rel / row_bytes;
   const uint64_t within = rel - row * row_bytes;
   if (within + 16 > row_bytes) return 0;
-  const uint64_t addr = s.ptr + strided_offset(s, row * row_elems) * s.elem + within;
+  const uint64_t outer = s.ndim == 2 ? row * (uint64_t)s.strides[0]  // matrix slice: no div
+                                     : strided_offset(s, row * row_elems);
+  const uint64_t addr = s.ptr + outer * s.elem + within;
   return (addr & 15) ? 0 : addr;
 }
 
@@ -250,6 +252,8 @@ __device__ static inline u32x4 gather16(const tpi_seg* __restrict__ segs, const 
   const uint64_t addr = c.ptr + rel;
   if (c.kind == TPI_SEG_CONTIG && rel + 16 <= c.nbytes && (addr & 15) == 0)
     return __builtin_nontemporal_load((const u32x4*)addr);
+  if (c.kind == TPI_SEG_TRANSPOSE && staged && rel + 16 <= c.nbytes)
+    return *(const u32x4*)sbuf;  // placed by k_transpose
   return gather_other(segs, c.idx, rel, sbuf, staged);
 }
 
@@ -262,6 +266,7 @@ __device__ static inline void scatter16(const tpi_seg* __restrict__ segs, const 
     *(u32x4*)addr = w;
     return;
   }
+  if (c.kind == TPI_SEG_TRANSPOSE && staged) return;  // k_transpose scatters it afterwards
   scatter_other(segs, c.idx, rel, w, staged);
 }
 
