@@ -296,13 +296,44 @@ def machine_logs(data: Dict[str, Any]) -> str:
 
 RUNNER_TEMPLATE = """#!/bin/sh
 # CML runner on the node-local runtime ({cloud}); generated by terraform-provider-iterative_amd
-{startup}
+{exports}{startup}
 HOME="$(mktemp -d)" exec $(command -v cml-runner || echo "$(command -v cml-internal || echo cml) runner") \\
 {flags}
 """
 
+# Credentials the runner's own `cml`/`leo` calls need, per cloud (resource_runner.go:329-349).
+RUNNER_CREDENTIALS = {
+    "aws": ("AWS_SECRET_ACCESS_KEY", "AWS_ACCESS_KEY_ID", "AWS_SESSION_TOKEN"),
+    "azure": ("AZURE_CLIENT_ID", "AZURE_CLIENT_SECRET", "AZURE_SUBSCRIPTION_ID",
+              "AZURE_TENANT_ID"),
+    "gcp": ("GOOGLE_APPLICATION_CREDENTIALS_DATA", "CML_GCP_ACCESS_TOKEN"),
+    "kubernetes": ("KUBERNETES_CONFIGURATION",),
+    "local": ("TPI_STATE_ROOT",),
+    "mi355x": ("TPI_STATE_ROOT", "TPI_MI355X_GPUS"),
+}
 
-def render_runner_script(data: Dict[str, Any]) -> str:
+
+def runner_credentials(cloud: str, environ=None) -> List[Tuple[str, str]]:
+    """(name, value) exports for the runner script.  GCP credentials are only forwarded when
+    they parse as a credentials JSON document, like ``gcp.LoadGCPCredentials``."""
+    import json
+
+    environ = os.environ if environ is None else environ
+    out = []
+    for name in RUNNER_CREDENTIALS.get(cloud or "", ()):
+        value = environ.get(name, "")
+        if name == "GOOGLE_APPLICATION_CREDENTIALS_DATA" and value:
+            try:
+                json.loads(value)
+            except ValueError:
+                value = ""
+        if cloud in ("local", "mi355x") and not value:
+            continue  # node defaults apply
+        out.append((name, value))
+    return out
+
+
+def render_runner_script(data: Dict[str, Any], environ=None) -> str:
     """Runner startup script (the node equivalent of ``renderScript``,
     ``resource_runner.go:298-400``): decoded user startup script + ``cml runner`` flags."""
     startup = ""
@@ -320,26 +351,39 @@ def render_runner_script(data: Dict[str, Any]) -> str:
         flags.append("--docker-volumes %s" % shell_quote(volume))
     if data.get("tf_resource"):
         flags.append("--tf-resource %s" % shell_quote(data["tf_resource"]))
+    exports = "".join("export %s=%s\n" % (name, shell_quote(value))
+                      for name, value in runner_credentials(data.get("cloud") or "", environ))
     return RUNNER_TEMPLATE.format(cloud=data.get("cloud") or "-", startup=startup,
+                                  exports=exports,
                                   flags=" \\\n".join("  " + f for f in flags))
+
+
+def _go_json(value) -> str:
+    """``encoding/json.Marshal`` byte-for-byte: compact, UTF-8, HTML-safe escapes."""
+    import json
+
+    text = json.dumps(value, separators=(",", ":"), ensure_ascii=False)
+    for char, esc in (("<", "\\u003c"), (">", "\\u003e"), ("&", "\\u0026"),
+                      ("\u2028", "\\u2028"), ("\u2029", "\\u2029")):
+        text = text.replace(char, esc)
+    return text
 
 
 def runner_tf_resource(data: Dict[str, Any], rid: str) -> str:
     """Synthetic state resource handed to ``cml runner --tf-resource`` (``ResourceType``,
-    ``resource_runner.go:405-531``) so the runner can destroy itself via the state."""
-    import json
-
-    attrs = {"id": rid, "name": rid, "cloud": data.get("cloud") or "",
-             "spot": bool(data.get("spot")), "region": data.get("region") or "",
-             "labels": "", "idle_timeout": int(data.get("idle_timeout") or 0), "repo": "",
-             "token": "", "driver": "", "custom_data": "", "image": "", "instance_gpu": "",
-             "instance_hdd_size": int(data.get("instance_hdd_size") or 0), "instance_ip": "",
-             "instance_launch_time": "", "instance_type": "", "ssh_name": "",
-             "ssh_private": "", "ssh_public": "", "aws_security_group": ""}
+    ``resource_runner.go:405-531``) so the runner can destroy itself via the state.  Field
+    order and encoding follow the Go structs, so the base64 matches the reference's."""
+    attrs = {"name": rid, "labels": "", "idle_timeout": int(data.get("idle_timeout") or 0),
+             "repo": "", "token": "", "driver": "", "cloud": data.get("cloud") or "",
+             "spot": bool(data.get("spot")), "custom_data": "", "id": rid, "image": "",
+             "instance_gpu": "", "instance_hdd_size": int(data.get("instance_hdd_size") or 0),
+             "instance_ip": "", "instance_launch_time": "", "instance_type": "",
+             "region": data.get("region") or "", "ssh_name": "", "ssh_private": "",
+             "ssh_public": "", "aws_security_group": ""}
     resource = {"mode": "managed", "type": "iterative_cml_runner", "name": "runner",
                 "provider": 'provider["registry.terraform.io/iterative/iterative"]',
                 "instances": [{"private": "", "schema_version": 0, "attributes": attrs}]}
-    return base64.b64encode(json.dumps(resource).encode()).decode()
+    return base64.b64encode(_go_json(resource).encode()).decode()
 
 
 def runner_create(data: Dict[str, Any], timeouts: Optional[Dict[str, float]] = None,

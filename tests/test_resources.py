@@ -136,3 +136,48 @@ def test_runner_requires_token(monkeypatch):
     data = normalize("iterative_cml_runner", {"repo": "r", "driver": "github", "cloud": "local"})
     result = resources.runner_create(data)
     assert not result.ok and "Token not found" in result.diagnostics[0].summary
+
+
+# Environment / schema fixtures of the reference's runner golden test
+# (iterative/resource_runner_test.go:56-89); the goldens are copied from its testdata.
+_GOLDEN_ENV = {
+    "AWS_SECRET_ACCESS_KEY": '0 value with "quotes" and spaces',
+    "AWS_ACCESS_KEY_ID": '1 value with "quotes" and spaces',
+    "AWS_SESSION_TOKEN": '2 value with "quotes" and spaces',
+    "AZURE_CLIENT_ID": '3 value with "quotes" and spaces',
+    "AZURE_CLIENT_SECRET": '4 value with "quotes" and spaces',
+    "AZURE_SUBSCRIPTION_ID": '5 value with "quotes" and spaces',
+    "AZURE_TENANT_ID": '6 value with "quotes" and spaces',
+    "GOOGLE_APPLICATION_CREDENTIALS_DATA": '7 value with "quotes" and spaces',
+    "KUBERNETES_CONFIGURATION": '8 value with "quotes" and spaces',
+}
+_GOLDEN_DIR = os.path.join(os.path.dirname(__file__), "testdata", "runner")
+
+
+def _golden(cloud):
+    with open(os.path.join(_GOLDEN_DIR, "script_template_cloud_%s.golden" % cloud)) as handle:
+        return handle.read()
+
+
+@pytest.mark.parametrize("cloud", ["aws", "azure", "gcp", "kubernetes", "invalid"])
+def test_runner_golden_parity(cloud):
+    """Credential exports and the --tf-resource payload match the reference's goldens."""
+    golden = _golden(cloud)
+    data = {"cloud": cloud, "region": '9 value with "quotes" and spaces',
+            "name": "", "single": True, "idle_timeout": 11, "instance_hdd_size": 12,
+            "token": '13 value with "quotes" and spaces',
+            "repo": '14 value with "quotes" and spaces',
+            "driver": '15 value with "quotes" and spaces',
+            "labels": '16 value with "quotes" and spaces'}
+    tf = resources.runner_tf_resource(data, "")
+    assert "--tf-resource " + tf in golden  # byte-identical JSON + base64
+    script = resources.render_runner_script(dict(data, tf_resource=tf), _GOLDEN_ENV)
+    exports = [line for line in script.splitlines() if line.startswith("export ")]
+    want = [line for line in golden.splitlines()
+            if line.startswith("export ") and "DEBIAN_FRONTEND" not in line]
+    assert exports == want
+    for flag in ("--labels", "--idle-timeout", "--driver", "--repo", "--token"):
+        mine = [line.strip(" \\") for line in script.splitlines() if line.strip().startswith(flag)]
+        theirs = [line.strip(" \\") for line in golden.splitlines()
+                  if line.strip().startswith(flag)]
+        assert mine == theirs, flag
