@@ -182,6 +182,30 @@ class Connection:
             config[key] = value.strip("'\"")
         return cls(backend=parts[0], container=rest, config=config)
 
+    @classmethod
+    def existing_bucket(cls, provider: str, container: str, path: str = "",
+                        config: Optional[Dict[str, str]] = None,
+                        credentials: Optional[Dict[str, str]] = None) -> "Connection":
+        """Connection of a pre-allocated ``storage.container`` per cloud (the reference's
+        ``ExistingS3Bucket`` / ``ExistingBucket`` / ``ExistingBlobContainer`` data sources,
+        ``task/{aws,gcp,az}/resources/data_source_*.go``)."""
+        config = dict(config or {})
+        credentials = credentials or {}
+        if provider == "aws":
+            return cls("s3", container, path, {
+                "provider": "AWS", "region": config.get("region", ""),
+                "access_key_id": credentials.get("AccessKeyID", ""),
+                "secret_access_key": credentials.get("SecretAccessKey", ""),
+                "session_token": credentials.get("SessionToken", "")})
+        if provider == "gcp":
+            return cls("googlecloudstorage", container, path, {
+                "service_account_credentials": credentials.get("ApplicationCredentials", "")})
+        if provider == "az":
+            return cls("azureblob", container, path, config)
+        if provider in ("local", "mi355x"):
+            return cls("local", container, path, config)
+        raise ValueError("no storage backend for provider %r" % provider)
+
     def local_path(self) -> str:
         if self.backend != "local":
             raise NotImplementedError(

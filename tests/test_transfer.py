@@ -123,3 +123,22 @@ def test_human_size():
     assert tr.human_size(0) == "0B"
     assert tr.human_size(1500) == "1.5kB"
     assert tr.human_size(10e9) == "10GB"
+
+
+def test_existing_bucket_connection_strings():
+    """Vectors of task/{aws,gcp}/resources/data_source_bucket_test.go."""
+    aws = tr.Connection.existing_bucket(
+        "aws", "pre-created-bucket", "subdirectory", {"region": "us-east-1"},
+        {"AccessKeyID": "access-key-id", "SecretAccessKey": "secret-access-key",
+         "SessionToken": "session-token"})
+    assert str(aws) == (":s3,access_key_id='access-key-id',provider='AWS',region='us-east-1',"
+                        "secret_access_key='secret-access-key',session_token='session-token'"
+                        ":pre-created-bucket/subdirectory")
+    gcp = tr.Connection.existing_bucket("gcp", "pre-created-bucket", "subdirectory",
+                                        credentials={"ApplicationCredentials":
+                                                     "gcp-credentials-json"})
+    assert str(gcp) == (":googlecloudstorage,service_account_credentials='gcp-credentials-json'"
+                        ":pre-created-bucket/subdirectory")
+    az = tr.Connection.existing_bucket("az", "container", "sub",
+                                       {"account": "a", "key": "k"})
+    assert str(az) == ":azureblob,account='a',key='k':container/sub"
