@@ -36,9 +36,13 @@ class RemoteProviderUnavailable(RuntimeError):
 
 class RemoteTask(Task):
     def __init__(self, cloud: Cloud, identifier: Identifier, task: TaskSpec):
+        from ..models.permissions import parse_permission_set
+
         self.cloud = cloud
         self.identifier = identifier
         self.task = task
+        # configuration errors first, with the reference's messages
+        parse_permission_set(cloud.provider, task.permission_set or "")
 
     def _fail(self, *_args, **_kwargs):
         raise RemoteProviderUnavailable(self.cloud.provider)

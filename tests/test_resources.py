@@ -181,3 +181,25 @@ def test_runner_golden_parity(cloud):
         theirs = [line.strip(" \\") for line in golden.splitlines()
                   if line.strip().startswith(flag)]
         assert mine == theirs, flag
+
+
+def test_permission_set_grammar():
+    from terraform_provider_iterative_amd.models.permissions import (PermissionSetError,
+                                                                     parse_permission_set)
+
+    # task/az/resources/data_source_permission_set_test.go vectors
+    ok = ("/subscriptions/cse78759-ef49-49f7-b371-f6841fa82182/resourceGroups/resource-group"
+          "/providers/Microsoft.ManagedIdentity/userAssignedIdentities/managed-identity")
+    assert parse_permission_set("az", ok + ", ")["user_assigned_identities"] == [ok]
+    with pytest.raises(PermissionSetError) as err:
+        parse_permission_set("az", "/subscriptions/no-valid")
+    assert str(err.value) == 'invalid user-assigned identity id: "/subscriptions/no-valid"'
+    assert parse_permission_set("aws", "arn:aws:iam::123:instance-profile/x")["arn"]
+    with pytest.raises(PermissionSetError, match="invalid IAM Instance Profile"):
+        parse_permission_set("aws", "role/x")
+    gcp = parse_permission_set("gcp", "sa@p.iam.gserviceaccount.com,scopes=storage-rw,custom")
+    assert gcp["scopes"] == ["https://www.googleapis.com/auth/devstorage.read_write", "custom"]
+    with pytest.raises(PermissionSetError, match="at least one scope"):
+        parse_permission_set("gcp", "sa@p")
+    assert parse_permission_set("k8s", "runner-sa") == {"service_account": "runner-sa"}
+    assert parse_permission_set("aws", "") is None
