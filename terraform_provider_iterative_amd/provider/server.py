@@ -24,7 +24,7 @@ import sys
 import tempfile
 import threading
 from concurrent import futures
-from typing import Any, Dict, List, Optional, Tuple
+from typing import Any, Dict, Optional, Tuple
 
 import grpc
 

@@ -1,7 +1,6 @@
 """Runtime on a real MI355X (``pytest -m gpu``): HBM workdir staging, the mi355x provider
 placing a rank on the GPU, and preempt/resume of a bf16 training job with device tensors."""
 import os
-import subprocess
 import sys
 import time
 

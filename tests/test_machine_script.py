@@ -5,7 +5,6 @@ import os
 import subprocess
 import time
 
-import pytest
 
 from terraform_provider_iterative_amd import _build
 from terraform_provider_iterative_amd.models.values import Variables

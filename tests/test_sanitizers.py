@@ -7,7 +7,6 @@ import subprocess
 
 import pytest
 
-from terraform_provider_iterative_amd import _build
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SAN = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer",
