@@ -29,7 +29,7 @@ __device__ static inline uint64_t umin64(uint64_t a, uint64_t b) { return a < b 
 
 enum { MODE_PACK = 0, MODE_UNPACK = 1, MODE_CRC = 2 };
 #define WG 256
-#define UNROLL 4
+#define UNROLL 8
 #define LDS_WORDS (16 * 256 + 4 * 256 + WG)
 
 __device__ static inline uint32_t raw16(const uint32_t* __restrict__ s, u32x4 w) {
