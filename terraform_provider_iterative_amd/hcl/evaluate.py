@@ -168,6 +168,21 @@ class Context:
                 return obj[int(_number(key))]
             return obj[_tostring(key)]
         if isinstance(node, Call):
+            if node.name in ("try", "can"):  # lazy: errors in an argument are the point
+                for arg in node.args:
+                    try:
+                        value = self.eval(arg)
+                    except (EvaluationError, KeyError, IndexError, TypeError, ValueError,
+                            AttributeError):
+                        if node.name == "can":
+                            return False
+                        continue
+                    if value is UNKNOWN:
+                        return UNKNOWN
+                    return True if node.name == "can" else value
+                if node.name == "can":
+                    return False
+                raise EvaluationError("try(): no expression succeeded")
             fn = self.functions.get(node.name)
             if fn is None:
                 raise EvaluationError("unknown function %s()" % node.name)

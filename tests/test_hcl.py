@@ -72,6 +72,10 @@ def test_expressions():
     assert ev('"\\u00e9\\n"') == "é\n"
     assert ev("!true") is False and ev("-(2)") == -2
     assert ev('{ "quoted key" = 1, bare: 2 }') == {"quoted key": 1, "bare": 2}
+    # docs/resources/task.md:94-104: try(join("\n", iterative_task.example.logs), "")
+    assert ev('try(join("\\n", var.missing), "")') == ""
+    assert ev('try(var.n * 2, 0)') == 6
+    assert ev('can(var.missing)') is False and ev('can(var.n)') is True
 
 
 def test_heredoc_plain_and_comments():
