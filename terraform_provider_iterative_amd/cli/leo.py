@@ -28,6 +28,7 @@ from ..models.values import (SPOT_DISABLED, SPOT_ENABLED, Environment, Firewall,
 from ..utils.identifier import new_random_identifier, parse_identifier
 from ..utils.logger import reduce_status, setup as setup_logging
 from ..utils.shell import quote_command
+from ..utils.watch import DirectoryWatch
 
 log = logging.getLogger("tpi")
 
@@ -196,6 +197,18 @@ def _log_lines(logs: List[str], timestamps: bool) -> List[str]:
 def cmd_read(args, cloud: Cloud, poll: float = 3.0) -> int:
     ident = parse_identifier(args.name)
     task = backends.new(cloud, ident, TaskSpec(environment=Environment(image="ubuntu")))
+    # node tasks: wake up on writes to the reports/supervisor directories (inotify) rather
+    # than sleeping the full poll interval
+    watch_dirs = [getattr(task, "reports_dir", None), getattr(task, "sup_dir", None)]
+    watch = DirectoryWatch([d for d in watch_dirs if d]) if args.follow else None
+    try:
+        return _read_loop(args, task, watch, poll)
+    finally:
+        if watch is not None:
+            watch.close()
+
+
+def _read_loop(args, task, watch, poll: float) -> int:
     last = 0
     first = True
     waiting = False
@@ -230,7 +243,10 @@ def cmd_read(args, cloud: Cloud, poll: float = 3.0) -> int:
             return 0
         if status == "failed":
             return 1
-        time.sleep(poll)
+        if watch is not None:
+            watch.wait(poll)
+        else:
+            time.sleep(poll)
 
 
 def cmd_list(args, cloud: Cloud) -> int:

@@ -185,3 +185,20 @@ def test_leo_reads_main_tf_defaults(tmp_path, env):
     d = config_defaults(str(tmp_path), environ={"TASK_MACHINE": "l"})
     assert d["cloud"] == "local" and d["machine"] == "l" and d["output"] == "results"
     assert d["environment"]["GREETING"] == "hello"
+
+
+def test_leo_read_follow_wakes_on_log_writes(tmp_path, env):
+    """Node tasks: --follow wakes on inotify events instead of the 3 s poll of the reference
+    (read.go:124), so it returns right after the task finishes."""
+    base = LEO + ["--cloud", "local"]
+    r = run(base + ["create", "--workdir", str(tmp_path), "--", "sh", "-c",
+                    "echo first; sleep 0.7; echo second"], str(tmp_path), env)
+    ident = r.stdout.strip().splitlines()[-1]
+    import time
+
+    t0 = time.time()
+    follow = run(base + ["read", "--follow", ident], str(tmp_path), env, timeout=60)
+    elapsed = time.time() - t0
+    assert "first" in follow.stdout and "second" in follow.stdout
+    assert elapsed < 2.5, elapsed  # 3 s polling would need >= 3 s
+    run(base + ["delete", ident], str(tmp_path), env)
