@@ -279,8 +279,8 @@ __device__ static inline void scatter16(const tpi_seg* __restrict__ segs, const 
 // reads), the store walks it row by row with consecutive lanes on consecutive C (coalesced
 // stream writes).  When C <= 64 the tile spans whole logical rows (TC = C, TR = 4096 / C),
 // so its stream bytes are one contiguous run -- small-C views such as channels-last conv
-// weights (C = kh*kw) keep full tiles.  The +1 element of padding per LDS column keeps the
-// transpose free of bank conflicts.
+// weights (C = kh*kw) keep full tiles.  Each LDS column is padded to an odd number of banks,
+// which keeps the transpose (nearly) free of bank conflicts (profiles/rocprof_views_round1.md).
 // DIR 0: tensor -> stream buffer (before the pack kernel), DIR 1: stream buffer -> tensor
 // (after the unpack kernel has verified the CRCs).  Only logical elements in [e_lo, e_hi)
 // (the part of the segment inside the current chunk) are touched.
@@ -302,8 +302,10 @@ struct TransposeArgs {
 // tile is tr whole logical rows of C (< 64) elements, so its stream bytes are contiguous.
 template <typename T, int DIR, bool FULLROWS>
 __global__ __launch_bounds__(256) void k_transpose(TransposeArgs a) {
-  __shared__ T tile[TP_ELEMS + 64];  // [tc][tr + 1]
-  const uint32_t tr = FULLROWS ? a.tr : 64u, tc = FULLROWS ? a.tc : 64u, ld = tr + 1;
+  // [tc][tr + pad]: the column stride is an odd number of 4-byte banks for every T <= 4 bytes
+  constexpr uint32_t pad = sizeof(T) < 4 ? 4 / sizeof(T) : 1;
+  __shared__ T tile[TP_ELEMS + 64 * 4];
+  const uint32_t tr = FULLROWS ? a.tr : 64u, tc = FULLROWS ? a.tc : 64u, ld = tr + pad;
   const uint32_t n = FULLROWS ? tr * tc : (uint32_t)TP_ELEMS;
   const uint32_t trs = FULLROWS ? (uint32_t)__ffs(tr) - 1 : 6u;  // tr is a power of two
   const uint64_t pair = a.t_lo + blockIdx.x / a.ct;
