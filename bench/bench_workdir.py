@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Config 2: 1 x MI355X ``iterative_task`` with a large synthetic workdir + PyTorch-ROCm
-``train.py`` (examples/train.py), driven through ``tpi apply``/``destroy`` like a user.
+``train.py`` (examples/train/train.py), driven through ``tpi apply``/``destroy`` like a user.
 
 Reports apply -> first-log latency, workdir push GB/s (task storage), HBM staging GB/s,
 training step time and the end-to-end wall time.
@@ -34,7 +34,7 @@ resource "iterative_task" "train" {
   script = <<-END
     #!/bin/sh
     echo "task started on $TPI_MACHINE_IDENTITY"
-    exec %(python)s %(root)s/examples/train.py --stage --steps %(steps)d
+    exec %(python)s %(root)s/examples/train/train.py --stage --steps %(steps)d
   END
 }
 '''

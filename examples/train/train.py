@@ -18,8 +18,8 @@ import os
 import sys
 import time
 
-ROOT = os.environ.get("TPI_FRAMEWORK_ROOT") or os.path.dirname(os.path.dirname(
-    os.path.abspath(__file__)))
+ROOT = os.environ.get("TPI_FRAMEWORK_ROOT") or os.path.dirname(os.path.dirname(os.path.dirname(
+    os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
 

@@ -73,7 +73,7 @@ def test_mi355x_task_sees_its_gpu(cloud):
 
 def test_preempt_resume_training_on_gpu(cloud, tmp_path):
     env = {"TPI_FRAMEWORK_ROOT": ROOT, "TPI_TASK": "true"}
-    script = ("#!/bin/sh\nexec %s %s/examples/train.py --steps 60 --hidden 256 --layers 2 "
+    script = ("#!/bin/sh\nexec %s %s/examples/train/train.py --steps 60 --hidden 256 --layers 2 "
               "--batch 4 --seq 64 --sleep 0.05\n" % (sys.executable, ROOT))
     spec = Task(size=Size(machine="m+mi355x"),
                 environment=Environment(script=script, timeout=600, variables=Variables(env)))
