@@ -26,9 +26,7 @@ from ..models.values import (Environment, Firewall, FirewallRule, NotImplemented
 from ..utils import analytics
 from ..utils.identifier import (new_deterministic_identifier, new_random_identifier,
                                 parse_identifier)
-from ..utils.runner_status import has_status
 from ..utils.shell import quote as shell_quote
-from ..utils.ssh import private_pem, public_from_private_pem
 
 log = logging.getLogger("tpi")
 
@@ -246,7 +244,11 @@ def machine_create(data: Dict[str, Any], timeouts: Optional[Dict[str, float]] = 
     diags: List[Diagnostic] = []
     try:
         if not state.get("ssh_private"):
+            from ..utils.ssh import private_pem  # machines only: keep task CLIs light
+
             state["ssh_private"] = private_pem()
+        from ..utils.ssh import public_from_private_pem
+
         state["ssh_public"] = public_from_private_pem(state["ssh_private"])
     except Exception as error:
         return Result("", state, [Diagnostic("error", "Failed creating the key pair: %s" % error)])
@@ -415,6 +417,8 @@ def runner_create(data: Dict[str, Any], timeouts: Optional[Dict[str, float]] = N
     if not created.ok:
         return Result("", created.state, diags)
     state = created.state
+    from ..utils.runner_status import has_status
+
     budget = _timeouts("iterative_cml_runner", timeouts).create - 60.0
     deadline = time.time() + max(budget, 1.0)
     logs = ""

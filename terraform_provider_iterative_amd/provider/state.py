@@ -13,13 +13,22 @@ import copy
 import fcntl
 import json
 import os
-import uuid
 from contextlib import contextmanager
 from typing import Any, Dict, Iterator, List, Optional, Tuple
 
 PROVIDER_ADDR = 'provider["registry.terraform.io/iterative/iterative"]'
 TERRAFORM_VERSION = "1.5.7"
 SCHEMA_TIMEOUT_KEY = "e2bfb730-ecaa-11e6-8f88-34363bc7c4c0"  # terraform-plugin-sdk timeouts key
+
+
+def _uuid4() -> str:
+    """Random (version 4) UUID string; avoids importing ``uuid`` (which imports ``platform``)
+    on the CLI's hot path."""
+    raw = bytearray(os.urandom(16))
+    raw[6] = (raw[6] & 0x0F) | 0x40
+    raw[8] = (raw[8] & 0x3F) | 0x80
+    h = raw.hex()
+    return "%s-%s-%s-%s-%s" % (h[:8], h[8:12], h[12:16], h[16:20], h[20:])
 
 
 class StateError(RuntimeError):
@@ -63,7 +72,7 @@ def parse_address(addr: str) -> Tuple[str, str, Any]:
 class State:
     def __init__(self, data: Optional[Dict[str, Any]] = None):
         self.data = data or {"version": 4, "terraform_version": TERRAFORM_VERSION, "serial": 0,
-                             "lineage": str(uuid.uuid4()), "outputs": {}, "resources": [],
+                             "lineage": _uuid4(), "outputs": {}, "resources": [],
                              "check_results": None}
         if self.data.get("version") != 4:
             raise StateError("unsupported state version %r" % self.data.get("version"))
@@ -99,7 +108,7 @@ class State:
             except BlockingIOError:
                 raise StateError("Error acquiring the state lock (%s is held by another "
                                  "process)" % lock_path) from None
-            info = {"ID": str(uuid.uuid4()), "Operation": operation, "Info": "",
+            info = {"ID": _uuid4(), "Operation": operation, "Info": "",
                     "Who": "%s@%s" % (os.environ.get("USER", "?"), os.uname().nodename),
                     "Version": TERRAFORM_VERSION, "Path": os.path.abspath(path)}
             os.ftruncate(fd, 0)

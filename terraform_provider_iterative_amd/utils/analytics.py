@@ -13,11 +13,8 @@ import hashlib
 import json
 import logging
 import os
-import platform
 import re
-import subprocess
 import threading
-import uuid
 from typing import Any, Dict, List, Optional
 
 log = logging.getLogger("tpi.analytics")
@@ -37,6 +34,8 @@ EXCLUDED_GROUPS = {
 
 
 def deterministic(data: str) -> str:
+    import uuid
+
     ns = uuid.uuid5(uuid.NAMESPACE_DNS, "iterative.ai")
     dk = hashlib.scrypt(data.encode(), salt=ns.bytes, n=1 << 16, r=8, p=1, dklen=8,
                         maxmem=256 << 20)
@@ -82,6 +81,8 @@ def _read_id(path: str) -> str:
     try:
         data = json.loads(raw)
     except ValueError:
+        import uuid
+
         return str(uuid.UUID(bytes=raw[:16])) if len(raw) >= 16 else raw.decode().strip()
     if isinstance(data, dict) and isinstance(data.get("user_id"), str):
         return data["user_id"]
@@ -107,6 +108,8 @@ def user_id(environ=None) -> str:
         elif ci == "github":
             raw = "%s %s" % (environ.get("GITHUB_ACTOR", ""), environ.get("GITHUB_ACTOR_ID", ""))
         else:
+            import subprocess
+
             try:
                 raw = subprocess.run(["git", "log", "-1", "--pretty=format:'%ae'"],
                                      capture_output=True, text=True, timeout=5).stdout
@@ -116,6 +119,8 @@ def user_id(environ=None) -> str:
     base = _config_dir(environ)
     old = os.path.join(base, "dvc", "user_id")
     new = os.path.join(base, "iterative", "telemetry")
+    import uuid
+
     ident = str(uuid.uuid4())
     if not os.path.exists(new):
         if os.path.exists(old):
@@ -155,6 +160,8 @@ def resource_data(data: Optional[Dict[str, Any]]) -> Dict[str, Any]:
 
 def payload(action: str, error: Optional[BaseException], extra: Dict[str, Any],
             environ=None) -> Dict[str, Any]:
+    import platform
+
     environ = os.environ if environ is None else environ
     extra = dict(extra)
     extra["ci"] = guess_ci(environ)
