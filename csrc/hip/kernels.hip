@@ -15,6 +15,12 @@
 //   every load instruction of the workgroup reads one contiguous 8 KiB span (2 x dwordx4 per
 //   lane, 4 stripes in flight per lane); lanes 0..3 fold the 256 lane digests.
 //
+// Grid mapping: workgroup i handles tile i (linear).  The hardware deals consecutive
+// workgroups round-robin over the 8 XCDs; these kernels stream every byte exactly once and
+// tiles share no cache lines (tiles are 4 KiB multiples, transposes move whole 128-byte
+// lines), so there is no cross-workgroup L2 reuse for an XCD-aware remap to preserve.  The
+// only shared reads, the 20 KiB of CRC tables, hit in every XCD's L2 after the first wave.
+//
 // Reference hot paths: N2 (machine-script.sh.tpl:118-124 mtime poll),
 // N4 (machine-script.sh.tpl:89,118-124 rclone data sync/restore).
 #include <hip/hip_runtime.h>
