@@ -51,7 +51,40 @@ def main():
                      "MB": round(nbytes / 1e6)}
         del cases[name], plan, stream, crcs, t
         torch.cuda.empty_cache()
+    out["many_small"] = many_small()
     print(json.dumps(out))
+
+
+
+def many_small(n=20000):
+    """Checkpoint of many small tensors (norm weights / biases): descriptor walking cost."""
+    import torch
+
+    from terraform_provider_iterative_amd.checkpoint import Checkpointer
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(0)
+    tensors = {"p%d" % i: torch.randn(1000 + (i % 7) * 13, device=dev, generator=g)
+               for i in range(n)}
+    nbytes = sum(t.numel() * 4 for t in tensors.values())
+    out = {}
+    with Checkpointer(tensors, codec="none") as ck:
+        ck.save()
+        ck.restore()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            ck.save()
+        t1 = time.perf_counter()
+        for _ in range(3):
+            ck.restore()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+    out["tensors"] = n
+    out["MB"] = round(nbytes / 1e6)
+    out["save_GBps"] = round(3 * nbytes / (t1 - t0) / 1e9, 1)
+    out["restore_GBps"] = round(3 * nbytes / (t2 - t1) / 1e9, 1)
+    return out
 
 
 if __name__ == "__main__":

@@ -8,7 +8,10 @@ from the same region (or from the persisted file) and verifies every tile.
 
 Region layout (also the persisted file format)::
 
-    0              b"TPICKPT1" | u64 header_len | JSON header (see ``_header``)
+    0              b"TPICKPT2" | u64 header_len | u64 entries_offset | u64 entries_len
+    32             JSON header (see ``_header``; small: sizes, codec, CRC, metadata)
+    entries_offset JSON list of tensor entries (name/dtype/shape/offset; fixed per plan,
+                   identified in the header by its SHA-256, so a restore never parses it)
     crc_offset     u32 CRC32C per (raw) tile                  (4 KiB aligned)
     csize_offset   u32 encoded blob size per tile (codec "tpz1" only)
     stream_offset  packed stream (``ops.packing`` layout), or with ``codec="tpz1"`` the
@@ -22,6 +25,7 @@ either encoding.
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import json
 import os
 import struct
@@ -33,12 +37,12 @@ import numpy as np
 
 from ..ops import codec as tpz
 from ..ops import hip, native
-from ..ops.packing import PackPlan, TensorEntry, align_up
+from ..ops.packing import PackPlan, align_up
 from ..ops.packing import pack as host_pack, unpack as host_unpack
 from .host import HostRegion
 
-MAGIC = b"TPICKPT1"
-PREAMBLE = 16
+MAGIC = b"TPICKPT2"
+PREAMBLE = 32
 MODES = {"sdma": 0, "direct": 1}
 CODECS = ("none", "tpz1")
 
@@ -160,12 +164,13 @@ class DeviceEngine:
             pass
 
 
-def _layout(header_len: int, ntiles: int, total: int, tile_bytes: int):
-    crc_offset = align_up(PREAMBLE + header_len, 4096)
+def _layout(header_cap: int, entries_len: int, ntiles: int, total: int, tile_bytes: int):
+    entries_offset = align_up(PREAMBLE + header_cap, 4096)
+    crc_offset = align_up(entries_offset + entries_len, 4096)
     csize_offset = crc_offset + 4 * ntiles
     stream_offset = align_up(csize_offset + 4 * ntiles, 4096)
     capacity = max(total, tpz.bound(total, tile_bytes))
-    return crc_offset, csize_offset, stream_offset, stream_offset + capacity
+    return entries_offset, crc_offset, csize_offset, stream_offset, stream_offset + capacity
 
 
 class Checkpointer:
@@ -194,10 +199,13 @@ class Checkpointer:
         if codec != "none" and self.mode != MODES["sdma"]:
             raise ValueError("the codec needs the staged (sdma) pipeline")
         self.codec = codec
-        entries_json = json.dumps([e.to_json() for e in self.plan.entries]).encode()
-        self.header_cap = len(entries_json) + self.HEADER_RESERVE
-        self.crc_offset, self.csize_offset, self.stream_offset, self.size = _layout(
-            self.header_cap, self.plan.ntiles, self.plan.total, self.plan.tile_bytes)
+        # entries are serialised once; saves copy the bytes, restores compare the digest
+        self._entries_blob = json.dumps([e.to_json() for e in self.plan.entries]).encode()
+        self._entries_digest = hashlib.sha256(self._entries_blob).hexdigest()
+        self.header_cap = self.HEADER_RESERVE
+        (self.entries_offset, self.crc_offset, self.csize_offset, self.stream_offset,
+         self.size) = _layout(self.header_cap, len(self._entries_blob), self.plan.ntiles,
+                              self.plan.total, self.plan.tile_bytes)
         self.engine = None
         numa_node = -1
         if self.plan.on_device:
@@ -222,22 +230,27 @@ class Checkpointer:
     # -- header ------------------------------------------------------------------------------
     def _header(self, complete: bool, crc: int, metadata: Optional[Dict], codec: str = "none",
                 stream_bytes: Optional[int] = None) -> Dict:
-        return {"format": 2, "complete": complete, "tile_bytes": self.plan.tile_bytes,
+        return {"format": 3, "complete": complete, "tile_bytes": self.plan.tile_bytes,
                 "total": self.plan.total, "ntiles": self.plan.ntiles,
+                "ntensors": len(self.plan.entries), "entries_sha256": self._entries_digest,
+                "entries_offset": self.entries_offset, "entries_len": len(self._entries_blob),
                 "crc_offset": self.crc_offset, "csize_offset": self.csize_offset,
                 "stream_offset": self.stream_offset, "codec": codec,
                 "stream_bytes": self.plan.total if stream_bytes is None else stream_bytes,
                 "crc32c": crc, "saved_at": time.time(), "saves": self.saves,
-                "metadata": metadata or {},
-                "entries": [e.to_json() for e in self.plan.entries]}
+                "metadata": metadata or {}}
 
     def _write_header(self, header: Dict) -> None:
         blob = json.dumps(header).encode()
         if len(blob) > self.header_cap:
             raise CheckpointError("checkpoint metadata too large (%d bytes)" % len(blob))
+        n = len(self._entries_blob)
+        self.region.array(self.entries_offset, n)[:] = np.frombuffer(self._entries_blob,
+                                                                      np.uint8)
         pre = self.region.array(0, PREAMBLE + len(blob))
         pre[PREAMBLE:] = np.frombuffer(blob, np.uint8)
-        pre[:PREAMBLE] = np.frombuffer(MAGIC + struct.pack("<Q", len(blob)), np.uint8)
+        pre[:PREAMBLE] = np.frombuffer(MAGIC + struct.pack("<QQQ", len(blob),
+                                                           self.entries_offset, n), np.uint8)
 
     def _invalidate(self) -> None:
         self.region.array(0, 8)[:] = 0
@@ -249,6 +262,12 @@ class Checkpointer:
             raise CheckpointError("no checkpoint (bad magic)")
         (n,) = struct.unpack("<Q", raw[8:16])
         return json.loads(buf[PREAMBLE:PREAMBLE + n].tobytes())
+
+    def entries(self) -> list:
+        """Tensor entries recorded in the region (parsed on demand)."""
+        header = self.header()
+        raw = self.region.array(header["entries_offset"], header["entries_len"]).tobytes()
+        return json.loads(raw)
 
     def header(self) -> Dict:
         return self.read_header(self.region.array(0, self.crc_offset))
@@ -351,11 +370,10 @@ class Checkpointer:
         return res
 
     def _check_compatible(self, header: Dict) -> None:
-        entries = [TensorEntry.from_json(e) for e in header["entries"]]
         if (header["total"] != self.plan.total or header["tile_bytes"] != self.plan.tile_bytes
                 or header.get("stream_offset") != self.stream_offset
                 or header.get("crc_offset") != self.crc_offset
-                or entries != self.plan.entries):
+                or header.get("entries_sha256") != self._entries_digest):
             raise CheckpointError("checkpoint layout does not match the bound tensors")
 
     def persist(self, path: str) -> str:
@@ -375,7 +393,7 @@ class Checkpointer:
     def load(self, path: str) -> TransferResult:
         """Read a persisted checkpoint file into the region, then :meth:`restore`."""
         with open(path, "rb") as f:
-            head = np.frombuffer(f.read(self.crc_offset), np.uint8)
+            head = np.frombuffer(f.read(PREAMBLE + self.header_cap), np.uint8)
             header = self.read_header(head)
             self._check_compatible(header)
             f.seek(0)
@@ -406,11 +424,16 @@ class Checkpointer:
         self.close()
 
 
-def describe_checkpoint(path: str) -> Dict:
-    """Header of a persisted checkpoint file (no tensors needed)."""
+def describe_checkpoint(path: str, entries: bool = True) -> Dict:
+    """Header of a persisted checkpoint file (no tensors needed), with its tensor entries
+    unless ``entries=False``."""
     with open(path, "rb") as f:
         pre = f.read(PREAMBLE)
         if pre[:8] != MAGIC:
             raise CheckpointError("%s is not a checkpoint" % path)
-        (n,) = struct.unpack("<Q", pre[8:16])
-        return json.loads(f.read(n))
+        n, entries_offset, entries_len = struct.unpack("<QQQ", pre[8:32])
+        header = json.loads(f.read(n))
+        if entries:
+            f.seek(entries_offset)
+            header["entries"] = json.loads(f.read(entries_len))
+        return header
