@@ -437,3 +437,30 @@ def describe_checkpoint(path: str, entries: bool = True) -> Dict:
             f.seek(entries_offset)
             header["entries"] = json.loads(f.read(entries_len))
         return header
+
+
+def verify_checkpoint(path: str) -> Dict:
+    """Integrity check of a persisted checkpoint without its tensors: decode the stream (if
+    encoded) and compare every tile's CRC32C with the recorded one (host, native code)."""
+    header = describe_checkpoint(path, entries=False)
+    if not header.get("complete"):
+        return {"complete": False, "bad_tiles": None, "first_bad": None}
+    ntiles, tile, total = header["ntiles"], header["tile_bytes"], header["total"]
+    data = np.memmap(path, dtype=np.uint8, mode="r")
+    crcs = np.array(data[header["crc_offset"]:header["crc_offset"] + 4 * ntiles].view(np.uint32))
+    start = header["stream_offset"]
+    stream = data[start:start + int(header["stream_bytes"])]
+    first_malformed = -1
+    if header.get("codec", "none") == "tpz1":
+        sizes = np.array(data[header["csize_offset"]:header["csize_offset"] + 4 * ntiles]
+                         .view(np.uint32))
+        stream, first_malformed = tpz.decode(np.ascontiguousarray(stream), sizes, total, tile)
+    from ..ops.hashing import crc32c_tiles
+
+    actual = crc32c_tiles(np.ascontiguousarray(stream), tile_bytes=tile)
+    bad = np.nonzero(actual != crcs)[0]
+    return {"complete": True, "codec": header.get("codec", "none"), "tiles": ntiles,
+            "bad_tiles": int(len(bad)), "first_bad": int(bad[0]) if len(bad) else -1,
+            "first_malformed_blob": int(first_malformed),
+            "crc32c": native().crc32c_combine_tiles_ptr(crcs.ctypes.data, ntiles, tile, total)
+            == header.get("crc32c")}

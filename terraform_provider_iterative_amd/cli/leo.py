@@ -133,7 +133,30 @@ def build_parser(defaults: Dict[str, Any]) -> argparse.ArgumentParser:
     destroy_runner.add_argument("name")
     preempt = sub.add_parser("preempt", help=argparse.SUPPRESS)
     preempt.add_argument("name")
+    checkpoint = sub.add_parser("checkpoint", help=argparse.SUPPRESS)
+    checkpoint.add_argument("path")
+    checkpoint.add_argument("--verify", action="store_true",
+                            help="decode and CRC-check every tile")
     return root
+
+
+def cmd_checkpoint(args) -> int:
+    """Summary (and with ``--verify`` an integrity check) of a persisted checkpoint file."""
+    import json
+
+    from ..checkpoint import describe_checkpoint, verify_checkpoint
+
+    info = describe_checkpoint(args.path)
+    summary = {k: info.get(k) for k in ("format", "complete", "codec", "total", "stream_bytes",
+                                         "ntiles", "tile_bytes", "ntensors", "saved_at",
+                                         "saves", "metadata")}
+    if info.get("total"):
+        summary["ratio"] = round(int(info["stream_bytes"]) / int(info["total"]), 4)
+    if args.verify:
+        summary["verify"] = verify_checkpoint(args.path)
+    print(json.dumps(summary, indent=1, sort_keys=True))
+    ok = not args.verify or (summary["verify"].get("bad_tiles") == 0)
+    return 0 if info.get("complete") and ok else 1
 
 
 def _cloud(args) -> Cloud:
@@ -292,6 +315,8 @@ def main(argv: Optional[List[str]] = None) -> int:
     args = parser.parse_args(argv)
     setup_logging(verbose=args.verbose)
     try:
+        if args.command == "checkpoint":  # file inspection: no cloud involved
+            return cmd_checkpoint(args)
         return COMMANDS[args.command](args, _cloud(args))
     except SystemExit:
         raise

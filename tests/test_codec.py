@@ -81,3 +81,36 @@ def test_checkpointer_codec_roundtrip_host(tmp_path):
     with Checkpointer(dst, tile_bytes=8192) as ck:  # a raw-configured reader loads it too
         ck.load(path)
     assert all(torch.equal(dst[k], ref[k]) for k in ref)
+
+
+def test_leo_checkpoint_verify(tmp_path):
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from terraform_provider_iterative_amd.checkpoint import (Checkpointer, describe_checkpoint,
+                                                             verify_checkpoint)
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = {k: v.clone() for k, v in _float_streams().items()}
+    with Checkpointer(src, tile_bytes=8192, codec="tpz1") as ck:
+        ck.save({"step": 4})
+        path = ck.persist(str(tmp_path / "z.tpi"))
+    assert verify_checkpoint(path)["bad_tiles"] == 0
+    leo = [sys.executable, os.path.join(root, "bin", "leo")]
+    out = subprocess.run(leo + ["checkpoint", "--verify", path], capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+    info = json.loads(out.stdout)
+    assert info["codec"] == "tpz1" and info["metadata"] == {"step": 4} and info["ratio"] < 1
+    # flip a byte in the encoded stream -> the verifier names the tile
+    off = describe_checkpoint(path)["stream_offset"] + 5000
+    with open(path, "r+b") as f:
+        f.seek(off)
+        b = f.read(1)
+        f.seek(off)
+        f.write(bytes([b[0] ^ 0x40]))
+    bad = verify_checkpoint(path)
+    assert bad["bad_tiles"] >= 1 and bad["first_bad"] == 0
+    out = subprocess.run(leo + ["checkpoint", "--verify", path], capture_output=True, text=True)
+    assert out.returncode == 1
