@@ -323,7 +323,7 @@ int tpi_save(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* ho
   auto t0 = std::chrono::steady_clock::now();
   if (prepare(e, segs, n, total)) return -1;
   e->hash_valid = false;  // host content no longer matches the last sync's digests
-  if (wait_stream) {
+  if (wait_stream != TPI_NO_STREAM) {
     HIP_OK(hipEventRecord(e->ev_wait, (hipStream_t)wait_stream));
     HIP_OK(hipStreamWaitEvent(e->compute, e->ev_wait, 0));
   }
@@ -380,7 +380,7 @@ int tpi_restore(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, const
   const uint32_t init_full = init_for(tile);
   const uint32_t init_last = init_for(total % tile ? total % tile : tile);
   unsigned long long bad_init[2] = {0ull, ~0ull};
-  if (signal_stream) {
+  if (signal_stream != TPI_NO_STREAM) {
     // The unpack overwrites the caller's tensors: order it after the caller's pending work
     // on them (e.g. a zero_() still queued on torch's stream).
     HIP_OK(hipEventRecord(e->ev_wait, (hipStream_t)signal_stream));
@@ -418,7 +418,7 @@ int tpi_restore(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, const
   unsigned long long bad[2];
   HIP_OK(hipMemcpyAsync(bad, e->d_bad, sizeof(bad), hipMemcpyDeviceToHost, e->compute));
   HIP_OK(hipEventRecord(e->ev_done, e->compute));
-  if (signal_stream) HIP_OK(hipStreamWaitEvent((hipStream_t)signal_stream, e->ev_done, 0));
+  if (signal_stream != TPI_NO_STREAM) HIP_OK(hipStreamWaitEvent((hipStream_t)signal_stream, e->ev_done, 0));
   HIP_OK(hipStreamSynchronize(e->compute));
   HIP_OK(hipStreamSynchronize(e->copy));
   *bad_tiles = bad[0];
@@ -454,7 +454,7 @@ int tpi_sync(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* ho
   if (!e->d_count) HIP_OK(hipMalloc(&e->d_count, sizeof(unsigned int)));
   if (e->hash_ntiles != ntiles) e->hash_valid = false;
   const int all = full || !e->hash_valid;
-  if (wait_stream) {
+  if (wait_stream != TPI_NO_STREAM) {
     HIP_OK(hipEventRecord(e->ev_wait, (hipStream_t)wait_stream));
     HIP_OK(hipStreamWaitEvent(e->compute, e->ev_wait, 0));
   }
@@ -559,7 +559,7 @@ int tpi_save_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* 
   const uint64_t ntiles = (total + tile - 1) / tile;
   if (prepare_codec(e, ntiles)) return -1;
   e->hash_valid = false;
-  if (wait_stream) {
+  if (wait_stream != TPI_NO_STREAM) {
     HIP_OK(hipEventRecord(e->ev_wait, (hipStream_t)wait_stream));
     HIP_OK(hipStreamWaitEvent(e->compute, e->ev_wait, 0));
   }
@@ -604,6 +604,90 @@ int tpi_save_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* 
   return 0;
 }
 
+// Asynchronous checkpoints, step 1: pack the tensors (+ tile CRCs) into a device snapshot
+// buffer, ordered after `wait_stream`'s pending work; `wait_stream` then waits for the pack,
+// so training kernels queued afterwards cannot overwrite tensors before they are captured.
+// Nothing blocks the host.
+int tpi_snapshot(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* dev_dst,
+                 uint32_t* dev_crcs, uint64_t wait_stream) {
+  Range range("tpi_snapshot");
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (prepare(e, segs, n, total)) return -1;
+  e->hash_valid = false;
+  if (wait_stream != TPI_NO_STREAM) {
+    HIP_OK(hipEventRecord(e->ev_wait, (hipStream_t)wait_stream));
+    HIP_OK(hipStreamWaitEvent(e->compute, e->ev_wait, 0));
+  }
+  const uint64_t tile = e->tile;
+  HIP_OK(tpi_launch_transposes(segs, n, 0, total, dev_dst, 0, e->compute));
+  HIP_OK(tpi_launch_stream_crc(0, e->d_segs, n, 0, total, dev_dst, tile, e->tables, dev_crcs,
+                               init_for(tile), init_for(total % tile ? total % tile : tile),
+                               nullptr, 1, e->compute));
+  HIP_OK(hipEventRecord(e->ev_done, e->compute));
+  if (wait_stream != TPI_NO_STREAM) HIP_OK(hipStreamWaitEvent((hipStream_t)wait_stream, e->ev_done, 0));
+  return 0;
+}
+
+// Step 2 (called from a background thread): move a snapshot to host memory, raw or TPZ1
+// encoded chunk by chunk, plus its CRCs.  Runs only on the engine's streams, concurrently
+// with whatever the training stream does.
+int tpi_spill(tpi_engine* e, const void* dev_src, const uint32_t* dev_crcs, uint64_t total,
+              void* host_dst, uint32_t* crcs_out, uint32_t* csizes_out, int codec,
+              uint64_t* stream_bytes, tpi_stats* stats) {
+  Range range("tpi_spill");
+  std::lock_guard<std::mutex> lk(e->mu);
+  auto t0 = std::chrono::steady_clock::now();
+  HIP_OK(hipSetDevice(e->device));
+  const uint64_t tile = e->tile;
+  const uint64_t ntiles = (total + tile - 1) / tile;
+  // the snapshot was packed on `compute`; everything below is ordered after it
+  HIP_OK(hipEventRecord(e->ev_wait, e->compute));
+  HIP_OK(hipStreamWaitEvent(e->copy, e->ev_wait, 0));
+  uint8_t* dst = (uint8_t*)host_dst;
+  const uint8_t* src = (const uint8_t*)dev_src;
+  uint64_t out = 0, nchunks = 0;
+  if (!codec) {
+    for (uint64_t base = 0; base < total; base += e->chunk, ++nchunks)
+      HIP_OK(hipMemcpyAsync(dst + base, src + base, std::min(e->chunk, total - base),
+                            hipMemcpyDeviceToHost, e->copy));
+    out = total;
+  } else {
+    if (prepare_codec(e, ntiles)) return -1;
+    for (uint64_t base = 0, k = 0; base < total; base += e->chunk, ++k) {
+      const int b = (int)(k % e->nbuf);
+      const uint64_t len = std::min(e->chunk, total - base);
+      const uint64_t t0i = base / tile, nt = (len + tile - 1) / tile;
+      if (k >= (uint64_t)e->nbuf) HIP_OK(hipStreamWaitEvent(e->compute, e->ev_b[b], 0));
+      HIP_OK(tpi_launch_tpz_encode(src + base, len, tile, e->d_meta, e->d_csize + t0i,
+                                   e->staging[b], e->compute));
+      HIP_OK(hipMemcpyAsync(csizes_out + t0i, e->d_csize + t0i, nt * sizeof(uint32_t),
+                            hipMemcpyDeviceToHost, e->compute));
+      HIP_OK(hipEventRecord(e->ev_a[b], e->compute));
+      HIP_OK(hipEventSynchronize(e->ev_a[b]));
+      uint64_t clen = 0;
+      for (uint64_t i = 0; i < nt; ++i) clen += csizes_out[t0i + i];
+      HIP_OK(hipStreamWaitEvent(e->copy, e->ev_a[b], 0));
+      HIP_OK(hipMemcpyAsync(dst + out, e->staging[b], clen, hipMemcpyDeviceToHost, e->copy));
+      HIP_OK(hipEventRecord(e->ev_b[b], e->copy));
+      out += clen;
+      nchunks = k + 1;
+    }
+  }
+  HIP_OK(hipMemcpyAsync(crcs_out, dev_crcs, ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                        e->copy));
+  HIP_OK(hipStreamSynchronize(e->copy));
+  HIP_OK(hipStreamSynchronize(e->compute));
+  *stream_bytes = out;
+  if (stats) {
+    stats->copy_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    stats->pack_ms = 0;
+    stats->bytes = out;
+    stats->chunks = nchunks;
+  }
+  return 0;
+}
+
 // Compressed restore: H2D of each chunk's blobs -> staging[b], decode -> zraw, unpack+verify.
 int tpi_restore_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total,
                   const void* host_src, const uint32_t* crcs, const uint32_t* csizes,
@@ -628,7 +712,7 @@ int tpi_restore_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total,
   const uint32_t init_full = init_for(tile);
   const uint32_t init_last = init_for(total % tile ? total % tile : tile);
   unsigned long long bad_init[2] = {0ull, ~0ull};
-  if (signal_stream) {
+  if (signal_stream != TPI_NO_STREAM) {
     HIP_OK(hipEventRecord(e->ev_wait, (hipStream_t)signal_stream));
     HIP_OK(hipStreamWaitEvent(e->compute, e->ev_wait, 0));
   }
@@ -663,7 +747,7 @@ int tpi_restore_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total,
   unsigned long long bad[2];
   HIP_OK(hipMemcpyAsync(bad, e->d_bad, sizeof(bad), hipMemcpyDeviceToHost, e->compute));
   HIP_OK(hipEventRecord(e->ev_done, e->compute));
-  if (signal_stream) HIP_OK(hipStreamWaitEvent((hipStream_t)signal_stream, e->ev_done, 0));
+  if (signal_stream != TPI_NO_STREAM) HIP_OK(hipStreamWaitEvent((hipStream_t)signal_stream, e->ev_done, 0));
   HIP_OK(hipStreamSynchronize(e->compute));
   HIP_OK(hipStreamSynchronize(e->copy));
   *bad_tiles = bad[0];

@@ -43,6 +43,10 @@ typedef struct tpi_seg {
 
 enum { TPI_MODE_SDMA = 0, TPI_MODE_DIRECT = 1 };
 
+// Stream arguments are hipStream_t values: 0 is the null (default) stream -- what torch's
+// default stream is -- and TPI_NO_STREAM means "no ordering with any caller stream".
+#define TPI_NO_STREAM (~0ull)
+
 typedef struct tpi_engine tpi_engine;
 
 typedef struct tpi_stats {
@@ -67,11 +71,11 @@ uint64_t tpi_engine_chunk_bytes(const tpi_engine* e);
 
 // Pack `segs` (n entries, sorted by off) into a stream of `total` bytes written to `host_dst`
 // (pinned or host-mapped).  `crcs_out` (host, ceil(total/tile) entries) receives the CRC32C of
-// every tile.  `wait_stream` (may be 0) is a stream whose prior work must finish first.
+// every tile.  `wait_stream` (or TPI_NO_STREAM) is a stream whose prior work must finish first.
 int tpi_save(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* host_dst,
              uint32_t* crcs_out, int mode, uint64_t wait_stream, tpi_stats* stats);
 // Inverse: stream `total` bytes from `host_src`, verify each tile against `crcs`, scatter.
-// `signal_stream` (may be 0): the unpack starts after that stream's pending work and the
+// `signal_stream` (or TPI_NO_STREAM): the unpack starts after that stream's pending work and the
 // stream waits for the unpack before its later work.
 // Returns 0 and sets *bad_tiles (0 = all verified) / *first_bad (-1 if none).
 int tpi_restore(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total,
@@ -88,6 +92,16 @@ int tpi_restore_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total,
                   const void* host_src, const uint32_t* crcs, const uint32_t* csizes,
                   uint64_t signal_stream, uint64_t* bad_tiles, int64_t* first_bad,
                   tpi_stats* stats);
+// Asynchronous checkpoints: (1) pack into a device snapshot buffer (`dev_dst`, `total`
+// bytes; tile CRCs to `dev_crcs`), ordered after `wait_stream`'s work, with `wait_stream`
+// made to wait for the pack -- the host is not blocked; (2) from any thread, spill the
+// snapshot to `host_dst` (raw, or TPZ1-encoded when `codec` != 0, sizes to `csizes_out`)
+// and its CRCs to `crcs_out`.  *stream_bytes = bytes written to host_dst.
+int tpi_snapshot(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* dev_dst,
+                 uint32_t* dev_crcs, uint64_t wait_stream);
+int tpi_spill(tpi_engine* e, const void* dev_src, const uint32_t* dev_crcs, uint64_t total,
+              void* host_dst, uint32_t* crcs_out, uint32_t* csizes_out, int codec,
+              uint64_t* stream_bytes, tpi_stats* stats);
 // Device-buffer codec (tests / tools): encode `len` bytes of `raw` into contiguous blobs
 // (`meta_scratch`: ntiles*96 bytes, `csize`: ntiles u32), decode with blob offsets `coff`
 // (ntiles+1 u64, device).

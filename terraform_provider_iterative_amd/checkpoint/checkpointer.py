@@ -29,6 +29,7 @@ import hashlib
 import json
 import os
 import struct
+import threading
 import time
 from dataclasses import dataclass
 from typing import Any, Dict, Mapping, Optional, Sequence, Union
@@ -139,6 +140,25 @@ class DeviceEngine:
         return TransferResult(plan.total, time.perf_counter() - t0, int(st.chunks),
                               int(bad.value), int(first.value), wire_bytes=int(st.bytes))
 
+    def snapshot(self, plan: PackPlan, dev_dst: int, dev_crcs: int, wait_stream: int) -> None:
+        rc = self.lib.tpi_snapshot(self.handle, plan.segs.ctypes.data, len(plan.entries),
+                                   plan.total, ctypes.c_void_p(dev_dst),
+                                   ctypes.c_void_p(dev_crcs), wait_stream)
+        self.lib.check(rc, "tpi_snapshot")
+
+    def spill(self, dev_src: int, dev_crcs: int, total: int, host_addr: int,
+              crcs: np.ndarray, csizes: np.ndarray, codec: bool) -> TransferResult:
+        st = _Stats()
+        wire = ctypes.c_uint64(0)
+        t0 = time.perf_counter()
+        rc = self.lib.tpi_spill(self.handle, ctypes.c_void_p(dev_src), ctypes.c_void_p(dev_crcs),
+                                total, ctypes.c_void_p(host_addr), crcs.ctypes.data,
+                                csizes.ctypes.data, 1 if codec else 0, ctypes.byref(wire),
+                                ctypes.byref(st))
+        self.lib.check(rc, "tpi_spill")
+        return TransferResult(total, time.perf_counter() - t0, int(st.chunks),
+                              wire_bytes=int(wire.value))
+
     def sync(self, plan: PackPlan, host_addr: int, crcs: np.ndarray, full: bool,
              wait_stream: int) -> TransferResult:
         st = _Stats()
@@ -171,6 +191,29 @@ def _layout(header_cap: int, entries_len: int, ntiles: int, total: int, tile_byt
     stream_offset = align_up(csize_offset + 4 * ntiles, 4096)
     capacity = max(total, tpz.bound(total, tile_bytes))
     return entries_offset, crc_offset, csize_offset, stream_offset, stream_offset + capacity
+
+
+class PendingSave:
+    """An asynchronous save in flight (:meth:`Checkpointer.save_async`)."""
+
+    def __init__(self, stall_s: float):
+        self.stall_s = stall_s  # host time the caller spent in save_async
+        self._done = threading.Event()
+        self._result: Optional[TransferResult] = None
+        self._error: Optional[BaseException] = None
+        self._thread: Optional[threading.Thread] = None
+
+    def done(self) -> bool:
+        return self._done.is_set()
+
+    def result(self, timeout: Optional[float] = None) -> TransferResult:
+        if not self._done.wait(timeout):
+            raise TimeoutError("checkpoint spill still running")
+        if self._error is not None:
+            raise CheckpointError("asynchronous save failed: %s" % self._error) from self._error
+        return self._result
+
+    wait = result
 
 
 class Checkpointer:
@@ -224,6 +267,8 @@ class Checkpointer:
         self.csizes = self.region.array(self.csize_offset, 4 * self.plan.ntiles, np.uint32)
         self.saves = 0
         self._synced = False
+        self._snap = self._snap_crcs = None  # HBM snapshot of save_async
+        self._pending: Optional[PendingSave] = None
         self.last_save: Optional[TransferResult] = None
         self.last_restore: Optional[TransferResult] = None
 
@@ -275,6 +320,7 @@ class Checkpointer:
     # -- operations --------------------------------------------------------------------------
     def save(self, metadata: Optional[Dict] = None) -> TransferResult:
         """Pack every tensor into the region; returns bytes/seconds (GB/s via ``.gbps``)."""
+        self.wait_pending()
         self._invalidate()
         zipped = self.codec == "tpz1"
         dst = self.region.addr + self.stream_offset
@@ -307,6 +353,69 @@ class Checkpointer:
         self.last_save = res
         return res
 
+    def save_async(self, metadata: Optional[Dict] = None) -> PendingSave:
+        """Checkpoint without stalling the training stream on PCIe.
+
+        The tensors are packed (with tile CRCs) into a snapshot buffer in HBM -- a device-side
+        copy at TB/s, ordered on the current stream, which then waits for it, so tensors may
+        be updated right after this returns.  A background thread spills the snapshot to the
+        host region (TPZ1-encoded when the checkpointer's codec is on) and writes the header;
+        ``result()`` returns its :class:`TransferResult`.  The snapshot costs ``plan.total``
+        bytes of HBM (allocated on first use).  Host tensors fall back to a synchronous save.
+        """
+        self.wait_pending()
+        if self.engine is None:
+            t0 = time.perf_counter()
+            pending = PendingSave(0.0)
+            try:
+                pending._result = self.save(metadata)
+            except BaseException as error:  # surfaced by result()
+                pending._error = error
+            pending.stall_s = time.perf_counter() - t0
+            pending._done.set()
+            return pending
+        import torch
+
+        dev = torch.device("cuda", self.device_index)
+        if self._snap is None:
+            self._snap = torch.empty(self.plan.total, dtype=torch.uint8, device=dev)
+            self._snap_crcs = torch.empty(self.plan.ntiles, dtype=torch.int32, device=dev)
+        t0 = time.perf_counter()
+        self._invalidate()
+        self.engine.snapshot(self.plan, self._snap.data_ptr(), self._snap_crcs.data_ptr(),
+                             torch.cuda.current_stream(dev).cuda_stream)
+        pending = PendingSave(time.perf_counter() - t0)
+        self.saves += 1
+        zipped = self.codec == "tpz1"
+
+        def spill():
+            try:
+                res = self.engine.spill(self._snap.data_ptr(), self._snap_crcs.data_ptr(),
+                                        self.plan.total, self.region.addr + self.stream_offset,
+                                        self.crcs, self.csizes, zipped)
+                res.crc = native().crc32c_combine_tiles_ptr(
+                    self.crcs.ctypes.data, self.plan.ntiles, self.plan.tile_bytes,
+                    self.plan.total)
+                self._write_header(self._header(True, res.crc, metadata,
+                                                "tpz1" if zipped else "none", res.wire_bytes))
+                self.last_save = res
+                pending._result = res
+            except BaseException as error:  # surfaced by result()
+                pending._error = error
+            finally:
+                pending._done.set()
+
+        pending._thread = threading.Thread(target=spill, name="tpi-spill", daemon=True)
+        pending._thread.start()
+        self._pending = pending
+        return pending
+
+    def wait_pending(self) -> None:
+        """Block until an asynchronous save in flight has reached host memory."""
+        pending, self._pending = self._pending, None
+        if pending is not None:
+            pending.result()
+
     def sync(self, metadata: Optional[Dict] = None) -> TransferResult:
         """Incremental save: only tiles whose content changed since the previous ``sync`` are
         packed and spilled (the device-side replacement of the reference's 10-second
@@ -321,6 +430,7 @@ class Checkpointer:
             return res
         import torch
 
+        self.wait_pending()
         full = not self._synced
         self._invalidate()
         wait = torch.cuda.current_stream(self.device_index).cuda_stream
@@ -336,6 +446,7 @@ class Checkpointer:
 
     def restore(self, strict: bool = True) -> TransferResult:
         """Unpack + verify the region into the bound tensors."""
+        self.wait_pending()
         header = self.header()
         if not header.get("complete"):
             raise CheckpointError("checkpoint incomplete (save was interrupted)")
@@ -378,6 +489,7 @@ class Checkpointer:
 
     def persist(self, path: str) -> str:
         """Write the region (header, CRCs, stream) to ``path`` atomically."""
+        self.wait_pending()
         header = self.header()
         if not header.get("complete"):
             raise CheckpointError("nothing saved yet")
@@ -392,6 +504,7 @@ class Checkpointer:
 
     def load(self, path: str) -> TransferResult:
         """Read a persisted checkpoint file into the region, then :meth:`restore`."""
+        self.wait_pending()
         with open(path, "rb") as f:
             head = np.frombuffer(f.read(PREAMBLE + self.header_cap), np.uint8)
             header = self.read_header(head)
@@ -409,6 +522,11 @@ class Checkpointer:
         return self.restore()
 
     def close(self) -> None:
+        try:
+            self.wait_pending()
+        except CheckpointError:
+            pass
+        self._snap = self._snap_crcs = None
         if self.engine is not None:
             self.engine.close()
             self.engine = None

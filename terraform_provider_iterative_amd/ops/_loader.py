@@ -72,6 +72,8 @@ class HipLib:
             "tpi_save_z": (i32, [vp, vp, i32, u64, vp, vp, vp, u64, c.POINTER(u64), vp]),
             "tpi_restore_z": (i32, [vp, vp, i32, u64, vp, vp, vp, u64, c.POINTER(u64),
                                     c.POINTER(i64), vp]),
+            "tpi_snapshot": (i32, [vp, vp, i32, u64, vp, vp, u64]),
+            "tpi_spill": (i32, [vp, vp, vp, u64, vp, vp, vp, i32, c.POINTER(u64), vp]),
             "tpi_tpz_encode_device": (i32, [vp, u64, u64, vp, vp, vp, u64]),
             "tpi_tpz_decode_device": (i32, [vp, vp, u64, u64, vp, u64]),
             "tpi_stream_hash": (i32, [vp, i32, u64, u64, u64, vp, u64]),

@@ -98,3 +98,18 @@ def test_layout_mismatch(tmp_path):
             ck.restore()
     assert os.path.getsize(path) > 0
     assert np.uint32  # keep numpy import used
+
+
+def test_save_async_on_host_falls_back_to_sync():
+    src = _model(5)
+    ref = {k: v.clone() for k, v in src.items()}
+    with Checkpointer(src, tile_bytes=4096) as ck:
+        pending = ck.save_async({"step": 2})
+        res = pending.result(timeout=30)
+        assert pending.done() and res.bytes == ck.plan.total
+        assert ck.header()["complete"] and ck.header()["metadata"] == {"step": 2}
+        for v in src.values():
+            v.zero_()
+        ck.restore()
+    for k in ref:
+        assert torch.equal(src[k], ref[k]), k

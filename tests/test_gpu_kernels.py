@@ -315,3 +315,33 @@ def test_view_kinds_through_checkpointer_chunks(codec, mode):
         assert ck.sync().dirty_tiles == ck.plan.ntiles
         src["batched"][1, 2, 3] += 1
         assert ck.sync().dirty_tiles == 1
+
+
+@pytest.mark.parametrize("codec", ["none", "tpz1"])
+def test_save_async_snapshots_before_later_updates(codec, tmp_path):
+    """Tensors updated on the current stream right after save_async returns must not leak
+    into the checkpoint: the snapshot is ordered before them on the device."""
+    from terraform_provider_iterative_amd.checkpoint import Checkpointer
+
+    src = _tensors("cuda")
+    src.update({k: v for k, v in _views("cuda").items() if k.startswith("t_")})
+    ref = {k: v.clone() for k, v in src.items()}
+    kw = dict(tile_bytes=1 << 20, chunk_bytes=2 << 20, nbuf=2)
+    with Checkpointer(src, codec=codec, **kw) as ck:
+        pending = ck.save_async({"step": 11})
+        for v in src.values():  # queued immediately on the same (current) stream
+            v.add_(1) if v.dtype.is_floating_point else v.fill_(3)
+        res = pending.result(timeout=120)
+        assert res.bytes == ck.plan.total and ck.header()["metadata"] == {"step": 11}
+        assert ck.header()["codec"] == codec
+        path = ck.persist(str(tmp_path / "first.tpi"))
+        # a second async save reuses the snapshot buffer (waits for the first spill)
+        ck.save_async({"step": 12}).result(timeout=120)
+        assert ck.header()["metadata"] == {"step": 12}
+    dst = {k: torch.empty_strided(v.shape, v.stride(), dtype=v.dtype, device="cuda").zero_()
+           for k, v in ref.items()}
+    with Checkpointer(dst, **kw) as ck2:
+        ck2.load(path)
+        torch.cuda.synchronize()
+    for k in ref:
+        assert torch.equal(dst[k], ref[k]), k
