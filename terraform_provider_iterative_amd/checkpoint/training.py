@@ -91,6 +91,12 @@ class TrainingState:
     def save(self, metadata: Optional[Dict] = None):
         return self.checkpointer.save({**(metadata or {}), **self.host_metadata()})
 
+    def save_async(self, metadata: Optional[Dict] = None):
+        """Periodic checkpoint that stalls the training stream only for the HBM snapshot;
+        host-side tensors are captured now, with the snapshot (see
+        :meth:`Checkpointer.save_async`)."""
+        return self.checkpointer.save_async({**(metadata or {}), **self.host_metadata()})
+
     def restore_host(self, metadata: Dict) -> None:
         blobs = metadata.get("host_tensors", {})
         missing = sorted(set(self.host) - set(blobs))

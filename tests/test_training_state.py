@@ -70,3 +70,17 @@ def test_round_trip_resumes_exact_training_state(tmp_path):
     for k in want:
         if k.startswith(("model.", "optim.")):
             assert torch.equal(got2[k], want[k]), k
+
+
+def test_save_async_captures_host_tensors_at_call_time(tmp_path):
+    model, opt = _setup()
+    _train(model, opt, 2, 3)
+    with TrainingState(model, opt, path=str(tmp_path / "s"), tile_bytes=4096) as state:
+        want = _snapshot(model, opt)
+        pending = state.save_async({"step": 2})
+        pending.result(timeout=30)
+        _train(model, opt, 1, 4)
+        assert state.resume()["step"] == 2
+        got = _snapshot(model, opt)
+    for k in want:
+        assert torch.equal(got[k], want[k]), k
