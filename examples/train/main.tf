@@ -27,7 +27,7 @@ resource "iterative_task" "train" {
   }
   script = <<-END
     #!/bin/sh
-    exec python3 train.py --stage --steps 200
+    exec python3 train.py --stage --steps 200 --ckpt-every 50
   END
 }
 

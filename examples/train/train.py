@@ -36,6 +36,8 @@ def main():
     p.add_argument("--seq", type=int, default=512)
     p.add_argument("--stage", action="store_true", help="stage the workdir into HBM first")
     p.add_argument("--sleep", type=float, default=0.0, help="sleep per step (tests)")
+    p.add_argument("--ckpt-every", type=int, default=0,
+                   help="asynchronous checkpoint every N steps (0: only on SIGTERM/exit)")
     args = p.parse_args()
 
     import torch
@@ -95,7 +97,7 @@ def main():
     state.install()
 
     gen = torch.Generator(device=device).manual_seed(rank + 7)
-    t_steps = []
+    t_steps, stalls = [], []
     for step in range(start, args.steps):
         t0 = time.perf_counter()
         x = torch.randn(args.batch, args.seq, h, device=device, dtype=torch.bfloat16,
@@ -112,7 +114,15 @@ def main():
             log("step %d loss %.5f" % (step + 1, loss.item()))
         if args.sleep:
             time.sleep(args.sleep)
+        if args.ckpt_every and (step + 1) % args.ckpt_every == 0:
+            t_ck = time.perf_counter()
+            state.save_async({"step": step + 1})  # HBM snapshot; the PCIe spill runs behind
+            if device.type == "cuda":
+                torch.cuda.current_stream().synchronize()
+            stalls.append(time.perf_counter() - t_ck)
     res = state.save({"step": int(step_t.item()), "final": True})
+    if stalls:
+        stats["ckpt_stall_ms"] = 1e3 * max(stalls)
     if t_steps:
         stats["step_ms"] = 1e3 * sorted(t_steps)[len(t_steps) // 2]
     stats["final_save_GBps"] = res.gbps
