@@ -410,6 +410,23 @@ class Checkpointer:
         self._pending = pending
         return pending
 
+    def rollback(self, strict: bool = True) -> TransferResult:
+        """Restore the tensors from the last :meth:`save_async` snapshot still in HBM (device
+        to device, CRC-verified) -- e.g. to undo a diverged step without touching PCIe."""
+        if self._snap is None:
+            raise CheckpointError("no HBM snapshot (save_async was never called)")
+        self.wait_pending()
+        import torch
+
+        t0 = time.perf_counter()
+        bad, first = host_unpack(self.plan, self._snap, self._snap_crcs)
+        torch.cuda.current_stream(self.device_index).synchronize()
+        res = TransferResult(self.plan.total, time.perf_counter() - t0, 0, bad, first,
+                             wire_bytes=0)
+        if strict and bad:
+            raise CheckpointError("%d corrupt snapshot tile(s), first at %d" % (bad, first))
+        return res
+
     def wait_pending(self) -> None:
         """Block until an asynchronous save in flight has reached host memory."""
         pending, self._pending = self._pending, None
