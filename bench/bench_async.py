@@ -4,7 +4,8 @@
 ``save_async`` packs the state into an HBM snapshot on the current stream (the only part
 the training stream waits for) and spills it to host DRAM in the background.  Reports the
 stall (device time until the current stream is free again), the background spill time, and
-a blocking ``save`` of the same state for comparison.
+a blocking ``save`` of the same state for comparison, and ``rollback`` (restore from the
+HBM snapshot, device to device, CRC-verified).
 """
 from __future__ import annotations
 
@@ -47,6 +48,11 @@ def main():
         out["spill_GBps"] = round(ck.plan.total / (t2 - t0) / 1e9, 2)
         out["wire_bytes"] = res.wire_bytes
         torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        rb = ck.rollback()
+        out["rollback_ms"] = round((time.perf_counter() - t3) * 1e3, 2)
+        out["rollback_GBps"] = round(ck.plan.total / (time.perf_counter() - t3) / 1e9, 1)
+        out["rollback_verified"] = rb.bad_tiles == 0
         t3 = time.perf_counter()
         ck.save()
         out["blocking_save_s"] = round(time.perf_counter() - t3, 3)
