@@ -91,7 +91,8 @@ def main():
     # checkpoint header (bias correction needs them after a resume)
     state = TrainingState(model, opt, extra={"step": step_t}, path=spill)
     ck = state.checkpointer
-    meta = state.resume()
+    # ranks agree on the step to resume from (or all start fresh)
+    meta = state.resume_consistent() if world > 1 else state.resume()
     start = int(step_t.item())
     log("resumed from step %d" % start if meta else "fresh start")
     state.install()

@@ -113,6 +113,41 @@ class TrainingState:
             self.restore_host(meta)
         return meta
 
+    def resume_consistent(self, persist_path: Optional[str] = None, group=None,
+                          key: str = "step") -> Optional[Dict]:
+        """:meth:`resume` for data/tensor-parallel ranks: all ranks resume from checkpoints of
+        the same ``metadata[key]`` or none does.  A rank whose save did not complete (killed
+        during the spill) would otherwise restart from an older step than its peers; here the
+        group agrees first (``all_gather_object``) and falls back to a fresh start together.
+        Call on every rank of ``group`` (default: the world) after ``init_process_group``.
+        """
+        import torch.distributed as dist
+
+        meta = None
+        try:
+            header = self.checkpointer.header()
+            if header.get("complete"):
+                meta = header.get("metadata", {})
+        except Exception:  # no checkpoint in the region
+            meta = None
+        if meta is None and persist_path:
+            import os
+
+            from .checkpointer import describe_checkpoint
+
+            if os.path.exists(persist_path):
+                try:
+                    info = describe_checkpoint(persist_path, entries=False)
+                    meta = info.get("metadata", {}) if info.get("complete") else None
+                except Exception:
+                    meta = None
+        mine = None if meta is None else meta.get(key, True)
+        seen = [None] * dist.get_world_size(group)
+        dist.all_gather_object(seen, mine, group=group)
+        if any(v is None for v in seen) or len(set(map(repr, seen))) != 1:
+            return None  # disagreement: everybody starts fresh
+        return self.resume(persist_path)
+
     def install(self, persist_path: Optional[str] = None) -> None:
         """Checkpoint on SIGTERM (then exit 143 so the supervisor respawns the rank)."""
         preemption.register(self.checkpointer, persist_path)

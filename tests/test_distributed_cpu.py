@@ -72,3 +72,41 @@ def test_write_back(tmp_path):
     out = tmp_path / "out"
     staged.write_back(str(out))
     assert (out / "x.bin").read_bytes()[:6] == b"xyzabc"
+
+
+def _resume_worker(rank, world, port, root, results, steps):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from terraform_provider_iterative_amd.checkpoint import TrainingState
+
+        torch.manual_seed(rank)
+        model = torch.nn.Linear(8, 8)
+        opt = torch.optim.SGD(model.parameters(), lr=0.1)
+        spill = os.path.join(root, "rank%d" % rank)
+        with TrainingState(model, opt, path=spill, tile_bytes=4096) as state:
+            if steps[rank] is not None:  # this rank's previous incarnation saved at that step
+                state.save({"step": steps[rank]})
+            with torch.no_grad():
+                model.weight.zero_()
+            meta = state.resume_consistent()
+            results[rank] = (None if meta is None else meta["step"],
+                             float(model.weight.abs().sum()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("steps,agree", [((5, 5, 5), True), ((5, 4, 5), False),
+                                         ((5, None, 5), False)])
+def test_resume_consistent_all_or_nothing(tmp_path, steps, agree):
+    manager = mp.Manager()
+    results = manager.dict()
+    world = len(steps)
+    mp.spawn(_resume_worker, args=(world, _free_port(), str(tmp_path), results, steps),
+             nprocs=world)
+    for rank in range(world):
+        step, weight = results[rank]
+        if agree:
+            assert step == 5 and weight > 0  # restored
+        else:
+            assert step is None and weight == 0  # fresh start everywhere
