@@ -54,6 +54,8 @@ def parse_args(argv=None):
     p.add_argument("--broadcast-gb", type=float, default=10.0,
                    help="N>1: also measure the RCCL workdir fan-out of this many GB")
     p.add_argument("--verify", action="store_true", default=True)
+    p.add_argument("--no-async", action="store_true",
+                   help="skip the (untimed) save_async stall measurement")
     return p.parse_args(argv)
 
 
@@ -192,6 +194,21 @@ def main(argv=None):
         after = [ops.shard_hash(tensors[n].view(-1).view(torch.uint8)).cpu() for n in names]
         verified = all(torch.equal(x, y) for x, y in zip(before, after))
 
+    async_stall = None
+    if not args.no_async:  # untimed side measurement: training-stream stall of save_async
+        try:
+            ck.save_async().result()  # allocates the HBM snapshot
+            barrier()
+            a0 = time.perf_counter()
+            pending = ck.save_async({"async": True})
+            torch.cuda.current_stream(device).synchronize()
+            stall = time.perf_counter() - a0
+            pending.result()
+            async_stall = {"stall_ms": round(allmax(stall) * 1e3, 2),
+                           "spill_s": round(allmax(time.perf_counter() - a0), 3)}
+        except Exception as error:  # never lose the headline to the side measurement
+            async_stall = {"error": repr(error)}
+
     broadcast = None
     if world > 1 and args.broadcast_gb > 0:  # config 3: workdir fan-out over xGMI (untimed)
         try:
@@ -239,6 +256,7 @@ def main(argv=None):
             "first_log_latency": latency,
             "workdir_broadcast": broadcast,
             "restore_verified": verified,
+            "save_async": async_stall,
             "setup_s": round(setup_s, 2),
         }
         print(json.dumps(out), flush=True)
