@@ -196,18 +196,27 @@ def main(argv=None):
 
     async_stall = None
     if not args.no_async:  # untimed side measurement: training-stream stall of save_async
+        # every rank reaches every collective below, whatever fails locally (no deadlock)
+        err, stall, spill = None, 0.0, 0.0
         try:
             ck.save_async().result()  # allocates the HBM snapshot
-            barrier()
-            a0 = time.perf_counter()
-            pending = ck.save_async({"async": True})
-            torch.cuda.current_stream(device).synchronize()
-            stall = time.perf_counter() - a0
-            pending.result()
-            async_stall = {"stall_ms": round(allmax(stall) * 1e3, 2),
-                           "spill_s": round(allmax(time.perf_counter() - a0), 3)}
-        except Exception as error:  # never lose the headline to the side measurement
-            async_stall = {"error": repr(error)}
+        except Exception as error:
+            err = repr(error)
+        barrier()
+        if err is None:
+            try:
+                a0 = time.perf_counter()
+                pending = ck.save_async({"async": True})
+                torch.cuda.current_stream(device).synchronize()
+                stall = time.perf_counter() - a0
+                pending.result()
+                spill = time.perf_counter() - a0
+            except Exception as error:
+                err = repr(error)
+        failed = allmax(1.0 if err else 0.0)
+        stall, spill = allmax(stall), allmax(spill)
+        async_stall = ({"error": err or "failed on another rank"} if failed else
+                       {"stall_ms": round(stall * 1e3, 2), "spill_s": round(spill, 3)})
 
     broadcast = None
     if world > 1 and args.broadcast_gb > 0:  # config 3: workdir fan-out over xGMI (untimed)
