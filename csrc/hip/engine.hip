@@ -527,7 +527,7 @@ int prepare_codec(tpi_engine* e, uint64_t ntiles) {
   const uint64_t per_chunk = e->chunk / e->tile;
   if (!e->zraw) {
     HIP_OK(hipMalloc(&e->zraw, e->chunk));
-    HIP_OK(hipMalloc(&e->d_meta, per_chunk * 4 * sizeof(tpz_plane)));
+    HIP_OK(hipMalloc(&e->d_meta, tpz_meta_bytes(per_chunk)));
   }
   if (ntiles + 1 > e->z_cap) {
     if (e->d_csize) HIP_OK(hipFree(e->d_csize));

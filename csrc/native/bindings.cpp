@@ -159,6 +159,7 @@ PYBIND11_MODULE(_tpi_native, m) {
     return py::make_tuple(bad, first);
   });
   m.def("tpz_bound", [](uint64_t len) { return tpz_bound(len); });
+  m.def("tpz_meta_bytes", [](uint64_t ntiles) { return tpz_meta_bytes(ntiles); });
   m.def("tpz_encode_ptr", [](uintptr_t src, uint64_t total, uint64_t tile, uintptr_t dst,
                              uintptr_t csizes, int threads) {
     py::gil_scoped_release nogil;

@@ -214,15 +214,19 @@ uint64_t tpz_encode_stream(const void* src, uint64_t total, uint64_t tile, void*
   const uint64_t ntiles = (total + tile - 1) / tile;
   const uint8_t* s = (const uint8_t*)src;
   std::vector<tpz_plane> hdr(ntiles * 4);
+  std::vector<uint8_t> lens(ntiles * 64);  // HUF code lengths, 16 per plane
+  auto lens_of = [&](uint64_t t) { return (uint8_t(*)[16])(lens.data() + t * 64); };
   parallel_for(ntiles, threads, [&](uint64_t t) {
     const uint64_t lo = t * tile;
-    csizes[t] = (uint32_t)tpz_analyze_tile(s + lo, std::min(tile, total - lo), &hdr[t * 4]);
+    csizes[t] = (uint32_t)tpz_analyze_tile(s + lo, std::min(tile, total - lo), &hdr[t * 4],
+                                           lens_of(t));
   });
   std::vector<uint64_t> off(ntiles + 1, 0);
   for (uint64_t t = 0; t < ntiles; ++t) off[t + 1] = off[t] + csizes[t];
   parallel_for(ntiles, threads, [&](uint64_t t) {
     const uint64_t lo = t * tile;
-    tpz_emit_tile(s + lo, std::min(tile, total - lo), &hdr[t * 4], (uint8_t*)dst + off[t]);
+    tpz_emit_tile(s + lo, std::min(tile, total - lo), &hdr[t * 4], lens_of(t),
+                  (uint8_t*)dst + off[t]);
   });
   return off[ntiles];
 }

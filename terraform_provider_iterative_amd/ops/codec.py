@@ -53,7 +53,9 @@ def encode(data: Any, tile_bytes: int = DEFAULT_TILE_BYTES) -> Tuple[Any, Any]:
         _check(nbytes, tile_bytes)
         ntiles = -(-nbytes // tile_bytes)
         out = torch.empty(bound(nbytes, tile_bytes), dtype=torch.uint8, device=data.device)
-        meta = torch.empty(max(ntiles, 1) * HEADER_BYTES, dtype=torch.uint8, device=data.device)
+        # analyze -> encode scratch: plane headers, HUF code lengths and substream sizes
+        meta = torch.empty(native().tpz_meta_bytes(max(ntiles, 1)), dtype=torch.uint8,
+                           device=data.device)
         csize = torch.empty(max(ntiles, 1), dtype=torch.int32, device=data.device)
         lib = hip()
         lib.check(lib.tpi_tpz_encode_device(ptr, nbytes, tile_bytes, meta.data_ptr(),

@@ -45,6 +45,48 @@ def _a16(x: int) -> int:
     return (x + 15) & ~15
 
 
+def _huf_plane_py(blob: bytes, off: int, n: int, ngroups: int, m: int, nesc: int,
+                  dictionary: np.ndarray) -> np.ndarray:
+    """HUF plane: canonical Huffman over dictionary + escape (symbol m, then 8 raw bits),
+    LSB-first bits, substream s = groups s, s+256, ... (spec: csrc/common/tpz.h)."""
+    streams = min(256, ngroups)
+    lens = list(blob[off:off + 16])
+    ends = [int(x) for x in np.frombuffer(blob, np.uint32, streams, off + 16)]
+    base = off + 16 + _a16(4 * streams)
+    table = {}  # (length, MSB-first code) -> symbol
+    code = 0
+    for length in range(1, 12):
+        for s in range(m + 1):
+            if lens[s] == length:
+                table[(length, code)] = s
+                code += 1
+        code <<= 1
+    vals = np.zeros(n, np.uint8)
+    start = 0
+    for s in range(streams):
+        raw = np.frombuffer(blob, np.uint8, 4 * (ends[s] - start), base + 4 * start)
+        bits = np.unpackbits(raw, bitorder="little").tolist() + [0] * 32
+        pos = 0
+        for g in range(s, ngroups, 256):
+            for i in range(g * 32, min(g * 32 + 32, n)):
+                c, length = 0, 0
+                while (length, c) not in table:
+                    c = (c << 1) | bits[pos]
+                    pos += 1
+                    length += 1
+                    assert length <= 11, "no code"
+                sym = table[(length, c)]
+                if sym == m:
+                    vals[i] = sum(bits[pos + b] << b for b in range(8))
+                    pos += 8
+                else:
+                    vals[i] = dictionary[sym]
+        assert pos <= 32 * (ends[s] - start)
+        start = ends[s]
+    assert start == nesc
+    return vals
+
+
 def tpz_decode_tile_py(blob: bytes, length: int) -> np.ndarray:
     """Independent numpy decoder of one TPZ1 tile blob (spec: csrc/common/tpz.h)."""
     n = length // 4
@@ -57,6 +99,10 @@ def tpz_decode_tile_py(blob: bytes, length: int) -> np.ndarray:
         if k == 8:  # raw plane
             out[p::4] = np.frombuffer(blob, np.uint8, n, off)
             off += ngroups * 32
+            continue
+        if k == 9:  # Huffman plane
+            out[p::4] = _huf_plane_py(blob, off, n, ngroups, m, nesc, dictionary)
+            off += 16 + _a16(4 * min(256, ngroups)) + _a16(4 * nesc)
             continue
         if k == 0:  # constant plane
             out[p::4] = dictionary[0]

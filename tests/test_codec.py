@@ -51,6 +51,56 @@ def test_ratios_reflect_float_structure():
     assert ratio["random"] < 1.01  # incompressible data costs only the 96-byte headers
 
 
+def _modes(blob) -> list:
+    return [int(blob[24 * p]) for p in range(4)]
+
+
+def test_huffman_planes_code_float_exponents():
+    # the sign/exponent byte of N(0, s) values carries ~2.6 bits: HUF (k=9) beats DICT(3)
+    s = _float_streams()
+    for name, limit in (("bf16_weights", 0.69), ("fp32_moment", 0.85), ("fp32_sq", 0.85)):
+        raw = s[name].contiguous().view(-1).view(torch.uint8).numpy()
+        raw = raw[:len(raw) // 16 * 16]
+        enc, _ = codec.encode(raw, 1 << 20)
+        assert len(enc) / len(raw) < limit, name
+        assert 9 in _modes(enc), name
+
+
+def test_huffman_escapes_roundtrip():
+    # plane 3: geometric over ~40 values (dictionary misses -> inline escapes), plane 2: three
+    # skewed values, planes 0-1: noise
+    g = np.random.default_rng(5)
+    n = 300000
+    words = g.integers(0, 1 << 16, n, dtype=np.uint32)
+    words |= np.minimum(g.geometric(0.25, n) - 1, 255).astype(np.uint32) << 24
+    words |= g.choice(np.array([3, 7, 9], np.uint32), n, p=[0.7, 0.2, 0.1]) << 16
+    raw = words.view(np.uint8)
+    for tile in (4096, 65536, 1 << 18, 1 << 20):
+        enc, sizes = codec.encode(raw, tile)
+        dec, first = codec.decode(enc, sizes, len(raw), tile)
+        assert first == -1 and np.array_equal(dec, raw), tile
+        if tile >= 1 << 18:  # (small tiles may prefer DICT: substream index + word padding)
+            assert _modes(enc)[3] == 9 and _modes(enc)[2] == 9, tile
+        if tile == 1 << 18:
+            blob = enc[:int(sizes[0])].tobytes()
+            assert np.array_equal(tpz_decode_tile_py(blob, tile), raw[:tile])
+
+
+def test_huffman_stream_overrun_is_reported():
+    raw = _float_streams()["bf16_weights"].view(torch.uint8).numpy()
+    enc, sizes = codec.encode(raw, 1 << 20)
+    assert _modes(enc)[1] == 9
+    bad = enc.copy()
+    bad[24 + 4:24 + 8] = np.frombuffer(np.uint32(1).tobytes(), np.uint8)  # plane 1: 1 word
+    _, first = codec.decode(bad, sizes, len(raw), 1 << 20)
+    assert first == 0
+    bad = enc.copy()
+    sec1 = 96 + (len(raw) // 4 + 31) // 32 * 32  # plane 0 is RAW
+    bad[sec1 + 16 + 4 * 200] ^= 0x04  # plane 1: a substream end offset moves
+    _, first = codec.decode(bad, sizes, len(raw), 1 << 20)
+    assert first == 0
+
+
 def test_corrupt_blob_is_reported():
     raw = _float_streams()["bf16_weights"].view(torch.uint8).numpy()[:65536]
     enc, sizes = codec.encode(raw, 16384)
