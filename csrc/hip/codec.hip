@@ -1,21 +1,24 @@
 // CDNA4 kernels of the TPZ1 byte-plane checkpoint codec (format: csrc/common/tpz.h).
 //
 // The checkpoint spill is PCIe-bound (~56 GB/s per GPU) while HBM streams at >5 TB/s, so the
-// GPU spends a few microseconds per 256 MiB chunk shrinking what crosses the link:
+// GPU spends a few hundred microseconds per 256 MiB chunk shrinking what crosses the link:
 //
 //   k_tpz_analyze  one 256-thread workgroup per tile: sampled 4x256-bin histogram in LDS,
 //                  top-15 dictionary per plane (one wave per plane, wave64 max-reductions),
-//                  exact hit counts over the whole tile, cheapest mode per plane -> header +
-//                  blob size.
+//                  Huffman code lengths of dictionary + escape (one lane per plane, LDS
+//                  workspace), exact costs of every mode over the whole tile (lane s also sums
+//                  the HUF bits of substream s), cheapest mode per plane -> header + size.
 //   k_tpz_encode   one workgroup per tile: blob offset = sum of the earlier tiles' sizes of
 //                  the chunk, then rounds of 256 groups (a group = 128 tile bytes, one lane,
-//                  8 x dwordx4 loads): codes are fixed-width so they are stored directly;
+//                  8 x dwordx4 loads): DICT codes are fixed-width so they are stored directly;
 //                  escapes get their position from a workgroup exclusive scan of 4 packed
-//                  16-bit counters (one u64 scan per round).
-//   k_tpz_decode   the inverse, writing whole 128-byte groups of the raw tile.
+//                  16-bit counters (one u64 scan per round); a HUF plane appends the group's
+//                  codes to the lane's own substream (start = scan of the analyzed sizes).
+//   k_tpz_decode   the inverse, writing whole 128-byte groups of the raw tile; a HUF plane is
+//                  decoded by each lane from its own substream through a 2^11-entry LDS table.
 //
-// Every mode is a template (K = code width) so the 32-code group loops are fully unrolled and
-// the code words stay in registers (no scratch).
+// Every DICT mode is a template (K = code width) so the 32-code group loops are fully
+// unrolled and the code words stay in registers (no scratch).
 #include <hip/hip_runtime.h>
 
 #include "../common/tpz.h"
@@ -24,6 +27,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 #define CWG 256
+static_assert(CWG == TPZ_HUF_STREAMS, "HUF substream s is lane s of the codec workgroup");
 
 __device__ static inline uint64_t cmin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 
@@ -67,11 +71,17 @@ __device__ static inline void load_group(const uint8_t* t, uint64_t n, uint64_t 
 __global__ __launch_bounds__(CWG) void k_tpz_analyze(const uint8_t* __restrict__ raw,
                                                      uint64_t len, uint64_t tile,
                                                      tpz_plane* __restrict__ meta,
+                                                     uint8_t* __restrict__ hlen,
+                                                     uint32_t* __restrict__ hwords,
                                                      uint32_t* __restrict__ csize) {
   __shared__ uint32_t hist[4][256];
   __shared__ uint8_t rank[4][256];
+  __shared__ uint8_t cost[4][256];  // HUF bits per byte value
   __shared__ tpz_plane hdr[4];
-  __shared__ uint32_t s_hits[CWG / 64][16];
+  __shared__ uint8_t s_len[4][16];
+  __shared__ uint32_t s_cnt[4][16];
+  __shared__ tpz_huf_work s_work[4];
+  __shared__ uint32_t s_hits[CWG / 64][20];  // 16 hit counters + 4 HUF word sums
   __shared__ uint32_t s_size[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t tbase = (uint64_t)blockIdx.x * tile;
@@ -123,15 +133,25 @@ __global__ __launch_bounds__(CWG) void k_tpz_analyze(const uint8_t* __restrict__
     if (lane == 0) hdr[p].m = (uint8_t)m;
     // rank table of plane p
     for (int v = lane; v < 256; v += 64) rank[p][v] = 15;
+    if (lane < 16) s_len[p][lane] = 0;
   }
   __syncthreads();
-  if (tid < 4) {
-    for (int r = 0; r < hdr[tid].m; ++r) rank[tid][hdr[tid].dict[r]] = (uint8_t)r;
+  if (tid < 4) {  // rank table + Huffman code lengths of plane tid
+    const int p = tid, m = hdr[p].m;
+    for (int r = 0; r < m; ++r) rank[p][hdr[p].dict[r]] = (uint8_t)r;
+    tpz_huf_counts(hist[p], hdr[p].dict, m, (uint32_t)S, s_cnt[p]);
+    tpz_huf_lengths(s_cnt[p], m + 1, s_len[p], &s_work[p]);
+  }
+  __syncthreads();
+  for (int i = tid; i < 4 * 256; i += CWG) {
+    const int p = i >> 8;
+    const uint32_t r = rank[p][i & 255], m = hdr[p].m;
+    cost[p][i & 255] = (uint8_t)(r < m ? s_len[p][r] : s_len[p][m] + 8);
   }
   __syncthreads();
 
-  // exact hits per plane for thresholds rank < 1, 3, 7, 15
-  uint32_t hits[4][4];
+  // exact hits per plane for thresholds rank < 1, 3, 7, 15; HUF bits of substream tid
+  uint32_t hits[4][4], bits[4] = {0, 0, 0, 0};
 #pragma unroll
   for (int p = 0; p < 4; ++p)
 #pragma unroll
@@ -145,17 +165,25 @@ __global__ __launch_bounds__(CWG) void k_tpz_analyze(const uint8_t* __restrict__
       if ((uint32_t)j < valid) {
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-          const uint32_t r = rank[p][(w[j] >> (8 * p)) & 0xff];
+          const uint32_t v = (w[j] >> (8 * p)) & 0xff;
+          const uint32_t r = rank[p][v];
           hits[p][0] += r < 1;
           hits[p][1] += r < 3;
           hits[p][2] += r < 7;
           hits[p][3] += r < 15;
+          bits[p] += cost[p][v];
         }
       }
     }
   }
+  uint32_t words[4];
 #pragma unroll
-  for (int p = 0; p < 4; ++p)
+  for (int p = 0; p < 4; ++p) {
+    words[p] = (bits[p] + 31) >> 5;
+    hwords[((uint64_t)blockIdx.x * 4 + p) * CWG + tid] = words[p];
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       uint32_t v = hits[p][q];
@@ -163,25 +191,33 @@ __global__ __launch_bounds__(CWG) void k_tpz_analyze(const uint8_t* __restrict__
       for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
       if (lane == 0) s_hits[wave][4 * p + q] = v;
     }
+    uint32_t v = words[p];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) s_hits[wave][16 + p] = v;
+  }
   __syncthreads();
   if (tid < 4) {
     const int p = tid;
-    uint64_t h[4];
+    uint64_t h[4], hw = 0;
     for (int q = 0; q < 4; ++q) {
       h[q] = 0;
       for (int w = 0; w < CWG / 64; ++w) h[q] += s_hits[w][4 * p + q];
     }
+    for (int w = 0; w < CWG / 64; ++w) hw += s_hits[w][16 + p];
+    const uint64_t huf = (hdr[p].m >= 1 && h[0] != n) ? hw : ~0ull;
     uint64_t nesc = 0;
-    const int k = tpz_choose(n, ngroups, hdr[p].m, h, &nesc);
+    const int k = tpz_choose(n, ngroups, hdr[p].m, h, huf, &nesc);
     tpz_plane out;
     out.k = (uint8_t)k;
     out.pad[0] = out.pad[1] = 0;
     out.nesc = (uint32_t)nesc;
-    int used = 0;
-    if (k != TPZ_RAW) used = k == 0 ? 1 : ((1 << k) - 1 < hdr[p].m ? (1 << k) - 1 : hdr[p].m);
+    const int used = tpz_used(k, hdr[p].m);
     out.m = (uint8_t)used;
     for (int r = 0; r < 16; ++r) out.dict[r] = r < used ? hdr[p].dict[r] : 0;
     meta[(uint64_t)blockIdx.x * 4 + p] = out;
+    for (int i = 0; i < 16; ++i)
+      hlen[((uint64_t)blockIdx.x * 4 + p) * 16 + i] = k == TPZ_HUF ? s_len[p][i] : 0;
     s_size[p] = (uint32_t)tpz_plane_bytes(k, ngroups, nesc);
   }
   __syncthreads();
@@ -221,6 +257,34 @@ __device__ static inline uint32_t encode_codes(const uint32_t w[32], int p, cons
   return mask;
 }
 
+// Appends the HUF codes of one group's (valid) plane-p bytes to the lane's substream: LSB-first
+// bit buffer, a full u32 word is stored as soon as it exists (<= 19 bits per symbol).
+__device__ static inline void huf_encode_group(const uint32_t w[32], int p, uint32_t valid,
+                                               const uint8_t* rk, uint32_t m,
+                                               const uint16_t* code, const uint8_t* clen,
+                                               uint64_t& acc, int& nb,
+                                               uint32_t* __restrict__ stream, uint64_t& wp) {
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    if ((uint32_t)j < valid) {
+      const uint32_t v = (w[j] >> (8 * p)) & 0xff;
+      const uint32_t r = rk[v];
+      const uint32_t c = r < m ? r : m;
+      acc |= (uint64_t)code[c] << nb;
+      nb += clen[c];
+      if (c == m) {
+        acc |= (uint64_t)v << nb;
+        nb += 8;
+      }
+      if (nb >= 32) {
+        stream[wp++] = (uint32_t)acc;
+        acc >>= 32;
+        nb -= 32;
+      }
+    }
+  }
+}
+
 struct PlaneGeo {
   uint64_t sec, esc;  // byte offsets in the blob
   int k;
@@ -245,10 +309,14 @@ __device__ static inline void plane_geometry(const tpz_plane* h, uint64_t ngroup
 __global__ __launch_bounds__(CWG) void k_tpz_encode(const uint8_t* __restrict__ raw, uint64_t len,
                                                     uint64_t tile,
                                                     const tpz_plane* __restrict__ meta,
+                                                    const uint8_t* __restrict__ hlen,
+                                                    const uint32_t* __restrict__ hwords,
                                                     const uint32_t* __restrict__ csize,
                                                     uint8_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) tpz_plane hdr[4];
   __shared__ uint8_t rank[4][256];
+  __shared__ uint8_t s_clen[4][16];
+  __shared__ uint16_t s_code[4][16];
   __shared__ uint64_t s_wave[CWG / 64];
   const int tid = threadIdx.x;
   const uint64_t tbase = (uint64_t)blockIdx.x * tile;
@@ -263,7 +331,9 @@ __global__ __launch_bounds__(CWG) void k_tpz_encode(const uint8_t* __restrict__ 
   uint8_t* blob = out + obase;
 
   if (tid < 4) hdr[tid] = meta[(uint64_t)blockIdx.x * 4 + tid];
+  if (tid < 64) s_clen[tid >> 4][tid & 15] = hlen[(uint64_t)blockIdx.x * 64 + tid];
   __syncthreads();
+  if (tid < 4 && hdr[tid].k == TPZ_HUF) tpz_huf_codes(s_clen[tid], hdr[tid].m + 1, s_code[tid]);
   for (int i = tid; i < 4 * 256; i += CWG) {
     const int p = i >> 8, v = i & 255;
     uint8_t r = 15;
@@ -276,6 +346,28 @@ __global__ __launch_bounds__(CWG) void k_tpz_encode(const uint8_t* __restrict__ 
   PlaneGeo geo[4];
   uint64_t blob_bytes;
   plane_geometry(hdr, ngroups, geo, &blob_bytes);
+
+  // HUF planes: code lengths, substream end offsets (lane s starts where the scan of the
+  // analyzed sizes puts it), zeroed alignment padding; then one bit cursor per lane and plane
+  const uint64_t S = tpz_huf_streams(ngroups);
+  uint64_t hacc[4] = {0, 0, 0, 0}, hwp[4] = {0, 0, 0, 0};
+  int hnb[4] = {0, 0, 0, 0};
+  uint32_t* hstr[4] = {nullptr, nullptr, nullptr, nullptr};
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    if (geo[p].k != TPZ_HUF) continue;  // uniform: the header lives in LDS
+    uint8_t* sec = blob + geo[p].sec;
+    uint32_t* ends = (uint32_t*)(sec + 16);
+    hstr[p] = (uint32_t*)(sec + 16 + tpz_align16(4 * S));
+    const uint32_t mine = hwords[((uint64_t)blockIdx.x * 4 + p) * CWG + tid];
+    uint64_t tot;
+    hwp[p] = block_scan_u64(mine, s_wave, &tot);
+    if (tid < 16) sec[tid] = s_clen[p][tid];
+    if (tid < S) ends[tid] = (uint32_t)(hwp[p] + mine);
+    for (uint64_t i = S + tid; i < tpz_align16(4 * S) / 4; i += CWG) ends[i] = 0;
+    for (uint64_t i = geo[p].nesc + tid; i < tpz_align16(4 * (uint64_t)geo[p].nesc) / 4; i += CWG)
+      hstr[p][i] = 0;
+  }
 
   uint64_t run[4] = {0, 0, 0, 0};
   for (uint64_t base = 0; base < ngroups; base += CWG) {
@@ -308,6 +400,10 @@ __global__ __launch_bounds__(CWG) void k_tpz_encode(const uint8_t* __restrict__ 
           case 2: mask[p] = encode_codes<2>(w, p, rank[p], valid, sec + g * 8); break;
           case 3: mask[p] = encode_codes<3>(w, p, rank[p], valid, sec + g * 12); break;
           case 4: mask[p] = encode_codes<4>(w, p, rank[p], valid, sec + g * 16); break;
+          case TPZ_HUF:
+            huf_encode_group(w, p, valid, rank[p], hdr[p].m, s_code[p], s_clen[p], hacc[p],
+                             hnb[p], hstr[p], hwp[p]);
+            break;
           default: break;  // CONST: nothing stored
         }
       }
@@ -331,6 +427,9 @@ __global__ __launch_bounds__(CWG) void k_tpz_encode(const uint8_t* __restrict__ 
       run[p] += (tot >> (16 * p)) & 0xffff;
     }
   }
+#pragma unroll
+  for (int p = 0; p < 4; ++p)  // the last, partial word of each HUF substream
+    if (geo[p].k == TPZ_HUF && hnb[p] > 0) hstr[p][hwp[p]++] = (uint32_t)hacc[p];
   // zero the alignment padding of every section (keeps blobs deterministic)
   for (int p = 0; p < 4; ++p) {
     const int k = geo[p].k;
@@ -376,6 +475,39 @@ __device__ static inline uint32_t decode_codes(const uint8_t* src, const uint8_t
   return mask;
 }
 
+// Decodes one group's (valid) plane-p bytes from the lane's HUF substream into w[].  Words past
+// the substream's end read as zero (a corrupt blob decodes garbage; the tile CRC reports it).
+__device__ static inline void huf_decode_group(const uint32_t* __restrict__ stream,
+                                               const uint16_t* lut, const uint8_t* dict,
+                                               uint32_t m, int p, uint32_t valid,
+                                               uint64_t& acc, int& nb, uint32_t& ptr,
+                                               uint32_t end, uint32_t w[32]) {
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    if ((uint32_t)j < valid) {
+      if (nb < 32) {
+        const uint32_t x = ptr < end ? stream[ptr] : 0u;
+        ++ptr;
+        acc |= (uint64_t)x << nb;
+        nb += 32;
+      }
+      const uint32_t e = lut[acc & (TPZ_HUF_LUT - 1)];
+      const uint32_t c = e & 0xff, l = e >> 8;
+      acc >>= l;
+      nb -= (int)l;
+      uint32_t v;
+      if (c == m) {
+        v = (uint32_t)acc & 0xff;
+        acc >>= 8;
+        nb -= 8;
+      } else {
+        v = dict[c & 15];
+      }
+      w[j] |= v << (8 * p);
+    }
+  }
+}
+
 // coff[i] = offset of tile i's blob relative to `comp` + comp_base; coff has ntiles+1 entries.
 __global__ __launch_bounds__(CWG) void k_tpz_decode(const uint8_t* __restrict__ comp,
                                                     const uint64_t* __restrict__ coff,
@@ -383,6 +515,9 @@ __global__ __launch_bounds__(CWG) void k_tpz_decode(const uint8_t* __restrict__ 
                                                     uint64_t tile, uint8_t* __restrict__ raw) {
   __shared__ tpz_plane hdr[4];
   __shared__ uint8_t dict[4][16];
+  __shared__ uint8_t s_len[4][16];
+  __shared__ uint16_t s_rev[4][16];
+  __shared__ uint16_t lut[4][TPZ_HUF_LUT];  // HUF: low 11 stream bits -> symbol | length << 8
   __shared__ uint64_t s_wave[CWG / 64];
   __shared__ int s_ok;
   const int tid = threadIdx.x;
@@ -399,13 +534,22 @@ __global__ __launch_bounds__(CWG) void k_tpz_decode(const uint8_t* __restrict__ 
     if (ok) {
       for (int p = 0; p < 4; ++p) hdr[p] = ((const tpz_plane*)blob)[p];
       uint64_t off = TPZ_HDR;
-      for (int p = 0; p < 4; ++p) {
+      for (int p = 0; p < 4 && ok; ++p) {
         const int k = hdr[p].k;
-        if (!(k == TPZ_RAW || k <= 4) || hdr[p].nesc > n) ok = 0;
+        if (!(k == TPZ_RAW || k == TPZ_HUF || k <= 4)) ok = 0;
+        if (hdr[p].nesc > (k == TPZ_HUF ? 8 * n + ngroups : n)) ok = 0;
         if (k != TPZ_RAW && (hdr[p].m < 1 || hdr[p].m > TPZ_MAXDICT)) ok = 0;
-        if (ok) off += tpz_plane_bytes(k, ngroups, hdr[p].nesc);
+        if (!ok) break;
+        const uint64_t bytes = tpz_plane_bytes(k, ngroups, hdr[p].nesc);
+        if (off + bytes > avail) ok = 0;
+        if (ok && k == TPZ_HUF) {  // code lengths must form a complete prefix code
+          for (int s = 0; s < 16; ++s) s_len[p][s] = blob[off + s];
+          for (int s = hdr[p].m + 1; s < 16; ++s)
+            if (s_len[p][s]) ok = 0;
+          if (ok && !tpz_huf_codes(s_len[p], hdr[p].m + 1, s_rev[p])) ok = 0;
+        }
+        off += bytes;
       }
-      if (off > avail) ok = 0;
     }
     if (!ok)  // corrupt blob: decode as zeros; the tile CRC check reports it
       for (int p = 0; p < 4; ++p) {
@@ -418,10 +562,43 @@ __global__ __launch_bounds__(CWG) void k_tpz_decode(const uint8_t* __restrict__ 
   }
   __syncthreads();
   if (tid < 64) dict[tid >> 4][tid & 15] = hdr[tid >> 4].dict[tid & 15];
+  for (int p = 0; p < 4; ++p) {  // decode tables of the HUF planes (uniform branch)
+    if (hdr[p].k != TPZ_HUF) continue;
+    const int m = hdr[p].m;
+    for (int i = tid; i < TPZ_HUF_LUT; i += CWG) {
+      uint16_t e = 0;
+      for (int s = 0; s <= m; ++s) {
+        const uint32_t l = s_len[p][s];
+        if ((i & ((1u << l) - 1)) == s_rev[p][s]) e = (uint16_t)(s | (l << 8));
+      }
+      lut[p][i] = e;
+    }
+  }
   __syncthreads();
   PlaneGeo geo[4];
   uint64_t blob_bytes;
   plane_geometry(hdr, ngroups, geo, &blob_bytes);
+
+  // HUF cursors: lane s reads substream s = [end[s-1], end[s]) of each HUF plane
+  const uint64_t S = tpz_huf_streams(ngroups);
+  uint64_t hacc[4] = {0, 0, 0, 0};
+  int hnb[4] = {0, 0, 0, 0};
+  uint32_t hptr[4] = {0, 0, 0, 0}, hend[4] = {0, 0, 0, 0};
+  const uint32_t* hstr[4] = {nullptr, nullptr, nullptr, nullptr};
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    if (geo[p].k != TPZ_HUF) continue;
+    const uint8_t* sec = blob + geo[p].sec;
+    hstr[p] = (const uint32_t*)(sec + 16 + tpz_align16(4 * S));
+    if (tid < S) {
+      const uint32_t* ends = (const uint32_t*)(sec + 16);
+      const uint32_t e = ends[tid], s0 = tid ? ends[tid - 1] : 0u;
+      if (s0 <= e && e <= geo[p].nesc) {
+        hptr[p] = s0;
+        hend[p] = e;
+      }
+    }
+  }
 
   uint64_t run[4] = {0, 0, 0, 0};
   for (uint64_t base = 0; base < ngroups; base += CWG) {
@@ -432,6 +609,7 @@ __global__ __launch_bounds__(CWG) void k_tpz_decode(const uint8_t* __restrict__ 
     uint32_t mask[4] = {0, 0, 0, 0};
     const bool live = g < ngroups;
     if (live) {
+      const uint32_t valid = (uint32_t)cmin64(32, n - g * 32);
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         const uint8_t* sec = blob + geo[p].sec;
@@ -454,10 +632,13 @@ __global__ __launch_bounds__(CWG) void k_tpz_decode(const uint8_t* __restrict__ 
           case 2: mask[p] = decode_codes<2>(sec + g * 8, dict[p], p, w); break;
           case 3: mask[p] = decode_codes<3>(sec + g * 12, dict[p], p, w); break;
           case 4: mask[p] = decode_codes<4>(sec + g * 16, dict[p], p, w); break;
+          case TPZ_HUF:
+            huf_decode_group(hstr[p], lut[p], dict[p], hdr[p].m, p, valid, hacc[p], hnb[p],
+                             hptr[p], hend[p], w);
+            break;
           default: break;
         }
       }
-      const uint32_t valid = (uint32_t)cmin64(32, n - g * 32);
       if (valid < 32) {
         const uint32_t keep = (1u << valid) - 1;
 #pragma unroll
@@ -503,10 +684,16 @@ extern "C" hipError_t tpi_launch_tpz_encode(const void* raw, uint64_t len, uint6
                                             hipStream_t stream) {
   if (len == 0) return hipSuccess;
   const unsigned ntiles = (unsigned)((len + tile - 1) / tile);
+  // meta (tpz_meta_bytes(ntiles)): plane headers | HUF code lengths | HUF substream words
+  uint8_t* mb = (uint8_t*)meta;
+  tpz_plane* planes = (tpz_plane*)mb;
+  uint8_t* hlen = mb + (uint64_t)ntiles * TPZ_HDR;
+  uint32_t* hwords = (uint32_t*)(mb + (uint64_t)ntiles * (TPZ_HDR + 64));
   hipLaunchKernelGGL(k_tpz_analyze, dim3(ntiles), dim3(CWG), 0, stream, (const uint8_t*)raw, len,
-                     tile, (tpz_plane*)meta, csize);
+                     tile, planes, hlen, hwords, csize);
   hipLaunchKernelGGL(k_tpz_encode, dim3(ntiles), dim3(CWG), 0, stream, (const uint8_t*)raw, len,
-                     tile, (const tpz_plane*)meta, (const uint32_t*)csize, (uint8_t*)out);
+                     tile, (const tpz_plane*)planes, (const uint8_t*)hlen,
+                     (const uint32_t*)hwords, (const uint32_t*)csize, (uint8_t*)out);
   return hipGetLastError();
 }
 

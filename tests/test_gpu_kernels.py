@@ -165,6 +165,17 @@ def test_checkpointer_device_roundtrip(mode, tmp_path):
         assert torch.equal(dst[k], ref[k]), k
 
 
+def _geometric_exponents(n, g):
+    """u32 words: noise low bytes, a 3-value byte 2 and a geometric byte 3 over ~40 values
+    (Huffman planes with dictionary misses, i.e. inline escapes)."""
+    words = torch.randint(0, 1 << 16, (n,), dtype=torch.int64, generator=g)
+    u = torch.rand(n, generator=g, dtype=torch.float64)
+    geo = torch.clamp((torch.log1p(-u) / np.log(0.75)).floor(), max=255).to(torch.int64)
+    few = torch.tensor([3, 7, 9])[torch.multinomial(torch.tensor([0.7, 0.2, 0.1]), n, True,
+                                                     generator=g)]
+    return (words | (few << 16) | (geo << 24)).to(torch.int32).view(torch.uint8)
+
+
 def _codec_inputs():
     g = torch.Generator().manual_seed(7)
     parts = [
@@ -174,6 +185,7 @@ def _codec_inputs():
         torch.zeros(200000, dtype=torch.uint8),
         torch.randint(0, 256, (300016,), dtype=torch.uint8, generator=g),
         torch.randint(0, 5, (100000,), dtype=torch.int32, generator=g).view(torch.uint8),
+        _geometric_exponents(1 << 18, g),
     ]
     raw = torch.cat([p.reshape(-1) for p in parts])
     return raw[:raw.numel() // 16 * 16 - 48]  # short final tile, length % 128 != 0
@@ -199,7 +211,7 @@ def test_tpz_device_decode_corrupt_blob_fails_crc():
     raw = _codec_inputs()[:1 << 20]
     blobs, sizes = codec.encode(raw.numpy(), 65536)
     bad = blobs.copy()
-    bad[int(codec.offsets(sizes)[3])] = 9  # invalid plane mode in tile 3
+    bad[int(codec.offsets(sizes)[3])] = 7  # invalid plane mode in tile 3
     out, _ = codec.decode(torch.from_numpy(bad).cuda(), sizes, raw.numel(), 65536)
     got = crc_array(ops.crc32c_tiles(out, tile_bytes=65536)).tolist()
     want = ops.crc32c_tiles(raw.numpy(), tile_bytes=65536).tolist()
