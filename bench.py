@@ -221,11 +221,15 @@ def main(argv=None):
     broadcast = None
     if world > 1 and args.broadcast_gb > 0:  # config 3: workdir fan-out over xGMI (untimed)
         try:
-            from terraform_provider_iterative_amd.parallel.broadcast import measure
+            from terraform_provider_iterative_amd.parallel.broadcast import (
+                measure, measure_independent_h2d)
 
             nbytes = int(args.broadcast_gb * 1e9)
             broadcast = {m: measure(nbytes, method=m, iters=3, warmup=1, device=device)
                          for m in ("broadcast", "scatter_allgather")}
+            # baseline: every rank pulls its own copy over PCIe (the reference's per-VM copy)
+            broadcast["independent_h2d"] = measure_independent_h2d(nbytes, iters=2, warmup=1,
+                                                                   device=device)
         except Exception as error:  # never lose the headline to the side measurement
             broadcast = {"error": repr(error)}
 

@@ -120,3 +120,35 @@ def measure(nbytes: int, method: str = "auto", iters: int = 3, warmup: int = 1,
     t = float(worst.item())
     return {"method": choose_method(dist.get_world_size(group), method), "bytes": nbytes,
             "seconds": t, "GBps": nbytes / t / 1e9 if t > 0 else None, "verified": ok}
+
+
+def measure_independent_h2d(nbytes: int, iters: int = 3, warmup: int = 1, device=None,
+                            group=None, chunk: int = 2 << 30) -> Optional[dict]:
+    """The reference's fan-out analogue: every rank pulls its own copy of the ``nbytes``
+    workdir from host memory (each VM's ``rclone copy``, ``machine-script.sh.tpl:89``) --
+    concurrent H2D over every GPU's PCIe link from pinned host DRAM, ``chunk`` bytes at a
+    time.  Same return shape as :func:`measure`, for comparison with the xGMI fan-out."""
+    import torch
+
+    dist = _dist()
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return None
+    chunk = min(chunk, nbytes)
+    host = torch.full((chunk,), 7, dtype=torch.uint8).pin_memory()
+    buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    times = []
+    for i in range(warmup + iters):
+        dist.barrier(group=group)
+        t0 = time.perf_counter()
+        for lo in range(0, nbytes, chunk):
+            n = min(chunk, nbytes - lo)
+            buf[lo:lo + n].copy_(host[:n], non_blocking=True)
+        torch.cuda.synchronize(buf.device)
+        if i >= warmup:
+            times.append(time.perf_counter() - t0)
+    ok = bool((buf[:: max(1, nbytes // 4096)] == 7).all().item())
+    worst = torch.tensor([max(times)], dtype=torch.float64, device=device)
+    dist.all_reduce(worst, op=dist.ReduceOp.MAX, group=group)
+    t = float(worst.item())
+    return {"method": "independent_h2d", "bytes": nbytes, "seconds": t,
+            "GBps": nbytes / t / 1e9 if t > 0 else None, "verified": ok}

@@ -185,3 +185,44 @@ def test_ssh_keys_roundtrip_and_determinism():
         out = subprocess.run(["ssh-keygen", "-y", "-f", f.name], capture_output=True, text=True)
         os.unlink(f.name)
         assert out.returncode == 0 and out.stdout.split()[1] == k1.public_string().split()[1]
+
+
+def test_set_id_cml_prefix():
+    # iterative/utils/helpers_test.go:9-13
+    from terraform_provider_iterative_amd.utils.helpers import set_id
+
+    data = {"name": "example"}
+    assert set_id(data).startswith("cml-example-")
+    assert set_id(data) == data["id"]  # an existing id is kept
+
+
+def test_helpers_cml_snippet_and_env_lookup():
+    from terraform_provider_iterative_amd.utils.helpers import get_cml, multi_env_load_first
+
+    assert get_cml().endswith("npm install --global @dvcorg/cml")
+    assert get_cml("v0.18.1").endswith("@dvcorg/cml@v0.18.1")
+    assert get_cml("0.18.1").endswith("@dvcorg/cml@v0.18.1")
+    assert get_cml("github:iterative/cml#main").endswith("--global github:iterative/cml#main")
+    env = {"A": "", "B": "b", "C": "c"}
+    assert multi_env_load_first(["A", "B", "C"], env) == "b"
+    assert multi_env_load_first(["X"], env) == ""
+
+
+def test_cloud_descriptor():
+    import pytest
+
+    from terraform_provider_iterative_amd.models.cloud import (Cloud, Credentials,
+                                                               NodeCredentials,
+                                                               default_state_root,
+                                                               parse_region_selectors)
+
+    cloud = Cloud(provider="aws", region="us-east-1")
+    assert cloud.get_closest_region({"us-east": "us-east-1", "us-west": "us-west-1"}) == "us-east"
+    with pytest.raises(KeyError):
+        cloud.get_closest_region({"eu-west": "eu-west-1"})
+    assert cloud.timeouts.create == 900 and cloud.timeouts.read == 180
+    assert default_state_root({"TPI_STATE_ROOT": "/x"}) == "/x"
+    assert default_state_root({"HOME": "/h"}) == "/h/.local/state/tpi"
+    node = Cloud(credentials=Credentials(node=NodeCredentials("/srv/tpi")))
+    assert node.state_root() == "/srv/tpi"
+    assert parse_region_selectors("gpus=2-3, numa=1,us-west") == {"gpus": "2-3", "numa": "1"}
