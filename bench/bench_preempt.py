@@ -1,0 +1,160 @@
+#!/usr/bin/env python3
+"""Config 4 end to end: SIGTERM mid-task -> checkpoint pack -> host DRAM -> respawn -> restore.
+
+An ``iterative_task`` on ``cloud = "mi355x"`` runs a rank that holds ``--gb`` of synthetic
+AdamW state in HBM (bf16 params + fp32 moments, as ``bench.py``), registered with the
+preemption handler on a file-backed host region (``--spill-dir``, default ``/dev/shm``, so the
+spill outlives the rank process).  Once the rank reports ready, ``leo preempt`` (SIGUSR1 to the
+supervisor -> SIGTERM to the rank) fires; the rank spills and exits 143, the supervisor
+respawns it with a new machine identity, and the successor restores the state and checks the
+shard-hash digests recorded before the preemption.
+
+Reported from the task's phase journal (``supervisor/events.jsonl``): save time and GB/s, the
+respawn gap, process start -> restore done, restore GB/s, and signal -> state back in HBM.
+The reference recovers a spot VM by re-provisioning it and ``rclone copy``-ing the bucket's
+``data/`` prefix back (``machine-script.sh.tpl:89``); it publishes no numbers.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+RANK = r'''#!%(python)s
+import os, sys, time
+t_start = time.time()
+sys.path.insert(0, %(root)r)
+import torch
+t_import = time.time()
+from bench import synthetic_checkpoint
+from terraform_provider_iterative_amd import ops
+from terraform_provider_iterative_amd.checkpoint import Checkpointer, preemption
+
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+spill = %(spill)r
+nbytes = int(%(gb)r * 1e9)
+resuming = os.path.exists(spill)
+tensors = synthetic_checkpoint(nbytes, 8192, dev)
+torch.cuda.synchronize()
+t_alloc = time.time()
+ck = Checkpointer(tensors, path=spill, codec=%(codec)r)
+t_map = time.time()
+names = list(tensors)[:4]
+
+def digests():
+    return [ops.shard_hash(tensors[n].view(-1).view(torch.uint8)).cpu().tolist() for n in names]
+
+if resuming:
+    for t in tensors.values():
+        t.zero_()
+    torch.cuda.synchronize()
+    t0 = time.time()
+    meta = preemption.resume(ck)
+    torch.cuda.synchronize()
+    t1 = time.time()
+    ok = meta is not None and meta.get("digests") == digests()
+    print("restored %%d bytes in %%.3f s, verified %%s, process start -> restored %%.3f s "
+          "(python+torch %%.3f, HBM state %%.3f, host region map+register %%.3f)"
+          %% (ck.plan.total, t1 - t0, ok, t1 - t_start, t_import - t_start, t_alloc - t_import,
+             t_map - t_alloc), flush=True)
+    ck.close()
+    os.remove(spill)
+    sys.exit(0 if ok else 3)
+preemption.register(ck)
+preemption.on_preempt(lambda: {"digests": digests()})
+preemption.install()
+print("ready %%d bytes in HBM" %% ck.plan.total, flush=True)
+while True:
+    time.sleep(0.05)
+'''
+
+
+def main():
+    p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    p.add_argument("--gb", type=float, default=100.0)
+    p.add_argument("--codec", choices=("none", "tpz1"), default="tpz1")
+    p.add_argument("--spill-dir", default="/dev/shm")
+    p.add_argument("--timeout", type=float, default=900.0)
+    args = p.parse_args()
+
+    from terraform_provider_iterative_amd import backends
+    from terraform_provider_iterative_amd.models.cloud import (Cloud, Credentials,
+                                                               NodeCredentials)
+    from terraform_provider_iterative_amd.models.values import (Environment, Size, Task,
+                                                                Variables)
+    from terraform_provider_iterative_amd.utils.identifier import new_random_identifier
+
+    state = tempfile.mkdtemp(prefix="tpi-preempt-")
+    spill = os.path.join(args.spill_dir, "tpi-preempt-%d.spill" % os.getpid())
+    cloud = Cloud(provider="mi355x",
+                  credentials=Credentials(node=NodeCredentials(state_root=state)))
+    script = RANK % {"python": sys.executable, "root": ROOT, "spill": spill, "gb": args.gb,
+                     "codec": args.codec}
+    spec = Task(size=Size(machine="m+mi355x"),
+                environment=Environment(script=script, timeout=int(args.timeout) + 60,
+                                        variables=Variables({"TPI_TASK": "true"})))
+    task = backends.new(cloud, new_random_identifier("preempt"), spec)
+    result = {"config": "Preempt-recover: SIGTERM mid-task, %.0f GB checkpoint pack->host "
+                        "DRAM->restore (1 x MI355X, iterative_task)" % args.gb,
+              "codec": args.codec, "spill": spill}
+    try:
+        task.create()
+        deadline = time.time() + args.timeout
+        while time.time() < deadline and not any("ready" in l for l in task.logs()):
+            if not task.supervisor_running():
+                break
+            time.sleep(0.2)
+        if not any("ready" in l for l in task.logs()):
+            raise SystemExit("rank never became ready: %s" % task.logs())
+        t_preempt = time.time()
+        task.preempt()
+        status = task.wait(args.timeout)
+        logs = task.logs()
+        events = [(e.code, e.time.timestamp() if hasattr(e.time, "timestamp") else e.time,
+                   e.description) for e in task.events()]
+        result["status"] = status
+        result["logs_tail"] = [l.strip().splitlines()[-1] for l in logs if l.strip()]
+
+        def first(code, after=0.0):
+            for c, t, d in events:
+                if c == code and t >= after:
+                    return t, d
+            return None, None
+
+        t_sig, _ = first("preempt-signal")
+        t_saved, saved = first("checkpoint-saved")
+        t_respawn, _ = first("respawn", t_saved or 0.0)
+        t_start2, _ = first("rank-start", t_respawn or 0.0)
+        t_restored, restored = first("checkpoint-restored", t_respawn or 0.0)
+        if t_sig and t_saved:
+            result["save_s"] = round(t_saved - t_sig, 3)
+            result["save_journal"] = saved
+        if t_saved and t_respawn:
+            result["exit_to_respawn_s"] = round(t_respawn - t_saved, 3)
+        if t_start2 and t_restored:
+            result["rank_start_to_restored_s"] = round(t_restored - t_start2, 3)
+            result["restore_journal"] = restored
+        if t_restored:
+            result["signal_to_restored_s"] = round(t_restored - (t_sig or t_preempt), 3)
+        result["verified"] = any("verified True" in l for l in logs)
+        result["ok"] = bool(status.get("succeeded") == 1 and result["verified"])
+    finally:
+        try:
+            task.delete()
+        finally:
+            shutil.rmtree(state, ignore_errors=True)
+            if os.path.exists(spill):
+                os.remove(spill)
+    print(json.dumps(result))
+
+
+if __name__ == "__main__":
+    main()
