@@ -59,8 +59,9 @@ def parse_args(argv=None):
     return p.parse_args(argv)
 
 
-def synthetic_checkpoint(nbytes: int, hidden: int, device):
-    """bf16 weights + fp32 AdamW moments of transformer blocks until ``nbytes`` is reached."""
+def synthetic_checkpoint(nbytes: int, hidden: int, device, fill: bool = True):
+    """bf16 weights + fp32 AdamW moments of transformer blocks until ``nbytes`` is reached
+    (``fill=False``: uninitialised, for a process that is about to restore them)."""
     import torch
 
     h = hidden
@@ -82,7 +83,9 @@ def synthetic_checkpoint(nbytes: int, hidden: int, device):
                     break
                 n = min(numel, max(left // esz, 1))
                 t = torch.empty(n if n != numel else shape, dtype=dtype, device=device)
-                if kind == "param":
+                if not fill:
+                    pass
+                elif kind == "param":
                     t.normal_(0, 0.02, generator=gen)
                 elif kind == "exp_avg":
                     t.normal_(0, 1e-3, generator=gen)

@@ -35,14 +35,16 @@ import torch
 t_import = time.time()
 from bench import synthetic_checkpoint
 from terraform_provider_iterative_amd import ops
-from terraform_provider_iterative_amd.checkpoint import Checkpointer, preemption
+from terraform_provider_iterative_amd.checkpoint import Checkpointer, prefetch, preemption
 
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 spill = %(spill)r
 nbytes = int(%(gb)r * 1e9)
 resuming = os.path.exists(spill)
-tensors = synthetic_checkpoint(nbytes, 8192, dev)
+if resuming and %(prefetch)r:
+    prefetch(spill)  # map + pin the spill while the model state is being allocated
+tensors = synthetic_checkpoint(nbytes, 8192, dev, fill=not resuming)
 torch.cuda.synchronize()
 t_alloc = time.time()
 ck = Checkpointer(tensors, path=spill, codec=%(codec)r)
@@ -62,7 +64,7 @@ if resuming:
     t1 = time.time()
     ok = meta is not None and meta.get("digests") == digests()
     print("restored %%d bytes in %%.3f s, verified %%s, process start -> restored %%.3f s "
-          "(python+torch %%.3f, HBM state %%.3f, host region map+register %%.3f)"
+          "(python+torch %%.3f, HBM state %%.3f, host region map+register %%.3f after it)"
           %% (ck.plan.total, t1 - t0, ok, t1 - t_start, t_import - t_start, t_alloc - t_import,
              t_map - t_alloc), flush=True)
     ck.close()
@@ -83,6 +85,8 @@ def main():
     p.add_argument("--codec", choices=("none", "tpz1"), default="tpz1")
     p.add_argument("--spill-dir", default="/dev/shm")
     p.add_argument("--timeout", type=float, default=900.0)
+    p.add_argument("--no-prefetch", action="store_true",
+                   help="successor maps its host region only when the Checkpointer is built")
     args = p.parse_args()
 
     from terraform_provider_iterative_amd import backends
@@ -97,14 +101,14 @@ def main():
     cloud = Cloud(provider="mi355x",
                   credentials=Credentials(node=NodeCredentials(state_root=state)))
     script = RANK % {"python": sys.executable, "root": ROOT, "spill": spill, "gb": args.gb,
-                     "codec": args.codec}
+                     "codec": args.codec, "prefetch": not args.no_prefetch}
     spec = Task(size=Size(machine="m+mi355x"),
                 environment=Environment(script=script, timeout=int(args.timeout) + 60,
                                         variables=Variables({"TPI_TASK": "true"})))
     task = backends.new(cloud, new_random_identifier("preempt"), spec)
     result = {"config": "Preempt-recover: SIGTERM mid-task, %.0f GB checkpoint pack->host "
                         "DRAM->restore (1 x MI355X, iterative_task)" % args.gb,
-              "codec": args.codec, "spill": spill}
+              "codec": args.codec, "spill": spill, "prefetch": not args.no_prefetch}
     try:
         task.create()
         deadline = time.time() + args.timeout
@@ -132,6 +136,7 @@ def main():
         t_sig, _ = first("preempt-signal")
         t_saved, saved = first("checkpoint-saved")
         t_respawn, _ = first("respawn", t_saved or 0.0)
+        result["early_handoff"] = first("rank-released")[0] is not None
         t_start2, _ = first("rank-start", t_respawn or 0.0)
         t_restored, restored = first("checkpoint-restored", t_respawn or 0.0)
         if t_sig and t_saved:

@@ -18,6 +18,10 @@
 //    code the checkpoint handler uses after spilling to host DRAM), respawns the rank(s)
 //    with a new machine identity -- gang-wide when ranks are coupled by RCCL -- like the
 //    scaling group replacing a reclaimed spot VM (tpl:89, resource_auto_scaling_group.go);
+//  * early hand-off: a rank that has spilled its checkpoint writes "released" to TPI_NOTIFY_FD;
+//    its successor is spawned at once while the old process is still tearing down its
+//    address space (unpinning a 100 GB host region takes ~1.4 s), and the old one is reaped
+//    in the background;
 //  * SIGTERM/SIGINT/SIGHUP = stop (`leo stop`, scale to 0): ranks terminated, no status;
 //  * exits when no rank is left to run ("no waste" auto-cleanup, tpl:10-15), removing its
 //    GPU lease files.
@@ -155,6 +159,7 @@ struct Rank {
   pid_t pid = -1;
   int fd = -1;
   int logfd = -1;
+  int nfd = -1;  // read end of the rank's notify pipe (TPI_NOTIFY_FD in the rank)
   std::string uuid;
   std::string partial;
   enum State { PENDING, RUNNING, DONE, PREEMPTED } state = PENDING;
@@ -165,6 +170,7 @@ struct Rank {
   int exit_code = -1, exit_signal = 0;
   double started = 0;
   bool first_output = false;  // phase journal: first line of this incarnation seen
+  bool released = false;      // wrote "released" on its notify pipe
 };
 
 struct Spec {
@@ -259,23 +265,35 @@ class Supervisor {
       if (all_finished()) break;
       double timeout = 2.0;
       if (s_.deadline > 0 && !timed_out_) timeout = std::min(timeout, s_.deadline - t);
-      for (auto& r : ranks_)
-        if (r.pid > 0 && r.term_at > 0 && !r.killed)
-          timeout = std::min(timeout, r.term_at + s_.grace - t);
+      for (auto* list : {&ranks_, &detached_})
+        for (auto& r : *list)
+          if (r.pid > 0 && r.term_at > 0 && !r.killed)
+            timeout = std::min(timeout, r.term_at + s_.grace - t);
       if (respawn_at_ > 0) timeout = std::min(timeout, respawn_at_ - t);
       timeout = std::max(timeout, 0.0);
       std::vector<struct pollfd> pfds;
       pfds.push_back({sfd_, POLLIN, 0});
-      std::vector<Rank*> owners;
-      for (auto& r : ranks_)
-        if (r.fd >= 0) {
-          pfds.push_back({r.fd, POLLIN, 0});
-          owners.push_back(&r);
+      std::vector<std::pair<Rank*, bool>> owners;  // (rank, notify pipe?)
+      for (auto* list : {&ranks_, &detached_})
+        for (auto& r : *list) {
+          if (r.fd >= 0) {
+            pfds.push_back({r.fd, POLLIN, 0});
+            owners.push_back({&r, false});
+          }
+          if (r.nfd >= 0) {
+            pfds.push_back({r.nfd, POLLIN, 0});
+            owners.push_back({&r, true});
+          }
         }
       int rc = poll(pfds.data(), pfds.size(), (int)(timeout * 1000) + 1);
       if (rc < 0 && errno != EINTR) break;
-      for (size_t i = 1; i < pfds.size(); ++i)
-        if (pfds[i].revents & (POLLIN | POLLHUP | POLLERR)) pump(*owners[i - 1]);
+      bool released = false;
+      for (size_t i = 1; i < pfds.size(); ++i) {
+        if (!(pfds[i].revents & (POLLIN | POLLHUP | POLLERR))) continue;
+        if (owners[i - 1].second) released |= notified(*owners[i - 1].first);
+        else pump(*owners[i - 1].first);
+      }
+      if (released) handoff_released();
       if (pfds[0].revents & POLLIN) handle_signals();
       if (dirty_ || now() - last_state > 5) {
         write_state();
@@ -289,6 +307,7 @@ class Supervisor {
  private:
   Spec s_;
   std::vector<Rank> ranks_;
+  std::vector<Rank> detached_;  // released incarnations still exiting
   int sfd_ = -1;
   double started_ = 0, respawn_at_ = 0;
   bool stop_ = false, timed_out_ = false, dirty_ = true;
@@ -377,6 +396,7 @@ class Supervisor {
     add("TPI_TASK_DIRECTORY", s_.task_dir);
     add("TPI_RESTART_COUNT", std::to_string(r.restarts));
     add("TPI_EVENTS_FILE", s_.events_path);  // ranks journal checkpoint phases here
+    add("TPI_NOTIFY_FD", "3");                 // "released": spill done, respawn may start
     if (s_.deadline > 0) {
       add("TPI_DEADLINE", std::to_string((long long)s_.deadline));
       add("TPI_REMAINING_RUN_TIME", std::to_string((long long)(s_.deadline - now())));
@@ -407,8 +427,13 @@ class Supervisor {
     r.exit_signal = 0;
     std::string logpath = s_.reports_dir + "/task-" + r.uuid;
     r.logfd = open(logpath.c_str(), O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
-    int p[2];
+    int p[2], pn[2] = {-1, -1};
+    if (pipe2(pn, O_CLOEXEC)) pn[0] = pn[1] = -1;
     if (pipe2(p, O_CLOEXEC)) {
+      if (pn[0] >= 0) {
+        close(pn[0]);
+        close(pn[1]);
+      }
       event("rank-spawn-failed", {"rank " + std::to_string(r.index), strerror(errno)});
       r.state = Rank::DONE;
       write_status(r, "resources", "", "exited");
@@ -443,6 +468,10 @@ class Supervisor {
       if (devnull >= 0) dup2(devnull, 0);
       dup2(p[1], 1);
       dup2(p[1], 2);
+      if (pn[1] >= 0) {
+        if (pn[1] == 3) fcntl(3, F_SETFD, 0);
+        else dup2(pn[1], 3);
+      }
       if (chdir(s_.workdir.c_str())) {
         dprintf(2, "tpi-supervisor: chdir %s: %s\n", s_.workdir.c_str(), strerror(errno));
         _exit(126);
@@ -461,8 +490,10 @@ class Supervisor {
       _exit(127);
     }
     close(p[1]);
+    if (pn[1] >= 0) close(pn[1]);
     if (pid < 0) {
       close(p[0]);
+      if (pn[0] >= 0) close(pn[0]);
       event("rank-spawn-failed", {"rank " + std::to_string(r.index), strerror(errno)});
       r.state = Rank::DONE;
       write_status(r, "resources", "", "exited");
@@ -472,9 +503,12 @@ class Supervisor {
     fcntl(p[0], F_SETFL, fcntl(p[0], F_GETFL) | O_NONBLOCK);
     r.pid = pid;
     r.fd = p[0];
+    if (pn[0] >= 0) fcntl(pn[0], F_SETFL, fcntl(pn[0], F_GETFL) | O_NONBLOCK);
+    r.nfd = pn[0];
     r.state = Rank::RUNNING;
     r.started = now();
     r.first_output = false;
+    r.released = false;
     event("rank-start", {"rank " + std::to_string(r.index), "pid " + std::to_string(pid),
                          "machine " + r.uuid, "gpus " + (r.gpus.empty() ? "-" : r.gpus),
                          "restart " + std::to_string(r.restarts)});
@@ -523,6 +557,61 @@ class Supervisor {
     }
   }
 
+  // Notify pipe readable: returns true when the rank announced "released" and may be handed
+  // off (its spill is complete; the supervisor is terminating it as a preemption).
+  bool notified(Rank& r) {
+    char buf[256];
+    bool got = false;
+    for (;;) {
+      ssize_t n = read(r.nfd, buf, sizeof(buf));
+      if (n > 0) {
+        if (std::string(buf, (size_t)n).find("released") != std::string::npos) got = true;
+        continue;
+      }
+      if (n == 0) {
+        close(r.nfd);
+        r.nfd = -1;
+      } else if (errno == EINTR) {
+        continue;
+      }
+      break;
+    }
+    if (!got || r.pid <= 0 || r.state != Rank::RUNNING || stop_ || timed_out_) return false;
+    if (!(r.reason == TermReason::PREEMPT ||
+          (r.reason == TermReason::NONE && s_.respawn_on_sigterm)))
+      return false;
+    r.released = true;
+    return true;
+  }
+
+  // Released ranks become PREEMPTED now; their old process keeps draining its log and is
+  // reaped (or killed after the grace period) from detached_.
+  void handoff_released() {
+    for (auto& r : ranks_) {
+      if (!r.released || r.pid <= 0) continue;
+      r.released = false;
+      Rank old = r;
+      if (old.nfd >= 0) close(old.nfd);
+      old.nfd = -1;
+      old.state = Rank::DONE;
+      if (old.term_at == 0) old.term_at = now();
+      detached_.push_back(old);
+      std::vector<std::string> desc = {"rank " + std::to_string(r.index), "machine " + r.uuid,
+                                       "pid " + std::to_string(r.pid)};
+      r.pid = -1;
+      r.fd = -1;
+      r.logfd = -1;
+      r.partial.clear();
+      r.exit_code = 143;
+      r.state = Rank::PREEMPTED;
+      event("rank-released", desc);
+      if (s_.gang)
+        for (auto& o : ranks_)
+          if (o.state == Rank::RUNNING) terminate(o, TermReason::PREEMPT);
+      respawn_at_ = now() + s_.respawn_delay;
+    }
+  }
+
   void close_log(Rank& r) {
     if (r.logfd >= 0) {
       close(r.logfd);
@@ -541,13 +630,14 @@ class Supervisor {
   }
 
   void check_grace(double t) {
-    for (auto& r : ranks_)
-      if (r.pid > 0 && r.term_at > 0 && !r.killed && t >= r.term_at + s_.grace) {
-        kill(-r.pid, SIGKILL);
-        kill(r.pid, SIGKILL);
-        r.killed = true;
-        event("rank-killed", {"rank " + std::to_string(r.index), "grace period expired"});
-      }
+    for (auto* list : {&ranks_, &detached_})
+      for (auto& r : *list)
+        if (r.pid > 0 && r.term_at > 0 && !r.killed && t >= r.term_at + s_.grace) {
+          kill(-r.pid, SIGKILL);
+          kill(r.pid, SIGKILL);
+          r.killed = true;
+          event("rank-killed", {"rank " + std::to_string(r.index), "grace period expired"});
+        }
   }
 
   void check_deadline(double t) {
@@ -620,6 +710,19 @@ class Supervisor {
       int st = 0;
       pid_t pid = waitpid(-1, &st, WNOHANG);
       if (pid <= 0) return;
+      for (size_t i = 0; i < detached_.size(); ++i)
+        if (detached_[i].pid == pid) {
+          Rank& d = detached_[i];
+          if (d.fd >= 0) pump(d);
+          if (d.fd >= 0) close(d.fd);
+          close_log(d);
+          const std::string code = WIFSIGNALED(st) ? std::string("signal ") + signame(WTERMSIG(st))
+                                                   : "code " + std::to_string(WEXITSTATUS(st));
+          event("rank-released-exit", {"rank " + std::to_string(d.index), "machine " + d.uuid,
+                                       code});
+          detached_.erase(detached_.begin() + i);
+          break;
+        }
       for (auto& r : ranks_)
         if (r.pid == pid) on_exit(r, st);
     }
@@ -627,6 +730,10 @@ class Supervisor {
 
   void on_exit(Rank& r, int st) {
     if (r.fd >= 0) pump(r);  // drain what is already buffered
+    if (r.nfd >= 0) {
+      close(r.nfd);
+      r.nfd = -1;
+    }
     r.pid = -1;
     if (r.fd < 0) close_log(r);
     bool signaled = WIFSIGNALED(st);
@@ -674,7 +781,7 @@ class Supervisor {
   bool all_finished() {
     for (auto& r : ranks_)
       if (r.state != Rank::DONE || r.pid > 0) return false;
-    return true;
+    return detached_.empty();
   }
 
   int finish() {

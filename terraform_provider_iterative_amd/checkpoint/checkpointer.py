@@ -40,6 +40,7 @@ from ..ops import codec as tpz
 from ..ops import hip, native
 from ..ops.packing import PackPlan, align_up
 from ..ops.packing import pack as host_pack, unpack as host_unpack
+from . import host
 from .host import HostRegion
 
 MAGIC = b"TPICKPT2"
@@ -261,8 +262,9 @@ class Checkpointer:
                 if hip().tpi_device_numa_node(self.device_index, ctypes.byref(node)) == 0:
                     numa_node = node.value
             self.engine = DeviceEngine(self.device_index, chunk_bytes, nbuf, tile_bytes)
-        self.region = HostRegion(self.size, path, device=self.plan.on_device,
-                                 numa_node=numa_node, populate=populate)
+        adopted = host.adopt(path, self.size) if path and self.plan.on_device else None
+        self.region = adopted or HostRegion(self.size, path, device=self.plan.on_device,
+                                            numa_node=numa_node, populate=populate)
         self.crcs = self.region.array(self.crc_offset, 4 * self.plan.ntiles, np.uint32)
         self.csizes = self.region.array(self.csize_offset, 4 * self.plan.ntiles, np.uint32)
         self.saves = 0

@@ -121,3 +121,22 @@ def test_training_state_on_device_carries_cpu_step_counters(tmp_path):
     tensors2, host2 = collect(model, opt)
     for k, v in {**tensors2, **host2}.items():
         assert torch.equal(v, want[k]), k
+
+
+def test_prefetched_spill_region_is_adopted(tmp_path):
+    from terraform_provider_iterative_amd.checkpoint import Checkpointer, host, prefetch
+
+    spill = str(tmp_path / "spill")
+    src = {"w": torch.randn(1 << 20, device="cuda"), "b": torch.randn(4096, device="cuda")}
+    ref = {k: v.clone() for k, v in src.items()}
+    with Checkpointer(src, path=spill) as ck:
+        ck.save({"step": 3})
+    assert prefetch(spill) and spill in host._prefetched
+    dst = {k: torch.zeros_like(v) for k, v in ref.items()}
+    with Checkpointer(dst, path=spill) as ck:
+        assert spill not in host._prefetched  # adopted, not mapped a second time
+        assert ck.region.registered and ck.header()["metadata"] == {"step": 3}
+        assert ck.restore().bad_tiles == 0
+        torch.cuda.synchronize()
+    assert all(torch.equal(dst[k], ref[k]) for k in ref)
+    assert not prefetch(str(tmp_path / "missing"))

@@ -55,15 +55,17 @@ def _wait_for(task, text, timeout=60):
     raise AssertionError("%r never appeared in logs: %s" % (text, task.logs()))
 
 
-@pytest.mark.parametrize("how", ["supervisor", "rank-sigterm"])
+@pytest.mark.parametrize("how", ["supervisor", "rank-sigterm", "no-handoff"])
 def test_preempt_checkpoint_respawn_resume(cloud, how):
     script = TRAIN % {"python": sys.executable, "root": ROOT, "steps": 40}
-    spec = Task(environment=Environment(script=script, timeout=300,
-                                        variables=Variables({"TPI_TASK": "true"})))
+    env = {"TPI_TASK": "true"}
+    if how == "no-handoff":  # successor waits for the old process to exit
+        env["TPI_EARLY_HANDOFF"] = "0"
+    spec = Task(environment=Environment(script=script, timeout=300, variables=Variables(env)))
     task = backends.new(cloud, new_deterministic_identifier("preempt-" + how), spec)
     task.create()
     _wait_for(task, "step 5")
-    if how == "supervisor":
+    if how != "rank-sigterm":
         task.preempt()  # leo preempt: SIGUSR1 -> supervisor SIGTERMs the ranks
     else:  # an external agent SIGTERMs the rank process directly
         import json
@@ -81,7 +83,13 @@ def test_preempt_checkpoint_respawn_resume(cloud, how):
     assert resumed_at >= 5
     assert "final 40 40" in logs[1]
     codes = [e.code for e in task.events()]
-    assert "rank-preempted" in codes and "respawn" in codes
+    assert "respawn" in codes
+    if how == "no-handoff":
+        assert "rank-preempted" in codes and "rank-released" not in codes
+    else:  # early hand-off: respawned on "released", the old process reaped afterwards
+        assert "rank-released" in codes and "rank-released-exit" in codes
+        assert "checkpoint-released" in codes
+        assert codes.index("rank-released") < codes.index("respawn")
     # phase journal: start -> first output -> preempt -> saved -> respawn -> restored
     for phase in ("rank-start", "rank-first-output", "preempt-signal", "checkpoint-saved",
                   "checkpoint-restored"):
@@ -90,4 +98,28 @@ def test_preempt_checkpoint_respawn_resume(cloud, how):
         codes.index("checkpoint-restored")
     saved = [e for e in task.events() if e.code == "checkpoint-saved"][0]
     assert saved.description[0] == "rank 0" and saved.description[-1].endswith("GB/s")
+    task.delete()
+
+
+def test_successor_starts_while_released_rank_exits(cloud):
+    # the released rank lingers 2 s after "released" (a slow teardown): its successor must
+    # already be running, and the old process is still reaped and journalled
+    slow = TRAIN.replace("preemption.install()", "_orig = preemption.notify_released\n"
+                         "def _slow():\n    sent = _orig()\n    time.sleep(2)\n    return sent\n"
+                         "preemption.notify_released = _slow\npreemption.install()")
+    script = slow % {"python": sys.executable, "root": ROOT, "steps": 30}
+    spec = Task(environment=Environment(script=script, timeout=300,
+                                        variables=Variables({"TPI_TASK": "true"})))
+    task = backends.new(cloud, new_deterministic_identifier("preempt-overlap"), spec)
+    task.create()
+    _wait_for(task, "step 3")
+    task.preempt()
+    status = task.wait(90)
+    assert status["succeeded"] == 1, task.logs()
+    events = task.events()
+    released_exit = [e.time for e in events if e.code == "rank-released-exit"]
+    starts = [e.time for e in events if e.code == "rank-start"]
+    assert len(starts) == 2 and released_exit
+    assert starts[1] < released_exit[0]
+    assert "final 30 30" in task.logs()[1]
     task.delete()
