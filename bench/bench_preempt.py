@@ -41,6 +41,9 @@ dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 spill = %(spill)r
 nbytes = int(%(gb)r * 1e9)
+# warm standby: the successor waits here (imports done, spill being mapped) for its activation
+activated = preemption.standby(spill if %(prefetch)r else None) if %(standby)r else False
+t_active = time.time()
 resuming = os.path.exists(spill)
 if resuming and %(prefetch)r:
     prefetch(spill)  # map + pin the spill while the model state is being allocated
@@ -63,10 +66,11 @@ if resuming:
     torch.cuda.synchronize()
     t1 = time.time()
     ok = meta is not None and meta.get("digests") == digests()
-    print("restored %%d bytes in %%.3f s, verified %%s, process start -> restored %%.3f s "
-          "(python+torch %%.3f, HBM state %%.3f, host region map+register %%.3f after it)"
-          %% (ck.plan.total, t1 - t0, ok, t1 - t_start, t_import - t_start, t_alloc - t_import,
-             t_map - t_alloc), flush=True)
+    print("restored %%d bytes in %%.3f s, verified %%s, warm standby %%s, activation -> restored "
+          "%%.3f s (HBM state %%.3f, host region map+register %%.3f after it); process start -> "
+          "import done %%.3f s" %% (ck.plan.total, t1 - t0, ok, activated, t1 - t_active,
+                                  t_alloc - t_active, t_map - t_alloc, t_import - t_start),
+          flush=True)
     ck.close()
     os.remove(spill)
     sys.exit(0 if ok else 3)
@@ -85,6 +89,8 @@ def main():
     p.add_argument("--codec", choices=("none", "tpz1"), default="tpz1")
     p.add_argument("--spill-dir", default="/dev/shm")
     p.add_argument("--timeout", type=float, default=900.0)
+    p.add_argument("--no-standby", action="store_true",
+                   help="cold respawn: the successor starts after the predecessor released")
     p.add_argument("--no-prefetch", action="store_true",
                    help="successor maps its host region only when the Checkpointer is built")
     args = p.parse_args()
@@ -101,14 +107,16 @@ def main():
     cloud = Cloud(provider="mi355x",
                   credentials=Credentials(node=NodeCredentials(state_root=state)))
     script = RANK % {"python": sys.executable, "root": ROOT, "spill": spill, "gb": args.gb,
-                     "codec": args.codec, "prefetch": not args.no_prefetch}
+                     "codec": args.codec, "prefetch": not args.no_prefetch,
+                     "standby": not args.no_standby}
     spec = Task(size=Size(machine="m+mi355x"),
                 environment=Environment(script=script, timeout=int(args.timeout) + 60,
                                         variables=Variables({"TPI_TASK": "true"})))
     task = backends.new(cloud, new_random_identifier("preempt"), spec)
     result = {"config": "Preempt-recover: SIGTERM mid-task, %.0f GB checkpoint pack->host "
                         "DRAM->restore (1 x MI355X, iterative_task)" % args.gb,
-              "codec": args.codec, "spill": spill, "prefetch": not args.no_prefetch}
+              "codec": args.codec, "spill": spill, "prefetch": not args.no_prefetch,
+              "standby": not args.no_standby}
     try:
         task.create()
         deadline = time.time() + args.timeout
@@ -138,13 +146,14 @@ def main():
         t_respawn, _ = first("respawn", t_saved or 0.0)
         result["early_handoff"] = first("rank-released")[0] is not None
         t_start2, _ = first("rank-start", t_respawn or 0.0)
+        result["warm_standby_activated"] = first("standby-activated")[0] is not None
         t_restored, restored = first("checkpoint-restored", t_respawn or 0.0)
         if t_sig and t_saved:
             result["save_s"] = round(t_saved - t_sig, 3)
             result["save_journal"] = saved
         if t_saved and t_respawn:
             result["exit_to_respawn_s"] = round(t_respawn - t_saved, 3)
-        if t_start2 and t_restored:
+        if t_start2 and t_restored:  # (with a warm standby: activation -> restored)
             result["rank_start_to_restored_s"] = round(t_restored - t_start2, 3)
             result["restore_journal"] = restored
         if t_restored:

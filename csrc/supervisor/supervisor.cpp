@@ -22,6 +22,10 @@
 //    its successor is spawned at once while the old process is still tearing down its
 //    address space (unpinning a 100 GB host region takes ~1.4 s), and the old one is reaped
 //    in the background;
+//  * warm standby: when a rank that announced "standby" is preempted, its successor is spawned
+//    at once with TPI_STANDBY=1 and imports/maps what it can while the old rank is still
+//    spilling; it blocks in preemption.standby() until "go" arrives on TPI_STANDBY_FD, written
+//    when the old rank has released (or exited as preempted);
 //  * SIGTERM/SIGINT/SIGHUP = stop (`leo stop`, scale to 0): ranks terminated, no status;
 //  * exits when no rank is left to run ("no waste" auto-cleanup, tpl:10-15), removing its
 //    GPU lease files.
@@ -171,6 +175,8 @@ struct Rank {
   double started = 0;
   bool first_output = false;  // phase journal: first line of this incarnation seen
   bool released = false;      // wrote "released" on its notify pipe
+  bool standby_capable = false;  // announced "standby" (calls preemption.standby())
+  int gofd = -1;                 // standby only: write end of its activation pipe
 };
 
 struct Spec {
@@ -183,6 +189,7 @@ struct Spec {
   std::string master_addr = "127.0.0.1";
   int master_port = 29500;
   bool gang = true, fail_fast = true, respawn_on_sigterm = true, login_shell = false;
+  bool standby = true;
   int max_restarts = -1;
   double grace = 30, respawn_delay = 0;
   std::string reports_dir, state_path, events_path;
@@ -215,6 +222,7 @@ Spec load_spec(const std::string& path) {
   s.max_restarts = (int)v["max_restarts"].num(-1);
   s.grace = v["grace_seconds"].num(30);
   s.respawn_delay = v["respawn_delay"].num(0);
+  s.standby = v["standby"].boolean(true);
   s.reports_dir = v["reports_dir"].str(s.task_dir + "/reports");
   s.state_path = v["state_path"].str(s.task_dir + "/supervisor/state.json");
   s.events_path = v["events_path"].str(s.task_dir + "/supervisor/events.jsonl");
@@ -227,6 +235,7 @@ class Supervisor {
  public:
   explicit Supervisor(Spec spec) : s_(std::move(spec)) {
     ranks_.resize(s_.parallelism);
+    standby_.resize(s_.parallelism);
     for (int i = 0; i < s_.parallelism; ++i) {
       ranks_[i].index = i;
       ranks_[i].gpus = s_.rank_gpus[i];
@@ -274,7 +283,7 @@ class Supervisor {
       std::vector<struct pollfd> pfds;
       pfds.push_back({sfd_, POLLIN, 0});
       std::vector<std::pair<Rank*, bool>> owners;  // (rank, notify pipe?)
-      for (auto* list : {&ranks_, &detached_})
+      for (auto* list : {&ranks_, &detached_, &standby_})
         for (auto& r : *list) {
           if (r.fd >= 0) {
             pfds.push_back({r.fd, POLLIN, 0});
@@ -308,6 +317,7 @@ class Supervisor {
   Spec s_;
   std::vector<Rank> ranks_;
   std::vector<Rank> detached_;  // released incarnations still exiting
+  std::vector<Rank> standby_;   // per rank index: warm successor waiting for "go" (pid > 0)
   int sfd_ = -1;
   double started_ = 0, respawn_at_ = 0;
   bool stop_ = false, timed_out_ = false, dirty_ = true;
@@ -417,7 +427,7 @@ class Supervisor {
     return env;
   }
 
-  void spawn(Rank& r) {
+  void spawn(Rank& r, bool standby = false) {
     r.uuid = uuid4();
     r.partial.clear();
     r.reason = TermReason::NONE;
@@ -427,19 +437,22 @@ class Supervisor {
     r.exit_signal = 0;
     std::string logpath = s_.reports_dir + "/task-" + r.uuid;
     r.logfd = open(logpath.c_str(), O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
-    int p[2], pn[2] = {-1, -1};
+    int p[2], pn[2] = {-1, -1}, go[2] = {-1, -1};
     if (pipe2(pn, O_CLOEXEC)) pn[0] = pn[1] = -1;
-    if (pipe2(p, O_CLOEXEC)) {
-      if (pn[0] >= 0) {
-        close(pn[0]);
-        close(pn[1]);
-      }
+    if (standby && pipe2(go, O_CLOEXEC)) go[0] = go[1] = -1;
+    if (pipe2(p, O_CLOEXEC) || (standby && go[0] < 0)) {
+      for (int fd : {pn[0], pn[1], go[0], go[1]})
+        if (fd >= 0) close(fd);
       event("rank-spawn-failed", {"rank " + std::to_string(r.index), strerror(errno)});
       r.state = Rank::DONE;
       write_status(r, "resources", "", "exited");
       return;
     }
     std::vector<std::string> env = rank_env(r);
+    if (standby) {
+      env.push_back("TPI_STANDBY=1");
+      env.push_back("TPI_STANDBY_FD=4");
+    }
     std::vector<char*> envp;
     for (auto& e : env) envp.push_back(const_cast<char*>(e.c_str()));
     envp.push_back(nullptr);
@@ -468,10 +481,12 @@ class Supervisor {
       if (devnull >= 0) dup2(devnull, 0);
       dup2(p[1], 1);
       dup2(p[1], 2);
-      if (pn[1] >= 0) {
-        if (pn[1] == 3) fcntl(3, F_SETFD, 0);
-        else dup2(pn[1], 3);
-      }
+      // notify pipe -> fd 3, standby activation pipe -> fd 4 (via temporaries >= 10 so
+      // neither dup2 can clobber the other's source)
+      const int nt = pn[1] >= 0 ? fcntl(pn[1], F_DUPFD_CLOEXEC, 10) : -1;
+      const int gt = go[0] >= 0 ? fcntl(go[0], F_DUPFD_CLOEXEC, 10) : -1;
+      if (nt >= 0) dup2(nt, 3);
+      if (gt >= 0) dup2(gt, 4);
       if (chdir(s_.workdir.c_str())) {
         dprintf(2, "tpi-supervisor: chdir %s: %s\n", s_.workdir.c_str(), strerror(errno));
         _exit(126);
@@ -491,9 +506,11 @@ class Supervisor {
     }
     close(p[1]);
     if (pn[1] >= 0) close(pn[1]);
+    if (go[0] >= 0) close(go[0]);
     if (pid < 0) {
       close(p[0]);
       if (pn[0] >= 0) close(pn[0]);
+      if (go[1] >= 0) close(go[1]);
       event("rank-spawn-failed", {"rank " + std::to_string(r.index), strerror(errno)});
       r.state = Rank::DONE;
       write_status(r, "resources", "", "exited");
@@ -505,13 +522,81 @@ class Supervisor {
     r.fd = p[0];
     if (pn[0] >= 0) fcntl(pn[0], F_SETFL, fcntl(pn[0], F_GETFL) | O_NONBLOCK);
     r.nfd = pn[0];
+    r.gofd = go[1];
+    r.standby_capable = false;
     r.state = Rank::RUNNING;
     r.started = now();
     r.first_output = false;
     r.released = false;
-    event("rank-start", {"rank " + std::to_string(r.index), "pid " + std::to_string(pid),
+    event(standby ? "standby-start" : "rank-start",
+          {"rank " + std::to_string(r.index), "pid " + std::to_string(pid), "machine " + r.uuid,
+           "gpus " + (r.gpus.empty() ? "-" : r.gpus), "restart " + std::to_string(r.restarts)});
+  }
+
+  // Warm successor of rank r, spawned while r is being preempted.
+  void spawn_standby(Rank& r) {
+    Rank& sb = standby_[r.index];
+    if (!s_.standby || !r.standby_capable || sb.pid > 0 || stop_ || timed_out_) return;
+    if (s_.max_restarts >= 0 && r.restarts >= s_.max_restarts) return;
+    sb = Rank();
+    sb.index = r.index;
+    sb.gpus = r.gpus;
+    sb.restarts = r.restarts + 1;
+    spawn(sb, true);
+    if (sb.state != Rank::RUNNING) sb = Rank();
+  }
+
+  // Kill an unused standby; its process is reaped (and its log drained) from detached_.
+  void discard_standby(int index, const char* why) {
+    Rank& sb = standby_[index];
+    if (sb.pid <= 0) return;
+    if (sb.gofd >= 0) close(sb.gofd);  // EOF without "go": the standby exits on its own
+    sb.gofd = -1;
+    kill(-sb.pid, SIGKILL);
+    kill(sb.pid, SIGKILL);
+    sb.killed = true;
+    sb.term_at = now();
+    sb.state = Rank::DONE;
+    event("standby-discarded", {"rank " + std::to_string(index), "machine " + sb.uuid, why});
+    detached_.push_back(sb);
+    sb = Rank();
+  }
+
+  // Rank r (PREEMPTED) resumes in its standby: the standby becomes the rank's incarnation.
+  bool activate_standby(Rank& r) {
+    Rank& sb = standby_[r.index];
+    if (sb.pid <= 0) return false;
+    const char go[] = "go\n";
+    const bool sent = sb.gofd >= 0 && write(sb.gofd, go, 3) == 3;
+    if (sb.gofd >= 0) close(sb.gofd);
+    sb.gofd = -1;
+    if (!sent) {
+      discard_standby(r.index, "activation failed");
+      return false;
+    }
+    const int restarts = r.restarts;
+    r.uuid = sb.uuid;
+    r.pid = sb.pid;
+    r.fd = sb.fd;
+    r.logfd = sb.logfd;
+    r.nfd = sb.nfd;
+    r.partial = sb.partial;
+    r.started = sb.started;
+    r.first_output = sb.first_output;
+    r.standby_capable = sb.standby_capable;
+    r.restarts = restarts;
+    r.reason = TermReason::NONE;
+    r.term_at = 0;
+    r.killed = false;
+    r.released = false;
+    r.exit_code = -1;
+    r.exit_signal = 0;
+    r.state = Rank::RUNNING;
+    sb = Rank();
+    event("rank-start", {"rank " + std::to_string(r.index), "pid " + std::to_string(r.pid),
                          "machine " + r.uuid, "gpus " + (r.gpus.empty() ? "-" : r.gpus),
-                         "restart " + std::to_string(r.restarts)});
+                         "restart " + std::to_string(r.restarts), "warm standby"});
+    return true;
   }
 
   void emit_line(Rank& r, const std::string& line) {
@@ -565,7 +650,9 @@ class Supervisor {
     for (;;) {
       ssize_t n = read(r.nfd, buf, sizeof(buf));
       if (n > 0) {
-        if (std::string(buf, (size_t)n).find("released") != std::string::npos) got = true;
+        const std::string msg(buf, (size_t)n);
+        if (msg.find("released") != std::string::npos) got = true;
+        if (msg.find("standby") != std::string::npos) r.standby_capable = true;
         continue;
       }
       if (n == 0) {
@@ -645,6 +732,7 @@ class Supervisor {
     timed_out_ = true;
     respawn_at_ = 0;
     event("deadline", {"timeout reached"});
+    for (int i = 0; i < s_.parallelism; ++i) discard_standby(i, "deadline");
     for (auto& r : ranks_) {
       if (r.state == Rank::RUNNING) {
         terminate(r, TermReason::TIMEOUT);
@@ -664,6 +752,7 @@ class Supervisor {
         if (s_.max_restarts >= 0 && r.restarts >= s_.max_restarts) {
           write_status(r, "start-limit-hit", "", "exited");
           r.state = Rank::DONE;
+          discard_standby(r.index, "restart limit");
           event("rank-restart-limit", {"rank " + std::to_string(r.index)});
           continue;
         }
@@ -671,7 +760,7 @@ class Supervisor {
         total_restarts_++;
         event("respawn", {"rank " + std::to_string(r.index),
                           "restart " + std::to_string(r.restarts)});
-        spawn(r);
+        if (!activate_standby(r)) spawn(r);
       }
   }
 
@@ -687,6 +776,7 @@ class Supervisor {
             stop_ = true;
             respawn_at_ = 0;
             event("stop-requested", {std::string("signal ") + signame(si.ssi_signo)});
+            for (int i = 0; i < s_.parallelism; ++i) discard_standby(i, "stop");
             for (auto& r : ranks_) {
               if (r.state == Rank::RUNNING) terminate(r, TermReason::STOP);
               else if (r.state != Rank::DONE) r.state = Rank::DONE;
@@ -697,6 +787,8 @@ class Supervisor {
           if (!stop_ && !timed_out_) {
             event("preempt-requested", {"all ranks"});
             for (auto& r : ranks_) terminate(r, TermReason::PREEMPT);
+            for (auto& r : ranks_)
+              if (r.state == Rank::RUNNING) spawn_standby(r);
           }
           break;
         default: break;
@@ -723,6 +815,17 @@ class Supervisor {
           detached_.erase(detached_.begin() + i);
           break;
         }
+      for (auto& sb : standby_)
+        if (sb.pid == pid) {  // a standby died before it was activated
+          if (sb.fd >= 0) pump(sb);
+          for (int fd : {sb.fd, sb.nfd, sb.gofd})
+            if (fd >= 0) close(fd);
+          close_log(sb);
+          event("standby-exit", {"rank " + std::to_string(sb.index), "machine " + sb.uuid,
+                                 WIFSIGNALED(st) ? std::string("signal ") + signame(WTERMSIG(st))
+                                                 : "code " + std::to_string(WEXITSTATUS(st))});
+          sb = Rank();
+        }
       for (auto& r : ranks_)
         if (r.pid == pid) on_exit(r, st);
     }
@@ -746,11 +849,13 @@ class Supervisor {
     std::vector<std::string> desc = {"rank " + std::to_string(r.index), "machine " + r.uuid,
                                      (signaled ? "signal " : "code ") + code_s};
     if (r.reason == TermReason::STOP || stop_) {
+      discard_standby(r.index, "stop");
       r.state = Rank::DONE;  // scaled to zero: no status (the machine was "shut down")
       event("rank-stopped", desc);
       return;
     }
     if (r.reason == TermReason::TIMEOUT) {
+      discard_standby(r.index, "timeout");
       r.state = Rank::DONE;
       write_status(r, "timeout", code_s, status_s);
       event("rank-timeout", desc);
@@ -769,6 +874,7 @@ class Supervisor {
       return;
     }
     r.state = Rank::DONE;
+    discard_standby(r.index, "rank finished");
     std::string result = signaled ? "signal" : (code == 0 ? "success" : "exit-code");
     if (r.reason == TermReason::FAILFAST) result = "signal";
     write_status(r, result, code_s, status_s);
@@ -781,6 +887,8 @@ class Supervisor {
   bool all_finished() {
     for (auto& r : ranks_)
       if (r.state != Rank::DONE || r.pid > 0) return false;
+    for (auto& sb : standby_)
+      if (sb.pid > 0) return false;
     return detached_.empty();
   }
 

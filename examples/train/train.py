@@ -43,7 +43,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from terraform_provider_iterative_amd.checkpoint import TrainingState
+    from terraform_provider_iterative_amd.checkpoint import TrainingState, preemption
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -51,6 +51,11 @@ def main():
     device = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
     if device.type == "cuda":
         torch.cuda.set_device(device)
+    data_dir = os.environ.get("TPI_DATA_DIRECTORY", ".")
+    spill = os.path.join(data_dir, ".ckpt-rank%d" % rank)
+    # warm standby: a successor started while its preempted predecessor is still spilling waits
+    # here (torch imported, GPU up, spill region being mapped) until the supervisor activates it
+    preemption.standby(spill if device.type == "cuda" else None)
     if world > 1:
         dist.init_process_group("nccl" if device.type == "cuda" else "gloo",
                                 **({"device_id": device} if device.type == "cuda" else {}))
@@ -85,8 +90,6 @@ def main():
     model(x).float().pow(2).mean().backward()
     opt.step()
     opt.zero_grad(set_to_none=False)
-    data_dir = os.environ.get("TPI_DATA_DIRECTORY", ".")
-    spill = os.path.join(data_dir, ".ckpt-rank%d" % rank)
     # model + optimizer device state by reference; CPU-side Adam step counters ride in the
     # checkpoint header (bias correction needs them after a resume)
     state = TrainingState(model, opt, extra={"step": step_t}, path=spill)

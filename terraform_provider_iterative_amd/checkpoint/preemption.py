@@ -113,14 +113,54 @@ def _handoff_safe() -> bool:
 def notify_released() -> bool:
     """Tell the supervisor the spill is complete (``TPI_NOTIFY_FD``), so it can respawn this
     rank now instead of after the exit; returns whether a notification was sent."""
+    if not os.environ.get("TPI_NOTIFY_FD") or not _handoff_safe():
+        return False
+    return _notify(b"released\n")
+
+
+def _notify(message: bytes) -> bool:
     fd = os.environ.get("TPI_NOTIFY_FD")
-    if not fd or not _handoff_safe():
+    if not fd:
         return False
     try:
-        os.write(int(fd), b"released\n")
+        os.write(int(fd), message)
         return True
     except (OSError, ValueError):
         return False
+
+
+def standby(prefetch_path: Optional[str] = None) -> bool:
+    """Warm-standby point of a rank script: call it once the imports are done.
+
+    In a normal incarnation it announces to the supervisor that this script can run as a warm
+    standby and returns False at once.  When the rank is preempted, the supervisor then starts
+    its successor immediately with ``TPI_STANDBY=1``: that process gets here (torch imported,
+    GPU initialised) while the old rank is still spilling, starts mapping ``prefetch_path`` (the
+    spill region, :func:`..host.prefetch`) and blocks until the supervisor activates it --
+    right after the old rank has released -- then returns True and resumes from the spill.
+    A standby that is not needed is killed (or sees EOF and exits quietly).
+    """
+    if os.environ.get("TPI_STANDBY") != "1":
+        _notify(b"standby\n")
+        return False
+    if prefetch_path:
+        from .host import prefetch
+
+        prefetch(prefetch_path)
+    fd = int(os.environ.get("TPI_STANDBY_FD", "4"))
+    while True:
+        try:
+            msg = os.read(fd, 16)
+            break
+        except InterruptedError:
+            continue
+    if not msg.startswith(b"go"):
+        os._exit(0)  # discarded before activation
+    os.close(fd)
+    os.environ.pop("TPI_STANDBY", None)
+    journal("standby-activated")
+    _notify(b"standby\n")  # the activated process can itself be succeeded by a standby
+    return True
 
 
 def _handler(signum, frame):  # pragma: no cover - exercised in subprocess tests

@@ -123,3 +123,52 @@ def test_successor_starts_while_released_rank_exits(cloud):
     assert starts[1] < released_exit[0]
     assert "final 30 30" in task.logs()[1]
     task.delete()
+
+
+STANDBY = TRAIN.replace("spill = os.path.join(", "activated = preemption.standby()\nspill = os.path.join(")
+STANDBY = STANDBY.replace('print(("resumed', 'print("activated" if activated else "cold", flush=True)\nprint(("resumed')
+
+
+def test_warm_standby_takes_over(cloud):
+    script = STANDBY % {"python": sys.executable, "root": ROOT, "steps": 30}
+    spec = Task(environment=Environment(script=script, timeout=300,
+                                        variables=Variables({"TPI_TASK": "true"})))
+    task = backends.new(cloud, new_deterministic_identifier("preempt-standby"), spec)
+    task.create()
+    _wait_for(task, "step 3")
+    task.preempt()
+    status = task.wait(90)
+    logs = task.logs()
+    assert status["succeeded"] == 1 and len(logs) == 2, (status, logs)
+    assert "cold" in logs[0] and "activated" in logs[1] and "final 30 30" in logs[1]
+    events = task.events()
+    codes = [e.code for e in events]
+    for code in ("standby-start", "standby-activated", "rank-released", "respawn"):
+        assert code in codes, (code, codes)
+    assert "standby-discarded" not in codes
+    starts = [e for e in events if e.code == "rank-start"]
+    assert len(starts) == 2 and "warm standby" in starts[1].description
+    task.delete()
+
+
+def test_unused_standby_is_discarded(cloud):
+    # stop arrives while the preempted rank is still releasing: its standby must not run
+    slow = STANDBY.replace("preemption.install()", "_orig = preemption.notify_released\n"
+                           "def _slow():\n    time.sleep(3)\n    return _orig()\n"
+                           "preemption.notify_released = _slow\npreemption.install()")
+    script = slow % {"python": sys.executable, "root": ROOT, "steps": 30}
+    spec = Task(environment=Environment(script=script, timeout=300,
+                                        variables=Variables({"TPI_TASK": "true"})))
+    task = backends.new(cloud, new_deterministic_identifier("preempt-standby-stop"), spec)
+    task.create()
+    _wait_for(task, "step 3")
+    task.preempt()
+    deadline = time.time() + 30
+    while time.time() < deadline and "standby-start" not in [e.code for e in task.events()]:
+        time.sleep(0.05)
+    task.stop()
+    task.wait(60)
+    codes = [e.code for e in task.events()]
+    assert "standby-start" in codes and "standby-discarded" in codes, codes
+    assert "standby-activated" not in codes and not task.supervisor_running()
+    task.delete()
