@@ -89,8 +89,8 @@ def main():
     p.add_argument("--codec", choices=("none", "tpz1"), default="tpz1")
     p.add_argument("--spill-dir", default="/dev/shm")
     p.add_argument("--timeout", type=float, default=900.0)
-    p.add_argument("--no-standby", action="store_true",
-                   help="cold respawn: the successor starts after the predecessor released")
+    p.add_argument("--standby", action="store_true",
+                   help="warm standby successor (TPI_WARM_STANDBY=1), started at the preemption")
     p.add_argument("--no-prefetch", action="store_true",
                    help="successor maps its host region only when the Checkpointer is built")
     args = p.parse_args()
@@ -108,7 +108,7 @@ def main():
                   credentials=Credentials(node=NodeCredentials(state_root=state)))
     script = RANK % {"python": sys.executable, "root": ROOT, "spill": spill, "gb": args.gb,
                      "codec": args.codec, "prefetch": not args.no_prefetch,
-                     "standby": not args.no_standby}
+                     "standby": args.standby}
     spec = Task(size=Size(machine="m+mi355x"),
                 environment=Environment(script=script, timeout=int(args.timeout) + 60,
                                         variables=Variables({"TPI_TASK": "true"})))
@@ -116,7 +116,9 @@ def main():
     result = {"config": "Preempt-recover: SIGTERM mid-task, %.0f GB checkpoint pack->host "
                         "DRAM->restore (1 x MI355X, iterative_task)" % args.gb,
               "codec": args.codec, "spill": spill, "prefetch": not args.no_prefetch,
-              "standby": not args.no_standby}
+              "standby": args.standby}
+    if args.standby:
+        os.environ["TPI_WARM_STANDBY"] = "1"
     try:
         task.create()
         deadline = time.time() + args.timeout

@@ -22,7 +22,8 @@
 //    its successor is spawned at once while the old process is still tearing down its
 //    address space (unpinning a 100 GB host region takes ~1.4 s), and the old one is reaped
 //    in the background;
-//  * warm standby: when a rank that announced "standby" is preempted, its successor is spawned
+//  * warm standby (spec "standby", opt-in): when a rank that announced "standby" is preempted, its
+//    successor is spawned
 //    at once with TPI_STANDBY=1 and imports/maps what it can while the old rank is still
 //    spilling; it blocks in preemption.standby() until "go" arrives on TPI_STANDBY_FD, written
 //    when the old rank has released (or exited as preempted);
@@ -189,7 +190,7 @@ struct Spec {
   std::string master_addr = "127.0.0.1";
   int master_port = 29500;
   bool gang = true, fail_fast = true, respawn_on_sigterm = true, login_shell = false;
-  bool standby = true;
+  bool standby = false;
   int max_restarts = -1;
   double grace = 30, respawn_delay = 0;
   std::string reports_dir, state_path, events_path;
@@ -222,7 +223,7 @@ Spec load_spec(const std::string& path) {
   s.max_restarts = (int)v["max_restarts"].num(-1);
   s.grace = v["grace_seconds"].num(30);
   s.respawn_delay = v["respawn_delay"].num(0);
-  s.standby = v["standby"].boolean(true);
+  s.standby = v["standby"].boolean(false);
   s.reports_dir = v["reports_dir"].str(s.task_dir + "/reports");
   s.state_path = v["state_path"].str(s.task_dir + "/supervisor/state.json");
   s.events_path = v["events_path"].str(s.task_dir + "/supervisor/events.jsonl");

@@ -243,6 +243,9 @@ class NodeTask(Task):
             "max_restarts": int(os.environ.get("TPI_MAX_RESTARTS", "-1")),
             "grace_seconds": float(os.environ.get("TPI_GRACE_SECONDS", "30")),
             "respawn_delay": float(os.environ.get("TPI_RESPAWN_DELAY", "0")),
+            # warm standby successors (preemption.standby()): opt-in, they pay off when a
+            # spill takes longer than a rank's start-up (profiles/preempt_e2e_100g_round1.md)
+            "standby": os.environ.get("TPI_WARM_STANDBY", "0") == "1",
             "reports_dir": self.reports_dir,
             "state_path": os.path.join(self.sup_dir, "state.json"),
             "events_path": os.path.join(self.sup_dir, "events.jsonl"),

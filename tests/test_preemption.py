@@ -129,7 +129,8 @@ STANDBY = TRAIN.replace("spill = os.path.join(", "activated = preemption.standby
 STANDBY = STANDBY.replace('print(("resumed', 'print("activated" if activated else "cold", flush=True)\nprint(("resumed')
 
 
-def test_warm_standby_takes_over(cloud):
+def test_warm_standby_takes_over(cloud, monkeypatch):
+    monkeypatch.setenv("TPI_WARM_STANDBY", "1")
     script = STANDBY % {"python": sys.executable, "root": ROOT, "steps": 30}
     spec = Task(environment=Environment(script=script, timeout=300,
                                         variables=Variables({"TPI_TASK": "true"})))
@@ -151,7 +152,8 @@ def test_warm_standby_takes_over(cloud):
     task.delete()
 
 
-def test_unused_standby_is_discarded(cloud):
+def test_unused_standby_is_discarded(cloud, monkeypatch):
+    monkeypatch.setenv("TPI_WARM_STANDBY", "1")
     # stop arrives while the preempted rank is still releasing: its standby must not run
     slow = STANDBY.replace("preemption.install()", "_orig = preemption.notify_released\n"
                            "def _slow():\n    time.sleep(3)\n    return _orig()\n"
