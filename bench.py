@@ -56,6 +56,9 @@ def parse_args(argv=None):
     p.add_argument("--verify", action="store_true", default=True)
     p.add_argument("--no-async", action="store_true",
                    help="skip the (untimed) save_async stall measurement")
+    p.add_argument("--device", choices=("cuda", "cpu"), default="cuda",
+                   help="cpu: rehearse the multi-rank control flow on CPU tensors over gloo "
+                        "(tests; not a measurement of the MI355X path)")
     return p.parse_args(argv)
 
 
@@ -120,14 +123,23 @@ def main(argv=None):
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print("bench: WORLD_SIZE=%d but --gpus=%d" % (world, args.gpus), file=sys.stderr)
-    if not torch.cuda.is_available():
+    on_gpu = args.device == "cuda"
+    if on_gpu and not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (MI355X)")
     # TPI_BENCH_BACKEND=gloo rehearses the multi-rank flow on a box with fewer GPUs than ranks
     # (ranks then share devices); the real runs use RCCL ("nccl"), one rank per GPU.
-    backend = os.environ.get("TPI_BENCH_BACKEND", "nccl")
-    index = local_rank % torch.cuda.device_count()
-    torch.cuda.set_device(index)
-    device = torch.device("cuda", index)
+    backend = os.environ.get("TPI_BENCH_BACKEND", "nccl") if on_gpu else "gloo"
+    if on_gpu:
+        index = local_rank % torch.cuda.device_count()
+        torch.cuda.set_device(index)
+        device = torch.device("cuda", index)
+    else:
+        device = torch.device("cpu")
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
+
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=device)
@@ -137,7 +149,7 @@ def main(argv=None):
     def barrier():
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
+        sync()
 
     def allmax(value: float) -> float:
         if world == 1:
@@ -156,7 +168,7 @@ def main(argv=None):
     per_rank = int(args.total_gb * 1e9 / world)
     t_setup = time.perf_counter()
     tensors = synthetic_checkpoint(per_rank, args.hidden, device)
-    torch.cuda.synchronize()
+    sync()
     ck = Checkpointer(tensors, tile_bytes=int(args.tile_mb * (1 << 20)),
                       chunk_bytes=int(args.chunk_mb * (1 << 20)), nbuf=args.nbuf, mode=args.mode,
                       codec=args.codec)
@@ -189,13 +201,18 @@ def main(argv=None):
         from terraform_provider_iterative_amd import ops
 
         names = list(tensors)[:3]
-        before = [ops.shard_hash(tensors[n].view(-1).view(torch.uint8)).cpu() for n in names]
+
+        def digest(n):
+            out = ops.shard_hash(tensors[n].view(-1).view(torch.uint8))
+            return out.cpu().tolist() if hasattr(out, "cpu") else out.tolist()
+
+        before = [digest(n) for n in names]
         for n in names:
             tensors[n].zero_()
         ck.restore()
-        torch.cuda.synchronize()
-        after = [ops.shard_hash(tensors[n].view(-1).view(torch.uint8)).cpu() for n in names]
-        verified = all(torch.equal(x, y) for x, y in zip(before, after))
+        sync()
+        after = [digest(n) for n in names]
+        verified = before == after
 
     async_stall = None
     if not args.no_async:  # untimed side measurement: training-stream stall of save_async
@@ -210,7 +227,8 @@ def main(argv=None):
             try:
                 a0 = time.perf_counter()
                 pending = ck.save_async({"async": True})
-                torch.cuda.current_stream(device).synchronize()
+                if on_gpu:
+                    torch.cuda.current_stream(device).synchronize()
                 stall = time.perf_counter() - a0
                 pending.result()
                 spill = time.perf_counter() - a0
@@ -222,7 +240,7 @@ def main(argv=None):
                        {"stall_ms": round(stall * 1e3, 2), "spill_s": round(spill, 3)})
 
     broadcast = None
-    if world > 1 and args.broadcast_gb > 0:  # config 3: workdir fan-out over xGMI (untimed)
+    if world > 1 and args.broadcast_gb > 0 and on_gpu:  # config 3: workdir fan-out over xGMI (untimed)
         try:
             from terraform_provider_iterative_amd.parallel.broadcast import (
                 measure, measure_independent_h2d)
@@ -255,10 +273,12 @@ def main(argv=None):
             "vs_baseline": None,
             "dtype": "bf16",
             "data": ("synthetic random AdamW state: bf16 params N(0,0.02), fp32 exp_avg "
-                     "N(0,1e-3), fp32 exp_avg_sq N(0,1e-3)^2"),
+                     "N(0,1e-3), fp32 exp_avg_sq N(0,1e-3)^2"
+                     + ("" if on_gpu else "; CPU rehearsal, not an MI355X measurement")),
             "config": {"model": CONFIG_NAME, "global_batch": 1, "seq_len": None,
                        "parallelism": "shard%d" % world, "checkpoint_bytes": total,
-                       "tile_bytes": ck.plan.tile_bytes, "chunk_bytes": ck.engine.chunk_bytes,
+                       "tile_bytes": ck.plan.tile_bytes,
+                       "chunk_bytes": ck.engine.chunk_bytes if ck.engine else None,
                        "mode": args.mode, "codec": args.codec,
                        "tensors_per_rank": len(tensors)},
             "save_GBps": round(total * args.steps / save_max / 1e9, 3),

@@ -1,0 +1,42 @@
+"""bench.py contract on the multi-rank path the driver uses for N > 1 (``torch.distributed.run
+--nproc-per-node N``): rehearsed with 2 gloo ranks on CPU tensors -- one JSON line from rank 0,
+the whole-job aggregate, max-over-ranks timing, a verified restore."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_two_rank_rehearsal_prints_one_json_line(tmp_path):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu", "--total-gb", "0.02",
+           "--steps", "2", "--warmup", "1", "--no-latency", "--hidden", "256"]
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    out = subprocess.run(cmd, cwd=str(tmp_path), capture_output=True, text=True, timeout=300,
+                         env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert key in d, key
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1
+    assert d["value"] > 0 and d["higher_is_better"] is True and d["scaling"] == "strong"
+    assert d["config"]["parallelism"] == "shard2"
+    assert d["config"]["checkpoint_bytes"] >= 0.02e9
+    # value = both directions of the whole job's checkpoint bytes per timed second
+    expect = 2 * d["config"]["checkpoint_bytes"] * d["steps"] / (d["ms_per_step"] * d["steps"] / 1e3) / 1e9
+    assert abs(d["value"] - expect) / expect < 0.02
+    assert d["restore_verified"] is True
+    assert "CPU rehearsal" in d["data"]
