@@ -76,7 +76,7 @@ __global__ __launch_bounds__(CWG) void k_tpz_analyze(const uint8_t* __restrict__
                                                      uint32_t* __restrict__ csize) {
   __shared__ uint32_t hist[4][256];
   __shared__ uint8_t rank[4][256];
-  __shared__ uint8_t cost[4][256];  // HUF bits per byte value
+  __shared__ uint16_t rc[4][256];  // rank | HUF bits << 8 per byte value (one lookup)
   __shared__ tpz_plane hdr[4];
   __shared__ uint8_t s_len[4][16];
   __shared__ uint32_t s_cnt[4][16];
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(CWG) void k_tpz_analyze(const uint8_t* __restrict__
   for (int i = tid; i < 4 * 256; i += CWG) {
     const int p = i >> 8;
     const uint32_t r = rank[p][i & 255], m = hdr[p].m;
-    cost[p][i & 255] = (uint8_t)(r < m ? s_len[p][r] : s_len[p][m] + 8);
+    rc[p][i & 255] = (uint16_t)(r | (uint32_t)(r < m ? s_len[p][r] : s_len[p][m] + 8) << 8);
   }
   __syncthreads();
 
@@ -166,12 +166,12 @@ __global__ __launch_bounds__(CWG) void k_tpz_analyze(const uint8_t* __restrict__
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
           const uint32_t v = (w[j] >> (8 * p)) & 0xff;
-          const uint32_t r = rank[p][v];
+          const uint32_t e = rc[p][v], r = e & 0xff;
           hits[p][0] += r < 1;
           hits[p][1] += r < 3;
           hits[p][2] += r < 7;
           hits[p][3] += r < 15;
-          bits[p] += cost[p][v];
+          bits[p] += e >> 8;
         }
       }
     }
@@ -259,23 +259,17 @@ __device__ static inline uint32_t encode_codes(const uint32_t w[32], int p, cons
 
 // Appends the HUF codes of one group's (valid) plane-p bytes to the lane's substream: LSB-first
 // bit buffer, a full u32 word is stored as soon as it exists (<= 19 bits per symbol).
+// `tab[v]` = the complete bits of byte value v (its code, or the escape code followed by v)
+// | their count << 24: one LDS lookup per symbol.
 __device__ static inline void huf_encode_group(const uint32_t w[32], int p, uint32_t valid,
-                                               const uint8_t* rk, uint32_t m,
-                                               const uint16_t* code, const uint8_t* clen,
-                                               uint64_t& acc, int& nb,
+                                               const uint32_t* tab, uint64_t& acc, int& nb,
                                                uint32_t* __restrict__ stream, uint64_t& wp) {
 #pragma unroll
   for (int j = 0; j < 32; ++j) {
     if ((uint32_t)j < valid) {
-      const uint32_t v = (w[j] >> (8 * p)) & 0xff;
-      const uint32_t r = rk[v];
-      const uint32_t c = r < m ? r : m;
-      acc |= (uint64_t)code[c] << nb;
-      nb += clen[c];
-      if (c == m) {
-        acc |= (uint64_t)v << nb;
-        nb += 8;
-      }
+      const uint32_t e = tab[(w[j] >> (8 * p)) & 0xff];
+      acc |= (uint64_t)(e & 0xffffffu) << nb;
+      nb += (int)(e >> 24);
       if (nb >= 32) {
         stream[wp++] = (uint32_t)acc;
         acc >>= 32;
@@ -317,6 +311,7 @@ __global__ __launch_bounds__(CWG) void k_tpz_encode(const uint8_t* __restrict__ 
   __shared__ uint8_t rank[4][256];
   __shared__ uint8_t s_clen[4][16];
   __shared__ uint16_t s_code[4][16];
+  __shared__ uint32_t s_henc[4][256];  // HUF: bits | count << 24 per byte value
   __shared__ uint64_t s_wave[CWG / 64];
   const int tid = threadIdx.x;
   const uint64_t tbase = (uint64_t)blockIdx.x * tile;
@@ -342,6 +337,18 @@ __global__ __launch_bounds__(CWG) void k_tpz_encode(const uint8_t* __restrict__ 
     rank[p][v] = (hdr[p].k == TPZ_RAW || hdr[p].k == 0) ? 15 : r;
   }
   if (tid < TPZ_HDR / 16) ((u32x4*)blob)[tid] = ((const u32x4*)&hdr[0])[tid];
+  __syncthreads();
+  for (int i = tid; i < 4 * 256; i += CWG) {
+    const int p = i >> 8, v = i & 255;
+    if (hdr[p].k != TPZ_HUF) continue;
+    const uint32_t m = hdr[p].m, r = rank[p][v], c = r < m ? r : m;
+    uint32_t bits = s_code[p][c], l = s_clen[p][c];
+    if (c == m) {
+      bits |= (uint32_t)v << l;
+      l += 8;
+    }
+    s_henc[p][v] = bits | (l << 24);
+  }
   __syncthreads();
   PlaneGeo geo[4];
   uint64_t blob_bytes;
@@ -401,8 +408,7 @@ __global__ __launch_bounds__(CWG) void k_tpz_encode(const uint8_t* __restrict__ 
           case 3: mask[p] = encode_codes<3>(w, p, rank[p], valid, sec + g * 12); break;
           case 4: mask[p] = encode_codes<4>(w, p, rank[p], valid, sec + g * 16); break;
           case TPZ_HUF:
-            huf_encode_group(w, p, valid, rank[p], hdr[p].m, s_code[p], s_clen[p], hacc[p],
-                             hnb[p], hstr[p], hwp[p]);
+            huf_encode_group(w, p, valid, s_henc[p], hacc[p], hnb[p], hstr[p], hwp[p]);
             break;
           default: break;  // CONST: nothing stored
         }
@@ -481,15 +487,15 @@ __device__ static inline void huf_decode_group(const uint32_t* __restrict__ stre
                                                const uint16_t* lut, const uint8_t* dict,
                                                uint32_t m, int p, uint32_t valid,
                                                uint64_t& acc, int& nb, uint32_t& ptr,
-                                               uint32_t end, uint32_t w[32]) {
+                                               uint32_t end, uint32_t& nxt, uint32_t w[32]) {
 #pragma unroll
   for (int j = 0; j < 32; ++j) {
     if ((uint32_t)j < valid) {
-      if (nb < 32) {
-        const uint32_t x = ptr < end ? stream[ptr] : 0u;
-        ++ptr;
-        acc |= (uint64_t)x << nb;
+      if (nb < 32) {  // consume the word loaded one refill ago, start loading the next one
+        acc |= (uint64_t)nxt << nb;
         nb += 32;
+        nxt = ptr < end ? stream[ptr] : 0u;
+        ++ptr;
       }
       const uint32_t e = lut[acc & (TPZ_HUF_LUT - 1)];
       const uint32_t c = e & 0xff, l = e >> 8;
@@ -583,7 +589,7 @@ __global__ __launch_bounds__(CWG) void k_tpz_decode(const uint8_t* __restrict__ 
   const uint64_t S = tpz_huf_streams(ngroups);
   uint64_t hacc[4] = {0, 0, 0, 0};
   int hnb[4] = {0, 0, 0, 0};
-  uint32_t hptr[4] = {0, 0, 0, 0}, hend[4] = {0, 0, 0, 0};
+  uint32_t hptr[4] = {0, 0, 0, 0}, hend[4] = {0, 0, 0, 0}, hnxt[4] = {0, 0, 0, 0};
   const uint32_t* hstr[4] = {nullptr, nullptr, nullptr, nullptr};
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
@@ -598,6 +604,8 @@ __global__ __launch_bounds__(CWG) void k_tpz_decode(const uint8_t* __restrict__ 
         hend[p] = e;
       }
     }
+    hnxt[p] = hptr[p] < hend[p] ? hstr[p][hptr[p]] : 0u;  // software-pipelined refills
+    ++hptr[p];
   }
 
   uint64_t run[4] = {0, 0, 0, 0};
@@ -634,7 +642,7 @@ __global__ __launch_bounds__(CWG) void k_tpz_decode(const uint8_t* __restrict__ 
           case 4: mask[p] = decode_codes<4>(sec + g * 16, dict[p], p, w); break;
           case TPZ_HUF:
             huf_decode_group(hstr[p], lut[p], dict[p], hdr[p].m, p, valid, hacc[p], hnb[p],
-                             hptr[p], hend[p], w);
+                             hptr[p], hend[p], hnxt[p], w);
             break;
           default: break;
         }
