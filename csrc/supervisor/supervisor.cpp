@@ -237,6 +237,8 @@ class Supervisor {
   explicit Supervisor(Spec spec) : s_(std::move(spec)) {
     ranks_.resize(s_.parallelism);
     standby_.resize(s_.parallelism);
+    for (auto& kv : s_.env)
+      if (kv.first == "TPI_MACHINE_LOGS" && !kv.second.empty()) machine_logs_ = true;
     for (int i = 0; i < s_.parallelism; ++i) {
       ranks_[i].index = i;
       ranks_[i].gpus = s_.rank_gpus[i];
@@ -319,6 +321,7 @@ class Supervisor {
   std::vector<Rank> ranks_;
   std::vector<Rank> detached_;  // released incarnations still exiting
   std::vector<Rank> standby_;   // per rank index: warm successor waiting for "go" (pid > 0)
+  bool machine_logs_ = false;   // TPI_MACHINE_LOGS set in the task environment (tpl:109)
   int sfd_ = -1;
   double started_ = 0, respawn_at_ = 0;
   bool stop_ = false, timed_out_ = false, dirty_ = true;
@@ -333,6 +336,21 @@ class Supervisor {
     if (fd >= 0) {
       write_all(fd, line);
       close(fd);
+    }
+    if (machine_logs_) {  // TPI_MACHINE_LOGS: the node-side journal of every live machine
+      std::string text = utc_stamp(now()) + " tpi-supervisor: " + code;
+      for (auto& d : desc) text += " " + d;
+      text += "\n";
+      for (auto* list : {&ranks_, &standby_})
+        for (auto& r : *list)
+          if (r.pid > 0 && !r.uuid.empty()) {
+            const std::string path = s_.reports_dir + "/machine-" + r.uuid;
+            int mfd = open(path.c_str(), O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
+            if (mfd >= 0) {
+              write_all(mfd, text);
+              close(mfd);
+            }
+          }
     }
     dirty_ = true;
   }

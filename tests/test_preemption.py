@@ -174,3 +174,20 @@ def test_unused_standby_is_discarded(cloud, monkeypatch):
     assert "standby-start" in codes and "standby-discarded" in codes, codes
     assert "standby-activated" not in codes and not task.supervisor_running()
     task.delete()
+
+
+def test_machine_logs_journal(cloud):
+    # TPI_MACHINE_LOGS (machine-script.sh.tpl:109): reports/machine-<uuid> next to task-<uuid>
+    spec = Task(environment=Environment(script="#!/bin/sh\necho hi\n", timeout=60,
+                                        variables=Variables({"TPI_MACHINE_LOGS": "1"})))
+    task = backends.new(cloud, new_deterministic_identifier("machine-logs"), spec)
+    task.create()
+    status = task.wait(60)
+    assert status["succeeded"] == 1
+    names = os.listdir(task.reports_dir)
+    machine = [n for n in names if n.startswith("machine-")]
+    assert machine and ("task-" + machine[0][len("machine-"):]) in names
+    text = open(os.path.join(task.reports_dir, machine[0])).read()
+    assert "tpi-supervisor: rank-start rank 0" in text
+    assert len(task.logs()) == 1 and "hi" in task.logs()[0]  # machine-* is not a task log
+    task.delete()
