@@ -26,6 +26,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -56,6 +57,9 @@ def parse_args(argv=None):
     p.add_argument("--verify", action="store_true", default=True)
     p.add_argument("--no-async", action="store_true",
                    help="skip the (untimed) save_async stall measurement")
+    p.add_argument("--side-timeout", type=float, default=600.0,
+                   help="seconds the untimed side measurements may take before rank 0 prints "
+                        "the headline without them")
     p.add_argument("--device", choices=("cuda", "cpu"), default="cuda",
                    help="cpu: rehearse the multi-rank control flow on CPU tensors over gloo "
                         "(tests; not a measurement of the MI355X path)")
@@ -214,6 +218,70 @@ def main(argv=None):
         after = [digest(n) for n in names]
         verified = before == after
 
+    elapsed = allmax(elapsed)
+    save_max, restore_max = allmax(save_s), allmax(restore_s)
+    total = ck.plan.total * world  # packed bytes per direction per step (all ranks)
+    wire_total = int(allmax(float(wire))) * world  # (upper bound: max rank x N)
+    value = 2 * total * args.steps / elapsed / 1e9
+    out = None
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": ("synthetic random AdamW state: bf16 params N(0,0.02), fp32 exp_avg "
+                     "N(0,1e-3), fp32 exp_avg_sq N(0,1e-3)^2"
+                     + ("" if on_gpu else "; CPU rehearsal, not an MI355X measurement")),
+            "config": {"model": CONFIG_NAME, "global_batch": 1, "seq_len": None,
+                       "parallelism": "shard%d" % world, "checkpoint_bytes": total,
+                       "tile_bytes": ck.plan.tile_bytes,
+                       "chunk_bytes": ck.engine.chunk_bytes if ck.engine else None,
+                       "mode": args.mode, "codec": args.codec,
+                       "tensors_per_rank": len(tensors)},
+            "save_GBps": round(total * args.steps / save_max / 1e9, 3),
+            "restore_GBps": round(total * args.steps / restore_max / 1e9, 3),
+            "per_gpu_save_GBps": round(ck.plan.total * args.steps / save_max / 1e9, 3),
+            "per_gpu_restore_GBps": round(ck.plan.total * args.steps / restore_max / 1e9, 3),
+            "wire_bytes_per_step": wire_total,
+            "compression_ratio": round(wire_total / total, 4),
+            "save_wire_GBps": round(wire_total * args.steps / save_max / 1e9, 3),
+            "first_log_latency_s": (latency or {}).get("cli_s"),
+            "first_log_latency": latency,
+            "workdir_broadcast": None,
+            "restore_verified": verified,
+            "save_async": None,
+            "setup_s": round(setup_s, 2),
+        }
+
+    # Side measurements (collectives) run under a watchdog: should one of them hang, rank 0
+    # still prints the headline line, marked, and every rank leaves without the hung call.
+    printed = threading.Lock()
+
+    def emit(note=None):
+        if out is not None and printed.acquire(blocking=False):  # exactly one line
+            if note:
+                for key in ("save_async", "workdir_broadcast"):
+                    if out[key] is None:
+                        out[key] = {"error": note}
+            print(json.dumps(out), flush=True)
+
+    def expire():
+        emit("side measurement timed out after %.0f s" % args.side_timeout)
+        sys.stdout.flush()
+        os._exit(0)
+
+    watchdog = threading.Timer(args.side_timeout, expire)
+    watchdog.daemon = True
+    watchdog.start()
+
     async_stall = None
     if not args.no_async:  # untimed side measurement: training-stream stall of save_async
         # every rank reaches every collective below, whatever fails locally (no deadlock)
@@ -254,48 +322,11 @@ def main(argv=None):
         except Exception as error:  # never lose the headline to the side measurement
             broadcast = {"error": repr(error)}
 
-    elapsed = allmax(elapsed)
-    save_max, restore_max = allmax(save_s), allmax(restore_s)
-    total = ck.plan.total * world  # packed bytes per direction per step (all ranks)
-    wire_total = int(allmax(float(wire))) * world  # (upper bound: max rank x N)
-    value = 2 * total * args.steps / elapsed / 1e9
-    if rank == 0:
-        out = {
-            "metric": METRIC,
-            "value": round(value, 3),
-            "unit": "GB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "bf16",
-            "data": ("synthetic random AdamW state: bf16 params N(0,0.02), fp32 exp_avg "
-                     "N(0,1e-3), fp32 exp_avg_sq N(0,1e-3)^2"
-                     + ("" if on_gpu else "; CPU rehearsal, not an MI355X measurement")),
-            "config": {"model": CONFIG_NAME, "global_batch": 1, "seq_len": None,
-                       "parallelism": "shard%d" % world, "checkpoint_bytes": total,
-                       "tile_bytes": ck.plan.tile_bytes,
-                       "chunk_bytes": ck.engine.chunk_bytes if ck.engine else None,
-                       "mode": args.mode, "codec": args.codec,
-                       "tensors_per_rank": len(tensors)},
-            "save_GBps": round(total * args.steps / save_max / 1e9, 3),
-            "restore_GBps": round(total * args.steps / restore_max / 1e9, 3),
-            "per_gpu_save_GBps": round(ck.plan.total * args.steps / save_max / 1e9, 3),
-            "per_gpu_restore_GBps": round(ck.plan.total * args.steps / restore_max / 1e9, 3),
-            "wire_bytes_per_step": wire_total,
-            "compression_ratio": round(wire_total / total, 4),
-            "save_wire_GBps": round(wire_total * args.steps / save_max / 1e9, 3),
-            "first_log_latency_s": (latency or {}).get("cli_s"),
-            "first_log_latency": latency,
-            "workdir_broadcast": broadcast,
-            "restore_verified": verified,
-            "save_async": async_stall,
-            "setup_s": round(setup_s, 2),
-        }
-        print(json.dumps(out), flush=True)
+    watchdog.cancel()
+    if out is not None:
+        out["save_async"] = async_stall
+        out["workdir_broadcast"] = broadcast
+    emit()
     ck.close()
     if world > 1:
         dist.destroy_process_group()

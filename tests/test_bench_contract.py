@@ -16,18 +16,22 @@ def _port():
         return s.getsockname()[1]
 
 
-def test_two_rank_rehearsal_prints_one_json_line(tmp_path):
+def _run(tmp_path, *extra):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu", "--total-gb", "0.02",
-           "--steps", "2", "--warmup", "1", "--no-latency", "--hidden", "256"]
+           "--steps", "2", "--warmup", "1", "--no-latency", "--hidden", "256", *extra]
     env = dict(os.environ, OMP_NUM_THREADS="2")
     out = subprocess.run(cmd, cwd=str(tmp_path), capture_output=True, text=True, timeout=300,
                          env=env)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, out.stdout
-    d = json.loads(lines[0])
+    return json.loads(lines[0])
+
+
+def test_two_rank_rehearsal_prints_one_json_line(tmp_path):
+    d = _run(tmp_path)
     for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
                 "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
         assert key in d, key
@@ -40,3 +44,10 @@ def test_two_rank_rehearsal_prints_one_json_line(tmp_path):
     assert abs(d["value"] - expect) / expect < 0.02
     assert d["restore_verified"] is True
     assert "CPU rehearsal" in d["data"]
+
+
+def test_side_measurement_watchdog_keeps_the_headline(tmp_path):
+    # a side measurement that outlives --side-timeout must not cost the headline line
+    d = _run(tmp_path, "--side-timeout", "0.001")
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["restore_verified"] is True
+    assert d["save_async"] is None or "error" in d["save_async"] or "stall_ms" in d["save_async"]
