@@ -57,7 +57,7 @@ def parse_args(argv=None):
     p.add_argument("--verify", action="store_true", default=True)
     p.add_argument("--no-async", action="store_true",
                    help="skip the (untimed) save_async stall measurement")
-    p.add_argument("--side-timeout", type=float, default=600.0,
+    p.add_argument("--side-timeout", type=float, default=300.0,
                    help="seconds the untimed side measurements may take before rank 0 prints "
                         "the headline without them")
     p.add_argument("--device", choices=("cuda", "cpu"), default="cuda",
