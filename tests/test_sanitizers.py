@@ -72,3 +72,50 @@ def test_supervisor_under_asan_ubsan(tmp_path, monkeypatch):
                 assert marker not in text, text[-2000:]
     finally:
         task.delete()
+
+
+def test_supervisor_preemption_paths_under_asan_ubsan(tmp_path, monkeypatch):
+    # gang of 2 ranks: leo preempt -> spill -> "released" hand-off -> warm standbys activated
+    import sys
+    import time
+
+    from test_preemption import ROOT as _root, STANDBY
+
+    exe = str(tmp_path / "tpi-supervisor-asan")
+    _compile(exe, [os.path.join(ROOT, "csrc", "supervisor", "supervisor.cpp")])
+    monkeypatch.setenv("TPI_SUPERVISOR_BIN", exe)
+    monkeypatch.setenv("TPI_WARM_STANDBY", "1")
+    monkeypatch.setenv("ASAN_OPTIONS", ENV["ASAN_OPTIONS"])
+    from terraform_provider_iterative_amd import backends
+    from terraform_provider_iterative_amd.models.cloud import Cloud, Credentials, NodeCredentials
+    from terraform_provider_iterative_amd.models.values import Environment, Task, Variables
+    from terraform_provider_iterative_amd.utils.identifier import new_deterministic_identifier
+
+    script = STANDBY.replace('".spill")', '".spill" + os.environ["RANK"])') % {
+        "python": sys.executable, "root": _root, "steps": 30}
+    state = tmp_path / "state"
+    cloud = Cloud(provider="local",
+                  credentials=Credentials(node=NodeCredentials(state_root=str(state))))
+    spec = Task(parallelism=2, environment=Environment(
+        script=script, timeout=120, variables=Variables({"TPI_TASK": "true"})))
+    task = backends.new(cloud, new_deterministic_identifier("asan-preempt"), spec)
+    task.create()
+    try:
+        deadline = time.time() + 60
+        while time.time() < deadline and sum("step 3" in l for l in task.logs()) < 2:
+            time.sleep(0.05)
+        task.preempt()
+        status = task.wait(90)
+        logs = task.logs()
+        assert status["succeeded"] == 2 and status["failed"] == 0, (status, logs)
+        assert sum("activated" in l and "final 30 30" in l for l in logs) == 2, logs
+        codes = [e.code for e in task.events()]
+        assert codes.count("rank-released") == 2 and codes.count("standby-activated") == 2
+        for dirpath, _, files in os.walk(str(state)):
+            for f in files:
+                if f == "supervisor.log":
+                    text = open(os.path.join(dirpath, f), errors="replace").read()
+                    for marker in ("AddressSanitizer", "LeakSanitizer", "runtime error"):
+                        assert marker not in text, text[-2000:]
+    finally:
+        task.delete()
