@@ -26,7 +26,7 @@ resource "iterative_task" "train" {
   cloud   = "%(cloud)s"
   machine = "%(machine)s"
   timeout = 3600
-  environment = { TPI_FRAMEWORK_ROOT = "%(root)s" }
+  environment = { TPI_FRAMEWORK_ROOT = "%(root)s", TPI_STAGE_ZERO_COPY = "%(zc)s" }
   storage {
     workdir = "."
     output  = "results"
@@ -62,6 +62,9 @@ def main():
     p.add_argument("--cloud", default="mi355x")
     p.add_argument("--machine", default="m+mi355x")
     p.add_argument("--base", default=None, help="scratch directory (default $TMPDIR)")
+    p.add_argument("--zero-copy", choices=("0", "1"), default="0",
+                   help="stage large page-cached files by DMA from their pages (1) or through "
+                        "pinned bounce buffers (0)")
     args = p.parse_args()
     base = tempfile.mkdtemp(prefix="tpi-workdir-", dir=args.base)
     try:
@@ -77,7 +80,8 @@ def main():
         gen_s = time.perf_counter() - t
         with open(os.path.join(work, "main.tf"), "w") as handle:
             handle.write(MAIN_TF % {"cloud": args.cloud, "machine": args.machine, "root": ROOT,
-                                    "python": sys.executable, "steps": args.steps})
+                                    "python": sys.executable, "steps": args.steps,
+                                    "zc": args.zero_copy})
         env = dict(os.environ, TPI_STATE_ROOT=os.path.join(base, "state"))
         tpi = [sys.executable, os.path.join(ROOT, "bin", "tpi")]
         t0 = time.perf_counter()
@@ -114,6 +118,8 @@ def main():
             "apply_s": round(apply_s, 3),
             "push_GBps": round(total / apply_s / 1e9, 2) if apply_s else None,
             "stage_GBps": stats.get("stage_GBps"), "train_step_ms": stats.get("step_ms"),
+            "stage_stats": {k: stats.get(k) for k in ("load_s", "read_s", "zero_copy_files",
+                                                       "broadcast_s", "files")},
             "end_to_end_s": round(wall, 2), "apply_ok": apply.returncode == 0,
             "destroy_ok": d.returncode == 0,
         }

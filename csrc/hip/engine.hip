@@ -904,6 +904,16 @@ int tpi_host_register(void* ptr, uint64_t bytes) {
   return 0;
 }
 
+int tpi_host_register_ro(void* ptr, uint64_t bytes) {
+  HIP_OK(hipHostRegister(ptr, bytes, hipHostRegisterMapped | hipHostRegisterReadOnly));
+  return 0;
+}
+
+int tpi_h2d_async(void* dev_dst, const void* host_src, uint64_t bytes, uint64_t stream) {
+  HIP_OK(hipMemcpyAsync(dev_dst, host_src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+  return 0;
+}
+
 int tpi_host_unregister(void* ptr) {
   HIP_OK(hipHostUnregister(ptr));
   return 0;

@@ -143,6 +143,11 @@ void* tpi_host_map(const char* path, uint64_t bytes, int numa_node, int populate
 int tpi_host_unmap(void* ptr, uint64_t bytes);
 int tpi_host_register(void* ptr, uint64_t bytes);
 int tpi_host_unregister(void* ptr);
+// Read-only registration of an existing (e.g. page-cache file) mapping for DMA reads: the
+// zero-copy workdir staging path (runtime/workdir.py).  Populate the mapping first.
+int tpi_host_register_ro(void* ptr, uint64_t bytes);
+// hipMemcpyAsync host -> device on `stream` (0 = legacy default stream).
+int tpi_h2d_async(void* dev_dst, const void* host_src, uint64_t bytes, uint64_t stream);
 
 // Chunked host->device copy through the engine's copy stream (workdir staging).
 int tpi_h2d(tpi_engine* e, void* dev_dst, const void* host_src, uint64_t bytes);

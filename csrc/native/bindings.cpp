@@ -158,6 +158,12 @@ PYBIND11_MODULE(_tpi_native, m) {
     }
     return py::make_tuple(bad, first);
   });
+  m.def("resident_bytes", [](const std::string& path) {
+    uint64_t size = 0;
+    int tmpfs = 0;
+    const int64_t r = tpi::resident_bytes(path.c_str(), &size, &tmpfs);
+    return py::make_tuple(r, size, (bool)tmpfs);
+  });
   m.def("tpz_bound", [](uint64_t len) { return tpz_bound(len); });
   m.def("tpz_meta_bytes", [](uint64_t ntiles) { return tpz_meta_bytes(ntiles); });
   m.def("tpz_encode_ptr", [](uintptr_t src, uint64_t total, uint64_t tile, uintptr_t dst,

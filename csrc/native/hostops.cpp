@@ -4,8 +4,13 @@
 // csrc/hip/kernels.hip (tests compare both) and serve the `local` (CPU) backend.
 #include "hostops.h"
 
+#include <fcntl.h>
 #include <nmmintrin.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <sys/vfs.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -206,6 +211,40 @@ uint64_t unpack(const tpi_seg* segs, int n, uint64_t total, const void* stream, 
   });
   *first_bad = bad ? first.load() : -1;
   return bad;
+}
+
+int64_t resident_bytes(const char* path, uint64_t* size, int* tmpfs) {
+  *size = 0;
+  *tmpfs = 0;
+  int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return -1;
+  struct stat st;
+  struct statfs sf;
+  if (fstat(fd, &st) != 0) {
+    close(fd);
+    return -1;
+  }
+  if (fstatfs(fd, &sf) == 0) *tmpfs = sf.f_type == 0x01021994 /* TMPFS_MAGIC */;
+  *size = (uint64_t)st.st_size;
+  if (st.st_size == 0) {
+    close(fd);
+    return 0;
+  }
+  void* p = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) return -1;
+  const long page = sysconf(_SC_PAGESIZE);
+  const uint64_t pages = ((uint64_t)st.st_size + page - 1) / page;
+  std::vector<unsigned char> vec(pages);
+  int64_t resident = -1;
+  if (mincore(p, (size_t)st.st_size, vec.data()) == 0) {
+    resident = 0;
+    for (unsigned char v : vec) resident += (v & 1);
+    resident *= page;
+    if (resident > st.st_size) resident = st.st_size;
+  }
+  munmap(p, (size_t)st.st_size);
+  return resident;
 }
 
 uint64_t tpz_encode_stream(const void* src, uint64_t total, uint64_t tile, void* dst,

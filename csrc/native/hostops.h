@@ -19,6 +19,10 @@ void pack(const tpi_seg* segs, int n, uint64_t total, void* stream, uint64_t til
 uint64_t unpack(const tpi_seg* segs, int n, uint64_t total, const void* stream, uint64_t tile,
                 const uint32_t* crcs, int threads, int64_t* first_bad);
 
+// Page-cache residency of a file: bytes of its pages in memory (mincore), and whether it
+// lives on tmpfs/shmem (whose pages pin slowly for DMA).  Returns -1 if it cannot be mapped.
+int64_t resident_bytes(const char* path, uint64_t* size, int* tmpfs);
+
 // TPZ1 codec (csrc/common/tpz.h) over a stream of tiles: blobs are written back to back,
 // sizes to `csizes`; returns the compressed length.  Decode returns -1, or the first tile
 // whose blob is malformed (that tile is zero-filled).

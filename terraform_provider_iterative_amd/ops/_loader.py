@@ -84,6 +84,8 @@ class HipLib:
             "tpi_host_map": (vp, [c.c_char_p, u64, i32, i32]),
             "tpi_host_unmap": (i32, [vp, u64]),
             "tpi_host_register": (i32, [vp, u64]),
+            "tpi_host_register_ro": (i32, [vp, u64]),
+            "tpi_h2d_async": (i32, [vp, vp, u64, u64]),
             "tpi_host_unregister": (i32, [vp]),
             "tpi_h2d": (i32, [vp, vp, vp, u64]),
             "tpi_d2h": (i32, [vp, vp, vp, u64]),

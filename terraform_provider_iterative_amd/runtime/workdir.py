@@ -3,9 +3,13 @@
 ``stage_workdir`` turns the task's working directory into one device buffer:
 
 1. the root rank walks the tree with the rclone-compatible filters (native walker),
-2. reads file pieces with a pool of ``pread`` threads straight into two pinned host
-   buffers and streams them to HBM with async H2D copies on a side stream (read of chunk
-   k+1 overlaps the DMA of chunk k),
+2. optionally (``TPI_STAGE_ZERO_COPY=1``) DMAs large page-cache resident files (>= 64 MiB,
+   not on tmpfs) straight from their pages: 1 GiB windows are
+   mapped read-only with MAP_POPULATE and registered for DMA (~13 ms per GiB, measured on
+   MI355X: 57 GB/s H2D from such a mapping, ``scripts/exp/zerocopy_stage.py``), copies and
+   the next registration overlap; smaller files are read by a pool of ``pread`` threads
+   into two pinned bounce buffers and streamed with async H2D copies (read of chunk k+1
+   overlaps the DMA of chunk k),
 3. fans the buffer out to every rank over xGMI (:mod:`..parallel.broadcast`),
 4. optionally verifies the copy with the device shard-hash kernel on every rank.
 
@@ -15,6 +19,8 @@ give the change detection that replaces the reference's 10-second ``find -printf
 """
 from __future__ import annotations
 
+import ctypes
+import logging
 import os
 import time
 from dataclasses import dataclass, field
@@ -23,7 +29,10 @@ from typing import Dict, List, Optional, Tuple
 from ..ops import native, shard_hash
 from ..storage.transfer import make_filter, transfer_rules
 
+log = logging.getLogger("tpi.workdir")
+
 ALIGN = 4096
+ZERO_COPY_MIN = 64 << 20  # files at least this large are DMA'd from their page-cache pages
 
 
 @dataclass
@@ -93,9 +102,103 @@ def _pieces_for(root: str, files: List[FileEntry], lo: int, hi: int):
     return pieces
 
 
+def _runs(files: List[FileEntry], small: List[bool], total: int) -> List[Tuple[int, int]]:
+    """Buffer ranges [lo, hi) covering maximal sequences of consecutive small files (with
+    their alignment padding), so the bounce path never writes over a zero-copy file."""
+    runs: List[Tuple[int, int]] = []
+    start = None
+    for i, f in enumerate(files):
+        end = files[i + 1].offset if i + 1 < len(files) else total
+        if small[i]:
+            if start is None:
+                start = f.offset
+            if i + 1 == len(files) or not small[i + 1]:
+                runs.append((start, end))
+                start = None
+    return runs
+
+
+def _zero_copy(root: str, files: List[FileEntry], buffer, stream, window: int,
+               inflight: int = 3) -> float:
+    """H2D straight from the page cache: each window of a large file is mapped read-only
+    (MAP_POPULATE), registered for DMA and copied on ``stream``; windows are unregistered
+    once their copy completed, ``inflight`` of them overlap.  Returns the host-side seconds."""
+    import mmap
+
+    import torch
+
+    from ..ops import hip
+
+    lib = hip()
+    page = mmap.ALLOCATIONGRANULARITY
+    pending: List[tuple] = []
+    host_s = 0.0
+
+    def retire(entry):
+        ev, m, addr = entry
+        ev.synchronize()
+        lib.tpi_host_unregister(ctypes.c_void_p(addr))
+        m.close()
+
+    for f in files:
+        fd = os.open(os.path.join(root, f.path), os.O_RDONLY)
+        try:
+            for pos in range(0, f.size, window):
+                n = min(window, f.size - pos)
+                t = time.perf_counter()
+                base = pos // page * page
+                span = pos - base + n
+                m = mmap.mmap(fd, span, mmap.MAP_SHARED | getattr(mmap, "MAP_POPULATE", 0),
+                              mmap.PROT_READ, offset=base)
+                addr = _address(m)
+                lib.check(lib.tpi_host_register_ro(ctypes.c_void_p(addr), span),
+                          "hipHostRegister(read-only)")
+                lib.check(lib.tpi_h2d_async(ctypes.c_void_p(buffer.data_ptr() + f.offset + pos),
+                                            ctypes.c_void_p(addr + pos - base), n,
+                                            stream.cuda_stream), "hipMemcpyAsync")
+                ev = torch.cuda.Event()
+                ev.record(stream)
+                pending.append((ev, m, addr))
+                host_s += time.perf_counter() - t
+                if len(pending) >= inflight:
+                    retire(pending.pop(0))
+        finally:
+            os.close(fd)
+    for entry in pending:
+        retire(entry)
+    return host_s
+
+
+def _zero_copy_ok(root: str, f: FileEntry, zero_copy_min: int) -> bool:
+    """Opt-in (``TPI_STAGE_ZERO_COPY=1``); large, page-cache resident and not on tmpfs.
+
+    Measured on MI355X: freshly written 1 GB files stage at 39-50 GB/s this way against 23-37
+    through the bounce buffers (``scripts/exp/stage_modes.py``), but the task's data files
+    written by the push (``copy_file_range``) stage at 12 GB/s against 27-28 -- so the bounce
+    path stays the default.  A file read from disk would fault in single-threaded under
+    MAP_POPULATE, and shmem pages pin for DMA several times slower than the bounce copy."""
+    if f.size < zero_copy_min or os.environ.get("TPI_STAGE_ZERO_COPY", "0") != "1":
+        return False
+    resident, size, tmpfs = native().resident_bytes(os.path.join(root, f.path))
+    return not tmpfs and resident >= 0 and resident >= 0.9 * size
+
+
+def _address(m) -> int:
+    """Address of a (read-only) mmap's first byte."""
+    import numpy as np
+
+    return int(np.frombuffer(m, dtype=np.uint8).ctypes.data)
+
+
 def load_into(root: str, files: List[FileEntry], total: int, buffer,
-              chunk_bytes: int = 256 << 20, threads: int = 16) -> Dict[str, float]:
-    """Fill ``buffer`` (device or host uint8 tensor of ``total`` bytes) from the files."""
+              chunk_bytes: int = 256 << 20, threads: int = 16,
+              zero_copy_min: int = ZERO_COPY_MIN) -> Dict[str, float]:
+    """Fill ``buffer`` (device or host uint8 tensor of ``total`` bytes) from the files.
+
+    On the device, files of at least ``zero_copy_min`` bytes are DMA'd straight from their
+    page-cache pages (:func:`_zero_copy`); the rest go through two pinned bounce buffers
+    filled by a pool of ``pread`` threads, the read of chunk k+1 overlapping the DMA of k.
+    """
     import torch
 
     t0 = time.perf_counter()
@@ -111,38 +214,56 @@ def load_into(root: str, files: List[FileEntry], total: int, buffer,
     # the copies must land after whatever the caller queued on ``buffer`` (its allocation /
     # fill on the current stream)
     stream.wait_stream(torch.cuda.current_stream(buffer.device))
-    hosts = [torch.empty(min(chunk_bytes, max(total, 1)), dtype=torch.uint8, pin_memory=True)
-             for _ in range(2)]
-    events = [None, None]
-    for k, lo in enumerate(range(0, total, chunk_bytes)):
-        hi = min(total, lo + chunk_bytes)
-        slot = k % 2
-        if events[slot] is not None:
-            events[slot].synchronize()
-        host = hosts[slot]
-        t = time.perf_counter()
-        pieces = _pieces_for(root, files, lo, hi)
-        covered = lo
-        for _path, _foff, length, rel in sorted(pieces, key=lambda p: p[3]):
-            if lo + rel > covered:  # alignment gap: zero it so digests are deterministic
-                host[covered - lo:rel].zero_()
-            covered = lo + rel + length
-        if covered < hi:
-            host[covered - lo:hi - lo].zero_()
-        native().read_pieces(pieces, host.data_ptr(), threads)
-        read_s += time.perf_counter() - t
+    small = [not _zero_copy_ok(root, f, zero_copy_min) for f in files]
+    big = [f for f, s in zip(files, small) if not s]
+    zc_s = 0.0
+    if big:
         with torch.cuda.stream(stream):
-            buffer[lo:hi].copy_(host[:hi - lo], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(stream)
-        events[slot] = ev
+            buffer.zero_()  # alignment padding between zero-copied files (digests need zeros)
+        try:
+            zc_s = _zero_copy(root, big, buffer, stream, window=max(chunk_bytes, 1 << 30))
+        except Exception as error:  # e.g. a file system without mmap: bounce everything
+            log.warning("zero-copy staging unavailable (%s); using bounce buffers", error)
+            small = [True] * len(files)
+    runs = _runs(files, small, total)
+    if runs:
+        hosts = [torch.empty(min(chunk_bytes, max(total, 1)), dtype=torch.uint8,
+                             pin_memory=True) for _ in range(2)]
+        events = [None, None]
+        k = 0
+        for run_lo, run_hi in runs:
+            for lo in range(run_lo, run_hi, chunk_bytes):
+                hi = min(run_hi, lo + chunk_bytes)
+                slot = k % 2
+                k += 1
+                if events[slot] is not None:
+                    events[slot].synchronize()
+                host = hosts[slot]
+                t = time.perf_counter()
+                pieces = _pieces_for(root, files, lo, hi)
+                covered = lo
+                for _path, _foff, length, rel in sorted(pieces, key=lambda p: p[3]):
+                    if lo + rel > covered:  # alignment gap: zero it so digests are deterministic
+                        host[covered - lo:rel].zero_()
+                    covered = lo + rel + length
+                if covered < hi:
+                    host[covered - lo:hi - lo].zero_()
+                native().read_pieces(pieces, host.data_ptr(), threads)
+                read_s += time.perf_counter() - t
+                with torch.cuda.stream(stream):
+                    buffer[lo:hi].copy_(host[:hi - lo], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(stream)
+                events[slot] = ev
     stream.synchronize()
-    return {"seconds": time.perf_counter() - t0, "read_s": read_s, "bytes": total}
+    return {"seconds": time.perf_counter() - t0, "read_s": read_s, "zero_copy_host_s": zc_s,
+            "zero_copy_files": len(big), "bytes": total}
 
 
 def stage_workdir(root: Optional[str] = None, device=None, exclude: Optional[List[str]] = None,
                   group=None, src: int = 0, method: str = "auto", verify: bool = True,
-                  chunk_bytes: int = 256 << 20, threads: int = 16) -> StagedWorkdir:
+                  chunk_bytes: int = 256 << 20, threads: int = 16,
+                  zero_copy_min: int = ZERO_COPY_MIN) -> StagedWorkdir:
     """Stage ``root`` (default ``$TPI_DATA_DIRECTORY`` or cwd) into HBM on every rank."""
     import torch
 
@@ -174,9 +295,10 @@ def stage_workdir(root: Optional[str] = None, device=None, exclude: Optional[Lis
     buffer = alloc(total, dtype=torch.uint8, device=device)
     stats: Dict[str, float] = {"bytes": total, "files": len(files)}
     if rank == src:
-        load = load_into(root, files, total, buffer, chunk_bytes, threads)
+        load = load_into(root, files, total, buffer, chunk_bytes, threads, zero_copy_min)
         stats["load_s"] = load["seconds"]
         stats["read_s"] = load["read_s"]
+        stats["zero_copy_files"] = load.get("zero_copy_files", 0)
     if world > 1:
         from ..parallel.broadcast import broadcast_buffer, choose_method
 

@@ -24,7 +24,9 @@ def _gpu():
     ops.hip(required=True)
 
 
-def test_stage_workdir_on_device(tmp_path):
+@pytest.mark.parametrize("zero_copy_min", [1 << 40, 4096])  # bounce only / mixed
+def test_stage_workdir_on_device(tmp_path, zero_copy_min, monkeypatch):
+    monkeypatch.setenv("TPI_STAGE_ZERO_COPY", "1")
     from terraform_provider_iterative_amd.runtime.workdir import ALIGN, stage_workdir
 
     rng = np.random.default_rng(0)
@@ -33,7 +35,9 @@ def test_stage_workdir_on_device(tmp_path):
         p = tmp_path / rel
         p.parent.mkdir(parents=True, exist_ok=True)
         p.write_bytes(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
-    staged = stage_workdir(str(tmp_path), device=torch.device("cuda", 0), chunk_bytes=1 << 20)
+    staged = stage_workdir(str(tmp_path), device=torch.device("cuda", 0), chunk_bytes=1 << 20,
+                           zero_copy_min=zero_copy_min)
+    assert staged.stats.get("zero_copy_files", 0) == (2 if zero_copy_min == 4096 else 0)
     assert staged.buffer.device.type == "cuda"
     for rel, n in sizes.items():
         got = staged.tensor(rel).cpu().numpy().tobytes()
