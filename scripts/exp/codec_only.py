@@ -1,5 +1,5 @@
 """Run only the TPZ1 device encode + decode of a 2 GB AdamW-like state (for PMC passes)."""
-import os, sys, time
+import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch
 from terraform_provider_iterative_amd.ops import codec

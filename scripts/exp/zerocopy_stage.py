@@ -1,6 +1,6 @@
 """Experiment: H2D straight from page-cache pages of a file (mmap + hipHostRegister ReadOnly)
 vs pread into a pinned bounce buffer."""
-import ctypes, mmap, os, sys, time
+import ctypes, mmap, os, time
 import torch
 
 GB = int(float(os.environ.get("GB", "4")) * 1e9)

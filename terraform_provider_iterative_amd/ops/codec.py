@@ -18,7 +18,6 @@ import numpy as np
 from ._loader import hip, native
 from .hashing import DEFAULT_TILE_BYTES, _device_view, _is_device_tensor, _stream, host_buffer
 
-HEADER_BYTES = 96
 NAME = "tpz1"
 
 
