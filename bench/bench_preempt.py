@@ -31,6 +31,9 @@ RANK = r'''#!%(python)s
 import os, sys, time
 t_start = time.time()
 sys.path.insert(0, %(root)r)
+from terraform_provider_iterative_amd.checkpoint import early_prefetch
+if %(early)r and os.path.exists(%(spill)r):
+    early_prefetch(%(spill)r)  # map + pin the spill while torch is being imported
 import torch
 t_import = time.time()
 from bench import synthetic_checkpoint
@@ -93,6 +96,9 @@ def main():
                    help="warm standby successor (TPI_WARM_STANDBY=1), started at the preemption")
     p.add_argument("--no-prefetch", action="store_true",
                    help="successor maps its host region only when the Checkpointer is built")
+    p.add_argument("--early-prefetch", action="store_true",
+                   help="successor maps + pins the spill before importing torch (measured "
+                        "slower on MI355X: the pinning stalls the import)")
     args = p.parse_args()
 
     from terraform_provider_iterative_amd import backends
@@ -108,7 +114,7 @@ def main():
                   credentials=Credentials(node=NodeCredentials(state_root=state)))
     script = RANK % {"python": sys.executable, "root": ROOT, "spill": spill, "gb": args.gb,
                      "codec": args.codec, "prefetch": not args.no_prefetch,
-                     "standby": args.standby}
+                     "early": args.early_prefetch, "standby": args.standby}
     spec = Task(size=Size(machine="m+mi355x"),
                 environment=Environment(script=script, timeout=int(args.timeout) + 60,
                                         variables=Variables({"TPI_TASK": "true"})))
@@ -116,7 +122,7 @@ def main():
     result = {"config": "Preempt-recover: SIGTERM mid-task, %.0f GB checkpoint pack->host "
                         "DRAM->restore (1 x MI355X, iterative_task)" % args.gb,
               "codec": args.codec, "spill": spill, "prefetch": not args.no_prefetch,
-              "standby": args.standby}
+              "early_prefetch": args.early_prefetch, "standby": args.standby}
     if args.standby:
         os.environ["TPI_WARM_STANDBY"] = "1"
     try:

@@ -22,13 +22,16 @@ from ..ops import hip
 
 class HostRegion:
     def __init__(self, size: int, path: Optional[str] = None, *, device: bool = False,
-                 numa_node: int = -1, populate: bool = True):
+                 numa_node: int = -1, populate: bool = True, _mapped=None):
         self.size = size
         self.path = path
         self.device = device
         self.registered = False
         self._mmap = None
-        if device:
+        if _mapped is not None:  # adopted from early_prefetch(): python mmap, registered
+            self._mmap, self.addr = _mapped
+            self.registered = True
+        elif device:
             lib = hip()
             enc = path.encode() if path else None
             ptr = lib.tpi_host_map(enc, size, numa_node, 1 if populate else 0)
@@ -63,7 +66,14 @@ class HostRegion:
     def close(self) -> None:
         if self.addr is None:
             return
-        if self.device:
+        if self.device and self._mmap is not None:  # early-prefetched mapping
+            if self.registered:
+                hip().tpi_host_unregister(ctypes.c_void_p(self.addr))
+            try:
+                self._mmap.close()
+            except BufferError:
+                pass
+        elif self.device:
             lib = hip()
             if self.registered:
                 lib.tpi_host_unregister(ctypes.c_void_p(self.addr))
@@ -140,3 +150,58 @@ def adopt(path: str, size: int) -> Optional[HostRegion]:
         region.close()
         region = None
     return region
+
+
+def _torch_hip_library() -> str:
+    """Path of the HIP runtime torch loads (found without importing torch)."""
+    import importlib.util
+
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        raise ImportError("torch not found")
+    return os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+
+
+def early_prefetch(path: str) -> bool:
+    """:func:`prefetch` that may run BEFORE ``import torch``.
+
+    A background thread maps the spill file (MAP_POPULATE) and registers it with torch's own
+    HIP runtime library (loaded by path, so torch later binds to the same one), overlapping
+    the ~1.5 s of ``import torch`` of a respawned rank.  The next Checkpointer on ``path``
+    adopts the region.
+    """
+    if not path or not os.path.exists(path):
+        return False
+    size = os.path.getsize(path)
+    if size == 0:
+        return False
+    with _prefetch_lock:
+        if path in _prefetched:
+            return True
+        box: dict = {}
+
+        def work():
+            try:
+                fd = os.open(path, os.O_RDWR)
+                try:
+                    mm = mmap.mmap(fd, size, mmap.MAP_SHARED | getattr(mmap, "MAP_POPULATE", 0),
+                                   mmap.PROT_READ | mmap.PROT_WRITE)
+                finally:
+                    os.close(fd)
+                buf = (ctypes.c_char * size).from_buffer(mm)
+                addr = ctypes.addressof(buf)
+                del buf
+                lib = ctypes.CDLL(_torch_hip_library(), mode=ctypes.RTLD_GLOBAL)
+                lib.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
+                rc = lib.hipHostRegister(ctypes.c_void_p(addr), size, 0x2 | 0x1)  # mapped|portable
+                if rc != 0:
+                    mm.close()
+                    raise OSError("hipHostRegister failed (%d)" % rc)
+                box["region"] = HostRegion(size, path, device=True, _mapped=(mm, addr))
+            except Exception as error:  # surfaced as "not adopted"; the caller maps itself
+                box["error"] = error
+
+        thread = threading.Thread(target=work, name="tpi-early-prefetch", daemon=True)
+        thread.start()
+        _prefetched[path] = (thread, box)
+    return True

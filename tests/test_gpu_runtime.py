@@ -144,3 +144,20 @@ def test_prefetched_spill_region_is_adopted(tmp_path):
         torch.cuda.synchronize()
     assert all(torch.equal(dst[k], ref[k]) for k in ref)
     assert not prefetch(str(tmp_path / "missing"))
+
+
+def test_early_prefetched_region_is_adopted(tmp_path):
+    from terraform_provider_iterative_amd.checkpoint import Checkpointer, early_prefetch, host
+
+    spill = str(tmp_path / "spill")
+    src = {"w": torch.randn(1 << 20, device="cuda")}
+    ref = {k: v.clone() for k, v in src.items()}
+    with Checkpointer(src, path=spill, codec="tpz1") as ck:
+        ck.save({"step": 5})
+    assert early_prefetch(spill)
+    dst = {k: torch.zeros_like(v) for k, v in ref.items()}
+    with Checkpointer(dst, path=spill) as ck:
+        assert spill not in host._prefetched and ck.region._mmap is not None
+        assert ck.restore().bad_tiles == 0 and ck.header()["metadata"] == {"step": 5}
+        torch.cuda.synchronize()
+    assert torch.equal(dst["w"], ref["w"])
