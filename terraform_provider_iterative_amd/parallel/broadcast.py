@@ -73,20 +73,33 @@ def broadcast_buffer(buf, src: int = 0, group=None, method: str = "auto") -> flo
         if ops:
             for req in dist.batch_isend_irecv(ops):
                 req.wait()
-        try:
-            dist.all_gather_into_tensor(padded, shards[rank], group=group)
-        except (RuntimeError, AttributeError, NotImplementedError):
-            # gloo without allgather_into_tensor: list form into views of the buffer.
-            outs = [shards[r] for r in range(world)]
-            tmp = [torch.empty_like(shards[r]) for r in range(world)]
-            dist.all_gather(tmp, shards[rank].clone(), group=group)
-            for o, t in zip(outs, tmp):
-                o.copy_(t)
+        allgather_inplace(padded, group)
         if padded is not buf:
             buf.copy_(padded[:n])
     if on_device:
         torch.cuda.synchronize(buf.device)
     return time.perf_counter() - t0
+
+
+def allgather_inplace(padded, group=None) -> None:
+    """In-place all-gather of ``padded`` viewed as ``world`` equal shards: rank r's shard r
+    is kept, every other shard is filled from its owner.  RCCL takes the single-buffer
+    ``all_gather_into_tensor`` (one ring pass, no staging copy); gloo lacks it, so there
+    the list form gathers into scratch tensors that are copied back into the views."""
+    import torch
+
+    dist = _dist()
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    shards = padded.view(world, -1)
+    if padded.device.type == "cuda":
+        dist.all_gather_into_tensor(padded, shards[rank], group=group)
+        return
+    tmp = [torch.empty_like(shards[r]) for r in range(world)]
+    dist.all_gather(tmp, shards[rank].clone(), group=group)
+    for r in range(world):
+        if r != rank:
+            shards[r].copy_(tmp[r])
 
 
 def _global(rank: int, group) -> int:
