@@ -2,7 +2,7 @@
 from __future__ import annotations
 
 import os
-from dataclasses import replace
+from ..utils.record import replace
 from typing import List
 
 from ..models.cloud import (ALL_PROVIDERS, NODE_PROVIDERS, REMOTE_PROVIDERS, Cloud)

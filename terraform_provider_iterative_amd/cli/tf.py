@@ -24,9 +24,9 @@ import sys
 import threading
 import time
 from concurrent.futures import ThreadPoolExecutor
-from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Tuple
 
+from ..utils.record import field, record
 from ..hcl import Configuration, EvaluationError, HCLSyntaxError
 from ..hcl.evaluate import Context
 from ..models.schema import SchemaError, get_schema, force_new_changes, in_place_changes
@@ -39,7 +39,7 @@ from ..utils.logger import TpiFormatter, setup as setup_logging
 SUPPORTED_PREFIX = "iterative_"
 
 
-@dataclass
+@record
 class Desired:
     type: str
     name: str
@@ -52,7 +52,7 @@ class Desired:
         return address(self.type, self.name, self.index)
 
 
-@dataclass
+@record
 class Change:
     action: str  # create | delete | replace | update | noop
     type: str

@@ -7,7 +7,6 @@
 from __future__ import annotations
 
 import base64
-import hashlib
 import json
 import os
 from typing import Any, Callable, Dict, List, Optional
@@ -15,6 +14,12 @@ from typing import Any, Callable, Dict, List, Optional
 from .parser import (Attribute, Binary, Block, Body, Call, Conditional, ForExpr, GetAttr,
                      Index, Literal, ObjectExpr, Reference, Template, TupleExpr, Unary,
                      parse_file)
+
+
+def _hashlib():
+    import hashlib  # lazily: ~3 ms of CLI start-up, needed only by sha256() / md5()
+
+    return hashlib
 
 
 class EvaluationError(ValueError):
@@ -118,8 +123,8 @@ class Context:
             "min": min, "max": max, "abs": abs, "ceil": lambda x: -(-x // 1), "floor": lambda x: x // 1,
             "format": format_, "base64encode": lambda s: base64.b64encode(s.encode()).decode(),
             "base64decode": lambda s: base64.b64decode(s).decode(),
-            "sha256": lambda s: hashlib.sha256(s.encode()).hexdigest(),
-            "md5": lambda s: hashlib.md5(s.encode()).hexdigest(),
+            "sha256": lambda s: _hashlib().sha256(s.encode()).hexdigest(),
+            "md5": lambda s: _hashlib().md5(s.encode()).hexdigest(),
             "timestamp": lambda: __import__("datetime").datetime.utcnow().strftime("%Y-%m-%dT%H:%M:%SZ"),
             "__splat__": lambda v: v if isinstance(v, list) else [v],
         }

@@ -14,8 +14,9 @@ available in this environment; this parser is what ``leo`` and ``tpi`` read ``ma
 from __future__ import annotations
 
 import re
-from dataclasses import dataclass, field
 from typing import Any, List, Optional, Tuple, Union
+
+from ..utils.record import field, record
 
 
 class HCLSyntaxError(ValueError):
@@ -27,71 +28,71 @@ class HCLSyntaxError(ValueError):
 
 # ---- AST -----------------------------------------------------------------------------------
 
-@dataclass
+@record
 class Literal:
     value: Any
 
 
-@dataclass
+@record
 class Template:
     parts: List[Union[str, Any]]  # str chunks and expression nodes
 
 
-@dataclass
+@record
 class TupleExpr:
     items: List[Any]
 
 
-@dataclass
+@record
 class ObjectExpr:
     items: List[Tuple[Any, Any]]  # (key expr, value expr)
 
 
-@dataclass
+@record
 class Reference:
     name: str
 
 
-@dataclass
+@record
 class GetAttr:
     obj: Any
     name: str
 
 
-@dataclass
+@record
 class Index:
     obj: Any
     key: Any
 
 
-@dataclass
+@record
 class Call:
     name: str
     args: List[Any]
     expand_final: bool = False
 
 
-@dataclass
+@record
 class Unary:
     op: str
     operand: Any
 
 
-@dataclass
+@record
 class Binary:
     op: str
     left: Any
     right: Any
 
 
-@dataclass
+@record
 class Conditional:
     cond: Any
     then: Any
     other: Any
 
 
-@dataclass
+@record
 class ForExpr:
     key_var: Optional[str]
     value_var: str
@@ -102,14 +103,14 @@ class ForExpr:
     is_object: bool
 
 
-@dataclass
+@record
 class Attribute:
     name: str
     expr: Any
     line: int = 0
 
 
-@dataclass
+@record
 class Block:
     type: str
     labels: List[str]
@@ -117,7 +118,7 @@ class Block:
     line: int = 0
 
 
-@dataclass
+@record
 class Body:
     attributes: List[Attribute] = field(default_factory=list)
     blocks: List[Block] = field(default_factory=list)
@@ -146,7 +147,7 @@ _TOKEN_RE = re.compile(r"""
 """, re.X | re.S)
 
 
-@dataclass
+@record
 class Tok:
     kind: str
     value: Any

@@ -9,8 +9,9 @@ clear diagnostic instead of an "unknown provider" error (see ``backends/remote.p
 from __future__ import annotations
 
 import os
-from dataclasses import dataclass, field
 from typing import Dict, Mapping, Optional
+
+from ..utils.record import field, record
 
 PROVIDER_AWS = "aws"
 PROVIDER_GCP = "gcp"
@@ -28,7 +29,7 @@ DEFAULT_TIMEOUTS = {"create": 15 * 60.0, "read": 3 * 60.0, "update": 3 * 60.0,
                     "delete": 15 * 60.0}
 
 
-@dataclass
+@record
 class Timeouts:
     create: float = DEFAULT_TIMEOUTS["create"]
     read: float = DEFAULT_TIMEOUTS["read"]
@@ -36,19 +37,19 @@ class Timeouts:
     delete: float = DEFAULT_TIMEOUTS["delete"]
 
 
-@dataclass
+@record
 class AWSCredentials:
     access_key_id: str = ""
     secret_access_key: str = ""
     session_token: str = ""
 
 
-@dataclass
+@record
 class GCPCredentials:
     application_credentials: str = ""
 
 
-@dataclass
+@record
 class AZCredentials:
     client_id: str = ""
     client_secret: str = ""
@@ -56,12 +57,12 @@ class AZCredentials:
     tenant_id: str = ""
 
 
-@dataclass
+@record
 class K8SCredentials:
     config: str = ""
 
 
-@dataclass
+@record
 class NodeCredentials:
     """Credentials of the node-local runtime: where task state lives.
 
@@ -72,7 +73,7 @@ class NodeCredentials:
     state_root: str = ""
 
 
-@dataclass
+@record
 class Credentials:
     aws: Optional[AWSCredentials] = None
     gcp: Optional[GCPCredentials] = None
@@ -91,7 +92,7 @@ def default_state_root(environ: Optional[Mapping[str, str]] = None) -> str:
     return os.path.join(base, "tpi")
 
 
-@dataclass
+@record
 class Cloud:
     provider: str = PROVIDER_LOCAL
     region: str = "us-west"

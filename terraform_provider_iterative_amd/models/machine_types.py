@@ -13,8 +13,9 @@ the reference's GPU aliases map to the same GPU counts (``m+v100`` -> 1, ``l+v10
 from __future__ import annotations
 
 import re
-from dataclasses import dataclass
 from typing import Dict, Optional
+
+from ..utils.record import record
 
 GENERIC = ("s", "m", "l", "xl", "m+t4", "m+k80", "l+k80", "xl+k80", "m+v100", "l+v100",
            "xl+v100")
@@ -63,7 +64,7 @@ class MachineTypeError(ValueError):
     pass
 
 
-@dataclass(frozen=True)
+@record(frozen=True)
 class MachineType:
     name: str
     cpus: int

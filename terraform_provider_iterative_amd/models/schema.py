@@ -8,13 +8,14 @@ the Terraform plugin server (``provider/``) and validation.
 """
 from __future__ import annotations
 
-from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional
+
+from ..utils.record import field, record
 
 STRING, INT, FLOAT, BOOL, LIST, MAP, SET = "string", "int", "float", "bool", "list", "map", "set"
 
 
-@dataclass
+@record
 class Attr:
     type: str
     required: bool = False
@@ -32,7 +33,7 @@ class Attr:
         return self.type == SET and isinstance(self.elem, dict)
 
 
-@dataclass
+@record
 class ResourceSchema:
     name: str
     attributes: Dict[str, Attr]

@@ -9,8 +9,9 @@ import datetime as _dt
 import ipaddress
 import os
 import re
-from dataclasses import dataclass, field
 from typing import Dict, List, Mapping, Optional
+
+from ..utils.record import field, record
 
 
 class NotFoundError(Exception):
@@ -47,13 +48,13 @@ def new_status() -> Dict[str, int]:
     return {code: 0 for code in STATUS_CODES}
 
 
-@dataclass
+@record
 class Size:
     machine: str = "m"
     storage: int = -1
 
 
-@dataclass
+@record
 class Event:
     time: _dt.datetime
     code: str
@@ -74,7 +75,7 @@ class Event:
                    code=str(data["code"]), description=list(data.get("description") or []))
 
 
-@dataclass
+@record
 class RemoteStorage:
     """Pre-allocated storage container (``values.go:47-55``).
 
@@ -87,7 +88,7 @@ class RemoteStorage:
     config: Dict[str, str] = field(default_factory=dict)
 
 
-@dataclass
+@record
 class FirewallRule:
     """``nets``/``ports`` None = allow any; empty list = allow none (``values.go:73-84``)."""
 
@@ -95,7 +96,7 @@ class FirewallRule:
     ports: Optional[List[int]] = None
 
 
-@dataclass
+@record
 class Firewall:
     ingress: FirewallRule = field(default_factory=FirewallRule)
     egress: FirewallRule = field(default_factory=FirewallRule)
@@ -123,7 +124,7 @@ class Variables(dict):
         return result
 
 
-@dataclass
+@record
 class Environment:
     image: str = "ubuntu"
     script: str = ""
@@ -134,7 +135,7 @@ class Environment:
     exclude_list: List[str] = field(default_factory=list)
 
 
-@dataclass
+@record
 class Task:
     size: Size = field(default_factory=Size)
     environment: Environment = field(default_factory=Environment)

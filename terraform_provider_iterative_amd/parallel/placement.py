@@ -18,13 +18,14 @@ import json
 import os
 import time
 from contextlib import contextmanager
-from dataclasses import dataclass, field
 from typing import Dict, Iterator, List, Optional
+
+from ..utils.record import field, record
 
 KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
 
 
-@dataclass
+@record
 class GPU:
     index: int                 # HIP device index on this node
     gfx: str = ""              # e.g. "gfx950"

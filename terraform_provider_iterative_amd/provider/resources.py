@@ -15,9 +15,9 @@ import datetime as _dt
 import logging
 import os
 import time
-from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Tuple
 
+from ..utils.record import field, record
 from .. import backends
 from ..models.cloud import Cloud, Timeouts, PROVIDER_LOCAL, PROVIDER_MI355X
 from ..models.schema import get_schema
@@ -36,14 +36,14 @@ LOG_TPL = ("%s may take several minutes (consider increasing `timeout` "
            "task#timeout). Please wait.")
 
 
-@dataclass
+@record
 class Diagnostic:
     severity: str  # "error" | "warning"
     summary: str
     detail: str = ""
 
 
-@dataclass
+@record
 class Result:
     id: str
     state: Dict[str, Any]

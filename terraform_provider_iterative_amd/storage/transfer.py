@@ -11,9 +11,9 @@ import json
 import logging
 import os
 import posixpath
-from dataclasses import dataclass, field
 from typing import Dict, Iterable, List, Optional
 
+from ..utils.record import field, record
 from ..models.values import STATUS_FAILED, STATUS_SUCCEEDED, NotFoundError, new_status
 from ..ops import native
 
@@ -145,7 +145,7 @@ def status(remote: str, initial: Optional[Dict[str, int]] = None) -> Dict[str, i
     return result
 
 
-@dataclass
+@record
 class Connection:
     """rclone-style connection string (``storage.go:229-263``).
 

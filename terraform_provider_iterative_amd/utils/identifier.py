@@ -10,8 +10,8 @@ from __future__ import annotations
 import hashlib
 import re
 import secrets
-from dataclasses import dataclass
 
+from .record import record
 from .petname import generate as _petname
 
 DEFAULT_PREFIX = "tpi"
@@ -63,7 +63,7 @@ def normalize(identifier: str, truncate: int) -> str:
     return normalized
 
 
-@dataclass(frozen=True)
+@record(frozen=True)
 class Identifier:
     prefix: str
     name: str

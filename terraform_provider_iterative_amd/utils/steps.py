@@ -3,19 +3,20 @@ from __future__ import annotations
 
 import logging
 import time
-from dataclasses import dataclass
 from typing import Callable, Iterable, List, Optional
+
+from .record import record
 
 log = logging.getLogger("tpi")
 
 
-@dataclass
+@record
 class Step:
     description: str
     action: Callable[[], None]
 
 
-@dataclass
+@record
 class StepTiming:
     description: str
     seconds: float

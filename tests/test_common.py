@@ -226,3 +226,42 @@ def test_cloud_descriptor():
     node = Cloud(credentials=Credentials(node=NodeCredentials("/srv/tpi")))
     assert node.state_root() == "/srv/tpi"
     assert parse_region_selectors("gpus=2-3, numa=1,us-west") == {"gpus": "2-3", "numa": "1"}
+
+
+def test_record_matches_dataclass_semantics():
+    """utils/record.py: the dataclass subset the CLI-path value types rely on."""
+    import pytest as _pytest
+
+    from terraform_provider_iterative_amd.utils.record import (FrozenInstanceError, field,
+                                                                record, replace)
+
+    @record
+    class Point:
+        x: int
+        y: int = 2
+        tags: list = field(default_factory=list)
+
+    a, b = Point(1), Point(1)
+    assert (a.x, a.y, a.tags) == (1, 2, [])
+    assert a == b and a.tags is not b.tags
+    assert Point(1, 3, ["t"]) == Point(x=1, y=3, tags=["t"])
+    assert repr(Point(1)).endswith("Point(x=1, y=2, tags=[])")  # __qualname__, as dataclasses
+    assert replace(a, y=5) == Point(1, 5)
+    with _pytest.raises(TypeError):
+        Point()
+    with _pytest.raises(TypeError):
+        Point(1, z=3)
+    with _pytest.raises(TypeError):
+        Point(1, x=1)
+    with _pytest.raises(TypeError):
+        hash(a)
+
+    @record(frozen=True)
+    class Key:
+        name: str
+        n: int = 0
+
+    k = Key("a")
+    assert hash(k) == hash(Key("a")) and {k: 1}[Key("a")] == 1
+    with _pytest.raises(FrozenInstanceError):
+        k.n = 3
