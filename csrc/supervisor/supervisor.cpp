@@ -28,6 +28,9 @@
 //    spilling; it blocks in preemption.standby() until "go" arrives on TPI_STANDBY_FD, written
 //    when the old rank has released (or exited as preempted);
 //  * SIGTERM/SIGINT/SIGHUP = stop (`leo stop`, scale to 0): ranks terminated, no status;
+//  * control socket supervisor/control.sock (AF_UNIX, mode 0600; SURVEY.md §2.10 "local
+//    supervisor API"): one request line, one JSON reply line -- `ping`, `state` (live rank
+//    table, fresher than state.json), `preempt` (= SIGUSR1), `stop` (= SIGTERM);
 //  * exits when no rank is left to run ("no waste" auto-cleanup, tpl:10-15), removing its
 //    GPU lease files.
 //
@@ -42,6 +45,8 @@
 #include <string.h>
 #include <sys/prctl.h>
 #include <sys/signalfd.h>
+#include <sys/socket.h>
+#include <sys/un.h>
 #include <sys/stat.h>
 #include <sys/time.h>
 #include <sys/types.h>
@@ -193,7 +198,7 @@ struct Spec {
   bool standby = false;
   int max_restarts = -1;
   double grace = 30, respawn_delay = 0;
-  std::string reports_dir, state_path, events_path;
+  std::string reports_dir, state_path, events_path, control_path;
   std::vector<std::string> leases;
 };
 
@@ -227,6 +232,7 @@ Spec load_spec(const std::string& path) {
   s.reports_dir = v["reports_dir"].str(s.task_dir + "/reports");
   s.state_path = v["state_path"].str(s.task_dir + "/supervisor/state.json");
   s.events_path = v["events_path"].str(s.task_dir + "/supervisor/events.jsonl");
+  s.control_path = v["control_path"].str(s.task_dir + "/supervisor/control.sock");
   for (auto& l : v["leases"].a) s.leases.push_back(l.str());
   if (s.workdir.empty() || s.script.empty()) throw std::runtime_error("spec needs workdir+script");
   return s;
@@ -252,6 +258,7 @@ class Supervisor {
     sigprocmask(SIG_BLOCK, &mask, nullptr);
     sfd_ = signalfd(-1, &mask, SFD_CLOEXEC | SFD_NONBLOCK);
     signal(SIGPIPE, SIG_IGN);
+    open_control();
     started_ = now();
     event("supervisor-start", {"pid " + std::to_string(getpid()),
                                "parallelism " + std::to_string(s_.parallelism)});
@@ -297,16 +304,19 @@ class Supervisor {
             owners.push_back({&r, true});
           }
         }
+      size_t nrank_fds = pfds.size();
+      if (ctl_fd_ >= 0) pfds.push_back({ctl_fd_, POLLIN, 0});
       int rc = poll(pfds.data(), pfds.size(), (int)(timeout * 1000) + 1);
       if (rc < 0 && errno != EINTR) break;
       bool released = false;
-      for (size_t i = 1; i < pfds.size(); ++i) {
+      for (size_t i = 1; i < nrank_fds; ++i) {
         if (!(pfds[i].revents & (POLLIN | POLLHUP | POLLERR))) continue;
         if (owners[i - 1].second) released |= notified(*owners[i - 1].first);
         else pump(*owners[i - 1].first);
       }
       if (released) handoff_released();
       if (pfds[0].revents & POLLIN) handle_signals();
+      if (nrank_fds < pfds.size() && (pfds[nrank_fds].revents & POLLIN)) handle_control();
       if (dirty_ || now() - last_state > 5) {
         write_state();
         last_state = now();
@@ -323,6 +333,7 @@ class Supervisor {
   std::vector<Rank> standby_;   // per rank index: warm successor waiting for "go" (pid > 0)
   bool machine_logs_ = false;   // TPI_MACHINE_LOGS set in the task environment (tpl:109)
   int sfd_ = -1;
+  int ctl_fd_ = -1;
   double started_ = 0, respawn_at_ = 0;
   bool stop_ = false, timed_out_ = false, dirty_ = true;
   int total_restarts_ = 0;
@@ -370,7 +381,9 @@ class Supervisor {
     return n;
   }
 
-  void write_state(const char* phase = nullptr) {
+  void write_state(const char* phase = nullptr) { atomic_write(s_.state_path, state_json(phase)); }
+
+  std::string state_json(const char* phase = nullptr) {
     std::string p = phase ? phase
                     : stop_ ? "stopping"
                     : timed_out_ ? "timing-out"
@@ -392,7 +405,7 @@ class Supervisor {
              ", \"exit_signal\": " + std::to_string(r.exit_signal) + "}";
     }
     out += "]}\n";
-    atomic_write(s_.state_path, out);
+    return out;
   }
 
   void write_status(Rank& r, const std::string& result, const std::string& code,
@@ -791,29 +804,115 @@ class Supervisor {
         case SIGTERM:
         case SIGINT:
         case SIGHUP:
-          if (!stop_) {
-            stop_ = true;
-            respawn_at_ = 0;
-            event("stop-requested", {std::string("signal ") + signame(si.ssi_signo)});
-            for (int i = 0; i < s_.parallelism; ++i) discard_standby(i, "stop");
-            for (auto& r : ranks_) {
-              if (r.state == Rank::RUNNING) terminate(r, TermReason::STOP);
-              else if (r.state != Rank::DONE) r.state = Rank::DONE;
-            }
-          }
+          request_stop(std::string("signal ") + signame(si.ssi_signo));
           break;
         case SIGUSR1:
-          if (!stop_ && !timed_out_) {
-            event("preempt-requested", {"all ranks"});
-            for (auto& r : ranks_) terminate(r, TermReason::PREEMPT);
-            for (auto& r : ranks_)
-              if (r.state == Rank::RUNNING) spawn_standby(r);
-          }
+          request_preempt("signal USR1");
           break;
         default: break;
       }
     }
     reap();
+  }
+
+  void request_stop(const std::string& source) {
+    if (stop_) return;
+    stop_ = true;
+    respawn_at_ = 0;
+    event("stop-requested", {source});
+    for (int i = 0; i < s_.parallelism; ++i) discard_standby(i, "stop");
+    for (auto& r : ranks_) {
+      if (r.state == Rank::RUNNING) terminate(r, TermReason::STOP);
+      else if (r.state != Rank::DONE) r.state = Rank::DONE;
+    }
+    dirty_ = true;
+  }
+
+  bool request_preempt(const std::string& source) {
+    if (stop_ || timed_out_) return false;
+    event("preempt-requested", {"all ranks", source});
+    for (auto& r : ranks_) terminate(r, TermReason::PREEMPT);
+    for (auto& r : ranks_)
+      if (r.state == Rank::RUNNING) spawn_standby(r);
+    dirty_ = true;
+    return true;
+  }
+
+  // ---- control socket --------------------------------------------------------------------
+  // sun_path holds 108 bytes and task directories can be longer, so bind/connect go through
+  // /proc/self/fd/<dirfd>/<name> (the client in backends/node.py does the same).
+  void open_control() {
+    size_t slash = s_.control_path.rfind('/');
+    std::string dir = slash == std::string::npos ? "." : s_.control_path.substr(0, slash);
+    std::string name = slash == std::string::npos ? s_.control_path
+                                                  : s_.control_path.substr(slash + 1);
+    int dfd = open(dir.c_str(), O_PATH | O_DIRECTORY | O_CLOEXEC);
+    if (dfd < 0) return;
+    unlinkat(dfd, name.c_str(), 0);
+    struct sockaddr_un addr;
+    memset(&addr, 0, sizeof(addr));
+    addr.sun_family = AF_UNIX;
+    int n = snprintf(addr.sun_path, sizeof(addr.sun_path), "/proc/self/fd/%d/%s", dfd,
+                     name.c_str());
+    int fd = socket(AF_UNIX, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+    mode_t old = umask(077);  // the socket file is created 0600: owner-only control
+    bool ok = fd >= 0 && n > 0 && n < (int)sizeof(addr.sun_path) &&
+              bind(fd, (struct sockaddr*)&addr, sizeof(addr)) == 0 && listen(fd, 16) == 0;
+    umask(old);
+    close(dfd);
+    if (!ok) {
+      if (fd >= 0) close(fd);
+      event("control-unavailable", {strerror(errno)});
+      return;
+    }
+    ctl_fd_ = fd;
+  }
+
+  void close_control() {
+    if (ctl_fd_ < 0) return;
+    close(ctl_fd_);
+    ctl_fd_ = -1;
+    unlink(s_.control_path.c_str());
+  }
+
+  void handle_control() {
+    for (;;) {
+      int c = accept4(ctl_fd_, nullptr, nullptr, SOCK_CLOEXEC);
+      if (c < 0) return;  // EAGAIN: drained
+      // One request line; a client that sends nothing within 200 ms is dropped so the event
+      // loop never stalls on it.
+      std::string req;
+      char buf[256];
+      double until = now() + 0.2;
+      while (req.find('\n') == std::string::npos && req.size() < 4096) {
+        struct pollfd p = {c, POLLIN, 0};
+        int left = (int)((until - now()) * 1000);
+        if (left <= 0 || poll(&p, 1, left) <= 0) break;
+        ssize_t got = read(c, buf, sizeof(buf));
+        if (got <= 0) break;
+        req.append(buf, (size_t)got);
+      }
+      size_t end = req.find_first_of("\r\n");
+      if (end != std::string::npos) req.resize(end);
+      std::string reply;
+      if (req == "ping") {
+        reply = "{\"ok\": true, \"pid\": " + std::to_string(getpid()) +
+                ", \"task_id\": " + quote(s_.task_id) + "}\n";
+      } else if (req == "state") {
+        reply = state_json();
+      } else if (req == "preempt") {
+        bool ok = request_preempt("control socket");
+        reply = ok ? "{\"ok\": true}\n"
+                   : "{\"ok\": false, \"error\": \"task is stopping\"}\n";
+      } else if (req == "stop") {
+        request_stop("control socket");
+        reply = "{\"ok\": true}\n";
+      } else {
+        reply = "{\"ok\": false, \"error\": " + quote("unknown command: " + req) + "}\n";
+      }
+      write_all(c, reply);
+      close(c);
+    }
   }
 
   void reap() {
@@ -938,6 +1037,7 @@ class Supervisor {
       close_log(r);
     }
     for (auto& l : s_.leases) unlink(l.c_str());
+    close_control();
     event("supervisor-exit", {stop_ ? "stopped" : "all ranks finished"});
     write_state("stopped");
     signal_ready();

@@ -122,6 +122,35 @@ class NodeTask(Task):
     def _state(self) -> Dict:
         return _read_json(os.path.join(self.sup_dir, "state.json")) or {}
 
+    def control(self, command: str, timeout: float = 2.0) -> Optional[Dict]:
+        """One request on the supervisor's control socket (``supervisor/control.sock``:
+        ``ping``, ``state``, ``preempt``, ``stop``); the reply as a dict, or None when no
+        supervisor is listening.  The path is reached through ``/proc/self/fd`` because
+        AF_UNIX paths are limited to 108 bytes (the supervisor binds the same way)."""
+        try:
+            dfd = os.open(self.sup_dir, os.O_RDONLY | os.O_DIRECTORY)
+        except OSError:
+            return None
+        try:
+            with socket.socket(socket.AF_UNIX, socket.SOCK_STREAM) as sock:
+                sock.settimeout(timeout)
+                sock.connect("/proc/self/fd/%d/control.sock" % dfd)
+                sock.sendall(command.encode() + b"\n")
+                chunks = []
+                while True:
+                    data = sock.recv(65536)
+                    if not data:
+                        break
+                    chunks.append(data)
+        except OSError:
+            return None
+        finally:
+            os.close(dfd)
+        try:
+            return json.loads(b"".join(chunks).decode() or "null")
+        except ValueError:
+            return None
+
     def supervisor_running(self) -> bool:
         state = self._state()
         pid = int(state.get("pid", 0) or 0)
@@ -332,10 +361,11 @@ class NodeTask(Task):
         pid = int(state.get("pid", 0) or 0)
         if not pid or not pid_alive(pid) or state.get("phase") == "stopped":
             return
-        try:
-            os.kill(pid, signal.SIGTERM)
-        except ProcessLookupError:
-            return
+        if not (self.control("stop") or {}).get("ok"):
+            try:
+                os.kill(pid, signal.SIGTERM)
+            except ProcessLookupError:
+                return
         deadline = _now() + wait
         while _now() < deadline and pid_alive(pid):
             time.sleep(0.02)
@@ -346,7 +376,8 @@ class NodeTask(Task):
         pid = int(state.get("pid", 0) or 0)
         if not pid or not pid_alive(pid):
             raise NotFoundError("task %s is not running" % self.id)
-        os.kill(pid, signal.SIGUSR1)
+        if not (self.control("preempt") or {}).get("ok"):
+            os.kill(pid, signal.SIGUSR1)
 
     def push(self) -> None:
         directory = self.spec.environment.directory

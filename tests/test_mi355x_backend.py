@@ -129,3 +129,25 @@ def test_numa_preference(tmp_path):
     assert {g.numa_node for g in b} == {1}
     assert p.allocate("t1", 3) == a  # idempotent
     assert p.release("t1") == 3
+
+
+def test_control_socket(cloud):
+    """Supervisor control API: ping / live state / unknown / stop."""
+    task = _task(cloud, "control", "#!/bin/sh\necho started\nsleep 30\n", parallelism=2)
+    task.create()
+    deadline = time.time() + 10
+    while not task.logs() and time.time() < deadline:
+        time.sleep(0.05)
+    pong = task.control("ping")
+    assert pong["ok"] and pong["pid"] > 0 and pong["task_id"] == task.id
+    assert os.stat(os.path.join(task.sup_dir, "control.sock")).st_mode & 0o077 == 0
+    state = task.control("state")
+    assert [r["rank"] for r in state["ranks"]] == [0, 1]
+    assert all(r["state"] == "running" and r["pid"] > 0 for r in state["ranks"])
+    assert task.control("bogus")["ok"] is False
+    task.stop()  # goes through the socket
+    assert task.control("ping") is None  # socket removed at exit
+    assert not os.path.exists(os.path.join(task.sup_dir, "control.sock"))
+    codes = [(e.code, e.description) for e in task.events()]
+    assert any(c == "stop-requested" and "control socket" in d for c, d in codes)
+    task.delete()
