@@ -30,7 +30,8 @@
 //  * SIGTERM/SIGINT/SIGHUP = stop (`leo stop`, scale to 0): ranks terminated, no status;
 //  * control socket supervisor/control.sock (AF_UNIX, mode 0600; SURVEY.md §2.10 "local
 //    supervisor API"): one request line, one JSON reply line -- `ping`, `state` (live rank
-//    table, fresher than state.json), `preempt` (= SIGUSR1), `stop` (= SIGTERM);
+//    table, fresher than state.json), `preempt` (= SIGUSR1), `preempt <rank>` (one rank;
+//    the gang follows when `gang` is set), `stop` (= SIGTERM);
 //  * exits when no rank is left to run ("no waste" auto-cleanup, tpl:10-15), removing its
 //    GPU lease files.
 //
@@ -828,12 +829,17 @@ class Supervisor {
     dirty_ = true;
   }
 
-  bool request_preempt(const std::string& source) {
+  // rank < 0: every rank.  A single preempted rank takes its gang down with it when it exits
+  // (reap), like a reclaimed spot VM of a coupled group.
+  bool request_preempt(const std::string& source, int rank = -1) {
     if (stop_ || timed_out_) return false;
-    event("preempt-requested", {"all ranks", source});
-    for (auto& r : ranks_) terminate(r, TermReason::PREEMPT);
+    if (rank >= (int)ranks_.size() || (rank >= 0 && ranks_[rank].state != Rank::RUNNING))
+      return false;
+    event("preempt-requested", {rank < 0 ? "all ranks" : "rank " + std::to_string(rank), source});
     for (auto& r : ranks_)
-      if (r.state == Rank::RUNNING) spawn_standby(r);
+      if (rank < 0 || r.index == rank) terminate(r, TermReason::PREEMPT);
+    for (auto& r : ranks_)
+      if ((rank < 0 || r.index == rank) && r.state == Rank::RUNNING) spawn_standby(r);
     dirty_ = true;
     return true;
   }
@@ -900,10 +906,18 @@ class Supervisor {
                 ", \"task_id\": " + quote(s_.task_id) + "}\n";
       } else if (req == "state") {
         reply = state_json();
-      } else if (req == "preempt") {
-        bool ok = request_preempt("control socket");
+      } else if (req == "preempt" || req.compare(0, 8, "preempt ") == 0) {
+        int rank = -1;
+        bool parsed = true;
+        if (req.size() > 8) {
+          char* endp = nullptr;
+          long v = strtol(req.c_str() + 8, &endp, 10);
+          parsed = endp && *endp == '\0' && v >= 0 && v < (long)ranks_.size();
+          rank = (int)v;
+        }
+        bool ok = parsed && request_preempt("control socket", rank);
         reply = ok ? "{\"ok\": true}\n"
-                   : "{\"ok\": false, \"error\": \"task is stopping\"}\n";
+                   : "{\"ok\": false, \"error\": \"no running rank to preempt\"}\n";
       } else if (req == "stop") {
         request_stop("control socket");
         reply = "{\"ok\": true}\n";

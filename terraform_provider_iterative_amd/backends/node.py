@@ -370,14 +370,22 @@ class NodeTask(Task):
         while _now() < deadline and pid_alive(pid):
             time.sleep(0.02)
 
-    def preempt(self) -> None:
-        """Fault injection: preempt every rank (they checkpoint, then get respawned)."""
+    def preempt(self, rank: Optional[int] = None) -> None:
+        """Fault injection: preempt every rank, or only ``rank`` (its gang follows when the
+        ranks are coupled); they checkpoint, then get respawned."""
         state = self._state()
         pid = int(state.get("pid", 0) or 0)
         if not pid or not pid_alive(pid):
             raise NotFoundError("task %s is not running" % self.id)
-        if not (self.control("preempt") or {}).get("ok"):
-            os.kill(pid, signal.SIGUSR1)
+        if rank is None:
+            if not (self.control("preempt") or {}).get("ok"):
+                os.kill(pid, signal.SIGUSR1)
+            return
+        reply = self.control("preempt %d" % rank)
+        if reply is None:
+            raise NotFoundError("task %s has no control socket for per-rank preemption" % self.id)
+        if not reply.get("ok"):
+            raise NotFoundError("task %s: %s" % (self.id, reply.get("error")))
 
     def push(self) -> None:
         directory = self.spec.environment.directory

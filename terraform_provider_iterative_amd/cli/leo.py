@@ -133,6 +133,8 @@ def build_parser(defaults: Dict[str, Any]) -> argparse.ArgumentParser:
     destroy_runner.add_argument("name")
     preempt = sub.add_parser("preempt", help=argparse.SUPPRESS)
     preempt.add_argument("name")
+    preempt.add_argument("--rank", type=int, default=None,
+                         help="preempt only this rank (its gang follows when coupled)")
     checkpoint = sub.add_parser("checkpoint", help=argparse.SUPPRESS)
     checkpoint.add_argument("path")
     checkpoint.add_argument("--verify", action="store_true",
@@ -293,7 +295,10 @@ def cmd_preempt(args, cloud: Cloud) -> int:
     task = backends.new(cloud, parse_identifier(args.name), TaskSpec())
     if not hasattr(task, "preempt"):
         raise SystemExit("Error: provider %s cannot inject preemptions" % cloud.provider)
-    task.preempt()
+    if args.rank is None:
+        task.preempt()
+    else:
+        task.preempt(rank=args.rank)
     return 0
 
 

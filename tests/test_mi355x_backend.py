@@ -10,7 +10,8 @@ from terraform_provider_iterative_amd import backends
 from terraform_provider_iterative_amd.models.cloud import Cloud, Credentials, NodeCredentials
 from terraform_provider_iterative_amd.models.machine_types import (MachineTypeError,
                                                                    parse_node_machine)
-from terraform_provider_iterative_amd.models.values import Environment, Size, Task, Variables
+from terraform_provider_iterative_amd.models.values import (Environment, NotFoundError, Size, Task,
+                                                            Variables)
 from terraform_provider_iterative_amd.parallel.placement import (GPU, Placement,
                                                                  PlacementError, discover)
 from terraform_provider_iterative_amd.utils.identifier import new_deterministic_identifier
@@ -150,4 +151,30 @@ def test_control_socket(cloud):
     assert not os.path.exists(os.path.join(task.sup_dir, "control.sock"))
     codes = [(e.code, e.description) for e in task.events()]
     assert any(c == "stop-requested" and "control socket" in d for c, d in codes)
+    task.delete()
+
+
+def test_preempt_one_rank_over_control_socket(cloud):
+    """`leo preempt --rank 1`: only rank 1 is signalled; the coupled gang is respawned."""
+    script = "#!/bin/sh\necho \"up $RANK $TPI_MACHINE_IDENTITY\"\nsleep 30\n"
+    task = _task(cloud, "preemptone", script, parallelism=2)
+    task.create()
+    deadline = time.time() + 10
+    while sum(log.count("up ") for log in task.logs()) < 2 and time.time() < deadline:
+        time.sleep(0.05)
+    with pytest.raises(NotFoundError):
+        task.preempt(rank=7)  # no such rank
+    task.preempt(rank=1)
+    deadline = time.time() + 15
+    state = {}
+    while time.time() < deadline:
+        state = task.control("state") or {}
+        if state.get("ranks") and all(r["restarts"] == 1 and r["state"] == "running"
+                                      for r in state["ranks"]):
+            break
+        time.sleep(0.05)
+    assert [r["restarts"] for r in state["ranks"]] == [1, 1], state
+    events = [(e.code, e.description) for e in task.events()]
+    assert ("preempt-requested", ["rank 1", "control socket"]) in events
+    task.stop()
     task.delete()
