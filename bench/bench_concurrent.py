@@ -1,0 +1,154 @@
+#!/usr/bin/env python3
+"""Config 5: 4 concurrent 2-GPU ``iterative_task`` resources on one node (placement +
+auto-cleanup), driven through the node backend like ``tpi apply`` with Terraform's parallel
+resource walk (4 creates in flight at once).
+
+Reports, as one JSON line:
+
+* ``create_s`` / ``first_log_s`` per task (from the moment all creates were issued);
+* that the four GPU sets are disjoint and cover the node, and that a fifth task is refused
+  with a placement error (and how fast);
+* ``all_succeeded_s``: wall time until every supervisor exited with ``succeeded``;
+* ``reuse_s``: time from the last supervisor exit until an 8-GPU task is placed on the
+  released GPUs without any ``delete`` in between (lease auto-cleanup);
+* ``delete_s``: destroying all five tasks.
+
+In the reference, placement is a cloud API call per VM (ASG/MIG/VMSS resize, minutes); here
+it is a lease-file allocator (parallel/placement.py).  On a node with fewer than 8 GPUs the
+run uses 8 logical GPU slots (``TPI_MI355X_GPUS``) and says so in ``gpus``: the scripts only
+echo, so oversubscribing the slots measures the orchestration path, not the device.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+SCRIPT = "#!/bin/sh\necho \"rank $RANK of $WORLD_SIZE on GPUs $HIP_VISIBLE_DEVICES\"\nsleep %s\n"
+
+
+def _first_log(task, t0: float, timeout: float) -> float:
+    deadline = time.perf_counter() + timeout
+    while time.perf_counter() < deadline:
+        if any(chunk.strip() for chunk in task.logs()):
+            return time.perf_counter() - t0
+        time.sleep(0.0005)
+    raise TimeoutError("no log from %s" % task.get_identifier().long())
+
+
+def run(tasks: int = 4, gpus_per_task: int = 2, sleep: float = 1.0) -> dict:
+    from terraform_provider_iterative_amd.parallel.placement import discover
+
+    need = tasks * gpus_per_task
+    physical = len(discover())
+    saved = os.environ.get("TPI_MI355X_GPUS")
+    if physical < need:
+        os.environ["TPI_MI355X_GPUS"] = ",".join(str(i) for i in range(need))
+    try:
+        return _run(tasks, gpus_per_task, sleep, need, physical)
+    finally:  # repeats must see the node again, not this run's logical slots
+        if saved is None:
+            os.environ.pop("TPI_MI355X_GPUS", None)
+        else:
+            os.environ["TPI_MI355X_GPUS"] = saved
+
+
+def _run(tasks: int, gpus_per_task: int, sleep: float, need: int, physical: int) -> dict:
+    from terraform_provider_iterative_amd import backends
+    from terraform_provider_iterative_amd.models.cloud import (Cloud, Credentials,
+                                                               NodeCredentials)
+    from terraform_provider_iterative_amd.models.values import (Environment, Size, Task,
+                                                                Variables)
+    from terraform_provider_iterative_amd.parallel.placement import PlacementError
+    from terraform_provider_iterative_amd.utils.identifier import new_deterministic_identifier
+
+    state = tempfile.mkdtemp(prefix="tpi-concurrent-")
+    cloud = Cloud(provider="mi355x",
+                  credentials=Credentials(node=NodeCredentials(state_root=state)))
+
+    def make(name: str, n: int, script: str):
+        machine = "m+mi355x" if n == 1 else "16-64000+mi355x*%d" % n
+        spec = Task(size=Size(machine=machine), parallelism=1,
+                    environment=Environment(script=script, timeout=120,
+                                            variables=Variables({"TPI_TASK": "true"})))
+        return backends.new(cloud, new_deterministic_identifier(name), spec)
+
+    group = [make("conc-%d-%d" % (os.getpid(), i), gpus_per_task, SCRIPT % sleep)
+             for i in range(tasks)]
+    created = {}
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(tasks) as pool:
+        futures = {pool.submit(t.create): i for i, t in enumerate(group)}
+        for fut in cf.as_completed(futures):
+            fut.result()
+            created[futures[fut]] = time.perf_counter() - t0
+    first = [_first_log(t, t0, 30.0) for t in group]
+    sets = [sorted(t.gpus()) for t in group]
+    disjoint = len(set().union(*map(set, sets))) == need and all(len(s) == gpus_per_task
+                                                                 for s in sets)
+    extra = make("conc-extra-%d" % os.getpid(), 1, SCRIPT % 0)
+    t1 = time.perf_counter()
+    try:
+        extra.create()
+        refused, refuse_s = False, None
+    except PlacementError:
+        refused, refuse_s = True, time.perf_counter() - t1
+    extra.delete()
+    statuses = [t.wait(60.0) for t in group]
+    t_done = time.perf_counter()
+    all_ok = all(s.get("succeeded") == 1 for s in statuses)
+    again = make("conc-after-%d" % os.getpid(), need, SCRIPT % 0)
+    again.create()
+    reuse_s = time.perf_counter() - t_done
+    reused = sorted(again.gpus()) == list(range(need))
+    again.wait(30.0)
+    t2 = time.perf_counter()
+    for t in group + [again]:
+        t.delete()
+    delete_s = time.perf_counter() - t2
+    shutil.rmtree(state, ignore_errors=True)
+    return {
+        "config": "4 concurrent 2-GPU iterative_task resources on one node (placement + "
+                  "auto-cleanup)",
+        "gpus": {"physical": physical, "slots": need,
+                 "logical_slots": physical < need},
+        "create_s": [round(created[i], 4) for i in range(tasks)],
+        "first_log_s": [round(x, 4) for x in first],
+        "gpu_sets": sets, "disjoint": disjoint,
+        "fifth_refused": refused, "refuse_s": None if refuse_s is None else round(refuse_s, 4),
+        "all_succeeded": all_ok, "all_succeeded_s": round(t_done - t0, 3),
+        "task_sleep_s": sleep,
+        "reuse_s": round(reuse_s, 4), "reused_all_gpus": reused,
+        "delete_s": round(delete_s, 4),
+    }
+
+
+def main() -> int:
+    parser = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    parser.add_argument("--tasks", type=int, default=4)
+    parser.add_argument("--gpus-per-task", type=int, default=2)
+    parser.add_argument("--sleep", type=float, default=1.0)
+    parser.add_argument("--repeats", type=int, default=3)
+    args = parser.parse_args()
+    runs = [run(args.tasks, args.gpus_per_task, args.sleep) for _ in range(args.repeats)]
+    out = dict(runs[-1])
+    out["repeats"] = len(runs)
+    out["median_first_log_s"] = sorted(max(r["first_log_s"]) for r in runs)[len(runs) // 2]
+    out["median_reuse_s"] = sorted(r["reuse_s"] for r in runs)[len(runs) // 2]
+    out["ok"] = all(r["disjoint"] and r["fifth_refused"] and r["all_succeeded"]
+                    and r["reused_all_gpus"] for r in runs)
+    print(json.dumps(out))
+    return 0 if out["ok"] else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

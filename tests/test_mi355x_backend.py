@@ -178,3 +178,21 @@ def test_preempt_one_rank_over_control_socket(cloud):
     assert ("preempt-requested", ["rank 1", "control socket"]) in events
     task.stop()
     task.delete()
+
+
+def test_bench_concurrent_config5(monkeypatch, tmp_path):
+    """bench/bench_concurrent.py (config 5) on 8 logical slots: disjoint sets, refusal,
+    lease auto-cleanup."""
+    import importlib.util
+
+    monkeypatch.setenv("TPI_MI355X_GPUS", "0,1,2,3,4,5,6,7")
+    monkeypatch.setenv("TMPDIR", str(tmp_path))
+    spec = importlib.util.spec_from_file_location(
+        "bench_concurrent", os.path.join(os.path.dirname(os.path.dirname(__file__)), "bench",
+                                         "bench_concurrent.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    out = mod.run(tasks=4, gpus_per_task=2, sleep=0.2)
+    assert out["disjoint"] and out["fifth_refused"] and out["all_succeeded"]
+    assert out["reused_all_gpus"]
+    assert len(out["first_log_s"]) == 4
