@@ -34,6 +34,11 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 SCRIPT = "#!/bin/sh\necho \"rank $RANK of $WORLD_SIZE on GPUs $HIP_VISIBLE_DEVICES\"\nsleep %s\n"
+# --torch: every task also runs a bf16 matmul on each GPU it was given (real GPUs only)
+TORCH = ("%s -c \"import torch; n = torch.cuda.device_count(); "
+         "x = [torch.randn(4096, 4096, device=i, dtype=torch.bfloat16) for i in range(n)]; "
+         "print('devices', n, 'sum', sum(float((a @ a).float().abs().sum()) for a in x))\"\n"
+         % sys.executable)
 
 
 def _first_log(task, t0: float, timeout: float) -> float:
@@ -45,16 +50,19 @@ def _first_log(task, t0: float, timeout: float) -> float:
     raise TimeoutError("no log from %s" % task.get_identifier().long())
 
 
-def run(tasks: int = 4, gpus_per_task: int = 2, sleep: float = 1.0) -> dict:
+def run(tasks: int = 4, gpus_per_task: int = 2, sleep: float = 1.0,
+        torch_job: bool = False) -> dict:
     from terraform_provider_iterative_amd.parallel.placement import discover
 
     need = tasks * gpus_per_task
     physical = len(discover())
     saved = os.environ.get("TPI_MI355X_GPUS")
+    if torch_job and physical < need:
+        raise SystemExit("--torch needs %d GPUs, found %d" % (need, physical))
     if physical < need:
         os.environ["TPI_MI355X_GPUS"] = ",".join(str(i) for i in range(need))
     try:
-        return _run(tasks, gpus_per_task, sleep, need, physical)
+        return _run(tasks, gpus_per_task, sleep, need, physical, torch_job)
     finally:  # repeats must see the node again, not this run's logical slots
         if saved is None:
             os.environ.pop("TPI_MI355X_GPUS", None)
@@ -62,7 +70,8 @@ def run(tasks: int = 4, gpus_per_task: int = 2, sleep: float = 1.0) -> dict:
             os.environ["TPI_MI355X_GPUS"] = saved
 
 
-def _run(tasks: int, gpus_per_task: int, sleep: float, need: int, physical: int) -> dict:
+def _run(tasks: int, gpus_per_task: int, sleep: float, need: int, physical: int,
+         torch_job: bool) -> dict:
     from terraform_provider_iterative_amd import backends
     from terraform_provider_iterative_amd.models.cloud import (Cloud, Credentials,
                                                                NodeCredentials)
@@ -82,7 +91,8 @@ def _run(tasks: int, gpus_per_task: int, sleep: float, need: int, physical: int)
                                             variables=Variables({"TPI_TASK": "true"})))
         return backends.new(cloud, new_deterministic_identifier(name), spec)
 
-    group = [make("conc-%d-%d" % (os.getpid(), i), gpus_per_task, SCRIPT % sleep)
+    body = SCRIPT % sleep + (TORCH if torch_job else "")
+    group = [make("conc-%d-%d" % (os.getpid(), i), gpus_per_task, body)
              for i in range(tasks)]
     created = {}
     t0 = time.perf_counter()
@@ -111,14 +121,15 @@ def _run(tasks: int, gpus_per_task: int, sleep: float, need: int, physical: int)
     reuse_s = time.perf_counter() - t_done
     reused = sorted(again.gpus()) == list(range(need))
     again.wait(30.0)
+    devices = [_devices(t.logs()) for t in group] if torch_job else None
     t2 = time.perf_counter()
     for t in group + [again]:
         t.delete()
     delete_s = time.perf_counter() - t2
     shutil.rmtree(state, ignore_errors=True)
     return {
-        "config": "4 concurrent 2-GPU iterative_task resources on one node (placement + "
-                  "auto-cleanup)",
+        "config": "%d concurrent %d-GPU iterative_task resources on one node (placement + "
+                  "auto-cleanup)" % (tasks, gpus_per_task),
         "gpus": {"physical": physical, "slots": need,
                  "logical_slots": physical < need},
         "create_s": [round(created[i], 4) for i in range(tasks)],
@@ -129,7 +140,17 @@ def _run(tasks: int, gpus_per_task: int, sleep: float, need: int, physical: int)
         "task_sleep_s": sleep,
         "reuse_s": round(reuse_s, 4), "reused_all_gpus": reused,
         "delete_s": round(delete_s, 4),
+        "torch_job": torch_job,
+        "torch_devices": devices,
     }
+
+
+def _devices(logs) -> int:
+    for chunk in logs:
+        for line in chunk.splitlines():
+            if " devices " in " " + line.split("Z ", 1)[-1] + " ":
+                return int(line.split("devices", 1)[1].split()[0])
+    return 0
 
 
 def main() -> int:
@@ -138,14 +159,19 @@ def main() -> int:
     parser.add_argument("--gpus-per-task", type=int, default=2)
     parser.add_argument("--sleep", type=float, default=1.0)
     parser.add_argument("--repeats", type=int, default=3)
+    parser.add_argument("--torch", action="store_true",
+                        help="each task also runs a bf16 matmul on every GPU it was given")
     args = parser.parse_args()
-    runs = [run(args.tasks, args.gpus_per_task, args.sleep) for _ in range(args.repeats)]
+    runs = [run(args.tasks, args.gpus_per_task, args.sleep, args.torch)
+            for _ in range(args.repeats)]
     out = dict(runs[-1])
     out["repeats"] = len(runs)
     out["median_first_log_s"] = sorted(max(r["first_log_s"]) for r in runs)[len(runs) // 2]
     out["median_reuse_s"] = sorted(r["reuse_s"] for r in runs)[len(runs) // 2]
     out["ok"] = all(r["disjoint"] and r["fifth_refused"] and r["all_succeeded"]
-                    and r["reused_all_gpus"] for r in runs)
+                    and r["reused_all_gpus"] and (not r["torch_job"] or
+                                                  r["torch_devices"] == [args.gpus_per_task]
+                                                  * args.tasks) for r in runs)
     print(json.dumps(out))
     return 0 if out["ok"] else 1
 
