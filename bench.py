@@ -179,9 +179,15 @@ def main(argv=None):
     setup_s = time.perf_counter() - t_setup
     barrier()
 
-    for _ in range(args.warmup):
+    def progress(msg: str) -> None:  # stderr heartbeat: long (profiled) runs are not silent
+        if rank == 0:
+            print("bench: " + msg, file=sys.stderr, flush=True)
+
+    progress("setup %.1f s (%d bytes per rank)" % (setup_s, per_rank))
+    for i in range(args.warmup):
         ck.save({"warmup": True})
         ck.restore()
+        progress("warmup %d/%d" % (i + 1, args.warmup))
     barrier()
 
     save_s = restore_s = 0.0
@@ -197,6 +203,7 @@ def main(argv=None):
             raise SystemExit("bench: %d corrupt tiles after restore" % res.bad_tiles)
         save_s += b - a
         restore_s += c - b
+        progress("step %d/%d save %.3f s restore %.3f s" % (step + 1, args.steps, b - a, c - b))
     barrier()
     elapsed = time.perf_counter() - t0
 
