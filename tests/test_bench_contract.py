@@ -25,7 +25,8 @@ def _run(tmp_path, *extra):
     out = subprocess.run(cmd, cwd=str(tmp_path), capture_output=True, text=True, timeout=300,
                          env=env)
     assert out.returncode == 0, out.stderr[-3000:]
-    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert "bench: " not in out.stdout, out.stdout  # the heartbeat goes to stderr
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]  # (gloo prints too)
     assert len(lines) == 1, out.stdout
     return json.loads(lines[0])
 
