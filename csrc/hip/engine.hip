@@ -176,7 +176,11 @@ struct tpi_engine {
 extern "C" {
 
 const char* tpi_last_error(void) { return g_err.c_str(); }
-int tpi_version(void) { return 1; }
+#ifndef TPI_VERSION_STRING
+#define TPI_VERSION_STRING "0.0.0-dev"
+#endif
+int tpi_version(void) { return TPI_ABI_VERSION; }
+const char* tpi_version_string(void) { return TPI_VERSION_STRING; }
 
 int tpi_device_count(int* count) {
   HIP_OK(hipGetDeviceCount(count));
@@ -434,14 +438,19 @@ int tpi_restore(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, const
 }
 
 int tpi_sync(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* host_dst,
-             uint32_t* crcs_inout, int full, uint64_t wait_stream, uint64_t* dirty_tiles,
-             tpi_stats* stats) {
+             uint32_t* crcs_inout, uint64_t* dev_prev, int full, uint64_t wait_stream,
+             uint64_t* dirty_tiles, tpi_stats* stats) {
   Range range("tpi_sync");
   std::lock_guard<std::mutex> lk(e->mu);
   auto t0 = std::chrono::steady_clock::now();
+  // d_prev is overwritten with the new digests before the dirty tiles reach the host: until
+  // this call succeeds, the digests describe content the host may not have.
+  const bool was_valid = e->hash_valid;
+  e->hash_valid = false;
   if (prepare(e, segs, n, total)) return -1;
   const uint64_t tile = e->tile;
   const uint64_t ntiles = (total + tile - 1) / tile;
+  bool valid = was_valid;
   if (ntiles > e->hash_cap) {
     for (void* p : {(void*)e->d_hash, (void*)e->d_prev, (void*)e->d_idx})
       if (p) HIP_OK(hipFree(p));
@@ -449,11 +458,14 @@ int tpi_sync(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* ho
     HIP_OK(hipMalloc(&e->d_hash, e->hash_cap * sizeof(uint64_t)));
     HIP_OK(hipMalloc(&e->d_prev, e->hash_cap * sizeof(uint64_t)));
     HIP_OK(hipMalloc(&e->d_idx, e->hash_cap * sizeof(uint32_t)));
-    e->hash_valid = false;
+    valid = false;
   }
   if (!e->d_count) HIP_OK(hipMalloc(&e->d_count, sizeof(unsigned int)));
-  if (e->hash_ntiles != ntiles) e->hash_valid = false;
-  const int all = full || !e->hash_valid;
+  if (e->hash_ntiles != ntiles) valid = false;
+  // Caller-owned digests (one array per host slot, Checkpointer slots=2): the caller knows
+  // whether they describe the destination's content and says so with `full`.
+  uint64_t* prev = dev_prev ? dev_prev : e->d_prev;
+  const int all = full || (!dev_prev && !valid);
   if (wait_stream != TPI_NO_STREAM) {
     HIP_OK(hipEventRecord(e->ev_wait, (hipStream_t)wait_stream));
     HIP_OK(hipStreamWaitEvent(e->compute, e->ev_wait, 0));
@@ -462,7 +474,7 @@ int tpi_sync(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* ho
   HIP_OK(tpi_launch_stream_hash(e->d_segs, n, total, tile, TPI_SYNC_SEED, e->d_hash,
                                 e->compute));
   HIP_OK(hipMemsetAsync(e->d_count, 0, sizeof(unsigned int), e->compute));
-  HIP_OK(tpi_launch_dirty_tiles(e->d_hash, e->d_prev, ntiles, all, e->d_idx, e->d_count,
+  HIP_OK(tpi_launch_dirty_tiles(e->d_hash, prev, ntiles, all, e->d_idx, e->d_count,
                                 e->compute));
   unsigned int count = 0;
   HIP_OK(hipMemcpyAsync(&count, e->d_count, sizeof(count), hipMemcpyDeviceToHost, e->compute));
@@ -506,8 +518,10 @@ int tpi_sync(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* ho
                           hipMemcpyDeviceToHost, e->compute));
   HIP_OK(hipStreamSynchronize(e->copy));
   HIP_OK(hipStreamSynchronize(e->compute));
-  e->hash_valid = true;
-  e->hash_ntiles = ntiles;
+  if (!dev_prev) {
+    e->hash_valid = true;
+    e->hash_ntiles = ntiles;
+  }
   *dirty_tiles = count;
   if (stats) {
     stats->copy_ms =

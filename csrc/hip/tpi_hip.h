@@ -56,9 +56,13 @@ typedef struct tpi_stats {
   uint64_t chunks;
 } tpi_stats;
 
+// Bumped whenever a signature below changes (ops/_loader.py checks it).
+#define TPI_ABI_VERSION 2
+
 // Library / device
 const char* tpi_last_error(void);
-int tpi_version(void);
+int tpi_version(void);                 // TPI_ABI_VERSION
+const char* tpi_version_string(void);  // release version (_version.py)
 int tpi_device_count(int* count);
 int tpi_device_numa_node(int device, int* node);
 int tpi_device_pci_bus_id(int device, char* buf, int len);
@@ -114,9 +118,11 @@ int tpi_tpz_decode_device(const void* comp, const uint64_t* coff, uint64_t len, 
 // with the digests of the previous sync (kept in the engine), and pack + spill only the tiles
 // that changed into `host_dst` (stream offsets), updating their CRCs in `crcs_inout` (host,
 // full array).  `full` forces every tile (first sync).  *dirty_tiles receives the count.
+// `dev_prev` (device, ntiles u64, may be NULL = the engine's own): the digests the destination's
+// content was written with; updated in place.
 int tpi_sync(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* host_dst,
-             uint32_t* crcs_inout, int full, uint64_t wait_stream, uint64_t* dirty_tiles,
-             tpi_stats* stats);
+             uint32_t* crcs_inout, uint64_t* dev_prev, int full, uint64_t wait_stream,
+             uint64_t* dirty_tiles, tpi_stats* stats);
 // Digest of every tile (device output, ntiles u64); exposed for tests.
 int tpi_stream_hash(const tpi_seg* dev_segs, int n, uint64_t total, uint64_t tile_bytes,
                     uint64_t seed, uint64_t* dev_out, uint64_t stream);

@@ -26,6 +26,11 @@ const tpi_seg* seg_ptr(py::buffer& b, int& n) {
 PYBIND11_MODULE(_tpi_native, m) {
   m.doc() = "Host-side native runtime of the MI355X task orchestrator";
   m.attr("SEG_SIZE") = (int)sizeof(tpi_seg);
+#ifdef TPI_VERSION_STRING
+  m.attr("VERSION") = TPI_VERSION_STRING;
+#else
+  m.attr("VERSION") = "0.0.0-dev";
+#endif
 
   py::class_<tpi::Filter>(m, "Filter")
       .def(py::init<>())

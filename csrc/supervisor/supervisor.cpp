@@ -1061,7 +1061,15 @@ class Supervisor {
 
 }  // namespace
 
+#ifndef TPI_VERSION_STRING
+#define TPI_VERSION_STRING "0.0.0-dev"
+#endif
+
 int main(int argc, char** argv) {
+  if (argc >= 2 && std::string(argv[1]) == "--version") {
+    printf("tpi-supervisor %s\n", TPI_VERSION_STRING);
+    return 0;
+  }
   bool daemonize = argc >= 3 && std::string(argv[1]) == "--daemon";
   const char* spec_path = daemonize ? argv[2] : (argc >= 2 ? argv[1] : nullptr);
   if (!spec_path) {

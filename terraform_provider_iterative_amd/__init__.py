@@ -15,6 +15,6 @@ Layers (see docs/ARCHITECTURE.md):
   pinned-host checkpoint pipeline, HBM workdir staging, RCCL fan-out over xGMI
 """
 
-__version__ = "0.1.0"
+from ._version import __version__
 
 __all__ = ["__version__"]

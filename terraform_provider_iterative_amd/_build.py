@@ -2,16 +2,23 @@
 
 * ``_lib/_tpi_native*.so``  host C++ (pybind11): filters, walker/transfer, CRC32C, XXH64,
   CPU pack/unpack.
-* ``_lib/libtpi_hip.so``    HIP/CDNA4 kernels + checkpoint engine, ``--offload-arch=gfx950``,
-  linked against the libamdhip64 that ships with torch so one HIP runtime is loaded.
+* ``_lib/libtpi_hip.so``    HIP/CDNA4 kernels, checkpoint/staging engine and the RCCL task
+  communicator, ``--offload-arch=gfx950``, linked against the libamdhip64 that ships with
+  torch so one HIP runtime is loaded.
 * ``_lib/tpi-supervisor``   the on-node rank supervisor (C++ executable).
 
-Rebuilds are incremental on source mtimes.  ``python -m terraform_provider_iterative_amd._build``
-builds everything; ``__graft_entry__.build()`` calls :func:`build_all`.
+Nothing built is tracked by git.  A target is rebuilt when its ``.stamp`` (SHA-256 of the
+compile command and of every source/header it depends on) no longer matches -- content, not
+mtimes, so a fresh checkout (where every file has the checkout's mtime) always compiles from
+source.  ``python -m terraform_provider_iterative_amd._build`` builds everything;
+``__graft_entry__.build()`` calls :func:`build_all`.  The release version
+(``_version.py``, the reference's ``-X utils.Version``, ``Makefile:10``) is compiled into every
+native component as ``TPI_VERSION_STRING``.
 """
 from __future__ import annotations
 
 import glob
+import hashlib
 import os
 import shutil
 import subprocess
@@ -38,11 +45,36 @@ def _sources(*patterns: str) -> List[str]:
     return out
 
 
-def _stale(target: str, deps: Sequence[str]) -> bool:
+def version() -> str:
+    from ._version import __version__
+
+    return os.environ.get("TPI_VERSION", __version__)
+
+
+def _digest(cmd: Sequence[str], deps: Sequence[str]) -> str:
+    h = hashlib.sha256()
+    h.update("\0".join(c for c in cmd if ".tmp." not in c).encode())
+    for dep in sorted(set(deps)):
+        h.update(b"\0" + os.path.relpath(dep, ROOT).encode() + b"\0")
+        with open(dep, "rb") as handle:
+            h.update(handle.read())
+    return h.hexdigest()
+
+
+def _stale(target: str, cmd: Sequence[str], deps: Sequence[str]) -> bool:
+    """True unless ``target`` exists and its stamp matches the command + dependency content."""
     if not os.path.exists(target):
         return True
-    mtime = os.path.getmtime(target)
-    return any(os.path.getmtime(dep) > mtime for dep in deps)
+    try:
+        with open(target + ".stamp") as handle:
+            return handle.read().strip() != _digest(cmd, deps)
+    except OSError:
+        return True
+
+
+def _stamp(target: str, cmd: Sequence[str], deps: Sequence[str]) -> None:
+    with open(target + ".stamp", "w") as handle:
+        handle.write(_digest(cmd, deps) + "\n")
 
 
 def _run(cmd: List[str], verbose: bool) -> None:
@@ -58,20 +90,33 @@ def _atomic_output(target: str) -> str:
     return target + ".tmp.%d" % os.getpid()
 
 
+def _build(target: str, cmd: List[str], deps: Sequence[str], force: bool,
+           verbose: bool) -> str:
+    """Compile ``cmd`` (whose output is the placeholder ``@OUT@``) into ``target`` when stale."""
+    if not force and not _stale(target, cmd, deps):
+        return target
+    tmp = _atomic_output(target)
+    _run([tmp if c == "@OUT@" else c for c in cmd], verbose)
+    os.replace(tmp, target)
+    _stamp(target, cmd, deps)
+    return target
+
+
+def _define_version() -> str:
+    return '-DTPI_VERSION_STRING="%s"' % version()
+
+
 def build_native(force: bool = False, verbose: bool = False) -> str:
     srcs = _sources("native/*.cpp")
     deps = srcs + _sources("native/*.h", "common/*.h", "hip/tpi_hip.h")
-    if force or _stale(NATIVE_SO, deps):
-        import pybind11
+    import pybind11
 
-        tmp = _atomic_output(NATIVE_SO)
-        cxx = os.environ.get("CXX", "g++")
-        _run([cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-msse4.2", "-pthread",
-              "-fvisibility=hidden", "-Wall", "-Wno-unused-function",
-              "-I", pybind11.get_include(), "-I", sysconfig.get_paths()["include"],
-              *srcs, "-o", tmp], verbose)
-        os.replace(tmp, NATIVE_SO)
-    return NATIVE_SO
+    cxx = os.environ.get("CXX", "g++")
+    cmd = [cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-msse4.2", "-pthread",
+           "-fvisibility=hidden", "-Wall", "-Wno-unused-function", _define_version(),
+           "-I", pybind11.get_include(), "-I", sysconfig.get_paths()["include"],
+           *srcs, "-o", "@OUT@"]
+    return _build(NATIVE_SO, cmd, deps, force, verbose)
 
 
 def torch_lib_dir() -> str:
@@ -91,17 +136,14 @@ def hipcc() -> str:
 
 
 def build_hip(force: bool = False, verbose: bool = False) -> str:
-    srcs = _sources("hip/*.hip")
+    srcs = _sources("hip/*.hip", "hip/*.cpp")
     deps = srcs + _sources("hip/*.h", "common/*.h")
-    if force or _stale(HIP_SO, deps):
-        tl = torch_lib_dir()
-        tmp = _atomic_output(HIP_SO)
-        _run([hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
-              "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics",
-              *srcs, "-L" + tl, "-Wl,-rpath," + tl, "-L" + ROCM_LIB, "-Wl,-rpath," + ROCM_LIB,
-              "-lrocprofiler-sdk-roctx", "-o", tmp], verbose)
-        os.replace(tmp, HIP_SO)
-    return HIP_SO
+    tl = torch_lib_dir()
+    cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics", _define_version(),
+           *srcs, "-L" + tl, "-Wl,-rpath," + tl, "-L" + ROCM_LIB, "-Wl,-rpath," + ROCM_LIB,
+           "-lrocprofiler-sdk-roctx", "-o", "@OUT@"]
+    return _build(HIP_SO, cmd, deps, force, verbose)
 
 
 def build_supervisor(force: bool = False, verbose: bool = False) -> str:
@@ -109,12 +151,10 @@ def build_supervisor(force: bool = False, verbose: bool = False) -> str:
     if not srcs:
         return ""
     deps = srcs + _sources("supervisor/*.h")
-    if force or _stale(SUPERVISOR, deps):
-        tmp = _atomic_output(SUPERVISOR)
-        cxx = os.environ.get("CXX", "g++")
-        _run([cxx, "-O2", "-std=c++17", "-Wall", "-pthread", *srcs, "-o", tmp], verbose)
-        os.replace(tmp, SUPERVISOR)
-    return SUPERVISOR
+    cxx = os.environ.get("CXX", "g++")
+    cmd = [cxx, "-O2", "-std=c++17", "-Wall", "-pthread", _define_version(), *srcs,
+           "-o", "@OUT@"]
+    return _build(SUPERVISOR, cmd, deps, force, verbose)
 
 
 def build_all(force: bool = False, verbose: bool = False, hip: bool = True) -> List[str]:

@@ -323,8 +323,39 @@ class NodeTask(Task):
         log.info("Deletion completed")
 
     def _stop_quiet(self) -> None:
-        if os.path.isdir(self.root):
-            self.stop()
+        """Stop, and make sure nothing of the task still runs before its GPUs are handed to
+        another task and its directory is removed: ranks that outlive ``stop`` (a grace period
+        longer than the wait, a slow spill) are killed, process group by process group."""
+        if not os.path.isdir(self.root):
+            return
+        self.stop()
+        if self._alive_pids():
+            self._kill_remaining()
+
+    def _alive_pids(self) -> List[int]:
+        state = self._state()
+        pids = [int(state.get("pid", 0) or 0)]
+        pids += [int(r.get("pid", 0) or 0) for r in state.get("ranks") or []]
+        return [p for p in pids if p > 0 and pid_alive(p)]
+
+    def _kill_remaining(self, wait: float = 10.0) -> None:
+        state = self._state()
+        sup = int(state.get("pid", 0) or 0)
+        ranks = [int(r.get("pid", 0) or 0) for r in state.get("ranks") or []]
+        for pid in [p for p in ranks if p > 0] + ([sup] if sup > 0 else []):
+            for target in (-pid, pid):  # each rank leads its own process group
+                try:
+                    os.kill(target, signal.SIGKILL)
+                except (ProcessLookupError, PermissionError):
+                    pass
+        deadline = _now() + wait
+        while _now() < deadline and self._alive_pids():
+            time.sleep(0.02)
+        left = self._alive_pids()
+        if left:
+            raise RuntimeError("task %s: processes %s survive SIGKILL; not releasing its GPUs"
+                               % (self.id, left))
+        self._event("killed", "processes left after stop were killed")
 
     def _delete_storage(self) -> None:
         # With a pre-allocated container the data lives outside self.root and is kept
@@ -340,8 +371,8 @@ class NodeTask(Task):
         _write_json(spec_path, spec)
         # TPI_SUPERVISOR_BIN: an alternative build (e.g. the ASan/UBSan one of the tests)
         binary = os.environ.get("TPI_SUPERVISOR_BIN") or _build.SUPERVISOR
-        if binary == _build.SUPERVISOR and not os.path.exists(binary):
-            _build.build_supervisor()
+        if binary == _build.SUPERVISOR:
+            _build.build_supervisor()  # content-stamped: compiles only if the sources changed
         logfile = open(os.path.join(self.sup_dir, "supervisor.log"), "ab")
         try:
             proc = subprocess.Popen([binary, "--daemon", spec_path], stdin=subprocess.DEVNULL,

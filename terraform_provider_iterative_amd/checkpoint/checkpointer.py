@@ -18,9 +18,10 @@ Region layout (also the persisted file format)::
                    concatenated TPZ1 tile blobs (``ops.codec``)   (4 KiB aligned)
 
 The JSON header carries ``"complete": true`` only after a save finished, and is written last;
-``"codec"`` / ``"stream_bytes"`` say how the stream section is encoded and how long it is.
-The layout does not depend on the codec, so any reader bound to the same tensors loads
-either encoding.
+``"codec"`` / ``"stream_bytes"`` say how the stream section is encoded and how long it is;
+``"generation"`` orders the copies of a two-slot region (``Checkpointer(slots=2)``: two such
+layouts back to back, the newest complete one is the checkpoint).  The layout does not depend
+on the codec, so any reader bound to the same tensors loads either encoding.
 """
 from __future__ import annotations
 
@@ -32,7 +33,7 @@ import struct
 import threading
 import time
 from dataclasses import dataclass
-from typing import Any, Dict, Mapping, Optional, Sequence, Union
+from typing import Any, Dict, Mapping, Optional, Sequence, Tuple, Union
 
 import numpy as np
 
@@ -161,12 +162,13 @@ class DeviceEngine:
                               wire_bytes=int(wire.value))
 
     def sync(self, plan: PackPlan, host_addr: int, crcs: np.ndarray, full: bool,
-             wait_stream: int) -> TransferResult:
+             wait_stream: int, dev_prev: int = 0) -> TransferResult:
         st = _Stats()
         dirty = ctypes.c_uint64(0)
         t0 = time.perf_counter()
         rc = self.lib.tpi_sync(self.handle, plan.segs.ctypes.data, len(plan.entries), plan.total,
-                               ctypes.c_void_p(host_addr), crcs.ctypes.data, 1 if full else 0,
+                               ctypes.c_void_p(host_addr), crcs.ctypes.data,
+                               ctypes.c_void_p(dev_prev or None), 1 if full else 0,
                                wait_stream, ctypes.byref(dirty), ctypes.byref(st))
         self.lib.check(rc, "tpi_sync")
         res = TransferResult(int(st.bytes), time.perf_counter() - t0, int(st.chunks))
@@ -217,6 +219,19 @@ class PendingSave:
     wait = result
 
 
+class _Slot:
+    """One checkpoint copy inside the region: ``[preamble | header | entries | CRCs | blob
+    sizes | stream]`` at ``base`` (the persisted file format is exactly one slot)."""
+
+    def __init__(self, ck: "Checkpointer", index: int, base: int):
+        self.index = index
+        self.base = base
+        self.crcs = ck.region.array(base + ck.crc_offset, 4 * ck.plan.ntiles, np.uint32)
+        self.csizes = ck.region.array(base + ck.csize_offset, 4 * ck.plan.ntiles, np.uint32)
+        self.digests = None          # device u64 per tile: content of this slot (sync)
+        self.digests_valid = False   # ... describes what the slot holds right now
+
+
 class Checkpointer:
     """Save/restore a fixed set of tensors through one host region.
 
@@ -227,6 +242,14 @@ class Checkpointer:
     ``codec="tpz1"`` encodes every tile with the lossless byte-plane codec before it leaves
     the GPU (``csrc/hip/codec.hip``): the PCIe-bound spill then moves fewer bytes, which is
     what bounds save/restore throughput.  CRCs always cover the raw tiles.
+
+    ``slots=2`` keeps two copies (generation-numbered; a save always writes the older one and
+    the newer one stays valid until the new header lands), so a process killed in the middle
+    of a save -- past the grace period, OOM, a crash during a periodic :meth:`save_async`
+    spill -- still leaves the previous checkpoint to resume from, at twice the host memory.
+    With ``slots=1`` (default, the memory-lean choice for a preemption-only spill) a save
+    invalidates the one copy first: keep a persisted file (:meth:`persist`) if that gap
+    matters.
     """
 
     HEADER_RESERVE = 1 << 20  # room for metadata (e.g. host-side optimizer scalars)
@@ -234,7 +257,8 @@ class Checkpointer:
     def __init__(self, tensors: Union[Mapping[str, Any], Sequence[Any]],
                  path: Optional[str] = None, *, tile_bytes: int = 1 << 20,
                  chunk_bytes: int = 256 << 20, nbuf: int = 3, mode: str = "sdma",
-                 numa: bool = True, populate: bool = True, codec: str = "none"):
+                 numa: bool = True, populate: bool = True, codec: str = "none",
+                 slots: int = 1):
         self.plan = PackPlan.from_tensors(tensors, tile_bytes)
         self.path = path
         self.mode = MODES[mode]
@@ -242,14 +266,18 @@ class Checkpointer:
             raise ValueError("codec must be one of %s" % (CODECS,))
         if codec != "none" and self.mode != MODES["sdma"]:
             raise ValueError("the codec needs the staged (sdma) pipeline")
+        if slots not in (1, 2):
+            raise ValueError("slots must be 1 or 2")
         self.codec = codec
         # entries are serialised once; saves copy the bytes, restores compare the digest
         self._entries_blob = json.dumps([e.to_json() for e in self.plan.entries]).encode()
         self._entries_digest = hashlib.sha256(self._entries_blob).hexdigest()
         self.header_cap = self.HEADER_RESERVE
         (self.entries_offset, self.crc_offset, self.csize_offset, self.stream_offset,
-         self.size) = _layout(self.header_cap, len(self._entries_blob), self.plan.ntiles,
-                              self.plan.total, self.plan.tile_bytes)
+         slot_end) = _layout(self.header_cap, len(self._entries_blob), self.plan.ntiles,
+                             self.plan.total, self.plan.tile_bytes)
+        self.slot_bytes = align_up(slot_end, 4096)
+        self.size = self.slot_bytes * slots if slots > 1 else slot_end
         self.engine = None
         numa_node = -1
         if self.plan.on_device:
@@ -265,18 +293,54 @@ class Checkpointer:
         adopted = host.adopt(path, self.size) if path and self.plan.on_device else None
         self.region = adopted or HostRegion(self.size, path, device=self.plan.on_device,
                                             numa_node=numa_node, populate=populate)
-        self.crcs = self.region.array(self.crc_offset, 4 * self.plan.ntiles, np.uint32)
-        self.csizes = self.region.array(self.csize_offset, 4 * self.plan.ntiles, np.uint32)
+        self.slots = [_Slot(self, i, i * self.slot_bytes) for i in range(slots)]
         self.saves = 0
-        self._synced = False
         self._snap = self._snap_crcs = None  # HBM snapshot of save_async
         self._pending: Optional[PendingSave] = None
         self.last_save: Optional[TransferResult] = None
         self.last_restore: Optional[TransferResult] = None
 
+    # -- slots -------------------------------------------------------------------------------
+    def _slot_header(self, slot: _Slot) -> Optional[Dict]:
+        try:
+            header = self.read_header(self.region.array(slot.base, self.crc_offset))
+        except (CheckpointError, ValueError):
+            return None
+        return header if header.get("complete") else None
+
+    def _active(self) -> Optional[Tuple[_Slot, Dict]]:
+        """The complete slot with the newest generation, with its header."""
+        best = None
+        for slot in self.slots:
+            header = self._slot_header(slot)
+            if header is not None and (best is None or
+                                       header.get("generation", 0) > best[1].get("generation", 0)):
+                best = (slot, header)
+        return best
+
+    def _target(self) -> Tuple[_Slot, int]:
+        """(slot the next save writes, generation it gets): never the active one if there
+        are two slots."""
+        active = self._active()
+        generation = (active[1].get("generation", 0) + 1) if active else 1
+        if len(self.slots) == 1 or active is None:
+            return self.slots[0], generation
+        return self.slots[1 - active[0].index], generation
+
+    @property
+    def crcs(self) -> np.ndarray:
+        """Tile CRCs of the current checkpoint (or of slot 0 when there is none yet)."""
+        active = self._active()
+        return (active[0] if active else self.slots[0]).crcs
+
+    @property
+    def csizes(self) -> np.ndarray:
+        active = self._active()
+        return (active[0] if active else self.slots[0]).csizes
+
     # -- header ------------------------------------------------------------------------------
     def _header(self, complete: bool, crc: int, metadata: Optional[Dict], codec: str = "none",
-                stream_bytes: Optional[int] = None) -> Dict:
+                stream_bytes: Optional[int] = None, generation: int = 1) -> Dict:
         return {"format": 3, "complete": complete, "tile_bytes": self.plan.tile_bytes,
                 "total": self.plan.total, "ntiles": self.plan.ntiles,
                 "ntensors": len(self.plan.entries), "entries_sha256": self._entries_digest,
@@ -285,22 +349,23 @@ class Checkpointer:
                 "stream_offset": self.stream_offset, "codec": codec,
                 "stream_bytes": self.plan.total if stream_bytes is None else stream_bytes,
                 "crc32c": crc, "saved_at": time.time(), "saves": self.saves,
-                "metadata": metadata or {}}
+                "generation": generation, "metadata": metadata or {}}
 
-    def _write_header(self, header: Dict) -> None:
+    def _write_header(self, slot: _Slot, header: Dict) -> None:
         blob = json.dumps(header).encode()
         if len(blob) > self.header_cap:
             raise CheckpointError("checkpoint metadata too large (%d bytes)" % len(blob))
         n = len(self._entries_blob)
-        self.region.array(self.entries_offset, n)[:] = np.frombuffer(self._entries_blob,
-                                                                      np.uint8)
-        pre = self.region.array(0, PREAMBLE + len(blob))
+        self.region.array(slot.base + self.entries_offset, n)[:] = np.frombuffer(
+            self._entries_blob, np.uint8)
+        pre = self.region.array(slot.base, PREAMBLE + len(blob))
         pre[PREAMBLE:] = np.frombuffer(blob, np.uint8)
         pre[:PREAMBLE] = np.frombuffer(MAGIC + struct.pack("<QQQ", len(blob),
                                                            self.entries_offset, n), np.uint8)
 
-    def _invalidate(self) -> None:
-        self.region.array(0, 8)[:] = 0
+    def _invalidate(self, slot: _Slot) -> None:
+        self.region.array(slot.base, 8)[:] = 0
+        slot.digests_valid = False
 
     @staticmethod
     def read_header(buf: np.ndarray) -> Dict:
@@ -312,46 +377,54 @@ class Checkpointer:
 
     def entries(self) -> list:
         """Tensor entries recorded in the region (parsed on demand)."""
-        header = self.header()
-        raw = self.region.array(header["entries_offset"], header["entries_len"]).tobytes()
+        active = self._active()
+        base = active[0].base if active else 0
+        header = active[1] if active else self.header()
+        raw = self.region.array(base + header["entries_offset"], header["entries_len"]).tobytes()
         return json.loads(raw)
 
     def header(self) -> Dict:
+        """Header of the current checkpoint; raises :class:`CheckpointError` if none."""
+        active = self._active()
+        if active is not None:
+            return active[1]
         return self.read_header(self.region.array(0, self.crc_offset))
 
     # -- operations --------------------------------------------------------------------------
     def save(self, metadata: Optional[Dict] = None) -> TransferResult:
         """Pack every tensor into the region; returns bytes/seconds (GB/s via ``.gbps``)."""
         self.wait_pending()
-        self._invalidate()
+        slot, generation = self._target()
+        self._invalidate(slot)
         zipped = self.codec == "tpz1"
-        dst = self.region.addr + self.stream_offset
+        dst = self.region.addr + slot.base + self.stream_offset
         if self.engine is not None:
             import torch
 
             wait = torch.cuda.current_stream(self.device_index).cuda_stream
             if zipped:
-                res = self.engine.save_z(self.plan, dst, self.crcs, self.csizes, wait)
+                res = self.engine.save_z(self.plan, dst, slot.crcs, slot.csizes, wait)
             else:
-                res = self.engine.save(self.plan, dst, self.crcs, self.mode, wait)
+                res = self.engine.save(self.plan, dst, slot.crcs, self.mode, wait)
         else:
             t0 = time.perf_counter()
             if zipped:
                 raw, crcs = host_pack(self.plan)
                 blobs, sizes = tpz.encode(raw, self.plan.tile_bytes)
-                self.region.array(self.stream_offset, len(blobs))[:] = blobs
-                self.csizes[:] = sizes
+                self.region.array(slot.base + self.stream_offset, len(blobs))[:] = blobs
+                slot.csizes[:] = sizes
                 wire = len(blobs)
             else:
-                stream = self.region.array(self.stream_offset, self.plan.total)
+                stream = self.region.array(slot.base + self.stream_offset, self.plan.total)
                 _, crcs = host_pack(self.plan, stream)
                 wire = self.plan.total
-            self.crcs[:] = crcs
+            slot.crcs[:] = crcs
             res = TransferResult(self.plan.total, time.perf_counter() - t0, wire_bytes=wire)
-        res.crc = native().crc32c_combine_tiles_ptr(self.crcs.ctypes.data, self.plan.ntiles,
+        res.crc = native().crc32c_combine_tiles_ptr(slot.crcs.ctypes.data, self.plan.ntiles,
                                                      self.plan.tile_bytes, self.plan.total)
         self.saves += 1
-        self._write_header(self._header(True, res.crc, metadata, self.codec, res.wire_bytes))
+        self._write_header(slot, self._header(True, res.crc, metadata, self.codec,
+                                              res.wire_bytes, generation))
         self.last_save = res
         return res
 
@@ -364,6 +437,7 @@ class Checkpointer:
         host region (TPZ1-encoded when the checkpointer's codec is on) and writes the header;
         ``result()`` returns its :class:`TransferResult`.  The snapshot costs ``plan.total``
         bytes of HBM (allocated on first use).  Host tensors fall back to a synchronous save.
+        With ``slots=2`` the previous checkpoint stays valid for the whole spill.
         """
         self.wait_pending()
         if self.engine is None:
@@ -383,7 +457,8 @@ class Checkpointer:
             self._snap = torch.empty(self.plan.total, dtype=torch.uint8, device=dev)
             self._snap_crcs = torch.empty(self.plan.ntiles, dtype=torch.int32, device=dev)
         t0 = time.perf_counter()
-        self._invalidate()
+        slot, generation = self._target()
+        self._invalidate(slot)
         self.engine.snapshot(self.plan, self._snap.data_ptr(), self._snap_crcs.data_ptr(),
                              torch.cuda.current_stream(dev).cuda_stream)
         pending = PendingSave(time.perf_counter() - t0)
@@ -393,13 +468,15 @@ class Checkpointer:
         def spill():
             try:
                 res = self.engine.spill(self._snap.data_ptr(), self._snap_crcs.data_ptr(),
-                                        self.plan.total, self.region.addr + self.stream_offset,
-                                        self.crcs, self.csizes, zipped)
+                                        self.plan.total,
+                                        self.region.addr + slot.base + self.stream_offset,
+                                        slot.crcs, slot.csizes, zipped)
                 res.crc = native().crc32c_combine_tiles_ptr(
-                    self.crcs.ctypes.data, self.plan.ntiles, self.plan.tile_bytes,
+                    slot.crcs.ctypes.data, self.plan.ntiles, self.plan.tile_bytes,
                     self.plan.total)
-                self._write_header(self._header(True, res.crc, metadata,
-                                                "tpz1" if zipped else "none", res.wire_bytes))
+                self._write_header(slot, self._header(True, res.crc, metadata,
+                                                      "tpz1" if zipped else "none",
+                                                      res.wire_bytes, generation))
                 self.last_save = res
                 pending._result = res
             except BaseException as error:  # surfaced by result()
@@ -436,11 +513,13 @@ class Checkpointer:
             pending.result()
 
     def sync(self, metadata: Optional[Dict] = None) -> TransferResult:
-        """Incremental save: only tiles whose content changed since the previous ``sync`` are
-        packed and spilled (the device-side replacement of the reference's 10-second
-        newest-mtime poll + ``rclone sync``, machine-script.sh.tpl:118-124).
+        """Incremental save: only tiles whose content changed since the slot being written
+        was last synced are packed and spilled (the device-side replacement of the
+        reference's 10-second newest-mtime poll + ``rclone sync``, machine-script.sh.tpl:
+        118-124).
 
-        The first sync (and any sync after ``save``/``restore``) moves every tile.  Host
+        A slot's first sync -- and any sync after a full save, async save or load rewrote it
+        -- moves every tile; with ``slots=2`` every slot keeps its own tile digests.  Host
         tensors fall back to a full :meth:`save`.
         """
         if self.engine is None:
@@ -450,46 +529,53 @@ class Checkpointer:
         import torch
 
         self.wait_pending()
-        full = not self._synced
-        self._invalidate()
+        slot, generation = self._target()
+        full = not slot.digests_valid
+        self._invalidate(slot)
+        if slot.digests is None:
+            slot.digests = torch.zeros(self.plan.ntiles, dtype=torch.int64,
+                                       device=torch.device("cuda", self.device_index))
         wait = torch.cuda.current_stream(self.device_index).cuda_stream
-        res = self.engine.sync(self.plan, self.region.addr + self.stream_offset, self.crcs,
-                               full, wait)
-        res.crc = native().crc32c_combine_tiles_ptr(self.crcs.ctypes.data, self.plan.ntiles,
+        res = self.engine.sync(self.plan, self.region.addr + slot.base + self.stream_offset,
+                               slot.crcs, full, wait, slot.digests.data_ptr())
+        res.crc = native().crc32c_combine_tiles_ptr(slot.crcs.ctypes.data, self.plan.ntiles,
                                                      self.plan.tile_bytes, self.plan.total)
         self.saves += 1
-        self._synced = True
-        self._write_header(self._header(True, res.crc, metadata))
+        self._write_header(slot, self._header(True, res.crc, metadata, "none", None, generation))
+        slot.digests_valid = True
         self.last_save = res
         return res
 
     def restore(self, strict: bool = True) -> TransferResult:
-        """Unpack + verify the region into the bound tensors."""
+        """Unpack + verify the current checkpoint into the bound tensors."""
         self.wait_pending()
-        header = self.header()
-        if not header.get("complete"):
+        active = self._active()
+        if active is None:
+            header = self.header()  # raises "no checkpoint" unless an incomplete one is there
             raise CheckpointError("checkpoint incomplete (save was interrupted)")
+        slot, header = active
         self._check_compatible(header)
         zipped = header.get("codec", "none") == "tpz1"
-        src = self.region.addr + self.stream_offset
+        src = self.region.addr + slot.base + self.stream_offset
         if self.engine is not None:
             import torch
 
             sig = torch.cuda.current_stream(self.device_index).cuda_stream
             if zipped:
-                res = self.engine.restore_z(self.plan, src, self.crcs, self.csizes, sig)
+                res = self.engine.restore_z(self.plan, src, slot.crcs, slot.csizes, sig)
             else:
-                res = self.engine.restore(self.plan, src, self.crcs, self.mode, sig)
+                res = self.engine.restore(self.plan, src, slot.crcs, self.mode, sig)
         else:
             t0 = time.perf_counter()
             if zipped:
                 nbytes = int(header["stream_bytes"])
-                stream, _ = tpz.decode(self.region.array(self.stream_offset, nbytes),
-                                       self.csizes, self.plan.total, self.plan.tile_bytes)
+                stream, _ = tpz.decode(
+                    self.region.array(slot.base + self.stream_offset, nbytes),
+                    slot.csizes, self.plan.total, self.plan.tile_bytes)
             else:
                 nbytes = self.plan.total
-                stream = self.region.array(self.stream_offset, self.plan.total)
-            bad, first = host_unpack(self.plan, stream, self.crcs)
+                stream = self.region.array(slot.base + self.stream_offset, self.plan.total)
+            bad, first = host_unpack(self.plan, stream, slot.crcs)
             res = TransferResult(self.plan.total, time.perf_counter() - t0, 0, bad, first,
                                  wire_bytes=nbytes)
         res.crc = int(header.get("crc32c", 0))
@@ -507,13 +593,15 @@ class Checkpointer:
             raise CheckpointError("checkpoint layout does not match the bound tensors")
 
     def persist(self, path: str) -> str:
-        """Write the region (header, CRCs, stream) to ``path`` atomically."""
+        """Write the current checkpoint (header, CRCs, stream: one slot) to ``path``
+        atomically."""
         self.wait_pending()
-        header = self.header()
-        if not header.get("complete"):
+        active = self._active()
+        if active is None:
             raise CheckpointError("nothing saved yet")
+        slot, header = active
         tmp = path + ".tpi-partial"
-        data = self.region.array(0, self.stream_offset + int(header["stream_bytes"]))
+        data = self.region.array(slot.base, self.stream_offset + int(header["stream_bytes"]))
         with open(tmp, "wb") as f:
             f.write(memoryview(data))
             f.flush()
@@ -522,22 +610,32 @@ class Checkpointer:
         return path
 
     def load(self, path: str) -> TransferResult:
-        """Read a persisted checkpoint file into the region, then :meth:`restore`."""
+        """Read a persisted checkpoint file into the region (the slot a save would write, so
+        a bad file leaves the current checkpoint intact with ``slots=2``), then
+        :meth:`restore` it."""
         self.wait_pending()
+        slot, generation = self._target()
         with open(path, "rb") as f:
             head = np.frombuffer(f.read(PREAMBLE + self.header_cap), np.uint8)
             header = self.read_header(head)
             self._check_compatible(header)
-            f.seek(0)
+            if not header.get("complete"):
+                raise CheckpointError("%s holds an incomplete checkpoint" % path)
+            self._invalidate(slot)
+            f.seek(self.entries_offset)
             end = self.stream_offset + int(header["stream_bytes"])
-            dst = self.region.array(0, end)
+            dst = self.region.array(slot.base, end)
             view = memoryview(dst)
-            off = 0
+            off = self.entries_offset
             while off < end:
                 n = f.readinto(view[off:off + (64 << 20)])
                 if not n:
                     break
                 off += n
+        if off < end:
+            raise CheckpointError("%s is truncated (%d of %d bytes)" % (path, off, end))
+        header["generation"] = generation  # newest now; written last, like a save
+        self._write_header(slot, header)
         return self.restore()
 
     def close(self) -> None:
@@ -546,11 +644,13 @@ class Checkpointer:
         except CheckpointError:
             pass
         self._snap = self._snap_crcs = None
+        for slot in getattr(self, "slots", []):
+            slot.digests = None
         if self.engine is not None:
             self.engine.close()
             self.engine = None
         if self.region is not None:
-            self.crcs = None
+            self.slots = []
             self.region.close()
             self.region = None
 

@@ -193,18 +193,35 @@ def install(signals=(signal.SIGTERM,)) -> None:
 def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None) -> Optional[Dict]:
     """Restore from the host region (or ``persist_path``) if a complete checkpoint exists.
 
-    Returns the checkpoint metadata, or ``None`` for a fresh start.
+    Returns the checkpoint metadata, or ``None`` for a fresh start -- only when there is no
+    complete checkpoint anywhere.  A checkpoint that exists but fails verification (corrupt
+    tiles) has already been partly unpacked into the tensors, so it never turns into a fresh
+    start: the persisted copy is tried next, and if that fails too :class:`CheckpointError`
+    is raised.
     """
+    failure: Optional[CheckpointError] = None
     try:
         header = checkpointer.header()
-        if header.get("complete"):
+    except CheckpointError:  # no checkpoint in the region (bad magic)
+        header = None
+    if header is not None and header.get("complete"):
+        try:
             res = checkpointer.restore()
             journal("checkpoint-restored", "host region", *_describe(res))
             return header.get("metadata", {})
-    except CheckpointError:
-        pass
+        except CheckpointError as error:
+            failure = error
+            journal("checkpoint-corrupt", "host region", str(error))
     if persist_path and os.path.exists(persist_path):
-        res = checkpointer.load(persist_path)
+        try:
+            res = checkpointer.load(persist_path)
+        except CheckpointError as error:
+            journal("checkpoint-corrupt", persist_path, str(error))
+            raise CheckpointError("no usable checkpoint: host region: %s; %s: %s"
+                                  % (failure or "none", persist_path, error)) from error
         journal("checkpoint-restored", persist_path, *_describe(res))
         return checkpointer.header().get("metadata", {})
+    if failure is not None:
+        raise CheckpointError("checkpoint failed verification and no persisted copy exists: %s"
+                              % failure) from failure
     return None

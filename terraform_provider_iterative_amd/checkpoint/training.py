@@ -146,7 +146,22 @@ class TrainingState:
         dist.all_gather_object(seen, mine, group=group)
         if any(v is None for v in seen) or len(set(map(repr, seen))) != 1:
             return None  # disagreement: everybody starts fresh
-        return self.resume(persist_path)
+        # The headers agree, but a rank's data may still fail verification; then its tensors
+        # hold a partial unpack, so every rank aborts together rather than diverging.
+        error: Optional[BaseException] = None
+        try:
+            restored = self.resume(persist_path)
+        except Exception as exc:  # CheckpointError, I/O errors
+            error, restored = exc, None
+        ok = [None] * dist.get_world_size(group)
+        dist.all_gather_object(ok, error is None and restored is not None, group=group)
+        if not all(ok):
+            from .checkpointer import CheckpointError
+
+            bad = [r for r, v in enumerate(ok) if not v]
+            raise CheckpointError("ranks %s could not restore step %r: %s" % (
+                bad, mine, error or "restored on another rank only")) from error
+        return restored
 
     def install(self, persist_path: Optional[str] = None) -> None:
         """Checkpoint on SIGTERM (then exit 143 so the supervisor respawns the rank)."""

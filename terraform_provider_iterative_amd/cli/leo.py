@@ -21,6 +21,7 @@ import time
 from typing import Any, Dict, List, Optional
 
 from .. import backends
+from .._version import __version__
 from ..hcl import Configuration
 from ..models.cloud import Cloud, Credentials, NodeCredentials, Timeouts
 from ..models.values import (SPOT_DISABLED, SPOT_ENABLED, Environment, Firewall, FirewallRule,
@@ -95,6 +96,7 @@ def build_parser(defaults: Dict[str, Any]) -> argparse.ArgumentParser:
     root.add_argument("--region", default=d("region", "us-east"), help="cloud region")
     root.add_argument("--verbose", action="store_true", help="verbose output")
     root.add_argument("--state-root", default=None, help="node runtime state directory")
+    root.add_argument("--version", action="version", version="leo version " + __version__)
     sub = root.add_subparsers(dest="command", required=True)
 
     create = sub.add_parser("create", help="Create a task")

@@ -12,7 +12,7 @@ Semantics follow Terraform + the SDK: ForceNew attribute changes replace the res
 ``iterative_task``, resource_task.go:34), creation failures leave no state, ``-target``,
 ``-var``, ``-var-file``, ``TF_VAR_*``, ``-parallelism`` and ``count`` are supported.
 The real Terraform plugin protocol is served by ``terraform-provider-iterative`` (see
-``provider/plugin.py``) for sites that do have ``terraform``.
+``provider/server.py``) for sites that do have ``terraform``.
 """
 from __future__ import annotations
 
@@ -366,6 +366,7 @@ def build_parser() -> argparse.ArgumentParser:
     p = argparse.ArgumentParser(prog="tpi", description="Terraform-compatible engine for "
                                 "iterative_* resources on the MI355X node runtime")
     p.add_argument("-chdir", dest="chdir", default=None)
+    p.add_argument("-version", "--version", action="version", version=_version_text())
     sub = p.add_subparsers(dest="command", required=True)
 
     def common(sp, state=True, plan_opts=False):
@@ -396,7 +397,15 @@ def build_parser() -> argparse.ArgumentParser:
     sp = common(sub.add_parser("state"))
     sp.add_argument("subcommand", choices=("list", "show", "rm"))
     sp.add_argument("addresses", nargs="*")
+    sub.add_parser("version")
     return p
+
+
+def _version_text() -> str:
+    from .._version import __version__
+
+    return ("tpi v%s\non linux_amd64\n+ provider registry.terraform.io/iterative/iterative v%s"
+            % (__version__, __version__))
 
 
 def main(argv: Optional[List[str]] = None) -> int:
@@ -417,6 +426,9 @@ def main(argv: Optional[List[str]] = None) -> int:
 
 def _dispatch(args, verbose: bool) -> int:
     cmd = args.command
+    if cmd == "version":
+        print(_version_text())
+        return 0
     if cmd == "init":
         os.makedirs(".terraform", exist_ok=True)
         Configuration(".")

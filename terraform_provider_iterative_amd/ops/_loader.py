@@ -15,6 +15,8 @@ from typing import Optional
 
 from .. import _build
 
+ABI_VERSION = 2  # TPI_ABI_VERSION of csrc/hip/tpi_hip.h
+
 _lock = threading.Lock()
 _native = None
 _hip = None
@@ -31,7 +33,7 @@ def native():
         return _native
     with _lock:
         if _native is None:
-            if not os.path.exists(_build.NATIVE_SO) and _auto_build():
+            if _auto_build():  # content-stamped: a no-op unless the sources changed
                 _build.build_native()
             spec = importlib.util.spec_from_file_location("_tpi_native", _build.NATIVE_SO)
             if spec is None or spec.loader is None:
@@ -58,6 +60,7 @@ class HipLib:
         sig = {
             "tpi_last_error": (c.c_char_p, []),
             "tpi_version": (i32, []),
+            "tpi_version_string": (c.c_char_p, []),
             "tpi_device_count": (i32, [c.POINTER(i32)]),
             "tpi_device_numa_node": (i32, [i32, c.POINTER(i32)]),
             "tpi_device_pci_bus_id": (i32, [i32, c.c_char_p, i32]),
@@ -68,7 +71,7 @@ class HipLib:
             "tpi_save": (i32, [vp, vp, i32, u64, vp, vp, i32, u64, vp]),
             "tpi_restore": (i32, [vp, vp, i32, u64, vp, vp, i32, u64, c.POINTER(u64),
                                   c.POINTER(i64), vp]),
-            "tpi_sync": (i32, [vp, vp, i32, u64, vp, vp, i32, u64, c.POINTER(u64), vp]),
+            "tpi_sync": (i32, [vp, vp, i32, u64, vp, vp, vp, i32, u64, c.POINTER(u64), vp]),
             "tpi_save_z": (i32, [vp, vp, i32, u64, vp, vp, vp, u64, c.POINTER(u64), vp]),
             "tpi_restore_z": (i32, [vp, vp, i32, u64, vp, vp, vp, u64, c.POINTER(u64),
                                     c.POINTER(i64), vp]),
@@ -95,6 +98,11 @@ class HipLib:
             fn.restype = res
             fn.argtypes = args
         self.lib = lib
+        abi = lib.tpi_version()
+        if abi != ABI_VERSION:  # a stale build would be called with the wrong signatures
+            raise HipError("%s has ABI %d, this package needs %d (rebuild with "
+                           "__graft_entry__.build())" % (path, abi, ABI_VERSION))
+        self.version = lib.tpi_version_string().decode()
 
     def error(self) -> str:
         return (self.lib.tpi_last_error() or b"").decode(errors="replace")
@@ -126,7 +134,7 @@ def hip(required: bool = True) -> Optional[HipLib]:
             import torch  # noqa: F401  (maps torch's HIP runtime first)
 
             try:
-                if not os.path.exists(_build.HIP_SO) and _auto_build():
+                if _auto_build():
                     _build.build_hip()
                 _hip = HipLib(_build.HIP_SO)
             except Exception as error:

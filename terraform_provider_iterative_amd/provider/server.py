@@ -421,6 +421,11 @@ def _der_b64(cert_pem: bytes) -> str:
 def serve(environ=None, out=None) -> int:
     environ = os.environ if environ is None else environ
     out = out or sys.stdout
+    if "--version" in sys.argv[1:]:
+        from .._version import __version__
+
+        out.write("terraform-provider-iterative v%s\n" % __version__)
+        return 0
     if environ.get(MAGIC_COOKIE_KEY) != MAGIC_COOKIE_VALUE:
         sys.stderr.write("This binary is a plugin. These are not meant to be executed directly.\n"
                          "Please execute the program that consumes these plugins, which will\n"

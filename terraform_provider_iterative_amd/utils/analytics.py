@@ -17,9 +17,10 @@ import re
 import threading
 from typing import Any, Dict, List, Optional
 
+from .._version import __version__ as VERSION
+
 log = logging.getLogger("tpi.analytics")
 
-VERSION = "0.0.0"
 TIMEOUT = 5.0
 _pending: List[threading.Thread] = []
 

@@ -3,7 +3,7 @@
 Reference: ``task/common/identifier.go:16-115`` (format ``tpi-{name}-{salt8}-{check8}``,
 ``hash(seed, n)`` = first ``n`` base36 digits of the SHA-256 digest read as a big-endian
 integer, name normalised to ``[a-z0-9-]`` and truncated to 28 characters).  The golden
-vectors of ``identifier_test.go:41-74`` are pinned in ``tests/test_identifier.py``.
+vectors of ``identifier_test.go:41-74`` are pinned in ``tests/test_common.py``.
 """
 from __future__ import annotations
 

@@ -113,3 +113,70 @@ def test_save_async_on_host_falls_back_to_sync():
         ck.restore()
     for k in ref:
         assert torch.equal(src[k], ref[k]), k
+
+
+def test_two_slots_keep_the_previous_checkpoint_through_a_failed_save(monkeypatch):
+    from terraform_provider_iterative_amd.checkpoint import checkpointer as mod
+
+    src = _model(6)
+    with Checkpointer(src, tile_bytes=4096, slots=2) as ck:
+        assert ck.size == 2 * ck.slot_bytes
+        ck.save({"step": 1})
+        first = ck._active()[0].index
+        for v in src.values():
+            v.add_(1)
+        want = {k: v.clone() for k, v in src.items()}
+        ck.save({"step": 2})
+        assert ck._active()[0].index != first and ck.header()["generation"] == 2
+
+        def killed(*args, **kwargs):  # the process dies in the middle of the next save
+            raise RuntimeError("killed mid-save")
+
+        monkeypatch.setattr(mod, "host_pack", killed)
+        for v in src.values():
+            v.add_(1)
+        with pytest.raises(RuntimeError):
+            ck.save({"step": 3})
+        monkeypatch.undo()
+        assert ck.header()["metadata"] == {"step": 2}  # still the newest complete copy
+        ck.restore()
+        for k in want:
+            assert torch.equal(src[k], want[k]), k
+        ck.save({"step": 3})  # the interrupted slot is reused
+        assert ck.header()["generation"] == 3
+
+
+def test_single_slot_save_invalidates_first():
+    src = _model(7)
+    with Checkpointer(src, tile_bytes=4096) as ck:
+        ck.save({"step": 1})
+        ck._invalidate(ck._target()[0])  # what a save does before writing
+        with pytest.raises(CheckpointError):
+            ck.restore()
+
+
+def test_resume_refuses_a_corrupt_region_instead_of_starting_fresh(tmp_path):
+    from terraform_provider_iterative_amd.checkpoint import preemption
+
+    path = str(tmp_path / "spill")
+    src = _model(8)
+    ref = {k: v.clone() for k, v in src.items()}
+    with Checkpointer(src, path=path, tile_bytes=4096) as ck:
+        ck.save({"step": 5})
+        good = ck.persist(str(tmp_path / "good.tpi"))
+        ck.region.array(ck.slots[0].base + ck.stream_offset + 100, 1)[0] ^= 0x5A
+    for v in src.values():
+        v.zero_()
+    with Checkpointer(src, path=path, tile_bytes=4096) as ck:
+        with pytest.raises(CheckpointError, match="verification"):
+            preemption.resume(ck)  # no persisted copy: an error, never a fresh start
+        meta = preemption.resume(ck, persist_path=good)  # falls back to the persisted copy
+        assert meta == {"step": 5}
+    for k in ref:
+        assert torch.equal(src[k], ref[k]), k
+    os.remove(good)
+    with open(path, "r+b") as f:  # make the region unreadable too: both copies bad
+        f.seek(0)
+        f.write(b"\0" * 8)
+    with Checkpointer(src, path=path, tile_bytes=4096) as ck:
+        assert preemption.resume(ck) is None  # truly nothing saved: fresh start

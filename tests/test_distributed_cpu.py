@@ -110,3 +110,36 @@ def test_resume_consistent_all_or_nothing(tmp_path, steps, agree):
             assert step == 5 and weight > 0  # restored
         else:
             assert step is None and weight == 0  # fresh start everywhere
+
+
+def _corrupt_worker(rank, world, port, root, results):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from terraform_provider_iterative_amd.checkpoint import CheckpointError, TrainingState
+
+        torch.manual_seed(rank)
+        model = torch.nn.Linear(64, 64)
+        opt = torch.optim.SGD(model.parameters(), lr=0.1)
+        with TrainingState(model, opt, path=os.path.join(root, "rank%d" % rank),
+                           tile_bytes=4096) as state:
+            state.save({"step": 7})
+            ck = state.checkpointer
+            if rank == 1:  # this rank's spill got corrupted: every rank must abort together
+                ck.region.array(ck.slots[0].base + ck.stream_offset + 10, 1)[0] ^= 0xFF
+            try:
+                state.resume_consistent()
+                results[rank] = "resumed"
+            except CheckpointError as error:
+                results[rank] = "aborted: %s" % error
+    finally:
+        dist.destroy_process_group()
+
+
+def test_resume_consistent_aborts_every_rank_when_one_restore_fails(tmp_path):
+    manager = mp.Manager()
+    results = manager.dict()
+    mp.spawn(_corrupt_worker, args=(3, _free_port(), str(tmp_path), results), nprocs=3)
+    assert sorted(results) == [0, 1, 2]
+    for rank in range(3):
+        assert results[rank].startswith("aborted") and "[1]" in results[rank], results[rank]
