@@ -125,13 +125,16 @@ def test_incremental_sync_moves_only_dirty_tiles():
         # strided tensor change is detected too
         src["sliced"][0, 0, 0] = 42.0
         assert ck.sync().dirty_tiles == 1
-        # restore round trip after syncs, then a save invalidates digests -> next sync full
+        # restore round trip after syncs: the slot still holds what the tensors now hold, so
+        # the next sync moves nothing; a full save rewrites the slot -> the sync after is full
         ref = {k: v.clone() for k, v in src.items()}
         for v in src.values():
             v.zero_()
         ck.restore()
         torch.cuda.synchronize()
         assert all(torch.equal(src[k], ref[k]) for k in ref)
+        assert ck.sync().dirty_tiles == 0
+        ck.save()
         assert ck.sync().dirty_tiles == ck.plan.ntiles
 
 
