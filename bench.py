@@ -105,20 +105,80 @@ def synthetic_checkpoint(nbytes: int, hidden: int, device, fill: bool = True):
     return tensors
 
 
-def first_log_latency(timeout: float = 60.0):
+def first_log_latency(timeout: float = 60.0, parallelism: int = 1):
     try:
         from terraform_provider_iterative_amd.bench_latency import measure_first_log_latency
     except ImportError:
         return None
     try:
-        return measure_first_log_latency(timeout=timeout)
+        return measure_first_log_latency(timeout=timeout, parallelism=parallelism)
     except Exception as error:  # the headline must not die on the latency probe
         print("bench: first-log latency probe failed: %s" % error, file=sys.stderr)
         return None
 
 
+def launch_ranks(args, argv) -> int:
+    """``--gpus N`` without a launcher around us: start the N ranks ourselves (one process
+    per GPU, the same env contract as ``torch.distributed.run``), before anything here touches
+    the GPU, and exit with the first failing rank's code.  Only rank 0 prints the JSON line."""
+    import signal
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    argv = list(sys.argv[1:] if argv is None else argv)
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+                                      env=env, stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    print("bench: rank %d exited with %d; stopping the others"
+                          % (procs.index(p), code), file=sys.stderr)
+                    for q in live:
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.05)
+    except KeyboardInterrupt:
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        rc = 130
+    return rc
+
+
+def host_memory_check(per_rank: int, local_world: int) -> None:
+    """Each rank keeps its checkpoint region in (NUMA-local, pinned) host DRAM: refuse to
+    start when the node cannot hold all of them rather than letting the OOM killer pick."""
+    try:
+        with open("/proc/meminfo") as f:
+            info = {l.split(":")[0]: int(l.split()[1]) * 1024 for l in f if ":" in l}
+    except (OSError, ValueError, IndexError):
+        return
+    avail = info.get("MemAvailable")
+    need = int(per_rank * 1.02) * local_world  # region = stream + headers + codec bound
+    if avail is not None and need > avail:
+        raise SystemExit("bench: %d ranks x %.1f GB host regions need %.1f GB, only %.1f GB "
+                         "available" % (local_world, per_rank / 1e9, need / 1e9, avail / 1e9))
+
+
 def main(argv=None):
     args = parse_args(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        raise SystemExit(launch_ranks(args, argv))
     import torch
     import torch.distributed as dist
 
@@ -126,19 +186,32 @@ def main(argv=None):
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        print("bench: WORLD_SIZE=%d but --gpus=%d" % (world, args.gpus), file=sys.stderr)
+        raise SystemExit("bench: WORLD_SIZE=%d but --gpus=%d: the launcher and the flags "
+                         "disagree" % (world, args.gpus))
     on_gpu = args.device == "cuda"
     if on_gpu and not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (MI355X)")
     # TPI_BENCH_BACKEND=gloo rehearses the multi-rank flow on a box with fewer GPUs than ranks
     # (ranks then share devices); the real runs use RCCL ("nccl"), one rank per GPU.
     backend = os.environ.get("TPI_BENCH_BACKEND", "nccl") if on_gpu else "gloo"
+    pinned_cpus = None
     if on_gpu:
-        index = local_rank % torch.cuda.device_count()
+        ndev = torch.cuda.device_count()
+        if backend == "nccl" and world > ndev:
+            raise SystemExit("bench: %d ranks but %d visible GPUs (RCCL needs one GPU per rank)"
+                             % (world, ndev))
+        index = local_rank % ndev
         torch.cuda.set_device(index)
         device = torch.device("cuda", index)
+        # host side of the rank (pinned region first touch, CRC combine, codec bookkeeping)
+        # on the cores of the GPU's own socket
+        from terraform_provider_iterative_amd.parallel.placement import pin_to_device_numa
+
+        pinned_cpus = pin_to_device_numa(index)
     else:
         device = torch.device("cpu")
+    host_memory_check(int(args.total_gb * 1e9 / world),
+                      int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
 
     def sync():
         if on_gpu:
@@ -165,7 +238,8 @@ def main(argv=None):
 
     latency = None
     if rank == 0 and not args.no_latency:
-        latency = first_log_latency()
+        # an iterative_task with parallelism = N (one GPU per rank), like the job measured
+        latency = first_log_latency(parallelism=world)
 
     from terraform_provider_iterative_amd.checkpoint import Checkpointer
 
@@ -263,6 +337,8 @@ def main(argv=None):
             "first_log_latency_s": (latency or {}).get("cli_s"),
             "first_log_latency": latency,
             "workdir_broadcast": None,
+            "raw_GBps": None,
+            "rank0_cpu_affinity": len(pinned_cpus) if pinned_cpus else None,
             "restore_verified": verified,
             "save_async": None,
             "setup_s": round(setup_s, 2),
@@ -275,7 +351,7 @@ def main(argv=None):
     def emit(note=None):
         if out is not None and printed.acquire(blocking=False):  # exactly one line
             if note:
-                for key in ("save_async", "workdir_broadcast"):
+                for key in ("save_async", "raw_GBps", "workdir_broadcast"):
                     if out[key] is None:
                         out[key] = {"error": note}
             print(json.dumps(out), flush=True)
@@ -314,6 +390,31 @@ def main(argv=None):
         async_stall = ({"error": err or "failed on another rank"} if failed else
                        {"stall_ms": round(stall * 1e3, 2), "spill_s": round(spill, 3)})
 
+    raw = None
+    if args.codec != "none":  # untimed: the same checkpoint through the codec-free pipeline
+        err, rs, rr = None, 0.0, 0.0
+        ck.codec = "none"
+        try:
+            barrier()
+            a = time.perf_counter()
+            ck.save({"raw": True})
+            sync()
+            rs = time.perf_counter() - a
+            a = time.perf_counter()
+            ck.restore()
+            sync()
+            rr = time.perf_counter() - a
+        except Exception as error:
+            err = repr(error)
+        finally:
+            ck.codec = args.codec
+        failed = allmax(1.0 if err else 0.0)
+        rs, rr = allmax(rs), allmax(rr)
+        raw = ({"error": err or "failed on another rank"} if failed else
+               {"GBps": round(2 * total / (rs + rr) / 1e9, 3),
+                "save_GBps": round(total / rs / 1e9, 3),
+                "restore_GBps": round(total / rr / 1e9, 3)})
+
     broadcast = None
     if world > 1 and args.broadcast_gb > 0 and on_gpu:  # config 3: workdir fan-out over xGMI (untimed)
         try:
@@ -332,6 +433,7 @@ def main(argv=None):
     watchdog.cancel()
     if out is not None:
         out["save_async"] = async_stall
+        out["raw_GBps"] = raw
         out["workdir_broadcast"] = broadcast
     emit()
     ck.close()

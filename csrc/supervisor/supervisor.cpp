@@ -40,6 +40,7 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <poll.h>
+#include <sched.h>
 #include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -193,6 +194,7 @@ struct Spec {
   int parallelism = 1;
   std::vector<std::string> rank_gpus;        // HIP_VISIBLE_DEVICES (the task's GPU set)
   std::vector<std::string> rank_local_gpus;  // the rank's own GPUs, task-visible numbering
+  std::vector<std::vector<int>> rank_cpus;   // NUMA-local cores of the rank's GPUs (affinity)
   std::string master_addr = "127.0.0.1";
   int master_port = 29500;
   bool gang = true, fail_fast = true, respawn_on_sigterm = true, login_shell = false;
@@ -217,9 +219,13 @@ Spec load_spec(const std::string& path) {
   for (auto& r : v["ranks"].a) {
     s.rank_gpus.push_back(r["gpus"].str());
     s.rank_local_gpus.push_back(r["rank_gpus"].str());
+    std::vector<int> cpus;
+    for (auto& c : r["cpus"].a) cpus.push_back((int)c.num(-1));
+    s.rank_cpus.push_back(cpus);
   }
   s.rank_gpus.resize(s.parallelism);
   s.rank_local_gpus.resize(s.parallelism);
+  s.rank_cpus.resize(s.parallelism);
   s.master_addr = v["master_addr"].str("127.0.0.1");
   s.master_port = (int)v["master_port"].num(29500);
   s.gang = v["gang"].boolean(true);
@@ -520,6 +526,15 @@ class Supervisor {
       const int gt = go[0] >= 0 ? fcntl(go[0], F_DUPFD_CLOEXEC, 10) : -1;
       if (nt >= 0) dup2(nt, 3);
       if (gt >= 0) dup2(gt, 4);
+      // the rank's host work (pinned spills, page-cache reads, CRC combine) stays on the
+      // socket of its GPUs; best effort: a cpuset that excludes those cores keeps its own mask
+      if (!s_.rank_cpus[r.index].empty()) {
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        for (int c : s_.rank_cpus[r.index])
+          if (c >= 0 && c < CPU_SETSIZE) CPU_SET(c, &set);
+        (void)sched_setaffinity(0, sizeof(set), &set);
+      }
       if (chdir(s_.workdir.c_str())) {
         dprintf(2, "tpi-supervisor: chdir %s: %s\n", s_.workdir.c_str(), strerror(errno));
         _exit(126);

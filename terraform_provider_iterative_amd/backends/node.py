@@ -29,7 +29,7 @@ from ..models.cloud import PROVIDER_LOCAL, PROVIDER_MI355X, Cloud, parse_region_
 from ..models.machine_types import MachineType, parse_node_machine
 from ..models.values import (STATUS_RUNNING, Event, NotFoundError, NotImplementedErr,
                              RemoteStorage, Task as TaskSpec, new_status)
-from ..parallel.placement import Placement, PlacementError, pid_alive
+from ..parallel.placement import Placement, PlacementError, numa_cpus, pid_alive
 from ..storage import transfer as storage
 from ..utils.identifier import Identifier, parse_identifier
 from ..utils.steps import Step, StepTiming, run_steps
@@ -255,10 +255,15 @@ class NodeTask(Task):
             "RCLONE_REMOTE": str(storage.Connection("local", self.root)),
         })
         visible = ",".join(str(g) for g in gpus)
+        numa = [g.get("numa_node", -1) for g in d.get("gpu_info") or []]
         ranks = []
         for r in range(parallelism):
             mine = list(range(r * per, (r + 1) * per)) if per else []
-            ranks.append({"gpus": visible, "rank_gpus": ",".join(str(i) for i in mine)})
+            # affinity: the cores of the socket the rank's first GPU hangs off
+            node = numa[mine[0]] if mine and mine[0] < len(numa) else -1
+            cpus = numa_cpus(node) if os.environ.get("TPI_NUMA_PIN", "1") != "0" else []
+            ranks.append({"gpus": visible, "rank_gpus": ",".join(str(i) for i in mine),
+                          "cpus": cpus})
         if gpus:
             env["TPI_VISIBLE_GPUS"] = visible
         script_path = os.path.join(self.sup_dir, "script")

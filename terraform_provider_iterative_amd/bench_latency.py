@@ -28,6 +28,7 @@ resource "iterative_task" "latency" {
   name    = "latency-%(tag)s"
   cloud   = "%(cloud)s"
   machine = "%(machine)s"
+  parallelism = %(parallelism)d
   storage {
     workdir = "."
   }
@@ -39,16 +40,20 @@ resource "iterative_task" "latency" {
 '''
 
 
-def _first_log(state_root: str, timeout: float, t0: float, poll: float = 0.0005) -> Optional[float]:
+def _first_log(state_root: str, timeout: float, t0: float, poll: float = 0.0005,
+               count: int = 1) -> Optional[float]:
+    """Seconds from ``t0`` until ``count`` ranks' logs (``reports/task-*``) hold a line."""
     pattern = os.path.join(state_root, "*", "*", "reports", "task-*")
     deadline = t0 + timeout
     while time.perf_counter() < deadline:
+        seen = 0
         for path in glob.glob(pattern):
             try:
-                if os.path.getsize(path) > 0:
-                    return time.perf_counter() - t0
+                seen += os.path.getsize(path) > 0
             except OSError:
                 pass
+        if seen >= count:
+            return time.perf_counter() - t0
         time.sleep(poll)
     return None
 
@@ -59,8 +64,10 @@ def _cleanup(workdir: str, env: Dict[str, str]) -> None:
 
 
 def measure_first_log_latency(timeout: float = 60.0, cloud: Optional[str] = None,
-                              repeats: int = 3) -> Dict[str, float]:
-    """Returns ``{"cli_s": .., "api_s": .., "cloud": ..}`` (medians over ``repeats``)."""
+                              repeats: int = 3, parallelism: int = 1) -> Dict[str, float]:
+    """Returns ``{"cli_s": .., "api_s": .., "cloud": ..}`` (medians over ``repeats``): the
+    first log line of any rank; with ``parallelism`` N > 1 also ``cli_all_s`` / ``api_all_s``,
+    until every one of the N ranks (one GPU each on ``mi355x``) has logged."""
     gpu = False
     try:
         import torch
@@ -70,7 +77,7 @@ def measure_first_log_latency(timeout: float = 60.0, cloud: Optional[str] = None
         pass
     cloud = cloud or ("mi355x" if gpu else "local")
     machine = "m+mi355x" if cloud == "mi355x" else "s"
-    cli, api = [], []
+    cli, api, cli_all, api_all = [], [], [], []
     for i in range(repeats):
         base = tempfile.mkdtemp(prefix="tpi-latency-")
         try:
@@ -87,9 +94,12 @@ def measure_first_log_latency(timeout: float = 60.0, cloud: Optional[str] = None
                                      "-auto-approve"], cwd=work, env=env,
                                     stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
             latency = _first_log(env["TPI_STATE_ROOT"], timeout, t0)
+            every = _first_log(env["TPI_STATE_ROOT"], timeout, t0, count=parallelism)
             proc.wait(timeout=timeout)
             if latency is not None:
                 cli.append(latency)
+            if every is not None:
+                cli_all.append(every)
             _cleanup(work, env)
             # in-process API path
             from .provider import resources
@@ -103,12 +113,16 @@ def measure_first_log_latency(timeout: float = 60.0, cloud: Optional[str] = None
                 data = normalize("iterative_task", {
                     "name": "latency-api-%d%d" % (os.getpid(), i), "cloud": cloud,
                     "machine": machine, "storage": [{"workdir": "."}],
+                    "parallelism": parallelism,
                     "script": "#!/bin/sh\necho first log line\n"})
                 t1 = time.perf_counter()
                 result = resources.task_create(data)
                 lat = _first_log(os.environ["TPI_STATE_ROOT"], timeout, t1)
+                every = _first_log(os.environ["TPI_STATE_ROOT"], timeout, t1, count=parallelism)
                 if lat is not None:
                     api.append(lat)
+                if every is not None:
+                    api_all.append(every)
                 if result.id:
                     data["id"] = result.id
                     resources.task_delete(data)
@@ -125,7 +139,11 @@ def measure_first_log_latency(timeout: float = 60.0, cloud: Optional[str] = None
         xs = sorted(xs)
         return round(xs[len(xs) // 2], 4) if xs else None
 
-    return {"cli_s": median(cli), "api_s": median(api), "cloud": cloud, "samples": len(cli)}
+    out = {"cli_s": median(cli), "api_s": median(api), "cloud": cloud, "samples": len(cli),
+           "parallelism": parallelism}
+    if parallelism > 1:
+        out.update(cli_all_s=median(cli_all), api_all_s=median(api_all))
+    return out
 
 
 if __name__ == "__main__":

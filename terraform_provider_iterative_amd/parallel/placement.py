@@ -247,6 +247,41 @@ class Placement:
             return n
 
 
+def numa_cpus(node: int) -> List[int]:
+    """CPU cores of NUMA node ``node`` (empty when unknown)."""
+    if node is None or node < 0:
+        return []
+    return _cpulist(_read("/sys/devices/system/node/node%d/cpulist" % node))
+
+
+def pin_to_numa(node: int) -> Optional[List[int]]:
+    """Restrict this process to the cores of NUMA node ``node`` that it may already use
+    (``TPI_NUMA_PIN=0`` disables).  Returns the new affinity, or None if nothing changed."""
+    if os.environ.get("TPI_NUMA_PIN", "1") == "0" or not hasattr(os, "sched_setaffinity"):
+        return None
+    cpus = set(numa_cpus(node)) & set(os.sched_getaffinity(0))
+    if not cpus:
+        return None
+    os.sched_setaffinity(0, cpus)
+    return sorted(cpus)
+
+
+def pin_to_device_numa(device_index: int) -> Optional[List[int]]:
+    """:func:`pin_to_numa` for the socket of HIP device ``device_index`` (resolved through
+    its PCI bus id, so it agrees with HIP's numbering under any visible-device mask)."""
+    import ctypes
+
+    from ..ops import hip
+
+    lib = hip(required=False)
+    if lib is None:
+        return None
+    node = ctypes.c_int(-1)
+    if lib.tpi_device_numa_node(device_index, ctypes.byref(node)) != 0:
+        return None
+    return pin_to_numa(node.value)
+
+
 def _pid_alive(pid: int) -> bool:
     try:
         os.kill(pid, 0)

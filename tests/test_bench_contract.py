@@ -52,3 +52,32 @@ def test_side_measurement_watchdog_keeps_the_headline(tmp_path):
     d = _run(tmp_path, "--side-timeout", "0.001")
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["restore_verified"] is True
     assert d["save_async"] is None or "error" in d["save_async"] or "stall_ms" in d["save_async"]
+
+
+def test_bench_launches_its_own_ranks_without_torchrun(tmp_path):
+    # `python bench.py --gpus N` with no launcher around it starts the N ranks itself
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--device", "cpu",
+           "--total-gb", "0.012", "--steps", "1", "--warmup", "1", "--no-latency",
+           "--hidden", "256"]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "2"
+    out = subprocess.run(cmd, cwd=str(tmp_path), capture_output=True, text=True, timeout=300,
+                         env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 3 and d["config"]["parallelism"] == "shard3"
+    assert d["restore_verified"] is True
+    assert "GBps" in d["raw_GBps"]
+
+
+def test_bench_refuses_a_world_that_disagrees_with_gpus(tmp_path):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
+           "--total-gb", "0.01", "--no-latency"]
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run(cmd, cwd=str(tmp_path), capture_output=True, text=True, timeout=120,
+                         env=env)
+    assert out.returncode != 0
+    assert "disagree" in out.stderr

@@ -160,3 +160,19 @@ def test_log_capture_is_faithful(binary, tmp_path):
     assert len(stamp) == 20 and stamp.endswith("Z") and stamp[10] == "T"
     (status,) = _statuses(task).values()
     assert status == {"result": "success", "code": "0", "status": "exited"}
+
+
+def test_rank_cpu_affinity_from_spec(binary, tmp_path):
+    # the NUMA-local cores placed for a rank become its affinity mask (children inherit it)
+    allowed = sorted(os.sched_getaffinity(0))
+    want = allowed[:1]
+    task, spec = _spec(tmp_path, "#!/bin/sh\ngrep Cpus_allowed_list /proc/self/status\n",
+                       parallelism=2,
+                       ranks=[{"gpus": "", "rank_gpus": "", "cpus": want},
+                              {"gpus": "", "rank_gpus": ""}])
+    assert _run(binary, spec).returncode == 0
+    logs = _logs(task)
+    lines = sorted(l.split("\t")[-1].strip() for log in logs for l in log.splitlines() if l)
+    full = ",".join(map(str, allowed))
+    assert str(want[0]) in lines
+    assert len(lines) == 2 and any(l != str(want[0]) or full == str(want[0]) for l in lines)
