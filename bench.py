@@ -53,7 +53,9 @@ def parse_args(argv=None):
     p.add_argument("--hidden", type=int, default=8192)
     p.add_argument("--no-latency", action="store_true", help="skip apply->first-log")
     p.add_argument("--broadcast-gb", type=float, default=10.0,
-                   help="N>1: also measure the RCCL workdir fan-out of this many GB")
+                   help="also measure staging a workdir of this many GB into HBM on every "
+                        "rank (N>1: sharded H2D + xGMI all-gather vs RCCL broadcast vs "
+                        "independent H2D)")
     p.add_argument("--verify", action="store_true", default=True)
     p.add_argument("--no-async", action="store_true",
                    help="skip the (untimed) save_async stall measurement")
@@ -415,26 +417,26 @@ def main(argv=None):
                 "save_GBps": round(total / rs / 1e9, 3),
                 "restore_GBps": round(total / rr / 1e9, 3)})
 
-    broadcast = None
-    if world > 1 and args.broadcast_gb > 0 and on_gpu:  # config 3: workdir fan-out over xGMI (untimed)
+    fanout = None
+    if args.broadcast_gb > 0 and on_gpu:  # configs 2/3: workdir -> HBM on every rank (untimed)
         try:
-            from terraform_provider_iterative_amd.parallel.broadcast import (
-                measure, measure_independent_h2d)
+            import ctypes
 
-            nbytes = int(args.broadcast_gb * 1e9)
-            broadcast = {m: measure(nbytes, method=m, iters=3, warmup=1, device=device)
-                         for m in ("broadcast", "scatter_allgather")}
-            # baseline: every rank pulls its own copy over PCIe (the reference's per-VM copy)
-            broadcast["independent_h2d"] = measure_independent_h2d(nbytes, iters=2, warmup=1,
-                                                                   device=device)
+            from terraform_provider_iterative_amd.ops import hip
+            from terraform_provider_iterative_amd.parallel.fanout import measure_workdir_fanout
+
+            node = ctypes.c_int(-1)
+            hip().tpi_device_numa_node(device.index, ctypes.byref(node))
+            fanout = measure_workdir_fanout(int(args.broadcast_gb * 1e9), rank, world, device,
+                                            barrier, allmax, numa_node=node.value)
         except Exception as error:  # never lose the headline to the side measurement
-            broadcast = {"error": repr(error)}
+            fanout = {"error": repr(error)}
 
     watchdog.cancel()
     if out is not None:
         out["save_async"] = async_stall
         out["raw_GBps"] = raw
-        out["workdir_broadcast"] = broadcast
+        out["workdir_broadcast"] = fanout
     emit()
     ck.close()
     if world > 1:

@@ -30,6 +30,7 @@
 
 #include "../common/crc32c.h"
 #include "../common/tpz.h"
+#include "internal.h"
 #include "tpi_hip.h"
 
 extern "C" hipError_t tpi_launch_stream_crc(int mode, const tpi_seg* segs, int nseg,
@@ -139,6 +140,9 @@ int check_segments(const tpi_seg* segs, int n, uint64_t total) {
 }
 
 }  // namespace
+
+// Error reporting for the other translation units of the library (internal.h).
+int tpi_fail(const std::string& what) { return fail(what); }
 
 struct tpi_engine {
   int device = 0;

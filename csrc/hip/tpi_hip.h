@@ -57,7 +57,7 @@ typedef struct tpi_stats {
 } tpi_stats;
 
 // Bumped whenever a signature below changes (ops/_loader.py checks it).
-#define TPI_ABI_VERSION 2
+#define TPI_ABI_VERSION 3
 
 // Library / device
 const char* tpi_last_error(void);
@@ -158,6 +158,54 @@ int tpi_h2d_async(void* dev_dst, const void* host_src, uint64_t bytes, uint64_t 
 // Chunked host->device copy through the engine's copy stream (workdir staging).
 int tpi_h2d(tpi_engine* e, void* dev_dst, const void* host_src, uint64_t bytes);
 int tpi_d2h(tpi_engine* e, void* host_dst, const void* dev_src, uint64_t bytes);
+
+// ---- Workdir staging (N1): host files <-> a flat image (runtime/stage.py) ---------------------
+// Bytes [0, size) of `path` live at image offset `offset`; files sorted by offset, disjoint.
+typedef struct tpi_file {
+  const char* path;
+  uint64_t offset;
+  uint64_t size;
+} tpi_file;
+typedef struct tpi_loader tpi_loader;
+// device >= 0: the image is device memory, filled through a pinned ring of `nbuf` chunks of
+// `chunk_bytes` (NUMA node `numa_node`, < 0 = unbound) on the loader's copy stream; device < 0:
+// the image is host memory.  `threads` pread workers per chunk.
+tpi_loader* tpi_loader_create(int device, uint64_t chunk_bytes, int nbuf, int threads,
+                              int numa_node);
+void tpi_loader_destroy(tpi_loader* L);
+// Fill image bytes [lo, hi) of `dst` (image base) from the files; bytes no file covers are 0.
+// stats: copy_ms = wall, pack_ms = host read time, bytes, chunks.
+int tpi_loader_load(tpi_loader* L, const tpi_file* files, uint64_t nfiles, uint64_t lo,
+                    uint64_t hi, void* dst, tpi_stats* stats);
+// Write image ranges ([lo, hi) pairs, `nranges` of them) of `src` back into the files.
+int tpi_loader_store(tpi_loader* L, const tpi_file* files, uint64_t nfiles,
+                     const uint64_t* ranges, uint64_t nranges, const void* src,
+                     tpi_stats* stats);
+
+// ---- HIP IPC: a staged image mapped zero-copy by the rank processes ------------------------
+#define TPI_IPC_HANDLE_BYTES 64
+int tpi_ipc_handle(void* dev_ptr, uint8_t* out);
+int tpi_ipc_open(const uint8_t* handle, int device, void** out);
+int tpi_ipc_close(void* dev_ptr);
+
+// ---- Task communicator (RCCL over xGMI) ------------------------------------
+#define TPI_COMM_ID_BYTES 128
+typedef struct tpi_comm tpi_comm;
+int tpi_comm_unique_id(uint8_t* out);  // ncclGetUniqueId (rank 0 / the supervisor side)
+tpi_comm* tpi_comm_init_rank(const uint8_t* id, int nranks, int rank, int device);
+// One process driving `ndev` GPUs (the stager): out[i] = communicator of rank i on devices[i].
+int tpi_comm_init_all(int ndev, const int* devices, tpi_comm** out);
+void tpi_comm_destroy(tpi_comm* c);
+int tpi_comm_rank(const tpi_comm* c);
+int tpi_comm_size(const tpi_comm* c);
+// Collectives over the `n` communicators this thread drives (1 in a rank process, all of
+// them in a single-process stager), issued as one RCCL group on each communicator's own
+// stream; `sync` waits for completion.
+// In-place all-gather: rank r's shard sits at bufs[i] + r * shard_bytes.
+int tpi_comm_allgather_inplace(tpi_comm** comms, int n, void** bufs, uint64_t shard_bytes,
+                               int sync);
+int tpi_comm_broadcast(tpi_comm** comms, int n, void** bufs, uint64_t bytes, int root, int sync);
+int tpi_comm_sync(tpi_comm** comms, int n);
 
 #ifdef __cplusplus
 }

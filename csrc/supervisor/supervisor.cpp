@@ -203,6 +203,11 @@ struct Spec {
   double grace = 30, respawn_delay = 0;
   std::string reports_dir, state_path, events_path, control_path;
   std::vector<std::string> leases;
+  // workdir stager (spec "stager", runtime/stage.py): started before the ranks, holds the
+  // HBM copies of the workdir for the task's lifetime
+  std::vector<std::string> stager_argv;
+  std::string stager_manifest, stager_log, stager_gpus;
+  double stager_timeout = 600;
 };
 
 Spec load_spec(const std::string& path) {
@@ -241,6 +246,12 @@ Spec load_spec(const std::string& path) {
   s.events_path = v["events_path"].str(s.task_dir + "/supervisor/events.jsonl");
   s.control_path = v["control_path"].str(s.task_dir + "/supervisor/control.sock");
   for (auto& l : v["leases"].a) s.leases.push_back(l.str());
+  const Value& st = v["stager"];
+  for (auto& a : st["argv"].a) s.stager_argv.push_back(a.str());
+  s.stager_manifest = st["manifest"].str();
+  s.stager_log = st["log"].str(s.task_dir + "/supervisor/stager.log");
+  s.stager_gpus = st["gpus"].str();
+  s.stager_timeout = st["timeout"].num(600);
   if (s.workdir.empty() || s.script.empty()) throw std::runtime_error("spec needs workdir+script");
   return s;
 }
@@ -279,7 +290,15 @@ class Supervisor {
       event("deadline", {"deadline passed before start"});
       return finish();
     }
-    for (auto& r : ranks_) spawn(r);
+    if (!s_.stager_argv.empty()) {
+      // like the reference's restore before the task service starts (tpl:89): the workdir is
+      // in HBM before any rank runs; create returns at once ("staging" = the VM booting)
+      write_state("staging");
+      signal_ready();
+      stage();
+    }
+    for (auto& r : ranks_)
+      if (r.state == Rank::PENDING) spawn(r);
     write_state();
     signal_ready();
     double last_state = now();
@@ -344,6 +363,112 @@ class Supervisor {
   double started_ = 0, respawn_at_ = 0;
   bool stop_ = false, timed_out_ = false, dirty_ = true;
   int total_restarts_ = 0;
+  pid_t stager_pid_ = -1;
+  bool staged_ = false;
+
+  // ---- workdir stager ----------------------------------------------------------------------
+  void stage() {
+    int p[2];
+    if (pipe2(p, O_CLOEXEC)) {
+      event("stage-failed", {std::string("pipe: ") + strerror(errno)});
+      return;
+    }
+    int logfd = open(s_.stager_log.c_str(), O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
+    std::vector<std::string> env;
+    bool has_path = false;
+    for (auto& kv : s_.env) {
+      if (kv.first == "PATH") has_path = true;
+      env.push_back(kv.first + "=" + kv.second);
+    }
+    if (!has_path) env.push_back("PATH=/usr/local/sbin:/usr/local/bin:/usr/sbin:/usr/bin:/sbin:/bin");
+    if (!s_.stager_gpus.empty()) env.push_back("HIP_VISIBLE_DEVICES=" + s_.stager_gpus);
+    std::vector<char*> envp, argv;
+    for (auto& e : env) envp.push_back(const_cast<char*>(e.c_str()));
+    envp.push_back(nullptr);
+    for (auto& a : s_.stager_argv) argv.push_back(const_cast<char*>(a.c_str()));
+    argv.push_back(nullptr);
+    pid_t parent = getpid();
+    pid_t pid = fork();
+    if (pid == 0) {
+      setpgid(0, 0);
+      prctl(PR_SET_PDEATHSIG, SIGTERM);
+      if (getppid() != parent) _exit(127);
+      sigset_t none;
+      sigemptyset(&none);
+      sigprocmask(SIG_SETMASK, &none, nullptr);
+      int devnull = open("/dev/null", O_RDONLY);
+      if (devnull >= 0) dup2(devnull, 0);
+      dup2(p[1], 1);
+      if (logfd >= 0) dup2(logfd, 2);
+      if (chdir(s_.task_dir.c_str())) _exit(126);
+      execve(argv[0], argv.data(), envp.data());
+      dprintf(2, "tpi-supervisor: exec %s: %s\n", argv[0], strerror(errno));
+      _exit(127);
+    }
+    close(p[1]);
+    if (logfd >= 0) close(logfd);
+    if (pid < 0) {
+      close(p[0]);
+      event("stage-failed", {std::string("fork: ") + strerror(errno)});
+      return;
+    }
+    stager_pid_ = pid;
+    event("stager-start", {"pid " + std::to_string(pid)});
+    std::string out, why = "stager exited";
+    const double until = now() + s_.stager_timeout;
+    while (!stop_) {
+      const double left = until - now();
+      if (left <= 0) {
+        why = "timed out";
+        break;
+      }
+      struct pollfd pf[3] = {{p[0], POLLIN, 0}, {sfd_, POLLIN, 0}, {ctl_fd_, POLLIN, 0}};
+      int rc = poll(pf, ctl_fd_ >= 0 ? 3 : 2, (int)(std::min(left, 1.0) * 1000) + 1);
+      if (rc < 0 && errno != EINTR) break;
+      if (pf[0].revents & (POLLIN | POLLHUP | POLLERR)) {
+        char buf[4096];
+        ssize_t n = read(p[0], buf, sizeof(buf));
+        if (n <= 0) break;  // EOF: the stager died before staging finished
+        out.append(buf, (size_t)n);
+        size_t nl = out.find('\n');
+        if (nl != std::string::npos && out.compare(0, 7, "staged ") == 0) {
+          staged_ = true;
+          event("workdir-staged", {"manifest " + s_.stager_manifest, out.substr(7, nl - 7)});
+          break;
+        }
+      }
+      if (pf[1].revents & POLLIN) handle_signals();
+      if (ctl_fd_ >= 0 && (pf[2].revents & POLLIN)) handle_control();
+    }
+    close(p[0]);
+    if (!staged_) {
+      event("stage-failed", {stop_ ? "stopped" : why, "see " + s_.stager_log});
+      stop_stager();
+    }
+  }
+
+  // SIGTERM (the stager writes dirty shards back first), then SIGKILL after the grace period.
+  void stop_stager() {
+    if (stager_pid_ <= 0) return;
+    kill(stager_pid_, SIGTERM);
+    const double until = now() + std::max(s_.grace, 5.0);
+    int st = 0;
+    pid_t got = 0;
+    while ((got = waitpid(stager_pid_, &st, WNOHANG)) == 0 && now() < until) usleep(10000);
+    if (got == 0) {
+      kill(-stager_pid_, SIGKILL);
+      kill(stager_pid_, SIGKILL);
+      got = waitpid(stager_pid_, &st, 0);
+    }
+    if (got == stager_pid_) stager_exited(st);
+    stager_pid_ = -1;
+  }
+
+  void stager_exited(int st) {
+    event("stager-exit", {WIFSIGNALED(st) ? std::string("signal ") + signame(WTERMSIG(st))
+                                          : "code " + std::to_string(WEXITSTATUS(st))});
+    stager_pid_ = -1;
+  }
 
   void event(const std::string& code, const std::vector<std::string>& desc) {
     std::string line = "{\"time\": " + std::to_string(now()) + ", \"code\": " + quote(code) +
@@ -401,7 +526,8 @@ class Supervisor {
                       ", \"started_at\": " + std::to_string(started_) +
                       ", \"heartbeat\": " + std::to_string(now()) +
                       ", \"running\": " + std::to_string(running()) +
-                      ", \"restarts\": " + std::to_string(total_restarts_) + ", \"ranks\": [";
+                      ", \"restarts\": " + std::to_string(total_restarts_) +
+                      ", \"stager_pid\": " + std::to_string(stager_pid_) + ", \"ranks\": [";
     for (size_t i = 0; i < ranks_.size(); ++i) {
       auto& r = ranks_[i];
       out += std::string(i ? ", " : "") + "{\"rank\": " + std::to_string(r.index) +
@@ -446,6 +572,7 @@ class Supervisor {
     add("TPI_RESTART_COUNT", std::to_string(r.restarts));
     add("TPI_EVENTS_FILE", s_.events_path);  // ranks journal checkpoint phases here
     add("TPI_NOTIFY_FD", "3");                 // "released": spill done, respawn may start
+    if (staged_) add("TPI_HBM_WORKDIR", s_.stager_manifest);  // runtime/stage.py attach()
     if (s_.deadline > 0) {
       add("TPI_DEADLINE", std::to_string((long long)s_.deadline));
       add("TPI_REMAINING_RUN_TIME", std::to_string((long long)(s_.deadline - now())));
@@ -949,6 +1076,10 @@ class Supervisor {
       int st = 0;
       pid_t pid = waitpid(-1, &st, WNOHANG);
       if (pid <= 0) return;
+      if (pid == stager_pid_) {  // the stager died while ranks still use the images
+        stager_exited(st);
+        continue;
+      }
       for (size_t i = 0; i < detached_.size(); ++i)
         if (detached_[i].pid == pid) {
           Rank& d = detached_[i];
@@ -1065,6 +1196,7 @@ class Supervisor {
       }
       close_log(r);
     }
+    stop_stager();
     for (auto& l : s_.leases) unlink(l.c_str());
     close_control();
     event("supervisor-exit", {stop_ ? "stopped" : "all ranks finished"});

@@ -6,6 +6,7 @@
   communicator, ``--offload-arch=gfx950``, linked against the libamdhip64 that ships with
   torch so one HIP runtime is loaded.
 * ``_lib/tpi-supervisor``   the on-node rank supervisor (C++ executable).
+* ``_lib/tpi-stager``       the per-task workdir stager (C++/HIP executable on libtpi_hip).
 
 Nothing built is tracked by git.  A target is rebuilt when its ``.stamp`` (SHA-256 of the
 compile command and of every source/header it depends on) no longer matches -- content, not
@@ -36,6 +37,7 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0] or "gfx950"
 NATIVE_SO = os.path.join(LIB, "_tpi_native" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
 HIP_SO = os.path.join(LIB, "libtpi_hip.so")
 SUPERVISOR = os.path.join(LIB, "tpi-supervisor")
+STAGER = os.path.join(LIB, "tpi-stager")
 
 
 def _sources(*patterns: str) -> List[str]:
@@ -142,7 +144,7 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
     cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics", _define_version(),
            *srcs, "-L" + tl, "-Wl,-rpath," + tl, "-L" + ROCM_LIB, "-Wl,-rpath," + ROCM_LIB,
-           "-lrocprofiler-sdk-roctx", "-o", "@OUT@"]
+           "-lrccl", "-lrocprofiler-sdk-roctx", "-o", "@OUT@"]
     return _build(HIP_SO, cmd, deps, force, verbose)
 
 
@@ -157,10 +159,25 @@ def build_supervisor(force: bool = False, verbose: bool = False) -> str:
     return _build(SUPERVISOR, cmd, deps, force, verbose)
 
 
+def build_stager(force: bool = False, verbose: bool = False) -> str:
+    """The per-task workdir stager (links libtpi_hip.so next to it; no Python, no torch)."""
+    srcs = _sources("stager/*.cpp")
+    if not srcs:
+        return ""
+    hip_so = build_hip(force, verbose)
+    deps = srcs + [hip_so] + _sources("hip/tpi_hip.h", "common/*.h", "supervisor/json.h")
+    tl = torch_lib_dir()
+    cmd = [hipcc(), "-O2", "-std=c++17", "-Wall", "-pthread", _define_version(), *srcs,
+           "-L" + LIB, "-ltpi_hip", "-Wl,-rpath,$ORIGIN", "-L" + tl, "-Wl,-rpath," + tl,
+           "-L" + ROCM_LIB, "-Wl,-rpath," + ROCM_LIB, "-o", "@OUT@"]
+    return _build(STAGER, cmd, deps, force, verbose)
+
+
 def build_all(force: bool = False, verbose: bool = False, hip: bool = True) -> List[str]:
     outs = [build_native(force, verbose), build_supervisor(force, verbose)]
     if hip:
         outs.append(build_hip(force, verbose))
+        outs.append(build_stager(force, verbose))
     return [o for o in outs if o]
 
 

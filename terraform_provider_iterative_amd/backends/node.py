@@ -267,7 +267,9 @@ class NodeTask(Task):
         if gpus:
             env["TPI_VISIBLE_GPUS"] = visible
         script_path = os.path.join(self.sup_dir, "script")
+        stager = self._stager(d, per, visible, numa)
         return {
+            "stager": stager,
             "task_id": self.id, "task_dir": self.root, "workdir": self.data_dir,
             "script": script_path, "env": env, "deadline": d.get("deadline", 0),
             "parallelism": parallelism, "ranks": ranks,
@@ -285,6 +287,31 @@ class NodeTask(Task):
             "events_path": os.path.join(self.sup_dir, "events.jsonl"),
             "leases": [self.placement.lease_path(g) for g in gpus],
         }
+
+    def _stager(self, d: Dict, per: int, visible: str, numa: List[int]) -> Optional[Dict]:
+        """The supervisor's ``stager`` entry when the workdir goes to HBM before the ranks
+        start (:mod:`..runtime.stage`), else None."""
+        from ..runtime import stage
+
+        environ = dict(os.environ)
+        environ.update({k: v for k, v in (d.get("environment") or {}).items() if v is not None})
+        if not stage.mode(environ, self.provider, 1 << 62):
+            return None  # disabled, or a backend that never stages: skip the walk
+        files, nbytes = stage.layout(self.data_dir)
+        kind = stage.mode(environ, self.provider, nbytes)
+        parallelism = d["parallelism"]
+        if kind == "hbm" and not per:
+            return None
+        if not kind or nbytes == 0:
+            return None
+        devices = [r * per for r in range(parallelism)] if kind == "hbm" else \
+            list(range(parallelism))
+        node = [numa[i] if i < len(numa) else -1 for i in devices] if kind == "hbm" else \
+            [-1] * parallelism
+        entry = stage.plan(self.data_dir, self.sup_dir, devices, node, environ,
+                           host=kind == "host", files=files, nbytes=nbytes)
+        entry["gpus"] = visible
+        return entry
 
     def _write_script(self) -> None:
         script = self.spec.environment.script or (self._saved or {}).get("script", "")
@@ -339,7 +366,7 @@ class NodeTask(Task):
 
     def _alive_pids(self) -> List[int]:
         state = self._state()
-        pids = [int(state.get("pid", 0) or 0)]
+        pids = [int(state.get("pid", 0) or 0), int(state.get("stager_pid", 0) or 0)]
         pids += [int(r.get("pid", 0) or 0) for r in state.get("ranks") or []]
         return [p for p in pids if p > 0 and pid_alive(p)]
 
@@ -347,6 +374,7 @@ class NodeTask(Task):
         state = self._state()
         sup = int(state.get("pid", 0) or 0)
         ranks = [int(r.get("pid", 0) or 0) for r in state.get("ranks") or []]
+        ranks.append(int(state.get("stager_pid", 0) or 0))
         for pid in [p for p in ranks if p > 0] + ([sup] if sup > 0 else []):
             for target in (-pid, pid):  # each rank leads its own process group
                 try:

@@ -15,7 +15,7 @@ from typing import Optional
 
 from .. import _build
 
-ABI_VERSION = 2  # TPI_ABI_VERSION of csrc/hip/tpi_hip.h
+ABI_VERSION = 3  # TPI_ABI_VERSION of csrc/hip/tpi_hip.h
 
 _lock = threading.Lock()
 _native = None
@@ -92,6 +92,22 @@ class HipLib:
             "tpi_host_unregister": (i32, [vp]),
             "tpi_h2d": (i32, [vp, vp, vp, u64]),
             "tpi_d2h": (i32, [vp, vp, vp, u64]),
+            "tpi_loader_create": (vp, [i32, u64, i32, i32, i32]),
+            "tpi_loader_destroy": (None, [vp]),
+            "tpi_loader_load": (i32, [vp, vp, u64, u64, u64, vp, vp]),
+            "tpi_loader_store": (i32, [vp, vp, u64, vp, u64, vp, vp]),
+            "tpi_ipc_handle": (i32, [vp, c.c_char_p]),
+            "tpi_ipc_open": (i32, [c.c_char_p, i32, c.POINTER(vp)]),
+            "tpi_ipc_close": (i32, [vp]),
+            "tpi_comm_unique_id": (i32, [c.c_char_p]),
+            "tpi_comm_init_rank": (vp, [c.c_char_p, i32, i32, i32]),
+            "tpi_comm_init_all": (i32, [i32, c.POINTER(i32), c.POINTER(vp)]),
+            "tpi_comm_destroy": (None, [vp]),
+            "tpi_comm_rank": (i32, [vp]),
+            "tpi_comm_size": (i32, [vp]),
+            "tpi_comm_allgather_inplace": (i32, [c.POINTER(vp), i32, c.POINTER(vp), u64, i32]),
+            "tpi_comm_broadcast": (i32, [c.POINTER(vp), i32, c.POINTER(vp), u64, i32, i32]),
+            "tpi_comm_sync": (i32, [c.POINTER(vp), i32]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)

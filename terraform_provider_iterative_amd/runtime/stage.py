@@ -1,0 +1,288 @@
+"""The task runtime's HBM workdir: plan the stager, attach to its copies from a rank.
+
+The reference restores a task's workdir on each of its ``parallelism`` machines before the
+script starts (``machine-script.sh.tpl:89``; ``resource_auto_scaling_group.go:70``) and
+re-syncs it every 10 s (``tpl:118-124``).  On the ``mi355x`` backend the supervisor starts
+``tpi-stager`` (``csrc/stager/stager.cpp``) first: the workdir becomes one flat image in HBM
+on every rank's GPU (sharded H2D over every GPU's own PCIe link + one in-place RCCL
+all-gather over xGMI), verified by the shard-hash kernel, and the stager stays up to write
+dirty shards back on the reference's cadence.  Ranks start with ``TPI_HBM_WORKDIR`` naming
+the stager's manifest and map their copy zero-copy with :func:`attach` -- no user code is
+needed for the staging itself.
+
+Knobs (task ``environment`` or the provider's environment):
+
+=========================  =====================================================================
+``TPI_STAGE``              ``auto`` (default: stage mi355x tasks whose workdir holds at least
+                           ``TPI_STAGE_MIN_BYTES``), ``hbm`` (always), ``host`` (images in
+                           ``/dev/shm``: CPU rehearsal, any backend), ``off``
+``TPI_STAGE_MIN_BYTES``    default 64 MiB
+``TPI_STAGE_METHOD``       ``sharded`` (default), ``broadcast``, ``independent``
+``TPI_SYNC_INTERVAL``      write-back cadence in seconds (default 10, as tpl:118-124; 0 = off)
+``TPI_STAGE_WRITEBACK``    ``1`` (default) / ``0``
+=========================  =====================================================================
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+from typing import Dict, List, Optional, Sequence, Tuple
+
+ALIGN = 4096
+DEFAULT_MIN_BYTES = 64 << 20
+METHODS = ("sharded", "broadcast", "independent")
+
+
+def _env(environ, key: str, default: str) -> str:
+    value = environ.get(key)
+    return default if value in (None, "") else str(value)
+
+
+def layout(root: str) -> Tuple[List[Tuple[str, int, int]], int]:
+    """Every regular file under ``root`` (already filtered by the push) as ``(relative path,
+    image offset, size)`` at 4 KiB-aligned offsets, sorted; and the unpadded image size."""
+    from ..ops import native
+    from ..storage.transfer import make_filter
+
+    files, off = [], 0
+    for rel, size, _mtime, _mode, is_dir in sorted(native().walk(root, make_filter([]))):
+        if is_dir:
+            continue
+        files.append((rel, off, int(size)))
+        off += (int(size) + ALIGN - 1) // ALIGN * ALIGN
+    return files, off
+
+
+def mode(environ, provider: str, nbytes: int) -> str:
+    """``"hbm"``, ``"host"`` or ``""`` (no staging) for a task of ``provider`` whose workdir
+    holds ``nbytes``."""
+    want = _env(environ, "TPI_STAGE", "auto").lower()
+    if want in ("off", "0", "no", "false"):
+        return ""
+    if want == "host":
+        return "host"
+    if provider != "mi355x":
+        return ""
+    if want == "hbm":
+        return "hbm"
+    return "hbm" if nbytes >= int(_env(environ, "TPI_STAGE_MIN_BYTES", str(DEFAULT_MIN_BYTES))) \
+        else ""
+
+
+def plan(root: str, sup_dir: str, devices: Sequence[int], numa: Sequence[int],
+         environ, host: bool = False, files=None, nbytes: Optional[int] = None) -> Dict:
+    """Write ``<sup_dir>/stage.json`` for ``tpi-stager`` and return the supervisor's
+    ``stager`` spec entry."""
+    from .. import _build
+
+    if files is None or nbytes is None:
+        files, nbytes = layout(root)
+    n = max(1, len(devices))
+    quantum = ALIGN * n
+    total = max(quantum, (nbytes + quantum - 1) // quantum * quantum)
+    method = _env(environ, "TPI_STAGE_METHOD", "sharded")
+    if method not in METHODS:
+        raise ValueError("TPI_STAGE_METHOD must be one of %s" % (METHODS,))
+    manifest = os.path.join(sup_dir, "stage-manifest.json")
+    spec = {
+        "root": root, "files": [list(f) for f in files], "total": total,
+        "devices": list(devices), "numa": list(numa), "method": method,
+        "chunk_bytes": int(_env(environ, "TPI_STAGE_CHUNK_BYTES", str(64 << 20))),
+        "nbuf": 4, "threads": int(_env(environ, "TPI_STAGE_THREADS", "8")),
+        "shard_bytes": 1 << 20, "manifest": manifest,
+        "events": os.path.join(sup_dir, "events.jsonl"),
+        "sync_interval": float(_env(environ, "TPI_SYNC_INTERVAL", "10")),
+        "writeback": _env(environ, "TPI_STAGE_WRITEBACK", "1") != "0",
+        "host": bool(host), "verify": True,
+        "shm_prefix": "/dev/shm/tpi-stage-%s" % os.path.basename(os.path.dirname(sup_dir)),
+    }
+    path = os.path.join(sup_dir, "stage.json")
+    with open(path + ".tmp", "w") as handle:
+        json.dump(spec, handle)
+    os.replace(path + ".tmp", path)
+    binary = os.environ.get("TPI_STAGER_BIN") or _build.STAGER
+    if binary == _build.STAGER:
+        _build.build_stager()
+    return {"argv": [binary, path], "manifest": manifest,
+            "log": os.path.join(sup_dir, "stager.log"),
+            "timeout": float(_env(environ, "TPI_STAGE_TIMEOUT", "600"))}
+
+
+# ---- rank side --------------------------------------------------------------------------------
+
+class _DLDevice(ctypes.Structure):
+    _fields_ = [("device_type", ctypes.c_int32), ("device_id", ctypes.c_int32)]
+
+
+class _DLDataType(ctypes.Structure):
+    _fields_ = [("code", ctypes.c_uint8), ("bits", ctypes.c_uint8), ("lanes", ctypes.c_uint16)]
+
+
+class _DLTensor(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("device", _DLDevice), ("ndim", ctypes.c_int32),
+                ("dtype", _DLDataType), ("shape", ctypes.POINTER(ctypes.c_int64)),
+                ("strides", ctypes.POINTER(ctypes.c_int64)), ("byte_offset", ctypes.c_uint64)]
+
+
+class _DLManagedTensor(ctypes.Structure):
+    _fields_ = [("dl_tensor", _DLTensor), ("manager_ctx", ctypes.c_void_p),
+                ("deleter", ctypes.c_void_p)]
+
+
+_KDL_ROCM = 10
+_KEEP: List[object] = []  # DLPack structs of live mappings (the mapping outlives the tensor)
+
+
+def _device_tensor(ptr: int, nbytes: int, device: int):
+    """A 1-D uint8 torch tensor over ``nbytes`` of device memory at ``ptr`` (no copy),
+    through a DLPack capsule (kDLROCM)."""
+    import torch
+    import torch.utils.dlpack
+
+    shape = (ctypes.c_int64 * 1)(nbytes)
+    mt = _DLManagedTensor()
+    mt.dl_tensor.data = ptr
+    mt.dl_tensor.device = _DLDevice(_KDL_ROCM, device)
+    mt.dl_tensor.ndim = 1
+    mt.dl_tensor.dtype = _DLDataType(1, 8, 1)  # kDLUInt, 8 bits
+    mt.dl_tensor.shape = shape
+    mt.dl_tensor.strides = None
+    mt.dl_tensor.byte_offset = 0
+    mt.manager_ctx = None
+    mt.deleter = None
+    _KEEP.append((mt, shape))
+    capsule_new = ctypes.pythonapi.PyCapsule_New
+    capsule_new.restype = ctypes.py_object
+    capsule_new.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p]
+    capsule = capsule_new(ctypes.addressof(mt), b"dltensor", None)
+    return torch.utils.dlpack.from_dlpack(capsule)
+
+
+class HbmWorkdir:
+    """A rank's zero-copy view of the staged workdir (:func:`attach`)."""
+
+    def __init__(self, manifest: Dict, rank: int, buffer, mapping: Optional[int] = None):
+        self.manifest = manifest
+        self.rank = rank
+        self.root = manifest["root"]
+        self.total = int(manifest["total"])
+        self.files = [(f[0], int(f[1]), int(f[2])) for f in manifest["files"]]
+        self._index = {f[0]: (f[1], f[2]) for f in self.files}
+        self.buffer = buffer  # 1-D uint8 tensor (device, or host for host-mode images)
+        self.stats = manifest.get("stats", {})
+        self._mapping = mapping
+
+    def tensor(self, path: str):
+        """The bytes of ``path`` (relative to the workdir) as a uint8 view of the image."""
+        off, size = self._index[path]
+        return self.buffer[off:off + size]
+
+    def paths(self) -> List[str]:
+        return [f[0] for f in self.files]
+
+    def digest(self, shard_bytes: int = 1 << 20):
+        from ..ops import shard_hash
+
+        return shard_hash(self.buffer, shard_bytes=shard_bytes)
+
+    def close(self) -> None:
+        self.buffer = None
+        if self._mapping:
+            from ..ops import hip
+
+            hip().tpi_ipc_close(ctypes.c_void_p(self._mapping))
+            self._mapping = None
+
+
+def attach(manifest: Optional[str] = None, rank: Optional[int] = None) -> HbmWorkdir:
+    """Map this rank's copy of the staged workdir (``$TPI_HBM_WORKDIR``)."""
+    path = manifest or os.environ.get("TPI_HBM_WORKDIR")
+    if not path:
+        raise RuntimeError("no staged workdir: TPI_HBM_WORKDIR is not set (TPI_STAGE=off, "
+                           "a small workdir, or staging failed -- see events.jsonl)")
+    with open(path) as handle:
+        data = json.load(handle)
+    rank = int(os.environ.get("RANK", "0")) if rank is None else rank
+    entry = data["ranks"][rank]
+    if data.get("host"):
+        import numpy as np
+        import torch
+
+        arr = np.memmap(entry["path"], dtype=np.uint8, mode="r+", shape=(int(data["total"]),))
+        return HbmWorkdir(data, rank, torch.from_numpy(arr))
+    from ..ops import hip
+
+    lib = hip()
+    device = int(entry["device"])
+    ptr = ctypes.c_void_p()
+    handle_bytes = bytes.fromhex(entry["ipc"])
+    lib.check(lib.tpi_ipc_open(handle_bytes, device, ctypes.byref(ptr)), "hipIpcOpenMemHandle")
+    buffer = _device_tensor(ptr.value, int(data["total"]), device)
+    return HbmWorkdir(data, rank, buffer, mapping=ptr.value)
+
+
+# ---- native loader (used by the stager binary; exposed for ranks, benches and tests) ----------
+
+class _File(ctypes.Structure):
+    _fields_ = [("path", ctypes.c_char_p), ("offset", ctypes.c_uint64),
+                ("size", ctypes.c_uint64)]
+
+
+class _Stats(ctypes.Structure):
+    _fields_ = [("pack_ms", ctypes.c_double), ("copy_ms", ctypes.c_double),
+                ("bytes", ctypes.c_uint64), ("chunks", ctypes.c_uint64)]
+
+
+class Loader:
+    """``tpi_loader``: files <-> image bytes.  ``device >= 0``: the image is device memory,
+    filled through a NUMA-local pinned ring (pread workers overlap the H2D copies);
+    ``device = -1``: a host image."""
+
+    def __init__(self, device: int = -1, chunk_bytes: int = 64 << 20, nbuf: int = 4,
+                 threads: int = 8, numa_node: int = -1):
+        from ..ops import hip
+
+        self.lib = hip()
+        self.handle = self.lib.tpi_loader_create(device, chunk_bytes, nbuf, threads, numa_node)
+        if not self.handle:
+            raise RuntimeError("loader: %s" % self.lib.error())
+
+    @staticmethod
+    def _files(root: str, files):
+        paths = [os.path.join(root, f[0]).encode() for f in files]
+        arr = (_File * max(1, len(files)))()
+        for i, (f, p) in enumerate(zip(files, paths)):
+            arr[i] = _File(p, int(f[1]), int(f[2]))
+        return arr, paths
+
+    def load(self, root: str, files, lo: int, hi: int, dst: int) -> Dict[str, float]:
+        """Fill image bytes ``[lo, hi)`` of the image at address ``dst``."""
+        arr, _keep = self._files(root, files)
+        st = _Stats()
+        self.lib.check(self.lib.tpi_loader_load(self.handle, arr, len(files), lo, hi,
+                                                ctypes.c_void_p(dst), ctypes.byref(st)),
+                       "tpi_loader_load")
+        return {"ms": st.copy_ms, "read_ms": st.pack_ms, "bytes": int(st.bytes),
+                "chunks": int(st.chunks)}
+
+    def store(self, root: str, files, ranges, src: int) -> Dict[str, float]:
+        """Write image ``ranges`` (``[(lo, hi), ...]``) of the image at ``src`` to the files."""
+        arr, _keep = self._files(root, files)
+        flat = (ctypes.c_uint64 * max(1, 2 * len(ranges)))(*[x for r in ranges for x in r])
+        st = _Stats()
+        self.lib.check(self.lib.tpi_loader_store(self.handle, arr, len(files), flat, len(ranges),
+                                                 ctypes.c_void_p(src), ctypes.byref(st)),
+                       "tpi_loader_store")
+        return {"ms": st.copy_ms, "bytes": int(st.bytes)}
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.tpi_loader_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

@@ -1,0 +1,175 @@
+"""Runtime workdir staging (runtime/stage.py + csrc/stager/stager.cpp + the supervisor).
+
+On CPU the stager runs in host mode (images in /dev/shm, ``TPI_STAGE=host``): the same
+loader (pinned-ring code path aside), layout, sharded fan-out schedule, digest verification,
+supervisor hand-off and dirty-shard write-back as on the GPUs.  The reference behaviour it
+replaces: the workdir is restored before the script runs on every machine
+(machine-script.sh.tpl:89) and re-synced every 10 s (tpl:118-124).
+"""
+import json
+import os
+import sys
+import time
+
+import pytest
+
+from terraform_provider_iterative_amd import _build, backends
+from terraform_provider_iterative_amd.models.cloud import Cloud, Credentials, NodeCredentials
+from terraform_provider_iterative_amd.models.values import Environment, Size, Task, Variables
+from terraform_provider_iterative_amd.runtime import stage
+from terraform_provider_iterative_amd.utils.identifier import new_deterministic_identifier
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def stager_binary():
+    return _build.build_stager()
+
+
+@pytest.fixture()
+def cloud(tmp_path, monkeypatch):
+    monkeypatch.setenv("TPI_MI355X_GPUS", "0,1,2,3,4,5,6,7")
+    monkeypatch.setenv("PYTHONPATH", ROOT)
+    return Cloud(provider="mi355x",
+                 credentials=Credentials(node=NodeCredentials(state_root=str(tmp_path / "st"))))
+
+
+def _workdir(tmp_path):
+    work = tmp_path / "work"
+    (work / "sub").mkdir(parents=True)
+    rng = __import__("random").Random(7)
+    sizes = {"a.bin": 3 << 20, "b.txt": 5, "sub/c.dat": 4096 * 3 + 17, "sub/empty": 0,
+             "z.bin": (1 << 20) + 1}
+    for name, size in sizes.items():
+        (work / name).write_bytes(bytes(rng.getrandbits(8) for _ in range(min(size, 4096))) *
+                                  (size // 4096) + bytes(rng.getrandbits(8)
+                                                         for _ in range(size % 4096)))
+    return work, sizes
+
+
+def _task(cloud, name, script, work, parallelism=2, env=None):
+    variables = {"TPI_TASK": "true"}
+    variables.update(env or {})
+    spec = Task(size=Size(machine="m+mi355x"), parallelism=parallelism,
+                environment=Environment(script=script, variables=Variables(variables),
+                                        timeout=120, directory=str(work)))
+    return backends.new(cloud, new_deterministic_identifier(name), spec)
+
+
+def test_layout_aligns_and_sorts(tmp_path):
+    work, sizes = _workdir(tmp_path)
+    files, total = stage.layout(str(work))
+    assert [f[0] for f in files] == sorted(sizes)
+    for rel, off, size in files:
+        assert off % 4096 == 0 and size == sizes[rel]
+    last = files[-1]
+    assert total == last[1] + (last[2] + 4095) // 4096 * 4096
+
+
+def test_mode_selection():
+    assert stage.mode({}, "mi355x", 1 << 30) == "hbm"
+    assert stage.mode({}, "mi355x", 1 << 10) == ""           # below TPI_STAGE_MIN_BYTES
+    assert stage.mode({"TPI_STAGE": "hbm"}, "mi355x", 1) == "hbm"
+    assert stage.mode({"TPI_STAGE": "off"}, "mi355x", 1 << 30) == ""
+    assert stage.mode({}, "local", 1 << 30) == ""
+    assert stage.mode({"TPI_STAGE": "host"}, "local", 1) == "host"
+
+
+ATTACH = """#!/bin/sh
+exec python3 - <<'EOF'
+import os, hashlib
+from terraform_provider_iterative_amd.runtime.stage import attach
+w = attach()
+root = os.environ["TPI_DATA_DIRECTORY"]
+for rel in w.paths():
+    host = open(os.path.join(root, rel), "rb").read()
+    assert bytes(w.tensor(rel).numpy()) == host, rel
+flag = os.path.join(os.environ["TPI_TASK_DIRECTORY"], "verified-" + os.environ["RANK"])
+open(flag, "w").close()
+if os.environ["RANK"] == "0":  # change the copy only once every rank compared with the files
+    import glob, time
+    while len(glob.glob(os.path.join(os.environ["TPI_TASK_DIRECTORY"], "verified-*"))) < int(os.environ["WORLD_SIZE"]):
+        time.sleep(0.01)
+    w.tensor("a.bin")[:3] = __import__("torch").tensor(list(b"XYZ"), dtype=__import__("torch").uint8)
+print("attached rank", os.environ["RANK"], len(w.paths()), w.stats["verified"])
+EOF
+"""
+
+
+@pytest.mark.parametrize("method", ["sharded", "broadcast", "independent"])
+def test_host_mode_stage_attach_and_write_back(cloud, tmp_path, method):
+    work, sizes = _workdir(tmp_path)
+    task = _task(cloud, "stage-" + method, ATTACH, work, parallelism=3,
+                 env={"TPI_STAGE": "host", "TPI_STAGE_METHOD": method,
+                      "TPI_SYNC_INTERVAL": "0.2"})
+    task.create()
+    status = task.wait(60)
+    logs = "\n".join(task.logs())
+    assert status["succeeded"] == 3, (logs, open(os.path.join(task.sup_dir, "stager.log")).read())
+    assert logs.count("attached rank") == 3 and "True" in logs
+    codes = [e.code for e in task.events()]
+    assert "workdir-staged" in codes and "stager-exit" in codes
+    assert codes.index("workdir-staged") < codes.index("rank-start")
+    # rank 0 changed 3 bytes of a.bin in its copy: exactly that shard went back to the file
+    data = open(os.path.join(task.data_dir, "a.bin"), "rb").read()
+    assert data[:3] == b"XYZ" and len(data) == sizes["a.bin"]
+    assert data[3:] == (work / "a.bin").read_bytes()[3:]
+    syncs = [e for e in task.events() if e.code == "workdir-sync"]
+    assert any("dirty_shards 1" in e.description for e in syncs)
+    assert not any(n.startswith("tpi-stage-" + task.id) for n in os.listdir("/dev/shm"))
+    task.delete()
+
+
+def test_stage_failure_falls_back_to_the_host_workdir(cloud, tmp_path, monkeypatch):
+    work, _ = _workdir(tmp_path)
+    monkeypatch.setenv("TPI_STAGER_BIN", "/bin/false")
+    task = _task(cloud, "stage-fail", "#!/bin/sh\necho \"hbm=[$TPI_HBM_WORKDIR]\"\n", work,
+                 parallelism=1, env={"TPI_STAGE": "host"})
+    task.create()
+    assert task.wait(30)["succeeded"] == 1
+    assert "hbm=[]" in task.logs()[0]
+    assert "stage-failed" in [e.code for e in task.events()]
+    task.delete()
+
+
+def test_stop_while_staging(cloud, tmp_path, monkeypatch):
+    work, _ = _workdir(tmp_path)
+    slow = tmp_path / "slow-stager"
+    slow.write_text("#!/bin/sh\nsleep 60\n")
+    slow.chmod(0o755)
+    monkeypatch.setenv("TPI_STAGER_BIN", str(slow))
+    monkeypatch.setenv("TPI_GRACE_SECONDS", "1")
+    task = _task(cloud, "stage-stop", "#!/bin/sh\necho never\n", work, parallelism=1,
+                 env={"TPI_STAGE": "host"})
+    t0 = time.time()
+    task.create()  # returns while staging
+    assert time.time() - t0 < 10
+    assert task.status()["running"] == 0
+    task.stop(wait=30)
+    assert not task.supervisor_running()
+    assert time.time() - t0 < 20
+    assert not task.logs() or not any("never" in l for l in task.logs())
+    assert task.status() == {"running": 0, "succeeded": 0, "failed": 0}
+    task.delete()
+
+
+def test_loader_host_image_roundtrip(tmp_path):
+    import numpy as np
+
+    work, sizes = _workdir(tmp_path)
+    files, nbytes = stage.layout(str(work))
+    image = np.full(nbytes + 4096, 0xAB, dtype=np.uint8)
+    with stage.Loader(-1, chunk_bytes=1 << 20, threads=3) as loader:
+        # two ranges that split files mid-way, like the sharded load of two GPUs
+        half = nbytes // 2 // 4096 * 4096
+        loader.load(str(work), files, 0, half, image.ctypes.data)
+        loader.load(str(work), files, half, nbytes, image.ctypes.data)
+        for rel, off, size in files:
+            assert image[off:off + size].tobytes() == (work / rel).read_bytes()
+            pad = (size + 4095) // 4096 * 4096
+            assert not image[off + size:off + pad].any()  # gaps are zero
+        assert (image[nbytes:] == 0xAB).all()  # nothing beyond the range
+        image[5:8] = [1, 2, 3]
+        loader.store(str(work), files, [(0, 4096)], image.ctypes.data)
+    assert (work / "a.bin").read_bytes()[5:8] == b"\x01\x02\x03"
