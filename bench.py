@@ -418,7 +418,8 @@ def main(argv=None):
                 "restore_GBps": round(total / rr / 1e9, 3)})
 
     fanout = None
-    if args.broadcast_gb > 0 and on_gpu:  # configs 2/3: workdir -> HBM on every rank (untimed)
+    # configs 2/3: workdir -> HBM on every rank (untimed; RCCL needs one GPU per rank)
+    if args.broadcast_gb > 0 and on_gpu and (world == 1 or backend == "nccl"):
         try:
             import ctypes
 
