@@ -2,7 +2,8 @@
 """Config 2: 1 x MI355X ``iterative_task`` with a large synthetic workdir + PyTorch-ROCm
 ``train.py`` (examples/train/train.py), driven through ``tpi apply``/``destroy`` like a user.
 
-Reports apply -> first-log latency, workdir push GB/s (task storage), HBM staging GB/s,
+Reports apply -> first-log latency, workdir push GB/s (task storage), HBM staging GB/s
+(by the runtime's stager before the rank starts, or ``--stage off``: by train.py itself),
 training step time and the end-to-end wall time.
 """
 from __future__ import annotations
@@ -26,7 +27,7 @@ resource "iterative_task" "train" {
   cloud   = "%(cloud)s"
   machine = "%(machine)s"
   timeout = 3600
-  environment = { TPI_FRAMEWORK_ROOT = "%(root)s", TPI_STAGE_ZERO_COPY = "%(zc)s" }
+  environment = { TPI_FRAMEWORK_ROOT = "%(root)s", TPI_STAGE = "%(stage)s" }
   storage {
     workdir = "."
     output  = "results"
@@ -62,9 +63,9 @@ def main():
     p.add_argument("--cloud", default="mi355x")
     p.add_argument("--machine", default="m+mi355x")
     p.add_argument("--base", default=None, help="scratch directory (default $TMPDIR)")
-    p.add_argument("--zero-copy", choices=("0", "1"), default="0",
-                   help="stage large page-cached files by DMA from their pages (1) or through "
-                        "pinned bounce buffers (0)")
+    p.add_argument("--stage", choices=("auto", "off"), default="auto",
+                   help="auto: the runtime's stager puts the workdir in HBM before train.py "
+                        "starts; off: train.py stages it itself (library path)")
     args = p.parse_args()
     base = tempfile.mkdtemp(prefix="tpi-workdir-", dir=args.base)
     try:
@@ -81,7 +82,7 @@ def main():
         with open(os.path.join(work, "main.tf"), "w") as handle:
             handle.write(MAIN_TF % {"cloud": args.cloud, "machine": args.machine, "root": ROOT,
                                     "python": sys.executable, "steps": args.steps,
-                                    "zc": args.zero_copy})
+                                    "stage": args.stage})
         env = dict(os.environ, TPI_STATE_ROOT=os.path.join(base, "state"))
         tpi = [sys.executable, os.path.join(ROOT, "bin", "tpi")]
         t0 = time.perf_counter()
@@ -118,8 +119,11 @@ def main():
             "apply_s": round(apply_s, 3),
             "push_GBps": round(total / apply_s / 1e9, 2) if apply_s else None,
             "stage_GBps": stats.get("stage_GBps"), "train_step_ms": stats.get("step_ms"),
-            "stage_stats": {k: stats.get(k) for k in ("load_s", "read_s", "zero_copy_files",
-                                                       "broadcast_s", "files")},
+            "stage_stats": {k: stats.get(k) for k in ("attach_s", "load_ms", "read_ms",
+                                                       "fanout_ms", "verify_ms", "load_GBps",
+                                                       "staged_GBps", "verified", "load_s",
+                                                       "read_s", "files")},
+            "staging": "runtime (tpi-stager)" if args.stage == "auto" else "train.py",
             "end_to_end_s": round(wall, 2), "apply_ok": apply.returncode == 0,
             "destroy_ok": d.returncode == 0,
         }

@@ -62,7 +62,18 @@ def main():
     log("rank %d/%d on %s (machine %s)" % (rank, world, device,
                                           os.environ.get("TPI_MACHINE_IDENTITY", "-")))
     stats = {}
-    if args.stage:
+    if args.stage and os.environ.get("TPI_HBM_WORKDIR"):
+        # the runtime staged the workdir before this rank started (tpi-stager): map it
+        from terraform_provider_iterative_amd.runtime.stage import attach
+
+        t0 = time.perf_counter()
+        staged = attach()
+        stats["attach_s"] = time.perf_counter() - t0
+        stats["stage_GBps"] = staged.stats.get("staged_GBps")
+        stats.update({k: v for k, v in staged.stats.items() if isinstance(v, (int, float, bool, str))})
+        log("workdir in HBM: %d files, %.2f GB, attached in %.4fs (%s)" % (
+            len(staged.files), staged.total / 1e9, stats["attach_s"], json.dumps(stats)))
+    elif args.stage:  # staging disabled for the task (TPI_STAGE=off / small): do it here
         from terraform_provider_iterative_amd.runtime.workdir import stage_workdir
 
         t0 = time.perf_counter()

@@ -14,12 +14,12 @@
 #   prof         rocprofv3 --kernel-trace --stats of bench16 + rocpd summary
 #   pmc-codec    PMC pass over the codec kernels alone (one counter block per run)
 #   kernels      bench/bench_kernels.py (device kernel GB/s)
-#   workdir      bench/bench_workdir.py --gb 10 (config 2: staging into HBM)
+#   workdir      bench/bench_workdir.py --gb 10 (config 2: the runtime stages the workdir
+#                into HBM before train.py starts; GPU_ARGS_workdir="--stage off" = library path)
 #   preempt      bench/bench_preempt.py --gb 100 (config 4 end to end)
 #   async        bench/bench_async.py --gb 100
 #   concurrent   bench/bench_concurrent.py (config 5)
 #   rehearse     bench.py at 2 and 4 ranks sharing the one GPU (gloo control plane)
-#   stager       bench/bench_stager.py (runtime HBM staging + fan-out of a task workdir)
 #
 # Extra arguments for a job: GPU_ARGS_<job>="..." (e.g. GPU_ARGS_bench="--steps 5").
 set -o pipefail
@@ -60,8 +60,6 @@ run_job() {
              > "$OUT/async.json" 2> "$OUT/async.log" ;;
     concurrent) timeout -k 10 600 python bench/bench_concurrent.py $extra \
                   > "$OUT/concurrent.json" 2> "$OUT/concurrent.log" ;;
-    stager) timeout -k 10 600 python bench/bench_stager.py $extra \
-              > "$OUT/stager.json" 2> "$OUT/stager.log" ;;
     rehearse)
       for n in 2 4; do
         TPI_BENCH_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 \

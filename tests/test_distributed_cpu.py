@@ -74,6 +74,23 @@ def test_write_back(tmp_path):
     assert (out / "x.bin").read_bytes()[:6] == b"xyzabc"
 
 
+def test_sync_writes_back_only_dirty_shards(tmp_path):
+    from terraform_provider_iterative_amd.runtime.workdir import stage_workdir
+
+    root = tmp_path / "src"
+    root.mkdir()
+    (root / "a.bin").write_bytes(bytes(range(256)) * 8192)   # 2 MiB: 2 shards
+    (root / "b.bin").write_bytes(b"b" * 5000)
+    staged = stage_workdir(str(root), device=torch.device("cpu"))
+    assert staged.sync(str(root))["dirty_shards"] == 0
+    staged.tensor("a.bin")[(1 << 20) + 5] = 7       # second shard of a.bin only
+    res = staged.sync(str(root))
+    assert res["dirty_shards"] == 1 and res["bytes"] == 1 << 20
+    data = (root / "a.bin").read_bytes()
+    assert data[(1 << 20) + 5] == 7 and data[:1 << 20] == (bytes(range(256)) * 4096)
+    assert staged.sync(str(root))["dirty_shards"] == 0
+
+
 def _resume_worker(rank, world, port, root, results, steps):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
