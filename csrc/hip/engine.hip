@@ -22,6 +22,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <mutex>
 #include <string>
@@ -144,6 +145,22 @@ int check_segments(const tpi_seg* segs, int n, uint64_t total) {
 // Error reporting for the other translation units of the library (internal.h).
 int tpi_fail(const std::string& what) { return fail(what); }
 
+// Progressive pinning of a (large, existing) host region: a toucher thread faults the pages
+// in window by window with a pool of threads, a registrar thread hipHostRegisters each window
+// once it is touched.  `ready` = bytes from the base that are registered (a growing prefix),
+// so a restore can DMA window k while window k+1 is still being pinned.
+struct tpi_pinner {
+  uint8_t* base = nullptr;
+  uint64_t bytes = 0, window = 0;
+  int threads = 8;
+  int device = 0;
+  std::atomic<uint64_t> touched{0}, ready{0};
+  std::atomic<bool> failed{false}, stop{false};
+  std::thread toucher, registrar;
+  std::vector<uint8_t*> registered;
+  std::string error;
+};
+
 struct tpi_engine {
   int device = 0;
   uint64_t chunk = 0, tile = 0;
@@ -174,8 +191,48 @@ struct tpi_engine {
   uint32_t* d_csize = nullptr;
   uint64_t* d_coff = nullptr;
   size_t z_cap = 0;
+  // host region registered window by window (tpi_host_pin_start): host copies are split at
+  // window boundaries and wait until their window is pinned (tpi_engine_set_host_region)
+  const uint8_t* hbase = nullptr;
+  uint64_t hbytes = 0, hwin = 0;
+  tpi_pinner* pinner = nullptr;
   std::mutex mu;
 };
+
+
+namespace {
+
+// Wait until the pinner has registered `end` bytes of the region (false: pinning failed).
+bool wait_pinned(tpi_pinner* p, uint64_t end) {
+  while (p->ready.load(std::memory_order_acquire) < end) {
+    if (p->failed.load()) return false;
+    std::this_thread::sleep_for(std::chrono::microseconds(100));
+  }
+  return true;
+}
+
+// hipMemcpyAsync for the engine's pipelines: a host side inside a window-registered region is
+// split at window boundaries (one registration per window) and waits for its window.
+hipError_t region_copy(tpi_engine* e, void* dst, const void* src, size_t n, hipMemcpyKind kind,
+                       hipStream_t s) {
+  const uint8_t* h = (const uint8_t*)(kind == hipMemcpyHostToDevice ? src : dst);
+  if (!e->hwin || kind == hipMemcpyDeviceToDevice || h < e->hbase || h >= e->hbase + e->hbytes)
+    return hipMemcpyAsync(dst, src, n, kind, s);
+  uint64_t off = (uint64_t)(h - e->hbase), done = 0;
+  while (done < n) {
+    const uint64_t at = off + done;
+    const uint64_t len = std::min<uint64_t>(n - done, (at / e->hwin + 1) * e->hwin - at);
+    if (e->pinner && !wait_pinned(e->pinner, std::min(e->hbytes, at + len)))
+      return hipErrorInvalidValue;
+    hipError_t err =
+        hipMemcpyAsync((uint8_t*)dst + done, (const uint8_t*)src + done, len, kind, s);
+    if (err != hipSuccess) return err;
+    done += len;
+  }
+  return hipSuccess;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -309,7 +366,7 @@ int prepare(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total) {
     HIP_OK(hipMalloc(&e->d_crcs, e->crc_cap * sizeof(uint32_t)));
   }
   // Descriptors are tiny; a synchronous copy keeps the host array's lifetime simple.
-  HIP_OK(hipMemcpyAsync(e->d_segs, segs, n * sizeof(tpi_seg), hipMemcpyHostToDevice,
+  HIP_OK(region_copy(e, e->d_segs, segs, n * sizeof(tpi_seg), hipMemcpyHostToDevice,
                         e->compute));
   return 0;
 }
@@ -355,13 +412,13 @@ int tpi_save(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* ho
                                    e->d_crcs, init_full, init_last, nullptr, 1, e->compute));
       HIP_OK(hipEventRecord(e->ev_a[b], e->compute));
       HIP_OK(hipStreamWaitEvent(e->copy, e->ev_a[b], 0));
-      HIP_OK(hipMemcpyAsync(dst + base, e->staging[b], len, hipMemcpyDeviceToHost, e->copy));
+      HIP_OK(region_copy(e, dst + base, e->staging[b], len, hipMemcpyDeviceToHost, e->copy));
       HIP_OK(hipEventRecord(e->ev_b[b], e->copy));
       nchunks = k + 1;
     }
   }
   const uint64_t ntiles = (total + tile - 1) / tile;
-  HIP_OK(hipMemcpyAsync(crcs_out, e->d_crcs, ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost,
+  HIP_OK(region_copy(e, crcs_out, e->d_crcs, ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost,
                         e->compute));
   HIP_OK(hipStreamSynchronize(e->copy));
   HIP_OK(hipStreamSynchronize(e->compute));
@@ -394,9 +451,9 @@ int tpi_restore(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, const
     HIP_OK(hipEventRecord(e->ev_wait, (hipStream_t)signal_stream));
     HIP_OK(hipStreamWaitEvent(e->compute, e->ev_wait, 0));
   }
-  HIP_OK(hipMemcpyAsync(e->d_crcs, crcs, ntiles * sizeof(uint32_t), hipMemcpyHostToDevice,
+  HIP_OK(region_copy(e, e->d_crcs, crcs, ntiles * sizeof(uint32_t), hipMemcpyHostToDevice,
                         e->compute));
-  HIP_OK(hipMemcpyAsync(e->d_bad, bad_init, sizeof(bad_init), hipMemcpyHostToDevice,
+  HIP_OK(region_copy(e, e->d_bad, bad_init, sizeof(bad_init), hipMemcpyHostToDevice,
                         e->compute));
   uint64_t nchunks = 0;
   if (mode == TPI_MODE_DIRECT) {
@@ -413,7 +470,7 @@ int tpi_restore(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, const
       const int b = (int)(k % e->nbuf);
       const uint64_t len = std::min(e->chunk, total - base);
       if (k >= (uint64_t)e->nbuf) HIP_OK(hipStreamWaitEvent(e->copy, e->ev_b[b], 0));
-      HIP_OK(hipMemcpyAsync(e->staging[b], src + base, len, hipMemcpyHostToDevice, e->copy));
+      HIP_OK(region_copy(e, e->staging[b], src + base, len, hipMemcpyHostToDevice, e->copy));
       HIP_OK(hipEventRecord(e->ev_a[b], e->copy));
       HIP_OK(hipStreamWaitEvent(e->compute, e->ev_a[b], 0));
       HIP_OK(tpi_launch_stream_crc(1, e->d_segs, n, base, len, e->staging[b], tile, e->tables,
@@ -424,7 +481,7 @@ int tpi_restore(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, const
     }
   }
   unsigned long long bad[2];
-  HIP_OK(hipMemcpyAsync(bad, e->d_bad, sizeof(bad), hipMemcpyDeviceToHost, e->compute));
+  HIP_OK(region_copy(e, bad, e->d_bad, sizeof(bad), hipMemcpyDeviceToHost, e->compute));
   HIP_OK(hipEventRecord(e->ev_done, e->compute));
   if (signal_stream != TPI_NO_STREAM) HIP_OK(hipStreamWaitEvent((hipStream_t)signal_stream, e->ev_done, 0));
   HIP_OK(hipStreamSynchronize(e->compute));
@@ -481,14 +538,14 @@ int tpi_sync(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* ho
   HIP_OK(tpi_launch_dirty_tiles(e->d_hash, prev, ntiles, all, e->d_idx, e->d_count,
                                 e->compute));
   unsigned int count = 0;
-  HIP_OK(hipMemcpyAsync(&count, e->d_count, sizeof(count), hipMemcpyDeviceToHost, e->compute));
+  HIP_OK(region_copy(e, &count, e->d_count, sizeof(count), hipMemcpyDeviceToHost, e->compute));
   HIP_OK(hipStreamSynchronize(e->compute));
   std::vector<uint32_t> idx(count);
   if (count) {
     HIP_OK(hipMemcpy(idx.data(), e->d_idx, count * sizeof(uint32_t), hipMemcpyDeviceToHost));
     std::sort(idx.begin(), idx.end());  // ascending: consecutive tiles coalesce into one DMA
     HIP_OK(hipMemcpy(e->d_idx, idx.data(), count * sizeof(uint32_t), hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpyAsync(e->d_crcs, crcs_inout, ntiles * sizeof(uint32_t),
+    HIP_OK(region_copy(e, e->d_crcs, crcs_inout, ntiles * sizeof(uint32_t),
                           hipMemcpyHostToDevice, e->compute));
   }
   // 3. pack the dirty tiles compactly, 4. DMA each run of consecutive tiles to its place
@@ -510,7 +567,7 @@ int tpi_sync(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* ho
       while (r < m && idx[first + r] == idx[first + r - 1] + 1) ++r;
       const uint64_t start = (uint64_t)idx[first + j] * tile;
       const uint64_t end = std::min<uint64_t>(total, (uint64_t)(idx[first + r - 1] + 1) * tile);
-      HIP_OK(hipMemcpyAsync(dst + start, (uint8_t*)e->staging[b] + (uint64_t)j * tile,
+      HIP_OK(region_copy(e, dst + start, (uint8_t*)e->staging[b] + (uint64_t)j * tile,
                             end - start, hipMemcpyDeviceToHost, e->copy));
       j = r;
     }
@@ -518,7 +575,7 @@ int tpi_sync(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* ho
     batches = k + 1;
   }
   if (count)
-    HIP_OK(hipMemcpyAsync(crcs_inout, e->d_crcs, ntiles * sizeof(uint32_t),
+    HIP_OK(region_copy(e, crcs_inout, e->d_crcs, ntiles * sizeof(uint32_t),
                           hipMemcpyDeviceToHost, e->compute));
   HIP_OK(hipStreamSynchronize(e->copy));
   HIP_OK(hipStreamSynchronize(e->compute));
@@ -595,19 +652,19 @@ int tpi_save_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* 
                                  e->d_crcs, init_full, init_last, nullptr, 1, e->compute));
     HIP_OK(tpi_launch_tpz_encode(e->zraw, len, tile, e->d_meta, e->d_csize + t0i,
                                  e->staging[b], e->compute));
-    HIP_OK(hipMemcpyAsync(csizes_out + t0i, e->d_csize + t0i, nt * sizeof(uint32_t),
+    HIP_OK(region_copy(e, csizes_out + t0i, e->d_csize + t0i, nt * sizeof(uint32_t),
                           hipMemcpyDeviceToHost, e->compute));
     HIP_OK(hipEventRecord(e->ev_a[b], e->compute));
     HIP_OK(hipEventSynchronize(e->ev_a[b]));
     uint64_t clen = 0;
     for (uint64_t i = 0; i < nt; ++i) clen += csizes_out[t0i + i];
     HIP_OK(hipStreamWaitEvent(e->copy, e->ev_a[b], 0));
-    HIP_OK(hipMemcpyAsync(dst + out, e->staging[b], clen, hipMemcpyDeviceToHost, e->copy));
+    HIP_OK(region_copy(e, dst + out, e->staging[b], clen, hipMemcpyDeviceToHost, e->copy));
     HIP_OK(hipEventRecord(e->ev_b[b], e->copy));
     out += clen;
     nchunks = k + 1;
   }
-  HIP_OK(hipMemcpyAsync(crcs_out, e->d_crcs, ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost,
+  HIP_OK(region_copy(e, crcs_out, e->d_crcs, ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost,
                         e->compute));
   HIP_OK(hipStreamSynchronize(e->copy));
   HIP_OK(hipStreamSynchronize(e->compute));
@@ -666,7 +723,7 @@ int tpi_spill(tpi_engine* e, const void* dev_src, const uint32_t* dev_crcs, uint
   uint64_t out = 0, nchunks = 0;
   if (!codec) {
     for (uint64_t base = 0; base < total; base += e->chunk, ++nchunks)
-      HIP_OK(hipMemcpyAsync(dst + base, src + base, std::min(e->chunk, total - base),
+      HIP_OK(region_copy(e, dst + base, src + base, std::min(e->chunk, total - base),
                             hipMemcpyDeviceToHost, e->copy));
     out = total;
   } else {
@@ -678,20 +735,20 @@ int tpi_spill(tpi_engine* e, const void* dev_src, const uint32_t* dev_crcs, uint
       if (k >= (uint64_t)e->nbuf) HIP_OK(hipStreamWaitEvent(e->compute, e->ev_b[b], 0));
       HIP_OK(tpi_launch_tpz_encode(src + base, len, tile, e->d_meta, e->d_csize + t0i,
                                    e->staging[b], e->compute));
-      HIP_OK(hipMemcpyAsync(csizes_out + t0i, e->d_csize + t0i, nt * sizeof(uint32_t),
+      HIP_OK(region_copy(e, csizes_out + t0i, e->d_csize + t0i, nt * sizeof(uint32_t),
                             hipMemcpyDeviceToHost, e->compute));
       HIP_OK(hipEventRecord(e->ev_a[b], e->compute));
       HIP_OK(hipEventSynchronize(e->ev_a[b]));
       uint64_t clen = 0;
       for (uint64_t i = 0; i < nt; ++i) clen += csizes_out[t0i + i];
       HIP_OK(hipStreamWaitEvent(e->copy, e->ev_a[b], 0));
-      HIP_OK(hipMemcpyAsync(dst + out, e->staging[b], clen, hipMemcpyDeviceToHost, e->copy));
+      HIP_OK(region_copy(e, dst + out, e->staging[b], clen, hipMemcpyDeviceToHost, e->copy));
       HIP_OK(hipEventRecord(e->ev_b[b], e->copy));
       out += clen;
       nchunks = k + 1;
     }
   }
-  HIP_OK(hipMemcpyAsync(crcs_out, dev_crcs, ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost,
+  HIP_OK(region_copy(e, crcs_out, dev_crcs, ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost,
                         e->copy));
   HIP_OK(hipStreamSynchronize(e->copy));
   HIP_OK(hipStreamSynchronize(e->compute));
@@ -734,11 +791,11 @@ int tpi_restore_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total,
     HIP_OK(hipEventRecord(e->ev_wait, (hipStream_t)signal_stream));
     HIP_OK(hipStreamWaitEvent(e->compute, e->ev_wait, 0));
   }
-  HIP_OK(hipMemcpyAsync(e->d_crcs, crcs, ntiles * sizeof(uint32_t), hipMemcpyHostToDevice,
+  HIP_OK(region_copy(e, e->d_crcs, crcs, ntiles * sizeof(uint32_t), hipMemcpyHostToDevice,
                         e->compute));
-  HIP_OK(hipMemcpyAsync(e->d_coff, coff.data(), (ntiles + 1) * sizeof(uint64_t),
+  HIP_OK(region_copy(e, e->d_coff, coff.data(), (ntiles + 1) * sizeof(uint64_t),
                         hipMemcpyHostToDevice, e->compute));
-  HIP_OK(hipMemcpyAsync(e->d_bad, bad_init, sizeof(bad_init), hipMemcpyHostToDevice,
+  HIP_OK(region_copy(e, e->d_bad, bad_init, sizeof(bad_init), hipMemcpyHostToDevice,
                         e->compute));
   HIP_OK(hipEventRecord(e->ev_wait, e->compute));
   HIP_OK(hipStreamWaitEvent(e->copy, e->ev_wait, 0));
@@ -750,7 +807,7 @@ int tpi_restore_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total,
     const uint64_t t0i = base / tile, nt = (len + tile - 1) / tile;
     const uint64_t cbeg = coff[t0i], cend = coff[t0i + nt];
     if (k >= (uint64_t)e->nbuf) HIP_OK(hipStreamWaitEvent(e->copy, e->ev_b[b], 0));
-    HIP_OK(hipMemcpyAsync(e->staging[b], src + cbeg, cend - cbeg, hipMemcpyHostToDevice,
+    HIP_OK(region_copy(e, e->staging[b], src + cbeg, cend - cbeg, hipMemcpyHostToDevice,
                           e->copy));
     HIP_OK(hipEventRecord(e->ev_a[b], e->copy));
     HIP_OK(hipStreamWaitEvent(e->compute, e->ev_a[b], 0));
@@ -763,7 +820,7 @@ int tpi_restore_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total,
     nchunks = k + 1;
   }
   unsigned long long bad[2];
-  HIP_OK(hipMemcpyAsync(bad, e->d_bad, sizeof(bad), hipMemcpyDeviceToHost, e->compute));
+  HIP_OK(region_copy(e, bad, e->d_bad, sizeof(bad), hipMemcpyDeviceToHost, e->compute));
   HIP_OK(hipEventRecord(e->ev_done, e->compute));
   if (signal_stream != TPI_NO_STREAM) HIP_OK(hipStreamWaitEvent((hipStream_t)signal_stream, e->ev_done, 0));
   HIP_OK(hipStreamSynchronize(e->compute));
@@ -932,6 +989,86 @@ int tpi_h2d_async(void* dev_dst, const void* host_src, uint64_t bytes, uint64_t 
   return 0;
 }
 
+tpi_pinner* tpi_host_pin_start(void* base, uint64_t bytes, uint64_t window, int threads) {
+  int device = 0;
+  if (hipGetDevice(&device) != hipSuccess) device = 0;
+  auto* p = new tpi_pinner();
+  p->base = (uint8_t*)base;
+  p->bytes = bytes;
+  p->window = std::max<uint64_t>(2ull << 20, window / (2ull << 20) * (2ull << 20));
+  p->threads = std::max(1, threads);
+  p->device = device;
+  p->toucher = std::thread([p] {
+    const uint64_t page = 4096;
+    for (uint64_t w = 0; w < p->bytes && !p->stop.load(); w += p->window) {
+      const uint64_t end = std::min(p->bytes, w + p->window);
+      const uint64_t per = ((end - w) / p->threads + page - 1) / page * page;
+      std::vector<std::thread> pool;
+      for (int t = 0; t < p->threads; ++t)
+        pool.emplace_back([p, w, end, per, t, page] {
+          const uint64_t b = w + (uint64_t)t * per, e = std::min(end, b + per);
+          volatile const uint8_t* q = p->base;
+          uint8_t sink = 0;
+          for (uint64_t o = b; o < e; o += page) sink ^= q[o];  // read fault: no data change
+          (void)sink;
+        });
+      for (auto& t : pool) t.join();
+      p->touched.store(end, std::memory_order_release);
+    }
+  });
+  p->registrar = std::thread([p] {
+    (void)hipSetDevice(p->device);
+    for (uint64_t w = 0; w < p->bytes && !p->stop.load(); w += p->window) {
+      const uint64_t end = std::min(p->bytes, w + p->window);
+      while (p->touched.load(std::memory_order_acquire) < end && !p->stop.load())
+        std::this_thread::sleep_for(std::chrono::microseconds(100));
+      if (p->stop.load()) break;
+      hipError_t err = hipHostRegister(p->base + w, end - w,
+                                       hipHostRegisterMapped | hipHostRegisterPortable);
+      if (err != hipSuccess) {
+        p->error = std::string("hipHostRegister(window) : ") + hipGetErrorString(err);
+        p->failed.store(true);
+        return;
+      }
+      p->registered.push_back(p->base + w);
+      p->ready.store(end, std::memory_order_release);
+    }
+  });
+  return p;
+}
+
+uint64_t tpi_host_pin_ready(const tpi_pinner* p) { return p->ready.load(); }
+uint64_t tpi_host_pin_window(const tpi_pinner* p) { return p->window; }
+
+// Wait for the whole region (0) or report the pinning error (-1).
+int tpi_host_pin_wait(tpi_pinner* p) {
+  if (p->toucher.joinable()) p->toucher.join();
+  if (p->registrar.joinable()) p->registrar.join();
+  if (p->failed.load()) return fail(p->error);
+  return 0;
+}
+
+// Stop (if still running), unregister every pinned window, free the pinner.
+int tpi_host_pin_release(tpi_pinner* p) {
+  if (!p) return 0;
+  p->stop.store(true);
+  if (p->toucher.joinable()) p->toucher.join();
+  if (p->registrar.joinable()) p->registrar.join();
+  for (uint8_t* w : p->registered) (void)hipHostUnregister(w);
+  delete p;
+  return 0;
+}
+
+int tpi_engine_set_host_region(tpi_engine* e, void* base, uint64_t bytes, uint64_t window,
+                               tpi_pinner* pinner) {
+  std::lock_guard<std::mutex> lk(e->mu);
+  e->hbase = (const uint8_t*)base;
+  e->hbytes = bytes;
+  e->hwin = window;
+  e->pinner = pinner;
+  return 0;
+}
+
 int tpi_host_unregister(void* ptr) {
   HIP_OK(hipHostUnregister(ptr));
   return 0;
@@ -940,7 +1077,7 @@ int tpi_host_unregister(void* ptr) {
 int tpi_h2d(tpi_engine* e, void* dev_dst, const void* host_src, uint64_t bytes) {
   std::lock_guard<std::mutex> lk(e->mu);
   HIP_OK(hipSetDevice(e->device));
-  HIP_OK(hipMemcpyAsync(dev_dst, host_src, bytes, hipMemcpyHostToDevice, e->copy));
+  HIP_OK(region_copy(e, dev_dst, host_src, bytes, hipMemcpyHostToDevice, e->copy));
   HIP_OK(hipStreamSynchronize(e->copy));
   return 0;
 }
@@ -948,7 +1085,7 @@ int tpi_h2d(tpi_engine* e, void* dev_dst, const void* host_src, uint64_t bytes) 
 int tpi_d2h(tpi_engine* e, void* host_dst, const void* dev_src, uint64_t bytes) {
   std::lock_guard<std::mutex> lk(e->mu);
   HIP_OK(hipSetDevice(e->device));
-  HIP_OK(hipMemcpyAsync(host_dst, dev_src, bytes, hipMemcpyDeviceToHost, e->copy));
+  HIP_OK(region_copy(e, host_dst, dev_src, bytes, hipMemcpyDeviceToHost, e->copy));
   HIP_OK(hipStreamSynchronize(e->copy));
   return 0;
 }

@@ -57,7 +57,7 @@ typedef struct tpi_stats {
 } tpi_stats;
 
 // Bumped whenever a signature below changes (ops/_loader.py checks it).
-#define TPI_ABI_VERSION 3
+#define TPI_ABI_VERSION 4
 
 // Library / device
 const char* tpi_last_error(void);
@@ -152,6 +152,20 @@ int tpi_host_unregister(void* ptr);
 // Read-only registration of an existing (e.g. page-cache file) mapping for DMA reads: the
 // zero-copy workdir staging path (runtime/workdir.py).  Populate the mapping first.
 int tpi_host_register_ro(void* ptr, uint64_t bytes);
+// Progressive pinning of an existing mapping (e.g. a preempted rank's spill file): pages are
+// read-faulted by `threads` workers and hipHostRegister-ed window by window in background
+// threads; tpi_host_pin_ready() is the registered prefix in bytes.  Release unregisters.
+typedef struct tpi_pinner tpi_pinner;
+tpi_pinner* tpi_host_pin_start(void* base, uint64_t bytes, uint64_t window, int threads);
+uint64_t tpi_host_pin_ready(const tpi_pinner* p);
+uint64_t tpi_host_pin_window(const tpi_pinner* p);
+int tpi_host_pin_wait(tpi_pinner* p);
+int tpi_host_pin_release(tpi_pinner* p);
+// The engine's host region is registered per `window` (pinner may be NULL once complete): its
+// copies are split at window boundaries and wait for their window (restore overlaps pinning).
+// Only the staged (sdma) pipelines support such a region.
+int tpi_engine_set_host_region(tpi_engine* e, void* base, uint64_t bytes, uint64_t window,
+                               tpi_pinner* pinner);
 // hipMemcpyAsync host -> device on `stream` (0 = legacy default stream).
 int tpi_h2d_async(void* dev_dst, const void* host_src, uint64_t bytes, uint64_t stream);
 

@@ -828,6 +828,7 @@ class Supervisor {
         const std::string msg(buf, (size_t)n);
         if (msg.find("released") != std::string::npos) got = true;
         if (msg.find("standby") != std::string::npos) r.standby_capable = true;
+        if (msg.find("restored") != std::string::npos) release_predecessors(r.index);
         continue;
       }
       if (n == 0) {
@@ -844,6 +845,18 @@ class Supervisor {
       return false;
     r.released = true;
     return true;
+  }
+
+  // The successor of rank `index` has restored its state: a predecessor that lingers after its
+  // spill (keeping its host region pinned so its teardown cannot slow the restore's DMA) may
+  // exit now.
+  void release_predecessors(int index) {
+    for (auto& d : detached_)
+      if (d.index == index && d.pid > 0) {
+        kill(d.pid, SIGUSR2);
+        event("predecessor-exit-requested", {"rank " + std::to_string(index),
+                                             "machine " + d.uuid});
+      }
   }
 
   // Released ranks become PREEMPTED now; their old process keeps draining its log and is

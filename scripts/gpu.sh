@@ -17,6 +17,7 @@
 #   workdir      bench/bench_workdir.py --gb 10 (config 2: the runtime stages the workdir
 #                into HBM before train.py starts; GPU_ARGS_workdir="--stage off" = library path)
 #   preempt      bench/bench_preempt.py --gb 100 (config 4 end to end)
+#   preempt-standby  the same with a warm standby successor (TPI_WARM_STANDBY=1)
 #   async        bench/bench_async.py --gb 100
 #   concurrent   bench/bench_concurrent.py (config 5)
 #   rehearse     bench.py at 2 and 4 ranks sharing the one GPU (gloo control plane)
@@ -56,6 +57,8 @@ run_job() {
                > "$OUT/workdir.json" 2> "$OUT/workdir.log" ;;
     preempt) timeout -k 10 900 python bench/bench_preempt.py --gb 100 $extra \
                > "$OUT/preempt.json" 2> "$OUT/preempt.log" ;;
+    preempt-standby) timeout -k 10 900 python bench/bench_preempt.py --gb 100 --standby $extra \
+                       > "$OUT/preempt-standby.json" 2> "$OUT/preempt-standby.log" ;;
     async) timeout -k 10 900 python bench/bench_async.py --gb 100 $extra \
              > "$OUT/async.json" 2> "$OUT/async.log" ;;
     concurrent) timeout -k 10 600 python bench/bench_concurrent.py $extra \

@@ -291,8 +291,16 @@ class Checkpointer:
                     numa_node = node.value
             self.engine = DeviceEngine(self.device_index, chunk_bytes, nbuf, tile_bytes)
         adopted = host.adopt(path, self.size) if path and self.plan.on_device else None
+        if adopted is not None and adopted.pinner and self.mode != MODES["sdma"]:
+            adopted.close()  # the direct (zero-copy kernel) path needs one registration
+            adopted = None
         self.region = adopted or HostRegion(self.size, path, device=self.plan.on_device,
                                             numa_node=numa_node, populate=populate)
+        if self.engine is not None and self.region.pinner:
+            # a progressively pinned region (prefetch()): copies wait for their 1 GiB window
+            hip().tpi_engine_set_host_region(self.engine.handle, ctypes.c_void_p(self.region.addr),
+                                             self.region.size, self.region.window,
+                                             self.region.pinner)
         self.slots = [_Slot(self, i, i * self.slot_bytes) for i in range(slots)]
         self.saves = 0
         self._snap = self._snap_crcs = None  # HBM snapshot of save_async

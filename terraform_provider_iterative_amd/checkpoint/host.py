@@ -20,16 +20,37 @@ import numpy as np
 from ..ops import hip
 
 
+PIN_WINDOW = 1 << 30  # progressive pinning: registration granule
+
+
 class HostRegion:
+    """``progressive=True`` (device regions): map without populating and pin in the
+    background, window by window (``tpi_host_pin_start``); the engine's copies wait for their
+    window, so a restore streams while the rest of the region is still being pinned."""
+
     def __init__(self, size: int, path: Optional[str] = None, *, device: bool = False,
-                 numa_node: int = -1, populate: bool = True, _mapped=None):
+                 numa_node: int = -1, populate: bool = True, _mapped=None,
+                 progressive: bool = False, window: int = PIN_WINDOW, threads: int = 8):
         self.size = size
         self.path = path
         self.device = device
         self.registered = False
         self._mmap = None
+        self.pinner = None
+        self.window = 0
         if _mapped is not None:  # adopted from early_prefetch(): python mmap, registered
             self._mmap, self.addr = _mapped
+            self.registered = True
+        elif device and progressive:
+            lib = hip()
+            enc = path.encode() if path else None
+            ptr = lib.tpi_host_map(enc, size, numa_node, 0)
+            if not ptr:
+                raise MemoryError("tpi_host_map(%d bytes) failed: %s" % (size, lib.error()))
+            self.addr = int(ptr)
+            self.pinner = lib.tpi_host_pin_start(ctypes.c_void_p(self.addr), size, window,
+                                                 threads)
+            self.window = int(lib.tpi_host_pin_window(self.pinner))
             self.registered = True
         elif device:
             lib = hip()
@@ -75,7 +96,10 @@ class HostRegion:
                 pass
         elif self.device:
             lib = hip()
-            if self.registered:
+            if self.pinner:  # unregisters every pinned window
+                lib.tpi_host_pin_release(self.pinner)
+                self.pinner = None
+            elif self.registered:
                 lib.tpi_host_unregister(ctypes.c_void_p(self.addr))
             lib.tpi_host_unmap(ctypes.c_void_p(self.addr), self.size)
         elif self._mmap is not None:
@@ -97,14 +121,16 @@ _prefetched: Dict[str, Tuple[threading.Thread, dict]] = {}
 _prefetch_lock = threading.Lock()
 
 
-def prefetch(path: str, device_index: Optional[int] = None, numa: bool = True) -> bool:
-    """Map and register an existing spill file in a background thread.
+def prefetch(path: str, device_index: Optional[int] = None, numa: bool = True,
+             window: int = PIN_WINDOW) -> bool:
+    """Start mapping and pinning an existing spill file in the background.
 
-    A respawned rank calls this right after ``import torch``: mapping and pinning a 100 GB
-    region takes ~2 s (``profiles/preempt_e2e_100g_round1.json``), which then overlaps the
-    rank's model construction instead of preceding the restore.  The next
-    :class:`~.checkpointer.Checkpointer` on ``path`` adopts the region.  Returns False when
-    there is nothing to prefetch.
+    A respawned rank calls this right after ``import torch``: the region is mapped at once and
+    pinned progressively (``HostRegion(progressive=True)``: read-faulted and registered 1 GiB
+    window by window in native threads), so the restore of the next
+    :class:`~.checkpointer.Checkpointer` on ``path`` -- which adopts the region -- starts on
+    the first pinned window instead of waiting ~2 s for all 100 GB
+    (``profiles/preempt_e2e_100g_round1.md``).  Returns False when there is nothing to prefetch.
     """
     if not path or not os.path.exists(path):
         return False
@@ -123,17 +149,12 @@ def prefetch(path: str, device_index: Optional[int] = None, numa: bool = True) -
             if hip().tpi_device_numa_node(dev, ctypes.byref(value)) == 0:
                 node = value.value
         box: dict = {}
-
-        def work():
-            try:
-                box["region"] = HostRegion(size, path, device=True, numa_node=node,
-                                           populate=True)
-            except Exception as error:  # surfaced as "not adopted"; the caller maps itself
-                box["error"] = error
-
-        thread = threading.Thread(target=work, name="tpi-prefetch", daemon=True)
-        thread.start()
-        _prefetched[path] = (thread, box)
+        try:
+            box["region"] = HostRegion(size, path, device=True, numa_node=node,
+                                       progressive=True, window=window)
+        except Exception as error:  # surfaced as "not adopted"; the caller maps itself
+            box["error"] = error
+        _prefetched[path] = (None, box)
     return True
 
 
@@ -144,7 +165,8 @@ def adopt(path: str, size: int) -> Optional[HostRegion]:
     if entry is None:
         return None
     thread, box = entry
-    thread.join()
+    if thread is not None:
+        thread.join()
     region = box.get("region")
     if region is not None and region.size != size:
         region.close()

@@ -163,6 +163,28 @@ def standby(prefetch_path: Optional[str] = None) -> bool:
     return True
 
 
+def _linger() -> None:
+    """After an early hand-off, stay alive (host region still pinned) until the supervisor
+    says the successor restored (SIGUSR2) or ``TPI_LINGER_SECONDS`` (default 20) pass: the
+    kernel's unpinning of a 100 GB region on exit (~1.4 s) would otherwise run during the
+    successor's restore and halve its DMA rate (profiles/preempt_e2e_100g_round1.md)."""
+    try:
+        timeout = float(os.environ.get("TPI_LINGER_SECONDS", "20"))
+    except ValueError:
+        timeout = 20.0
+    if timeout <= 0 or not hasattr(signal, "sigtimedwait"):
+        return
+    sys.stdout.flush()
+    signal.pthread_sigmask(signal.SIG_BLOCK, [signal.SIGUSR2])
+    got = signal.sigtimedwait([signal.SIGUSR2], timeout)
+    journal("predecessor-exit", "successor restored" if got else "linger timeout")
+
+
+def notify_restored() -> bool:
+    """Tell the supervisor this incarnation restored its state (its predecessor may go)."""
+    return _notify(b"restored\n")
+
+
 def _handler(signum, frame):  # pragma: no cover - exercised in subprocess tests
     if _fired.is_set():
         return
@@ -176,6 +198,7 @@ def _handler(signum, frame):  # pragma: no cover - exercised in subprocess tests
         code = PREEMPTED_EXIT_CODE
         if notify_released():
             journal("checkpoint-released", "successor may start")
+            _linger()
     except Exception as error:
         print("tpi: preemption checkpoint FAILED: %s" % error, file=sys.stderr, flush=True)
         code = 1
@@ -208,6 +231,7 @@ def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None) -> Op
         try:
             res = checkpointer.restore()
             journal("checkpoint-restored", "host region", *_describe(res))
+            notify_restored()
             return header.get("metadata", {})
         except CheckpointError as error:
             failure = error
@@ -220,6 +244,7 @@ def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None) -> Op
             raise CheckpointError("no usable checkpoint: host region: %s; %s: %s"
                                   % (failure or "none", persist_path, error)) from error
         journal("checkpoint-restored", persist_path, *_describe(res))
+        notify_restored()
         return checkpointer.header().get("metadata", {})
     if failure is not None:
         raise CheckpointError("checkpoint failed verification and no persisted copy exists: %s"

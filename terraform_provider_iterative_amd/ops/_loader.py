@@ -15,7 +15,7 @@ from typing import Optional
 
 from .. import _build
 
-ABI_VERSION = 3  # TPI_ABI_VERSION of csrc/hip/tpi_hip.h
+ABI_VERSION = 4  # TPI_ABI_VERSION of csrc/hip/tpi_hip.h
 
 _lock = threading.Lock()
 _native = None
@@ -92,6 +92,12 @@ class HipLib:
             "tpi_host_unregister": (i32, [vp]),
             "tpi_h2d": (i32, [vp, vp, vp, u64]),
             "tpi_d2h": (i32, [vp, vp, vp, u64]),
+            "tpi_host_pin_start": (vp, [vp, u64, u64, i32]),
+            "tpi_host_pin_ready": (u64, [vp]),
+            "tpi_host_pin_window": (u64, [vp]),
+            "tpi_host_pin_wait": (i32, [vp]),
+            "tpi_host_pin_release": (i32, [vp]),
+            "tpi_engine_set_host_region": (i32, [vp, vp, u64, u64, vp]),
             "tpi_loader_create": (vp, [i32, u64, i32, i32, i32]),
             "tpi_loader_destroy": (None, [vp]),
             "tpi_loader_load": (i32, [vp, vp, u64, u64, u64, vp, vp]),

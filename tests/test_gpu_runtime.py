@@ -146,6 +146,41 @@ def test_prefetched_spill_region_is_adopted(tmp_path):
     assert not prefetch(str(tmp_path / "missing"))
 
 
+@pytest.mark.parametrize("codec", ["none", "tpz1"])
+def test_progressively_pinned_region_restores_across_windows(tmp_path, codec):
+    # 2 MiB registration windows: chunks (1 MiB tiles, 3 MiB chunks) and compressed blobs
+    # straddle window boundaries, the restore runs while later windows are still pinning,
+    # and later saves into the windowed region split their copies the same way
+    from terraform_provider_iterative_amd.checkpoint import Checkpointer, host, prefetch
+
+    spill = str(tmp_path / "spill")
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    src = {"w": torch.randn(5 << 20, device="cuda", generator=gen).to(torch.bfloat16),
+           "m": torch.randn(3 << 20, device="cuda", generator=gen) * 1e-3,
+           "t": torch.randn(999, 777, device="cuda", generator=gen).t()}
+    ref = {k: v.clone() for k, v in src.items()}
+    kw = dict(tile_bytes=1 << 20, chunk_bytes=3 << 20, nbuf=2, codec=codec)
+    with Checkpointer(src, path=spill, **kw) as ck:
+        ck.save({"step": 9})
+    assert prefetch(spill, window=2 << 20)
+    dst = {k: torch.zeros_like(v) for k, v in ref.items()}
+    with Checkpointer(dst, path=spill, **kw) as ck:
+        assert ck.region.pinner and ck.region.window == 2 << 20
+        assert ck.restore().bad_tiles == 0 and ck.header()["metadata"] == {"step": 9}
+        torch.cuda.synchronize()
+        assert all(torch.equal(dst[k], ref[k]) for k in ref)
+        for v in dst.values():
+            v.mul_(2)
+        want = {k: v.clone() for k, v in dst.items()}
+        ck.save({"step": 10})
+        for v in dst.values():
+            v.zero_()
+        assert ck.restore().bad_tiles == 0
+        torch.cuda.synchronize()
+        assert all(torch.equal(dst[k], want[k]) for k in want)
+    assert spill not in host._prefetched
+
+
 def test_early_prefetched_region_is_adopted(tmp_path):
     from terraform_provider_iterative_amd.checkpoint import Checkpointer, early_prefetch, host
 
