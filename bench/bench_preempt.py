@@ -93,7 +93,8 @@ def main():
     p.add_argument("--spill-dir", default="/dev/shm")
     p.add_argument("--timeout", type=float, default=900.0)
     p.add_argument("--standby", action="store_true",
-                   help="warm standby successor (TPI_WARM_STANDBY=1), started at the preemption")
+                   help="the rank script calls preemption.standby(): its successor is started "
+                        "warm at the preemption (the supervisor's default for such scripts)")
     p.add_argument("--no-prefetch", action="store_true",
                    help="successor maps its host region only when the Checkpointer is built")
     p.add_argument("--early-prefetch", action="store_true",
@@ -123,8 +124,7 @@ def main():
                         "DRAM->restore (1 x MI355X, iterative_task)" % args.gb,
               "codec": args.codec, "spill": spill, "prefetch": not args.no_prefetch,
               "early_prefetch": args.early_prefetch, "standby": args.standby}
-    if args.standby:
-        os.environ["TPI_WARM_STANDBY"] = "1"
+    os.environ["TPI_WARM_STANDBY"] = "1" if args.standby else "0"
     try:
         task.create()
         deadline = time.time() + args.timeout

@@ -279,9 +279,11 @@ class NodeTask(Task):
             "max_restarts": int(os.environ.get("TPI_MAX_RESTARTS", "-1")),
             "grace_seconds": float(os.environ.get("TPI_GRACE_SECONDS", "30")),
             "respawn_delay": float(os.environ.get("TPI_RESPAWN_DELAY", "0")),
-            # warm standby successors (preemption.standby()): opt-in, they pay off when a
-            # spill takes longer than a rank's start-up (profiles/preempt_e2e_100g_round1.md)
-            "standby": os.environ.get("TPI_WARM_STANDBY", "0") == "1",
+            # warm standby successors for ranks that call preemption.standby(): the successor's
+            # imports overlap the spill; with progressive pinning and the lingering predecessor
+            # 100 GB recover in 3.6 s signal-to-restored instead of 5.1 s
+            # (profiles/preempt_e2e_100g_round2.md).  TPI_WARM_STANDBY=0 disables.
+            "standby": os.environ.get("TPI_WARM_STANDBY", "1") != "0",
             "reports_dir": self.reports_dir,
             "state_path": os.path.join(self.sup_dir, "state.json"),
             "events_path": os.path.join(self.sup_dir, "events.jsonl"),
