@@ -45,7 +45,10 @@ def parse_args(argv=None):
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--total-gb", type=float, default=100.0,
                    help="checkpoint size summed over all ranks (GB, 1e9 bytes)")
-    p.add_argument("--mode", choices=("sdma", "direct"), default="sdma")
+    p.add_argument("--mode", choices=("sdma", "direct"), default="sdma",
+                   help="sdma: staged pipeline, D2H on an SDMA copy engine (d2h_engine in the "
+                        "JSON; TPI_D2H_ENGINE=blit for HIP's blit kernels), H2D on HIP's copy "
+                        "engine; direct: kernels read/write host-mapped memory")
     p.add_argument("--codec", choices=("none", "tpz1"), default="tpz1")
     p.add_argument("--tile-mb", type=float, default=1.0)
     p.add_argument("--chunk-mb", type=float, default=256.0)
@@ -328,6 +331,7 @@ def main(argv=None):
                        "tile_bytes": ck.plan.tile_bytes,
                        "chunk_bytes": ck.engine.chunk_bytes if ck.engine else None,
                        "mode": args.mode, "codec": args.codec,
+                       "d2h_engine": ck.engine.d2h_engine if ck.engine else None,
                        "tensors_per_rank": len(tensors)},
             "save_GBps": round(total * args.steps / save_max / 1e9, 3),
             "restore_GBps": round(total * args.steps / restore_max / 1e9, 3),

@@ -196,6 +196,9 @@ struct tpi_engine {
   const uint8_t* hbase = nullptr;
   uint64_t hbytes = 0, hwin = 0;
   tpi_pinner* pinner = nullptr;
+  // D2H on an SDMA engine (sdma.cpp), one lane per staging buffer + one for direct spills;
+  // nullptr = hipMemcpyAsync on the copy stream (TPI_D2H_ENGINE=blit, or no engine)
+  tpi_sdma* sdma = nullptr;
   std::mutex mu;
 };
 
@@ -230,6 +233,64 @@ hipError_t region_copy(tpi_engine* e, void* dst, const void* src, size_t n, hipM
     done += len;
   }
   return hipSuccess;
+}
+
+// D2H of one piece on SDMA lane `lane`, split at pinned-window boundaries like region_copy.
+int sdma_region_d2h(tpi_engine* e, int lane, void* dst, const void* src, size_t n) {
+  const uint8_t* h = (const uint8_t*)dst;
+  if (!e->hwin || h < e->hbase || h >= e->hbase + e->hbytes)
+    return tpi_sdma_d2h(e->sdma, lane, dst, src, n);
+  uint64_t off = (uint64_t)(h - e->hbase), done = 0;
+  while (done < n) {
+    const uint64_t at = off + done;
+    const uint64_t len = std::min<uint64_t>(n - done, (at / e->hwin + 1) * e->hwin - at);
+    if (e->pinner && !wait_pinned(e->pinner, std::min(e->hbytes, at + len)))
+      return fail("host region pinning failed");
+    if (tpi_sdma_d2h(e->sdma, lane, (uint8_t*)dst + done, (const uint8_t*)src + done, len))
+      return -1;
+    done += len;
+  }
+  return 0;
+}
+
+// The pipelines' D2H legs.  Staging buffer b is free again once its copies are done:
+//   blit: the copy stream records copied[b]; the producer stream waits for it.
+//   SDMA: the copies of buffer b are signalled on lane b; the host waits for the lane before
+//         the producer writes the buffer again, and issues a copy once the producer's event
+//         (packed[b]) has completed.
+int staging_free(tpi_engine* e, int b, hipStream_t producer) {
+  if (e->sdma) return tpi_sdma_wait(e->sdma, b);
+  HIP_OK(hipStreamWaitEvent(producer, e->ev_b[b], 0));
+  return 0;
+}
+
+// Make the producer's work up to now (recorded as packed[b]) the precondition of the copies
+// that follow for buffer b.
+int staging_ready(tpi_engine* e, int b, hipStream_t producer) {
+  HIP_OK(hipEventRecord(e->ev_a[b], producer));
+  if (e->sdma) {
+    HIP_OK(hipEventSynchronize(e->ev_a[b]));
+  } else {
+    HIP_OK(hipStreamWaitEvent(e->copy, e->ev_a[b], 0));
+  }
+  return 0;
+}
+
+int staging_d2h(tpi_engine* e, int b, void* dst, const void* src, size_t n) {
+  if (e->sdma) return sdma_region_d2h(e, b, dst, src, n);
+  HIP_OK(region_copy(e, dst, src, n, hipMemcpyDeviceToHost, e->copy));
+  return 0;
+}
+
+int staging_sent(tpi_engine* e, int b) {
+  if (!e->sdma) HIP_OK(hipEventRecord(e->ev_b[b], e->copy));
+  return 0;
+}
+
+int drain_d2h(tpi_engine* e) {
+  if (e->sdma && tpi_sdma_wait_all(e->sdma)) return -1;
+  HIP_OK(hipStreamSynchronize(e->copy));
+  return 0;
 }
 
 }  // namespace
@@ -313,6 +374,7 @@ tpi_engine* tpi_engine_create(int device, uint64_t chunk_bytes, int nbuf, uint64
     tpi_engine_destroy(e);
     return nullptr;
   }
+  e->sdma = tpi_sdma_open(device, nbuf + 1);
   return e;
 }
 
@@ -322,6 +384,7 @@ void tpi_engine_destroy(tpi_engine* e) {
   (void)hipSetDevice(e->device);
   if (e->compute) (void)hipStreamSynchronize(e->compute);
   if (e->copy) (void)hipStreamSynchronize(e->copy);
+  tpi_sdma_close(e->sdma);  // waits for copies still in flight
   for (void* p : e->staging)
     if (p) (void)hipFree(p);
   for (hipEvent_t ev : e->ev_a)
@@ -346,6 +409,7 @@ void tpi_engine_destroy(tpi_engine* e) {
 
 uint64_t tpi_engine_tile_bytes(const tpi_engine* e) { return e->tile; }
 uint64_t tpi_engine_chunk_bytes(const tpi_engine* e) { return e->chunk; }
+uint32_t tpi_engine_d2h_engine(const tpi_engine* e) { return tpi_sdma_engine(e->sdma); }
 
 }  // extern "C"
 
@@ -354,6 +418,8 @@ namespace {
 int prepare(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total) {
   if (check_segments(segs, n, total)) return -1;
   HIP_OK(hipSetDevice(e->device));
+  // a previous call that failed half-way may have left copies out of a staging buffer
+  if (e->sdma && tpi_sdma_wait_all(e->sdma)) return -1;
   if ((size_t)n > e->seg_cap) {
     if (e->d_segs) HIP_OK(hipFree(e->d_segs));
     e->seg_cap = std::max<size_t>(n, 64);
@@ -406,21 +472,20 @@ int tpi_save(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* ho
     for (uint64_t base = 0, k = 0; base < total; base += e->chunk, ++k) {
       const int b = (int)(k % e->nbuf);
       const uint64_t len = std::min(e->chunk, total - base);
-      if (k >= (uint64_t)e->nbuf) HIP_OK(hipStreamWaitEvent(e->compute, e->ev_b[b], 0));
+      if (k >= (uint64_t)e->nbuf && staging_free(e, b, e->compute)) return -1;
       HIP_OK(tpi_launch_transposes(segs, n, base, len, e->staging[b], 0, e->compute));
       HIP_OK(tpi_launch_stream_crc(0, e->d_segs, n, base, len, e->staging[b], tile, e->tables,
                                    e->d_crcs, init_full, init_last, nullptr, 1, e->compute));
-      HIP_OK(hipEventRecord(e->ev_a[b], e->compute));
-      HIP_OK(hipStreamWaitEvent(e->copy, e->ev_a[b], 0));
-      HIP_OK(region_copy(e, dst + base, e->staging[b], len, hipMemcpyDeviceToHost, e->copy));
-      HIP_OK(hipEventRecord(e->ev_b[b], e->copy));
+      if (staging_ready(e, b, e->compute) || staging_d2h(e, b, dst + base, e->staging[b], len) ||
+          staging_sent(e, b))
+        return -1;
       nchunks = k + 1;
     }
   }
   const uint64_t ntiles = (total + tile - 1) / tile;
   HIP_OK(region_copy(e, crcs_out, e->d_crcs, ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost,
                         e->compute));
-  HIP_OK(hipStreamSynchronize(e->copy));
+  if (drain_d2h(e)) return -1;
   HIP_OK(hipStreamSynchronize(e->compute));
   if (stats) {
     stats->copy_ms =
@@ -557,27 +622,27 @@ int tpi_sync(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* ho
   for (uint64_t first = 0, k = 0; first < count; first += per_buf, ++k) {
     const int b = (int)(k % e->nbuf);
     const uint32_t m = (uint32_t)std::min<uint64_t>(per_buf, count - first);
-    if (k >= (uint64_t)e->nbuf) HIP_OK(hipStreamWaitEvent(e->compute, e->ev_b[b], 0));
+    if (k >= (uint64_t)e->nbuf && staging_free(e, b, e->compute)) return -1;
     HIP_OK(tpi_launch_pack_list(e->d_segs, n, total, e->d_idx + first, m, e->staging[b], tile,
                                 e->tables, e->d_crcs, init_full, init_last, e->compute));
-    HIP_OK(hipEventRecord(e->ev_a[b], e->compute));
-    HIP_OK(hipStreamWaitEvent(e->copy, e->ev_a[b], 0));
+    if (staging_ready(e, b, e->compute)) return -1;
     for (uint32_t j = 0; j < m;) {
       uint32_t r = j + 1;
       while (r < m && idx[first + r] == idx[first + r - 1] + 1) ++r;
       const uint64_t start = (uint64_t)idx[first + j] * tile;
       const uint64_t end = std::min<uint64_t>(total, (uint64_t)(idx[first + r - 1] + 1) * tile);
-      HIP_OK(region_copy(e, dst + start, (uint8_t*)e->staging[b] + (uint64_t)j * tile,
-                            end - start, hipMemcpyDeviceToHost, e->copy));
+      if (staging_d2h(e, b, dst + start, (uint8_t*)e->staging[b] + (uint64_t)j * tile,
+                      end - start))
+        return -1;
       j = r;
     }
-    HIP_OK(hipEventRecord(e->ev_b[b], e->copy));
+    if (staging_sent(e, b)) return -1;
     batches = k + 1;
   }
   if (count)
     HIP_OK(region_copy(e, crcs_inout, e->d_crcs, ntiles * sizeof(uint32_t),
                           hipMemcpyDeviceToHost, e->compute));
-  HIP_OK(hipStreamSynchronize(e->copy));
+  if (drain_d2h(e)) return -1;
   HIP_OK(hipStreamSynchronize(e->compute));
   if (!dev_prev) {
     e->hash_valid = true;
@@ -646,7 +711,7 @@ int tpi_save_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* 
     const int b = (int)(k % e->nbuf);
     const uint64_t len = std::min(e->chunk, total - base);
     const uint64_t t0i = base / tile, nt = (len + tile - 1) / tile;
-    if (k >= (uint64_t)e->nbuf) HIP_OK(hipStreamWaitEvent(e->compute, e->ev_b[b], 0));
+    if (k >= (uint64_t)e->nbuf && staging_free(e, b, e->compute)) return -1;
     HIP_OK(tpi_launch_transposes(segs, n, base, len, e->zraw, 0, e->compute));
     HIP_OK(tpi_launch_stream_crc(0, e->d_segs, n, base, len, e->zraw, tile, e->tables,
                                  e->d_crcs, init_full, init_last, nullptr, 1, e->compute));
@@ -658,15 +723,14 @@ int tpi_save_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* 
     HIP_OK(hipEventSynchronize(e->ev_a[b]));
     uint64_t clen = 0;
     for (uint64_t i = 0; i < nt; ++i) clen += csizes_out[t0i + i];
-    HIP_OK(hipStreamWaitEvent(e->copy, e->ev_a[b], 0));
-    HIP_OK(region_copy(e, dst + out, e->staging[b], clen, hipMemcpyDeviceToHost, e->copy));
-    HIP_OK(hipEventRecord(e->ev_b[b], e->copy));
+    if (!e->sdma) HIP_OK(hipStreamWaitEvent(e->copy, e->ev_a[b], 0));
+    if (staging_d2h(e, b, dst + out, e->staging[b], clen) || staging_sent(e, b)) return -1;
     out += clen;
     nchunks = k + 1;
   }
   HIP_OK(region_copy(e, crcs_out, e->d_crcs, ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost,
                         e->compute));
-  HIP_OK(hipStreamSynchronize(e->copy));
+  if (drain_d2h(e)) return -1;
   HIP_OK(hipStreamSynchronize(e->compute));
   *stream_bytes = out;
   if (stats) {
@@ -713,6 +777,7 @@ int tpi_spill(tpi_engine* e, const void* dev_src, const uint32_t* dev_crcs, uint
   std::lock_guard<std::mutex> lk(e->mu);
   auto t0 = std::chrono::steady_clock::now();
   HIP_OK(hipSetDevice(e->device));
+  if (e->sdma && tpi_sdma_wait_all(e->sdma)) return -1;
   const uint64_t tile = e->tile;
   const uint64_t ntiles = (total + tile - 1) / tile;
   // the snapshot was packed on `compute`; everything below is ordered after it
@@ -722,9 +787,15 @@ int tpi_spill(tpi_engine* e, const void* dev_src, const uint32_t* dev_crcs, uint
   const uint8_t* src = (const uint8_t*)dev_src;
   uint64_t out = 0, nchunks = 0;
   if (!codec) {
-    for (uint64_t base = 0; base < total; base += e->chunk, ++nchunks)
-      HIP_OK(region_copy(e, dst + base, src + base, std::min(e->chunk, total - base),
-                            hipMemcpyDeviceToHost, e->copy));
+    if (e->sdma) HIP_OK(hipEventSynchronize(e->ev_wait));
+    for (uint64_t base = 0; base < total; base += e->chunk, ++nchunks) {
+      const uint64_t len = std::min(e->chunk, total - base);
+      if (e->sdma) {
+        if (sdma_region_d2h(e, e->nbuf, dst + base, src + base, len)) return -1;
+      } else {
+        HIP_OK(region_copy(e, dst + base, src + base, len, hipMemcpyDeviceToHost, e->copy));
+      }
+    }
     out = total;
   } else {
     if (prepare_codec(e, ntiles)) return -1;
@@ -732,7 +803,7 @@ int tpi_spill(tpi_engine* e, const void* dev_src, const uint32_t* dev_crcs, uint
       const int b = (int)(k % e->nbuf);
       const uint64_t len = std::min(e->chunk, total - base);
       const uint64_t t0i = base / tile, nt = (len + tile - 1) / tile;
-      if (k >= (uint64_t)e->nbuf) HIP_OK(hipStreamWaitEvent(e->compute, e->ev_b[b], 0));
+      if (k >= (uint64_t)e->nbuf && staging_free(e, b, e->compute)) return -1;
       HIP_OK(tpi_launch_tpz_encode(src + base, len, tile, e->d_meta, e->d_csize + t0i,
                                    e->staging[b], e->compute));
       HIP_OK(region_copy(e, csizes_out + t0i, e->d_csize + t0i, nt * sizeof(uint32_t),
@@ -741,16 +812,15 @@ int tpi_spill(tpi_engine* e, const void* dev_src, const uint32_t* dev_crcs, uint
       HIP_OK(hipEventSynchronize(e->ev_a[b]));
       uint64_t clen = 0;
       for (uint64_t i = 0; i < nt; ++i) clen += csizes_out[t0i + i];
-      HIP_OK(hipStreamWaitEvent(e->copy, e->ev_a[b], 0));
-      HIP_OK(region_copy(e, dst + out, e->staging[b], clen, hipMemcpyDeviceToHost, e->copy));
-      HIP_OK(hipEventRecord(e->ev_b[b], e->copy));
+      if (!e->sdma) HIP_OK(hipStreamWaitEvent(e->copy, e->ev_a[b], 0));
+      if (staging_d2h(e, b, dst + out, e->staging[b], clen) || staging_sent(e, b)) return -1;
       out += clen;
       nchunks = k + 1;
     }
   }
   HIP_OK(region_copy(e, crcs_out, dev_crcs, ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost,
                         e->copy));
-  HIP_OK(hipStreamSynchronize(e->copy));
+  if (drain_d2h(e)) return -1;
   HIP_OK(hipStreamSynchronize(e->compute));
   *stream_bytes = out;
   if (stats) {
@@ -1085,6 +1155,10 @@ int tpi_h2d(tpi_engine* e, void* dev_dst, const void* host_src, uint64_t bytes) 
 int tpi_d2h(tpi_engine* e, void* host_dst, const void* dev_src, uint64_t bytes) {
   std::lock_guard<std::mutex> lk(e->mu);
   HIP_OK(hipSetDevice(e->device));
+  if (e->sdma) {
+    if (sdma_region_d2h(e, e->nbuf, host_dst, dev_src, bytes)) return -1;
+    return tpi_sdma_wait(e->sdma, e->nbuf);
+  }
   HIP_OK(region_copy(e, host_dst, dev_src, bytes, hipMemcpyDeviceToHost, e->copy));
   HIP_OK(hipStreamSynchronize(e->copy));
   return 0;

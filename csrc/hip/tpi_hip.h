@@ -72,6 +72,9 @@ tpi_engine* tpi_engine_create(int device, uint64_t chunk_bytes, int nbuf, uint64
 void tpi_engine_destroy(tpi_engine* e);
 uint64_t tpi_engine_tile_bytes(const tpi_engine* e);
 uint64_t tpi_engine_chunk_bytes(const tpi_engine* e);
+// SDMA engine bit (hsa_amd_sdma_engine_id_t) that carries the engine's device -> host copies,
+// 0 when they run as HIP blit kernels (TPI_D2H_ENGINE=blit or no engine available).
+uint32_t tpi_engine_d2h_engine(const tpi_engine* e);
 
 // Pack `segs` (n entries, sorted by off) into a stream of `total` bytes written to `host_dst`
 // (pinned or host-mapped).  `crcs_out` (host, ceil(total/tile) entries) receives the CRC32C of

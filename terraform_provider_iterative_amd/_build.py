@@ -144,7 +144,7 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
     cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics", _define_version(),
            *srcs, "-L" + tl, "-Wl,-rpath," + tl, "-L" + ROCM_LIB, "-Wl,-rpath," + ROCM_LIB,
-           "-lrccl", "-lrocprofiler-sdk-roctx", "-o", "@OUT@"]
+           "-lrccl", "-lrocprofiler-sdk-roctx", "-ldl", "-o", "@OUT@"]
     return _build(HIP_SO, cmd, deps, force, verbose)
 
 

@@ -90,6 +90,10 @@ class DeviceEngine:
             raise CheckpointError("engine creation failed: %s" % self.lib.error())
         self.handle = handle
         self.chunk_bytes = int(self.lib.tpi_engine_chunk_bytes(handle))
+        # which engine moves device -> host bytes: an SDMA copy engine ("sdma<i>") or, with
+        # TPI_D2H_ENGINE=blit / no engine, HIP's blit kernels on the CUs ("blit")
+        bit = int(self.lib.tpi_engine_d2h_engine(handle))
+        self.d2h_engine = "sdma%d" % (bit.bit_length() - 1) if bit else "blit"
 
     def save(self, plan: PackPlan, host_addr: int, crcs: np.ndarray, mode: int,
              wait_stream: int) -> TransferResult:
