@@ -129,12 +129,14 @@ def main():
             log("step %d loss %.5f" % (step + 1, loss.item()))
         if args.sleep:
             time.sleep(args.sleep)
+        t_ck = time.perf_counter()
         if args.ckpt_every and (step + 1) % args.ckpt_every == 0:
-            t_ck = time.perf_counter()
             state.save_async({"step": step + 1})  # HBM snapshot; the PCIe spill runs behind
-            if device.type == "cuda":
-                torch.cuda.current_stream().synchronize()
-            stalls.append(time.perf_counter() - t_ck)
+        elif not preemption.tick({"step": step + 1}):  # every TPI_SYNC_INTERVAL s (default 10)
+            continue
+        if device.type == "cuda":
+            torch.cuda.current_stream().synchronize()
+        stalls.append(time.perf_counter() - t_ck)
     res = state.save({"step": int(step_t.item()), "final": True})
     if stalls:
         stats["ckpt_stall_ms"] = 1e3 * max(stalls)

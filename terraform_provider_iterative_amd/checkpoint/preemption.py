@@ -91,6 +91,112 @@ def checkpoint_all(metadata: Optional[Dict] = None) -> List[float]:
     return rates
 
 
+# -- periodic checkpoint cadence (reference: the 10 s data-sync loop, machine-script.sh.tpl:
+#    118-124, which re-syncs the workdir to the bucket whenever its newest mtime changed) ------
+
+_tick_last: Optional[float] = None
+_tick_pending: Dict[int, object] = {}  # id(checkpointer) -> PendingSave of the last tick
+
+
+def sync_interval() -> float:
+    """Seconds between periodic checkpoints (``TPI_SYNC_INTERVAL``, default 10 as in the
+    reference; 0 or less disables :func:`tick`)."""
+    try:
+        return float(os.environ.get("TPI_SYNC_INTERVAL", "10"))
+    except ValueError:
+        return 10.0
+
+
+def _collect_finished() -> bool:
+    """Journal the async spills of earlier ticks that have completed; True if none is still
+    running."""
+    running = False
+    for key, pending in list(_tick_pending.items()):
+        if not pending.done():
+            running = True
+            continue
+        del _tick_pending[key]
+        try:
+            res = pending.result()
+            journal("checkpoint-synced", "async", *_describe(res),
+                    "stall %.1f ms" % (pending.stall_s * 1e3))
+        except CheckpointError as error:
+            journal("checkpoint-sync-failed", str(error))
+    return not running
+
+
+def _agree(due: bool) -> bool:
+    """Ranks of one job checkpoint the same step: with ``torch.distributed`` initialised the
+    decision is the minimum over ranks (one 4-byte all-reduce per call; every rank must call
+    :func:`tick` at the same steps)."""
+    dist = sys.modules.get("torch.distributed")
+    if dist is None or not dist.is_available() or not dist.is_initialized() or \
+            dist.get_world_size() < 2:
+        return due
+    import torch
+
+    device = "cpu"
+    if dist.get_backend() == "nccl":
+        device = torch.device("cuda", torch.cuda.current_device())
+    flag = torch.tensor([1 if due else 0], dtype=torch.int32, device=device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    return bool(flag.item())
+
+
+def tick(metadata: Optional[Dict] = None, force: bool = False) -> bool:
+    """Periodic checkpoint hook: call it at a step boundary (where the registered tensors are
+    consistent).  Every :func:`sync_interval` seconds it checkpoints every registered
+    :class:`Checkpointer` into its host region, so a rank that dies without a SIGTERM (OOM,
+    crash, SIGKILL after the grace period) still leaves a recent checkpoint behind.
+
+    ``TPI_SYNC_MODE``:
+      ``async`` (default)  HBM snapshot + background spill (:meth:`Checkpointer.save_async`):
+                           the training stream stalls only for the snapshot, the PCIe leg
+                           overlaps the next steps.  A tick that finds the previous spill still
+                           running is skipped, never queued.
+      ``sync``             incremental (:meth:`Checkpointer.sync`): only tiles whose device
+                           digest changed since the last tick cross PCIe -- cheapest for mostly
+                           frozen state (fine-tuning adapters, embeddings); blocks the caller.
+
+    The first call arms the timer.  Returns True when this call checkpointed.  Each completed
+    checkpoint is journalled (``checkpoint-synced``) with its bytes, wire bytes and time.  In a
+    multi-rank job all ranks decide together (:func:`_agree`), so they checkpoint the same step
+    and :meth:`TrainingState.resume_consistent` finds it on every rank.
+    """
+    global _tick_last
+    if _fired.is_set() or not _registered:
+        return False
+    now = time.monotonic()
+    idle = _collect_finished()
+    if _tick_last is None and not force:
+        _tick_last = now
+        return False
+    interval = sync_interval()
+    if interval <= 0 and not force:
+        return False
+    due = idle and (force or now - _tick_last >= interval)
+    if not _agree(due):
+        return False
+    meta = {"reason": "periodic"}
+    for cb in _callbacks:
+        extra = cb()
+        if extra:
+            meta.update(extra)
+    meta.update(metadata or {})
+    mode = os.environ.get("TPI_SYNC_MODE", "async")
+    for ck in _registered:
+        if mode == "sync":
+            t0 = time.perf_counter()
+            res = ck.sync(meta)
+            journal("checkpoint-synced", "incremental", "%d dirty tiles" % res.dirty_tiles,
+                    *_describe(res), "%.1f ms" % ((time.perf_counter() - t0) * 1e3))
+        else:
+            _tick_pending[id(ck)] = ck.save_async(meta)
+    _tick_last = now
+    _collect_finished()  # host tensors save synchronously: journal them now
+    return True
+
+
 def _handoff_safe() -> bool:
     """May the successor start while this process is still exiting?  Its teardown (unpinning
     the host region) takes ~1.4 s per 100 GB but holds this process's HBM until the end, so

@@ -160,3 +160,43 @@ def test_resume_consistent_aborts_every_rank_when_one_restore_fails(tmp_path):
     assert sorted(results) == [0, 1, 2]
     for rank in range(3):
         assert results[rank].startswith("aborted") and "[1]" in results[rank], results[rank]
+
+
+def _tick_worker(rank, world, port, root, results):
+    """Periodic checkpoints in a 2-rank job: rank 1's clock is not due at the first check,
+    so neither rank checkpoints; at the next check both do, at the same step."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TPI_SYNC_INTERVAL="0.2",
+                      TPI_EVENTS_FILE=os.path.join(root, "events.jsonl"), RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import time
+
+        from terraform_provider_iterative_amd.checkpoint import Checkpointer, preemption
+
+        state = {"w": torch.zeros(2048)}
+        ck = Checkpointer(state, path=os.path.join(root, "rank%d" % rank), tile_bytes=4096)
+        preemption.register(ck)
+        decisions = [preemption.tick()]  # arms the timer on every rank
+        time.sleep(0.25 if rank == 0 else 0.0)
+        state["w"].fill_(1)
+        decisions.append(preemption.tick({"step": 1}))  # rank 1 not due yet -> nobody
+        time.sleep(0.25)
+        state["w"].fill_(2)
+        decisions.append(preemption.tick({"step": 2}))  # both due
+        ck.wait_pending()
+        results[rank] = (decisions, ck.header()["metadata"].get("step"))
+        ck.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_periodic_tick_is_collective(tmp_path):
+    manager = mp.Manager()
+    results = manager.dict()
+    mp.spawn(_tick_worker, args=(2, _free_port(), str(tmp_path), results), nprocs=2)
+    for rank in range(2):
+        decisions, step = results[rank]
+        assert decisions == [False, False, True], (rank, decisions)
+        assert step == 2
+    lines = (tmp_path / "events.jsonl").read_text().splitlines()
+    assert sum('"checkpoint-synced"' in l for l in lines) == 2

@@ -191,3 +191,62 @@ def test_machine_logs_journal(cloud):
     assert "tpi-supervisor: rank-start rank 0" in text
     assert len(task.logs()) == 1 and "hi" in task.logs()[0]  # machine-* is not a task log
     task.delete()
+
+
+@pytest.fixture()
+def fresh_preemption(monkeypatch):
+    from terraform_provider_iterative_amd.checkpoint import preemption
+
+    monkeypatch.setattr(preemption, "_registered", [])
+    monkeypatch.setattr(preemption, "_callbacks", [])
+    monkeypatch.setattr(preemption, "_tick_pending", {})
+    monkeypatch.setattr(preemption, "_tick_last", None)
+    return preemption
+
+
+@pytest.mark.parametrize("mode", ["async", "sync"])
+def test_periodic_tick_checkpoints_at_the_interval(tmp_path, monkeypatch, fresh_preemption, mode):
+    """TPI_SYNC_INTERVAL cadence (machine-script.sh.tpl:118-124): a rank that dies without a
+    SIGTERM still leaves the last periodic checkpoint behind."""
+    import json
+
+    import torch
+
+    from terraform_provider_iterative_amd.checkpoint import Checkpointer
+
+    pre = fresh_preemption
+    events = tmp_path / "events.jsonl"
+    monkeypatch.setenv("TPI_SYNC_INTERVAL", "0.1")
+    monkeypatch.setenv("TPI_SYNC_MODE", mode)
+    monkeypatch.setenv("TPI_EVENTS_FILE", str(events))
+    state = {"w": torch.zeros(5000), "step": torch.zeros((), dtype=torch.int64)}
+    spill = str(tmp_path / "spill")
+    ck = Checkpointer(state, path=spill, tile_bytes=4096)
+    pre.register(ck)
+    pre.on_preempt(lambda: {"step": int(state["step"])})
+    assert pre.tick() is False  # arms the timer
+    state["w"].fill_(3)
+    state["step"].fill_(1)
+    assert pre.tick() is False  # not due yet
+    time.sleep(0.12)
+    assert pre.tick({"extra": "x"}) is True
+    ck.wait_pending()
+    meta = ck.header()["metadata"]
+    assert meta["step"] == 1 and meta["reason"] == "periodic" and meta["extra"] == "x"
+    assert pre.tick() is False  # interval restarts
+    monkeypatch.setenv("TPI_SYNC_INTERVAL", "0")
+    time.sleep(0.12)
+    assert pre.tick() is False  # 0 disables the cadence
+    assert pre.tick(force=True) is True
+    ck.wait_pending()
+    ck.close()
+    # the "crashed" rank's successor finds the periodic checkpoint
+    fresh = {"w": torch.zeros(5000), "step": torch.zeros((), dtype=torch.int64)}
+    ck2 = Checkpointer(fresh, path=spill, tile_bytes=4096)
+    assert pre.resume(ck2)["reason"] == "periodic"
+    assert torch.equal(fresh["w"], state["w"]) and int(fresh["step"]) == 1
+    ck2.close()
+    lines = [json.loads(l) for l in events.read_text().splitlines()]
+    synced = [l for l in lines if l["code"] == "checkpoint-synced"]
+    assert len(synced) == 2
+    assert synced[0]["description"][1] == ("incremental" if mode == "sync" else "async")
