@@ -111,7 +111,7 @@ struct Spec {
   std::vector<std::string> rel;
   std::vector<tpi_file> files;
   uint64_t total = 0, chunk = 64ull << 20, shard_bytes = 1ull << 20;
-  int nbuf = 4, threads = 8;
+  int nbuf = 4, threads = 16;
   std::vector<int> devices, numa;
   double sync_interval = 10;
   bool writeback = true, host = false, verify = true;
@@ -128,7 +128,7 @@ Spec load_spec(const std::string& path) {
   s.chunk = (uint64_t)v["chunk_bytes"].num((double)s.chunk);
   s.shard_bytes = (uint64_t)v["shard_bytes"].num((double)s.shard_bytes);
   s.nbuf = (int)v["nbuf"].num(4);
-  s.threads = (int)v["threads"].num(8);
+  s.threads = (int)v["threads"].num(16);
   s.sync_interval = v["sync_interval"].num(10);
   s.writeback = v["writeback"].boolean(true);
   s.host = v["host"].boolean(false);

@@ -20,6 +20,10 @@ Knobs (task ``environment`` or the provider's environment):
 ``TPI_STAGE_METHOD``       ``sharded`` (default), ``broadcast``, ``independent``
 ``TPI_SYNC_INTERVAL``      write-back cadence in seconds (default 10, as tpl:118-124; 0 = off)
 ``TPI_STAGE_WRITEBACK``    ``1`` (default) / ``0``
+``TPI_STAGE_THREADS``      page-cache reader threads per GPU loader (default 16: 10 GB on one
+                           MI355X stages at 39 GB/s with 8, 50 GB/s with 16 -- the PCIe-bound
+                           H2D then sets the pace; profiles/config2_stager_threads_round2.json)
+``TPI_STAGE_CHUNK_BYTES``  pinned ring chunk (default 64 MiB; 256 MiB was slower: 32 GB/s)
 =========================  =====================================================================
 """
 from __future__ import annotations
@@ -89,7 +93,7 @@ def plan(root: str, sup_dir: str, devices: Sequence[int], numa: Sequence[int],
         "root": root, "files": [list(f) for f in files], "total": total,
         "devices": list(devices), "numa": list(numa), "method": method,
         "chunk_bytes": int(_env(environ, "TPI_STAGE_CHUNK_BYTES", str(64 << 20))),
-        "nbuf": 4, "threads": int(_env(environ, "TPI_STAGE_THREADS", "8")),
+        "nbuf": 4, "threads": int(_env(environ, "TPI_STAGE_THREADS", "16")),
         "shard_bytes": 1 << 20, "manifest": manifest,
         "events": os.path.join(sup_dir, "events.jsonl"),
         "sync_interval": float(_env(environ, "TPI_SYNC_INTERVAL", "10")),
@@ -240,7 +244,7 @@ class Loader:
     ``device = -1``: a host image."""
 
     def __init__(self, device: int = -1, chunk_bytes: int = 64 << 20, nbuf: int = 4,
-                 threads: int = 8, numa_node: int = -1):
+                 threads: int = 16, numa_node: int = -1):
         from ..ops import hip
 
         self.lib = hip()
