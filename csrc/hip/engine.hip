@@ -235,11 +235,29 @@ hipError_t region_copy(tpi_engine* e, void* dst, const void* src, size_t n, hipM
   return hipSuccess;
 }
 
+// An SDMA engine can only reach host pages locked for the GPU; anything else (pageable
+// memory) would fault, so it takes HIP's staged path instead.
+bool host_locked(const void* p) {
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();  // not a HIP pointer: leave no error for the next caller to see
+    return false;
+  }
+  return at.type == hipMemoryTypeHost && at.devicePointer != nullptr;
+}
+
 // D2H of one piece on SDMA lane `lane`, split at pinned-window boundaries like region_copy.
+// The producer of `src` has completed (the caller synchronised on its event).
 int sdma_region_d2h(tpi_engine* e, int lane, void* dst, const void* src, size_t n) {
   const uint8_t* h = (const uint8_t*)dst;
-  if (!e->hwin || h < e->hbase || h >= e->hbase + e->hbytes)
+  if (!e->hwin || h < e->hbase || h >= e->hbase + e->hbytes) {
+    if (!host_locked(dst)) {
+      HIP_OK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, e->copy));
+      HIP_OK(hipStreamSynchronize(e->copy));
+      return 0;
+    }
     return tpi_sdma_d2h(e->sdma, lane, dst, src, n);
+  }
   uint64_t off = (uint64_t)(h - e->hbase), done = 0;
   while (done < n) {
     const uint64_t at = off + done;

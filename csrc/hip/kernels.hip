@@ -606,7 +606,9 @@ __global__ __launch_bounds__(WG) void k_stream_hash(const tpi_seg* __restrict__ 
   const uint64_t len = umin64(tile_bytes, total - gbase);
   SegCursor cur;
   seg_load(segs, nseg, seg_find(segs, nseg, gbase + lane * 16), cur);
-  uint64_t v = seed + (uint64_t)(lane + 1) * TPI_XXH_P1;
+  // two independent round chains per lane (low and high 8 bytes of each word): a single
+  // chain of dependent 64-bit multiplies left the kernel latency-bound (4.8 TB/s)
+  uint64_t va = seed + (uint64_t)(lane + 1) * TPI_XXH_P1, vb = va ^ TPI_XXH_P2;
   uint64_t nwords = 0;
   const uint64_t full_rows = len / TPI_ROW_BYTES;
   uint64_t row = 0;
@@ -620,19 +622,19 @@ __global__ __launch_bounds__(WG) void k_stream_hash(const tpi_seg* __restrict__ 
     }
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
-      v = tpi_xxh_round(v, ((uint64_t)w[u].y << 32) | w[u].x);
-      v = tpi_xxh_round(v, ((uint64_t)w[u].w << 32) | w[u].z);
+      va = tpi_xxh_round(va, ((uint64_t)w[u].y << 32) | w[u].x);
+      vb = tpi_xxh_round(vb, ((uint64_t)w[u].w << 32) | w[u].z);
     }
     nwords += UNROLL;
   }
   for (uint64_t rel = row * TPI_ROW_BYTES + lane * 16; rel < len; rel += TPI_ROW_BYTES) {
     advance(segs, nseg, gbase + rel, cur);
     const u32x4 w = gather16(segs, cur, gbase + rel, nullptr, false);
-    v = tpi_xxh_round(v, ((uint64_t)w.y << 32) | w.x);
-    v = tpi_xxh_round(v, ((uint64_t)w.w << 32) | w.z);
+    va = tpi_xxh_round(va, ((uint64_t)w.y << 32) | w.x);
+    vb = tpi_xxh_round(vb, ((uint64_t)w.w << 32) | w.z);
     ++nwords;
   }
-  uint64_t h = tpi_xxh_avalanche(v + nwords * 16);
+  uint64_t h = tpi_xxh_avalanche(va + ((vb << 31) | (vb >> 33)) + nwords * 16);
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) h ^= __shfl_xor(h, o, 64);
   if ((lane & 63) == 0) red[lane >> 6] = h;

@@ -19,6 +19,10 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <pthread.h>
+#include <sched.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <rccl/rccl.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
 #include <string.h>
@@ -44,12 +48,39 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
+// CPUs of NUMA node `node` (sysfs cpulist "0-63,128-191"); false if unknown.
+bool node_cpus(int node, cpu_set_t* set) {
+  if (node < 0) return false;
+  FILE* f = fopen(("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist").c_str(), "r");
+  if (!f) return false;
+  char buf[4096] = {0};
+  const bool ok = fgets(buf, sizeof(buf), f) != nullptr;
+  fclose(f);
+  if (!ok) return false;
+  CPU_ZERO(set);
+  int count = 0;
+  for (char* p = buf; *p && *p != '\n';) {
+    char* end = nullptr;
+    long lo = strtol(p, &end, 10), hi = lo;
+    if (end == p) break;
+    if (*end == '-') hi = strtol(end + 1, &end, 10);
+    for (long c = lo; c <= hi && c < CPU_SETSIZE; ++c, ++count) CPU_SET((int)c, set);
+    p = *end == ',' ? end + 1 : end;
+  }
+  return count > 0;
+}
+
 // Fork-join pool: run(fn) calls fn(0..n-1) once each (fn(0) on the caller) and returns when
-// all are done.  Workers sleep on a condition variable between jobs.
+// all are done.  Workers sleep on a condition variable between jobs.  With `cpus`, the
+// workers run on those CPUs (the NUMA node of the pinned ring they fill), so the page-cache
+// copies write the ring from its own socket instead of across the inter-socket link.
 class Pool {
  public:
-  explicit Pool(int n) : n_(std::max(1, n)) {
-    for (int i = 1; i < n_; ++i) workers_.emplace_back([this, i] { loop(i); });
+  explicit Pool(int n, const cpu_set_t* cpus = nullptr) : n_(std::max(1, n)) {
+    for (int i = 1; i < n_; ++i) {
+      workers_.emplace_back([this, i] { loop(i); });
+      if (cpus) pthread_setaffinity_np(workers_.back().native_handle(), sizeof(*cpus), cpus);
+    }
   }
   ~Pool() {
     {
@@ -201,7 +232,10 @@ tpi_loader* tpi_loader_create(int device, uint64_t chunk_bytes, int nbuf, int th
   L->device = device;
   L->chunk = std::max<uint64_t>(4096, chunk_bytes / 4096 * 4096);
   L->nbuf = std::max(2, nbuf);
-  L->pool = new Pool(std::max(1, threads));
+  cpu_set_t cpus;
+  const char* pin = getenv("TPI_STAGE_PIN_THREADS");
+  const bool bind = !(pin && pin[0] == '0') && node_cpus(numa_node, &cpus);
+  L->pool = new Pool(std::max(1, threads), bind ? &cpus : nullptr);
   if (device >= 0) {
     auto bail = [&](const std::string& what) -> tpi_loader* {
       tpi_fail(what);
