@@ -11,6 +11,7 @@ from ..utils.identifier import Identifier
 from .base import Resource, Task
 from .node import NodeTask, list_tasks as _node_list
 from .remote import RemoteProviderUnavailable, RemoteTask, list_tasks as _remote_list
+from .ssh import RemoteNodeTask, is_remote, list_tasks as _ssh_list
 
 
 class UnknownProviderError(ValueError):
@@ -29,6 +30,8 @@ def _retarget(cloud: Cloud) -> Cloud:
 def new(cloud: Cloud, identifier: Identifier, task: TaskSpec) -> Task:
     cloud = _retarget(cloud)
     if cloud.provider in NODE_PROVIDERS:
+        if is_remote(cloud):  # region = "host=...": the node runtime of another host
+            return RemoteNodeTask(cloud, identifier, task)
         return NodeTask(cloud, identifier, task)
     if cloud.provider in REMOTE_PROVIDERS:
         return RemoteTask(cloud, identifier, task)
@@ -38,11 +41,11 @@ def new(cloud: Cloud, identifier: Identifier, task: TaskSpec) -> Task:
 def list_tasks(cloud: Cloud) -> List[Identifier]:
     cloud = _retarget(cloud)
     if cloud.provider in NODE_PROVIDERS:
-        return _node_list(cloud)
+        return _ssh_list(cloud) if is_remote(cloud) else _node_list(cloud)
     if cloud.provider in REMOTE_PROVIDERS:
         return _remote_list(cloud)
     raise UnknownProviderError(cloud.provider)
 
 
-__all__ = ["new", "list_tasks", "Task", "Resource", "NodeTask", "RemoteTask",
+__all__ = ["new", "list_tasks", "Task", "Resource", "NodeTask", "RemoteTask", "RemoteNodeTask",
            "RemoteProviderUnavailable", "UnknownProviderError"]
