@@ -95,12 +95,19 @@ def main():
     p.add_argument("--standby", action="store_true",
                    help="the rank script calls preemption.standby(): its successor is started "
                         "warm at the preemption (the supervisor's default for such scripts)")
+    p.add_argument("--hot", action="store_true",
+                   help="hot standby (TPI_WARM_STANDBY=hot): the successor is started with the "
+                        "rank, so it is ready to restore behind the streamed spill")
+    p.add_argument("--no-stream", action="store_true",
+                   help="TPI_STREAM_HANDOFF=0: release the successor only after the spill")
     p.add_argument("--no-prefetch", action="store_true",
                    help="successor maps its host region only when the Checkpointer is built")
     p.add_argument("--early-prefetch", action="store_true",
                    help="successor maps + pins the spill before importing torch (measured "
                         "slower on MI355X: the pinning stalls the import)")
     args = p.parse_args()
+    if args.hot:
+        args.standby = True
 
     from terraform_provider_iterative_amd import backends
     from terraform_provider_iterative_amd.models.cloud import (Cloud, Credentials,
@@ -116,15 +123,21 @@ def main():
     script = RANK % {"python": sys.executable, "root": ROOT, "spill": spill, "gb": args.gb,
                      "codec": args.codec, "prefetch": not args.no_prefetch,
                      "early": args.early_prefetch, "standby": args.standby}
+    # the ranks' runtime knobs travel as task variables (the rank environment is the task's)
+    rank_env = {"TPI_TASK": "true", "TPI_STREAM_HANDOFF": "0" if args.no_stream else "1"}
+    for knob in ("TPI_D2H_ENGINE", "TPI_STREAM_TIMEOUT", "TPI_LINGER_SECONDS"):
+        if os.environ.get(knob):
+            rank_env[knob] = os.environ[knob]
     spec = Task(size=Size(machine="m+mi355x"),
                 environment=Environment(script=script, timeout=int(args.timeout) + 60,
-                                        variables=Variables({"TPI_TASK": "true"})))
+                                        variables=Variables(rank_env)))
     task = backends.new(cloud, new_random_identifier("preempt"), spec)
     result = {"config": "Preempt-recover: SIGTERM mid-task, %.0f GB checkpoint pack->host "
                         "DRAM->restore (1 x MI355X, iterative_task)" % args.gb,
               "codec": args.codec, "spill": spill, "prefetch": not args.no_prefetch,
-              "early_prefetch": args.early_prefetch, "standby": args.standby}
-    os.environ["TPI_WARM_STANDBY"] = "1" if args.standby else "0"
+              "early_prefetch": args.early_prefetch, "standby": args.standby,
+              "hot_standby": args.hot, "stream_handoff": not args.no_stream}
+    os.environ["TPI_WARM_STANDBY"] = "hot" if args.hot else ("1" if args.standby else "0")
     try:
         task.create()
         deadline = time.time() + args.timeout
@@ -151,7 +164,9 @@ def main():
 
         t_sig, _ = first("preempt-signal")
         t_saved, saved = first("checkpoint-saved")
-        t_respawn, _ = first("respawn", t_saved or 0.0)
+        # with a streamed hand-off the successor starts before the spill has finished
+        t_respawn, _ = first("respawn", t_sig or 0.0)
+        result["streamed"] = first("checkpoint-streaming")[0] is not None
         result["early_handoff"] = first("rank-released")[0] is not None
         t_start2, _ = first("rank-start", t_respawn or 0.0)
         result["warm_standby_activated"] = first("standby-activated")[0] is not None
@@ -159,13 +174,15 @@ def main():
         if t_sig and t_saved:
             result["save_s"] = round(t_saved - t_sig, 3)
             result["save_journal"] = saved
-        if t_saved and t_respawn:
-            result["exit_to_respawn_s"] = round(t_respawn - t_saved, 3)
+        if t_saved and t_respawn:  # negative: respawned while the spill was still running
+            result["saved_to_respawn_s"] = round(t_respawn - t_saved, 3)
         if t_start2 and t_restored:  # (with a warm standby: activation -> restored)
             result["rank_start_to_restored_s"] = round(t_restored - t_start2, 3)
             result["restore_journal"] = restored
         if t_restored:
             result["signal_to_restored_s"] = round(t_restored - (t_sig or t_preempt), 3)
+            if t_saved:
+                result["saved_to_restored_s"] = round(t_restored - t_saved, 3)
         result["verified"] = any("verified True" in l for l in logs)
         result["ok"] = bool(status.get("succeeded") == 1 and result["verified"])
     finally:

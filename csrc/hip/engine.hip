@@ -199,6 +199,9 @@ struct tpi_engine {
   // D2H on an SDMA engine (sdma.cpp), one lane per staging buffer + one for direct spills;
   // nullptr = hipMemcpyAsync on the copy stream (TPI_D2H_ENGINE=blit, or no engine)
   tpi_sdma* sdma = nullptr;
+  // streaming hand-off: a save publishes {tiles, stream bytes} already in host memory here
+  // (tpi_engine_set_progress); a reader in another process restores behind it
+  uint64_t* progress = nullptr;
   std::mutex mu;
 };
 
@@ -308,6 +311,56 @@ int staging_sent(tpi_engine* e, int b) {
 int drain_d2h(tpi_engine* e) {
   if (e->sdma && tpi_sdma_wait_all(e->sdma)) return -1;
   HIP_OK(hipStreamSynchronize(e->copy));
+  return 0;
+}
+
+// Streaming hand-off, save side.  Chunk j's end: first tile after it, stream bytes after it.
+struct ChunkMark {
+  uint64_t tile_end, byte_end;
+};
+
+// Publish that chunks [0, j] are in host memory: wait for chunk j's D2H (its lane, or its
+// copied event), copy the tile CRCs it completed to the host, then release-store the
+// progress words (bytes first, tiles last: a reader acquires tiles, then reads bytes).
+int publish_chunk(tpi_engine* e, const std::vector<ChunkMark>& marks, uint64_t j,
+                  uint64_t* tiles_published, uint32_t* crcs_out) {
+  const int b = (int)(j % (uint64_t)e->nbuf);
+  if (e->sdma) {
+    if (tpi_sdma_wait(e->sdma, b)) return -1;
+  } else {
+    HIP_OK(hipEventSynchronize(e->ev_b[b]));
+  }
+  const uint64_t t_end = marks[j].tile_end;
+  if (t_end > *tiles_published) {
+    HIP_OK(hipMemcpy(crcs_out + *tiles_published, e->d_crcs + *tiles_published,
+                     (t_end - *tiles_published) * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    *tiles_published = t_end;
+  }
+  __atomic_store_n(&e->progress[1], marks[j].byte_end, __ATOMIC_RELEASE);
+  __atomic_store_n(&e->progress[0], t_end, __ATOMIC_RELEASE);
+  return 0;
+}
+
+// Streaming hand-off, restore side: block until the writer has published `tiles` tiles.
+// Fails when the writer reports failure (words[2] == 3, the progress block's state word) or
+// makes no progress for `timeout_s` (it died).
+int wait_published(const uint64_t* words, uint64_t tiles, double timeout_s) {
+  uint64_t seen = __atomic_load_n(&words[0], __ATOMIC_ACQUIRE);
+  auto last = std::chrono::steady_clock::now();
+  while (seen < tiles) {
+    if (__atomic_load_n(&words[2], __ATOMIC_ACQUIRE) == 3)  // the writer reported a failure
+      return fail("the streamed checkpoint failed in its writer");
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+    const uint64_t now_tiles = __atomic_load_n(&words[0], __ATOMIC_ACQUIRE);
+    if (now_tiles != seen) {
+      seen = now_tiles;
+      last = std::chrono::steady_clock::now();
+    } else if (std::chrono::duration<double>(std::chrono::steady_clock::now() - last).count() >
+               timeout_s) {
+      return fail("streamed checkpoint stalled at tile " + std::to_string(seen) + " of " +
+                  std::to_string(tiles) + " (writer gone?)");
+    }
+  }
   return 0;
 }
 
@@ -487,6 +540,8 @@ int tpi_save(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* ho
     nchunks = 1;
   } else {
     uint8_t* dst = (uint8_t*)host_dst;
+    std::vector<ChunkMark> marks;
+    uint64_t published = 0;
     for (uint64_t base = 0, k = 0; base < total; base += e->chunk, ++k) {
       const int b = (int)(k % e->nbuf);
       const uint64_t len = std::min(e->chunk, total - base);
@@ -497,8 +552,15 @@ int tpi_save(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* ho
       if (staging_ready(e, b, e->compute) || staging_d2h(e, b, dst + base, e->staging[b], len) ||
           staging_sent(e, b))
         return -1;
+      marks.push_back({(base + len + tile - 1) / tile, base + len});
+      // chunk k is queued behind chunk k-1 on the engine: publishing k-1 keeps it busy
+      if (e->progress && k >= 1 && publish_chunk(e, marks, k - 1, &published, crcs_out))
+        return -1;
       nchunks = k + 1;
     }
+    if (e->progress && !marks.empty() &&
+        publish_chunk(e, marks, marks.size() - 1, &published, crcs_out))
+      return -1;
   }
   const uint64_t ntiles = (total + tile - 1) / tile;
   HIP_OK(region_copy(e, crcs_out, e->d_crcs, ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost,
@@ -724,7 +786,8 @@ int tpi_save_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* 
   const uint32_t init_full = init_for(tile);
   const uint32_t init_last = init_for(total % tile ? total % tile : tile);
   uint8_t* dst = (uint8_t*)host_dst;
-  uint64_t out = 0, nchunks = 0;
+  uint64_t out = 0, nchunks = 0, published = 0;
+  std::vector<ChunkMark> marks;
   for (uint64_t base = 0, k = 0; base < total; base += e->chunk, ++k) {
     const int b = (int)(k % e->nbuf);
     const uint64_t len = std::min(e->chunk, total - base);
@@ -744,8 +807,14 @@ int tpi_save_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* 
     if (!e->sdma) HIP_OK(hipStreamWaitEvent(e->copy, e->ev_a[b], 0));
     if (staging_d2h(e, b, dst + out, e->staging[b], clen) || staging_sent(e, b)) return -1;
     out += clen;
+    marks.push_back({t0i + nt, out});
+    if (e->progress && k >= 1 && publish_chunk(e, marks, k - 1, &published, crcs_out))
+      return -1;
     nchunks = k + 1;
   }
+  if (e->progress && !marks.empty() &&
+      publish_chunk(e, marks, marks.size() - 1, &published, crcs_out))
+    return -1;
   HIP_OK(region_copy(e, crcs_out, e->d_crcs, ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost,
                         e->compute));
   if (drain_d2h(e)) return -1;
@@ -1154,6 +1223,104 @@ int tpi_engine_set_host_region(tpi_engine* e, void* base, uint64_t bytes, uint64
   e->hbytes = bytes;
   e->hwin = window;
   e->pinner = pinner;
+  return 0;
+}
+
+int tpi_engine_set_progress(tpi_engine* e, uint64_t* words) {
+  std::lock_guard<std::mutex> lk(e->mu);
+  e->progress = words;
+  return 0;
+}
+
+// Restore from a region another process is still writing (streaming hand-off): the same
+// pipeline as tpi_restore / tpi_restore_z, but chunk k's H2D starts only once the writer has
+// published its tiles (progress words[0]); its CRCs (and blob sizes) are read from the host
+// then, and uploaded per chunk.  csizes == NULL: raw stream.
+int tpi_restore_stream(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total,
+                       const void* host_src, const uint32_t* crcs, const uint32_t* csizes,
+                       const uint64_t* words, double timeout_s, uint64_t signal_stream,
+                       uint64_t* bad_tiles, int64_t* first_bad, tpi_stats* stats) {
+  Range range("tpi_restore_stream");
+  std::lock_guard<std::mutex> lk(e->mu);
+  auto t0 = std::chrono::steady_clock::now();
+  if (prepare(e, segs, n, total)) return -1;
+  const uint64_t tile = e->tile;
+  const uint64_t ntiles = (total + tile - 1) / tile;
+  const bool zipped = csizes != nullptr;
+  if (zipped && prepare_codec(e, ntiles)) return -1;
+  e->hash_valid = false;
+  const uint32_t init_full = init_for(tile);
+  const uint32_t init_last = init_for(total % tile ? total % tile : tile);
+  unsigned long long bad_init[2] = {0ull, ~0ull};
+  if (signal_stream != TPI_NO_STREAM) {
+    HIP_OK(hipEventRecord(e->ev_wait, (hipStream_t)signal_stream));
+    HIP_OK(hipStreamWaitEvent(e->compute, e->ev_wait, 0));
+  }
+  HIP_OK(region_copy(e, e->d_bad, bad_init, sizeof(bad_init), hipMemcpyHostToDevice,
+                     e->compute));
+  std::vector<uint64_t> coff(ntiles + 1, 0);
+  const uint8_t* src = (const uint8_t*)host_src;
+  uint64_t nchunks = 0;
+  for (uint64_t base = 0, k = 0; base < total; base += e->chunk, ++k) {
+    const int b = (int)(k % e->nbuf);
+    const uint64_t len = std::min(e->chunk, total - base);
+    const uint64_t t0i = base / tile, nt = (len + tile - 1) / tile;
+    if (wait_published(words, t0i + nt, timeout_s)) return -1;
+    uint64_t cbeg = base, cend = base + len;
+    if (zipped) {
+      for (uint64_t i = t0i; i < t0i + nt; ++i) {
+        const uint64_t tl = std::min(tile, total - i * tile);
+        if (csizes[i] < TPZ_HDR || csizes[i] > tpz_bound(tl) || csizes[i] % 16)
+          return fail("corrupt compressed index at tile " + std::to_string(i));
+        coff[i + 1] = coff[i] + csizes[i];
+      }
+      cbeg = coff[t0i];
+      cend = coff[t0i + nt];
+    }
+    // the chunk's CRCs (and blob offsets) go up on the copy stream ahead of its bytes, so the
+    // kernels that wait for the bytes (copied[b]) see them too; slices of different chunks
+    // are disjoint (the shared boundary offset is rewritten with the same value)
+    if (k >= (uint64_t)e->nbuf) HIP_OK(hipStreamWaitEvent(e->copy, e->ev_b[b], 0));
+    if (zipped)
+      HIP_OK(hipMemcpyAsync(e->d_coff + t0i, coff.data() + t0i, (nt + 1) * sizeof(uint64_t),
+                            hipMemcpyHostToDevice, e->copy));
+    HIP_OK(region_copy(e, e->d_crcs + t0i, crcs + t0i, nt * sizeof(uint32_t),
+                       hipMemcpyHostToDevice, e->copy));
+    HIP_OK(region_copy(e, e->staging[b], src + cbeg, cend - cbeg, hipMemcpyHostToDevice,
+                       e->copy));
+    HIP_OK(hipEventRecord(e->ev_a[b], e->copy));
+    HIP_OK(hipStreamWaitEvent(e->compute, e->ev_a[b], 0));
+    if (zipped) {
+      HIP_OK(tpi_launch_tpz_decode(e->staging[b], e->d_coff + t0i, cbeg, len, tile, e->zraw,
+                                   e->compute));
+      HIP_OK(hipEventRecord(e->ev_b[b], e->compute));
+      HIP_OK(tpi_launch_stream_crc(1, e->d_segs, n, base, len, e->zraw, tile, e->tables,
+                                   e->d_crcs, init_full, init_last, e->d_bad, 1, e->compute));
+      HIP_OK(tpi_launch_transposes(segs, n, base, len, e->zraw, 1, e->compute));
+    } else {
+      HIP_OK(tpi_launch_stream_crc(1, e->d_segs, n, base, len, e->staging[b], tile, e->tables,
+                                   e->d_crcs, init_full, init_last, e->d_bad, 1, e->compute));
+      HIP_OK(tpi_launch_transposes(segs, n, base, len, e->staging[b], 1, e->compute));
+      HIP_OK(hipEventRecord(e->ev_b[b], e->compute));
+    }
+    nchunks = k + 1;
+  }
+  unsigned long long bad[2];
+  HIP_OK(region_copy(e, bad, e->d_bad, sizeof(bad), hipMemcpyDeviceToHost, e->compute));
+  HIP_OK(hipEventRecord(e->ev_done, e->compute));
+  if (signal_stream != TPI_NO_STREAM)
+    HIP_OK(hipStreamWaitEvent((hipStream_t)signal_stream, e->ev_done, 0));
+  HIP_OK(hipStreamSynchronize(e->compute));
+  HIP_OK(hipStreamSynchronize(e->copy));
+  *bad_tiles = bad[0];
+  *first_bad = bad[0] ? (int64_t)bad[1] : -1;
+  if (stats) {
+    stats->copy_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    stats->pack_ms = 0;
+    stats->bytes = zipped ? coff[ntiles] : total;
+    stats->chunks = nchunks;
+  }
   return 0;
 }
 

@@ -8,8 +8,8 @@
 // same as the blit kernels, i.e. the PCIe Gen5 x16 wire -- so the copy can leave the CUs at no
 // cost in bandwidth.
 //
-// The copies are issued with hsa_amd_memory_async_copy_on_engine() on the runtime's preferred
-// D2H engine.  HSA is reached through the runtime HIP itself loaded (found with
+// The copies are issued with hsa_amd_memory_async_copy_on_engine() on the highest of the
+// runtime's preferred D2H engines.  HSA is reached through the runtime HIP itself loaded (found with
 // dl_iterate_phdr, bound with dlsym): torch ships its own libhsa-runtime64, and a second HSA
 // runtime in the process must never be mapped.  Ordering with HIP streams is host-side: the
 // pipelines wait for the producing kernel's event before issuing a copy, and wait for the
@@ -163,14 +163,27 @@ tpi_sdma* tpi_sdma_open(int device, int lanes) {
   q.domain = (uint32_t)p.pciDomainID;
   h.iterate_agents(match_agent, &q);
   if (!q.found) return nullptr;
-  uint32_t avail = 0, pref = 0;
+  uint32_t avail = 0, pref = 0, h2d = 0;
   if (h.engine_status(q.cpu, q.gpu, &avail) != HSA_STATUS_SUCCESS || !avail) return nullptr;
   if (h.preferred_engine(q.cpu, q.gpu, &pref) != HSA_STATUS_SUCCESS) pref = 0;
-  const uint32_t pick = (pref & avail) ? (pref & avail) : avail;
+  if (h.preferred_engine(q.gpu, q.cpu, &h2d) != HSA_STATUS_SUCCESS) h2d = 0;
+  // Candidates: the runtime's preferred D2H engines, or -- when the runtime has no preference
+  // to report (torch's bundled HSA) -- engines 1-3, the host-facing engines next to engine 0
+  // (MI355X: 57 GB/s D2H each; engines 4+ serve xGMI at 7-13 GB/s, sdma_engines_round2.md).
+  // Never the engine HIP's H2D copies run on (preferred H2D, else engine 0): a restore that
+  // streams in while a save streams out (preemption hand-off) shared engine 0 with them and
+  // both directions fell to ~33 GB/s; on engine 2 they run side by side.
+  uint32_t pick = (pref & avail) ? (pref & avail) : (avail & 0xEu);
+  pick &= ~(h2d ? h2d : 0x1u);
+  if (!pick) pick = avail;
   tpi_sdma* s = new tpi_sdma();
   s->gpu = q.gpu;
   s->cpu = q.cpu;
-  s->engine = pick & (~pick + 1);  // lowest engine of the preferred set
+  s->engine = 1u << (31 - __builtin_clz(pick));  // highest candidate
+  if (env && strncmp(env, "sdma", 4) == 0 && env[4]) {  // TPI_D2H_ENGINE=sdma<i>: that engine
+    const int id = atoi(env + 4);
+    if (id >= 0 && id < 16 && (avail & (1u << id))) s->engine = 1u << id;
+  }
   s->lanes.resize(lanes > 0 ? lanes : 1);
   return s;
 }

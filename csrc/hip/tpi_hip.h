@@ -167,6 +167,17 @@ int tpi_host_pin_release(tpi_pinner* p);
 // The engine's host region is registered per `window` (pinner may be NULL once complete): its
 // copies are split at window boundaries and wait for their window (restore overlaps pinning).
 // Only the staged (sdma) pipelines support such a region.
+// Streaming hand-off (preemption).  While `words` is set, tpi_save / tpi_save_z publish into
+// it (host memory shared with the successor process) after each chunk's device -> host copy:
+// words[1] = stream bytes in host memory, then words[0] = tiles whose bytes and CRCs (and
+// blob sizes) are there, both release-stored.  NULL stops publishing.
+int tpi_engine_set_progress(tpi_engine* e, uint64_t* words);
+// Restore while another process is still writing the region: chunk k is copied once words[0]
+// covers its tiles; `timeout_s` without progress fails the call.  csizes == NULL: raw stream.
+int tpi_restore_stream(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total,
+                       const void* host_src, const uint32_t* crcs, const uint32_t* csizes,
+                       const uint64_t* words, double timeout_s, uint64_t signal_stream,
+                       uint64_t* bad_tiles, int64_t* first_bad, tpi_stats* stats);
 int tpi_engine_set_host_region(tpi_engine* e, void* base, uint64_t bytes, uint64_t window,
                                tpi_pinner* pinner);
 // hipMemcpyAsync host -> device on `stream` (0 = legacy default stream).

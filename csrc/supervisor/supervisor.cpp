@@ -184,6 +184,7 @@ struct Rank {
   bool first_output = false;  // phase journal: first line of this incarnation seen
   bool released = false;      // wrote "released" on its notify pipe
   bool standby_capable = false;  // announced "standby" (calls preemption.standby())
+  int hot_spawns = 0;            // hot standbys started for this incarnation
   int gofd = -1;                 // standby only: write end of its activation pipe
 };
 
@@ -199,6 +200,7 @@ struct Spec {
   int master_port = 29500;
   bool gang = true, fail_fast = true, respawn_on_sigterm = true, login_shell = false;
   bool standby = false;
+  bool standby_hot = false;  // keep the standby running before any preemption
   int max_restarts = -1;
   double grace = 30, respawn_delay = 0;
   std::string reports_dir, state_path, events_path, control_path;
@@ -241,6 +243,7 @@ Spec load_spec(const std::string& path) {
   s.grace = v["grace_seconds"].num(30);
   s.respawn_delay = v["respawn_delay"].num(0);
   s.standby = v["standby"].boolean(false);
+  s.standby_hot = s.standby && v["standby_hot"].boolean(false);
   s.reports_dir = v["reports_dir"].str(s.task_dir + "/reports");
   s.state_path = v["state_path"].str(s.task_dir + "/supervisor/state.json");
   s.events_path = v["events_path"].str(s.task_dir + "/supervisor/events.jsonl");
@@ -341,6 +344,7 @@ class Supervisor {
         else pump(*owners[i - 1].first);
       }
       if (released) handoff_released();
+      if (s_.standby_hot) keep_hot_standbys();
       if (pfds[0].revents & POLLIN) handle_signals();
       if (nrank_fds < pfds.size() && (pfds[nrank_fds].revents & POLLIN)) handle_control();
       if (dirty_ || now() - last_state > 5) {
@@ -721,6 +725,20 @@ class Supervisor {
     if (sb.state != Rank::RUNNING) sb = Rank();
   }
 
+  // Hot standby (spec "standby_hot"): every running, standby-capable rank keeps a successor
+  // that has already imported its framework and initialised the GPU, so on preemption it is
+  // activated the moment the old rank releases -- with a streamed spill, while the spill is
+  // still running.  At most two per incarnation (a standby that keeps dying is not retried).
+  void keep_hot_standbys() {
+    for (auto& r : ranks_) {
+      if (r.state != Rank::RUNNING || r.pid <= 0 || !r.standby_capable || r.term_at > 0 ||
+          standby_[r.index].pid > 0 || r.hot_spawns >= 2)
+        continue;
+      ++r.hot_spawns;
+      spawn_standby(r);
+    }
+  }
+
   // Kill an unused standby; its process is reaped (and its log drained) from detached_.
   void discard_standby(int index, const char* why) {
     Rank& sb = standby_[index];
@@ -759,6 +777,7 @@ class Supervisor {
     r.started = sb.started;
     r.first_output = sb.first_output;
     r.standby_capable = sb.standby_capable;
+    r.hot_spawns = 0;
     r.restarts = restarts;
     r.reason = TermReason::NONE;
     r.term_at = 0;

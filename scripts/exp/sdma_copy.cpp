@@ -4,7 +4,7 @@
 // measures what the copy engines themselves reach, one engine and split over several.
 //
 //   hipcc -O2 -std=c++17 scripts/exp/sdma_copy.cpp -lhsa-runtime64 -o scripts/exp/sdma_copy
-//   ./sdma_copy [GiB] [register|hostmalloc]
+//   ./sdma_copy [GiB] [register|thp|hostmalloc]
 #include <hip/hip_runtime.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
@@ -64,7 +64,9 @@ static double now() {
 
 int main(int argc, char** argv) {
   const double gib = argc > 1 ? atof(argv[1]) : 1.0;
-  const bool reg = !(argc > 2 && std::string(argv[2]) == "hostmalloc");
+  const std::string kind = argc > 2 ? argv[2] : "register";
+  const bool reg = kind != "hostmalloc";
+  const bool thp = kind == "thp";  // anonymous mapping with transparent huge pages
   const size_t n = (size_t)(gib * (1ull << 30));
   HIPCK(hipSetDevice(0));
   hipDeviceProp_t p;
@@ -93,8 +95,8 @@ int main(int argc, char** argv) {
   HIPCK(hipMemset(dev, 7, n));
   void* host = nullptr;
   if (reg) {
-    host = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_POPULATE,
-                -1, 0);
+    host = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (thp) madvise(host, n, MADV_HUGEPAGE);
     memset(host, 1, n);
     HIPCK(hipHostRegister(host, n, hipHostRegisterMapped | hipHostRegisterPortable));
   } else {
@@ -209,6 +211,45 @@ int main(int argc, char** argv) {
       printf("%s 256MiB chunks, 1 engine %.1f GB/s\n", dn, reps * n / t / 1e9);
     }
     hsa_signal_destroy(sig);
+  }
+  // bidirectional: D2H of one buffer on the preferred D2H engine while H2D of another runs on
+  // the preferred H2D engine (the streamed preemption hand-off does exactly this)
+  {
+    void* dev2 = nullptr;
+    HIPCK(hipMalloc(&dev2, n));
+    void* host2 = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (thp) madvise(host2, n, MADV_HUGEPAGE);
+    memset(host2, 3, n);
+    HIPCK(hipHostRegister(host2, n, hipHostRegisterMapped | hipHostRegisterPortable));
+    uint32_t de = d2h_pref ? (d2h_pref & (~d2h_pref + 1)) : 1, he = h2d_pref ? (h2d_pref & (~h2d_pref + 1)) : 1;
+    if (he == de) he = de << 1;
+    hsa_signal_t sa, sb;
+    HSACK(hsa_signal_create(1, 0, nullptr, &sa));
+    HSACK(hsa_signal_create(1, 0, nullptr, &sb));
+    double t = 0;
+    for (int r = -1; r < reps; ++r) {
+      hsa_signal_store_relaxed(sa, 1);
+      hsa_signal_store_relaxed(sb, 1);
+      double a0 = now();
+      HSACK(hsa_amd_memory_async_copy_on_engine(hdev, ag.cpu, dev, ag.gpu, n, 0, nullptr, sa,
+                                                (hsa_amd_sdma_engine_id_t)de, true));
+      HSACK(hsa_amd_memory_async_copy_on_engine(dev2, ag.gpu, host2, ag.cpu, n, 0, nullptr, sb,
+                                                (hsa_amd_sdma_engine_id_t)he, true));
+      while (hsa_signal_wait_scacquire(sa, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
+                                       HSA_WAIT_STATE_BLOCKED) >= 1) {
+      }
+      while (hsa_signal_wait_scacquire(sb, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
+                                       HSA_WAIT_STATE_BLOCKED) >= 1) {
+      }
+      if (r >= 0) t += now() - a0;
+    }
+    printf("bidir d2h(0x%x)+h2d(0x%x) each %.1f GB/s, aggregate %.1f GB/s\n", de, he,
+           reps * n / t / 1e9, 2.0 * reps * n / t / 1e9);
+    hsa_signal_destroy(sa);
+    hsa_signal_destroy(sb);
+    HIPCK(hipHostUnregister(host2));
+    munmap(host2, n);
+    HIPCK(hipFree(dev2));
   }
   // verify the D2H landed
   HIPCK(hipMemset(dev, 0x5a, n));

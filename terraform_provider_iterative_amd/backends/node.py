@@ -284,6 +284,9 @@ class NodeTask(Task):
             # 100 GB recover in 3.6 s signal-to-restored instead of 5.1 s
             # (profiles/preempt_e2e_100g_round2.md).  TPI_WARM_STANDBY=0 disables.
             "standby": os.environ.get("TPI_WARM_STANDBY", "1") != "0",
+            # TPI_WARM_STANDBY=hot: the successor is started with the rank, not at the
+            # preemption, so it can restore behind a streamed spill
+            "standby_hot": os.environ.get("TPI_WARM_STANDBY", "1") == "hot",
             "reports_dir": self.reports_dir,
             "state_path": os.path.join(self.sup_dir, "state.json"),
             "events_path": os.path.join(self.sup_dir, "events.jsonl"),

@@ -18,6 +18,11 @@ Region layout (also the persisted file format)::
                    concatenated TPZ1 tile blobs (``ops.codec``)   (4 KiB aligned)
 
 The JSON header carries ``"complete": true`` only after a save finished, and is written last;
+a *streamed* save (preemption hand-off, :meth:`Checkpointer.save` with ``on_stream``) first
+writes a header with ``"streaming": true`` and publishes its progress in a 64-byte block at
+``entries_offset - 64`` (u64: magic ``TPIPROG1``, generation, tiles in host memory, stream bytes
+of those tiles, state 1 streaming / 2 complete / 3 failed, writer pid), so a successor restores
+tile runs as they land instead of after the whole spill;
 ``"codec"`` / ``"stream_bytes"`` say how the stream section is encoded and how long it is;
 ``"generation"`` orders the copies of a two-slot region (``Checkpointer(slots=2)``: two such
 layouts back to back, the newest complete one is the checkpoint).  The layout does not depend
@@ -46,6 +51,8 @@ from .host import HostRegion
 
 MAGIC = b"TPICKPT2"
 PREAMBLE = 32
+PROGRESS_MAGIC = struct.unpack("<Q", b"TPIPROG1")[0]
+STREAM_RUNNING, STREAM_COMPLETE, STREAM_FAILED = 1, 2, 3
 MODES = {"sdma": 0, "direct": 1}
 CODECS = ("none", "tpz1")
 
@@ -146,6 +153,28 @@ class DeviceEngine:
         return TransferResult(plan.total, time.perf_counter() - t0, int(st.chunks),
                               int(bad.value), int(first.value), wire_bytes=int(st.bytes))
 
+    def set_progress(self, words_addr: int) -> None:
+        self.lib.check(self.lib.tpi_engine_set_progress(self.handle,
+                                                        ctypes.c_void_p(words_addr or None)),
+                       "tpi_engine_set_progress")
+
+    def restore_stream(self, plan: PackPlan, host_addr: int, crcs: np.ndarray,
+                       csizes: Optional[np.ndarray], words_addr: int, timeout: float,
+                       signal_stream: int) -> TransferResult:
+        st = _Stats()
+        bad = ctypes.c_uint64(0)
+        first = ctypes.c_int64(-1)
+        t0 = time.perf_counter()
+        rc = self.lib.tpi_restore_stream(
+            self.handle, plan.segs.ctypes.data, len(plan.entries), plan.total,
+            ctypes.c_void_p(host_addr), crcs.ctypes.data,
+            ctypes.c_void_p(csizes.ctypes.data if csizes is not None else None),
+            ctypes.c_void_p(words_addr), ctypes.c_double(timeout), signal_stream,
+            ctypes.byref(bad), ctypes.byref(first), ctypes.byref(st))
+        self.lib.check(rc, "tpi_restore_stream")
+        return TransferResult(plan.total, time.perf_counter() - t0, int(st.chunks),
+                              int(bad.value), int(first.value), wire_bytes=int(st.bytes))
+
     def snapshot(self, plan: PackPlan, dev_dst: int, dev_crcs: int, wait_stream: int) -> None:
         rc = self.lib.tpi_snapshot(self.handle, plan.segs.ctypes.data, len(plan.entries),
                                    plan.total, ctypes.c_void_p(dev_dst),
@@ -232,6 +261,9 @@ class _Slot:
         self.base = base
         self.crcs = ck.region.array(base + ck.crc_offset, 4 * ck.plan.ntiles, np.uint32)
         self.csizes = ck.region.array(base + ck.csize_offset, 4 * ck.plan.ntiles, np.uint32)
+        # streamed-save progress block (see module docstring); words 2-3 are what the engine
+        # publishes into
+        self.progress = ck.region.array(base + ck.entries_offset - 64, 64, np.uint64)
         self.digests = None          # device u64 per tile: content of this slot (sync)
         self.digests_valid = False   # ... describes what the slot holds right now
 
@@ -330,6 +362,36 @@ class Checkpointer:
                 best = (slot, header)
         return best
 
+    def _streaming(self) -> Optional[Tuple[_Slot, Dict]]:
+        """A slot a streamed save is writing (or has just finished) that is newer than the
+        newest complete checkpoint: what a preempted rank's successor restores."""
+        active = self._active()
+        floor = active[1].get("generation", 0) if active else 0
+        best = None
+        for slot in self.slots:
+            try:
+                header = self.read_header(self.region.array(slot.base, self.crc_offset))
+            except (CheckpointError, ValueError):
+                continue
+            prog = slot.progress
+            if (header.get("streaming") and not header.get("complete")
+                    and int(prog[0]) == PROGRESS_MAGIC
+                    and int(prog[1]) == header.get("generation")
+                    and int(prog[4]) in (STREAM_RUNNING, STREAM_COMPLETE)
+                    and header.get("generation", 0) > floor
+                    and (best is None or header["generation"] > best[1]["generation"])):
+                best = (slot, header)
+        return best
+
+    def latest(self) -> Optional[Dict]:
+        """Header of the newest restorable checkpoint -- complete, or being streamed by a
+        preempted predecessor -- or None."""
+        streaming = self._streaming()
+        if streaming is not None:
+            return streaming[1]
+        active = self._active()
+        return active[1] if active else None
+
     def _target(self) -> Tuple[_Slot, int]:
         """(slot the next save writes, generation it gets): never the active one if there
         are two slots."""
@@ -365,7 +427,7 @@ class Checkpointer:
 
     def _write_header(self, slot: _Slot, header: Dict) -> None:
         blob = json.dumps(header).encode()
-        if len(blob) > self.header_cap:
+        if len(blob) > self.header_cap - 128:  # the progress block sits at the reserve's end
             raise CheckpointError("checkpoint metadata too large (%d bytes)" % len(blob))
         n = len(self._entries_blob)
         self.region.array(slot.base + self.entries_offset, n)[:] = np.frombuffer(
@@ -377,6 +439,7 @@ class Checkpointer:
 
     def _invalidate(self, slot: _Slot) -> None:
         self.region.array(slot.base, 8)[:] = 0
+        slot.progress[:] = 0
         slot.digests_valid = False
 
     @staticmethod
@@ -403,42 +466,78 @@ class Checkpointer:
         return self.read_header(self.region.array(0, self.crc_offset))
 
     # -- operations --------------------------------------------------------------------------
-    def save(self, metadata: Optional[Dict] = None) -> TransferResult:
-        """Pack every tensor into the region; returns bytes/seconds (GB/s via ``.gbps``)."""
+    def save(self, metadata: Optional[Dict] = None,
+             on_stream: Optional[Any] = None) -> TransferResult:
+        """Pack every tensor into the region; returns bytes/seconds (GB/s via ``.gbps``).
+
+        ``on_stream`` (preemption hand-off): the save first writes a ``streaming`` header and
+        a progress block, calls ``on_stream()`` -- which lets the successor start -- and then
+        publishes every chunk as it reaches host memory, so :meth:`restore` in the successor
+        runs behind the spill over the other direction of the link instead of after it.
+        """
         self.wait_pending()
         slot, generation = self._target()
         self._invalidate(slot)
         zipped = self.codec == "tpz1"
         dst = self.region.addr + slot.base + self.stream_offset
-        if self.engine is not None:
-            import torch
+        streaming = on_stream is not None
+        if streaming:
+            prog = slot.progress
+            prog[1], prog[2], prog[3], prog[5] = generation, 0, 0, os.getpid()
+            prog[4] = STREAM_RUNNING
+            prog[0] = PROGRESS_MAGIC
+            header = self._header(False, 0, metadata, self.codec, None, generation)
+            header["streaming"] = True
+            self._write_header(slot, header)
+        try:
+            if streaming:
+                on_stream()
+            if self.engine is not None:
+                import torch
 
-            wait = torch.cuda.current_stream(self.device_index).cuda_stream
-            if zipped:
-                res = self.engine.save_z(self.plan, dst, slot.crcs, slot.csizes, wait)
+                wait = torch.cuda.current_stream(self.device_index).cuda_stream
+                if streaming:
+                    self.engine.set_progress(slot.progress.ctypes.data + 16)
+                try:
+                    if zipped:
+                        res = self.engine.save_z(self.plan, dst, slot.crcs, slot.csizes, wait)
+                    else:
+                        res = self.engine.save(self.plan, dst, slot.crcs, self.mode, wait)
+                finally:
+                    if streaming:
+                        self.engine.set_progress(0)
             else:
-                res = self.engine.save(self.plan, dst, slot.crcs, self.mode, wait)
-        else:
-            t0 = time.perf_counter()
-            if zipped:
-                raw, crcs = host_pack(self.plan)
-                blobs, sizes = tpz.encode(raw, self.plan.tile_bytes)
-                self.region.array(slot.base + self.stream_offset, len(blobs))[:] = blobs
-                slot.csizes[:] = sizes
-                wire = len(blobs)
-            else:
-                stream = self.region.array(slot.base + self.stream_offset, self.plan.total)
-                _, crcs = host_pack(self.plan, stream)
-                wire = self.plan.total
-            slot.crcs[:] = crcs
-            res = TransferResult(self.plan.total, time.perf_counter() - t0, wire_bytes=wire)
+                res = self._host_save(slot, zipped)
+        except BaseException:
+            if streaming:
+                slot.progress[4] = STREAM_FAILED
+            raise
         res.crc = native().crc32c_combine_tiles_ptr(slot.crcs.ctypes.data, self.plan.ntiles,
                                                      self.plan.tile_bytes, self.plan.total)
         self.saves += 1
         self._write_header(slot, self._header(True, res.crc, metadata, self.codec,
                                               res.wire_bytes, generation))
+        if streaming:
+            slot.progress[3] = res.wire_bytes
+            slot.progress[2] = self.plan.ntiles
+            slot.progress[4] = STREAM_COMPLETE
         self.last_save = res
         return res
+
+    def _host_save(self, slot: _Slot, zipped: bool) -> TransferResult:
+        t0 = time.perf_counter()
+        if zipped:
+            raw, crcs = host_pack(self.plan)
+            blobs, sizes = tpz.encode(raw, self.plan.tile_bytes)
+            self.region.array(slot.base + self.stream_offset, len(blobs))[:] = blobs
+            slot.csizes[:] = sizes
+            wire = len(blobs)
+        else:
+            stream = self.region.array(slot.base + self.stream_offset, self.plan.total)
+            _, crcs = host_pack(self.plan, stream)
+            wire = self.plan.total
+        slot.crcs[:] = crcs
+        return TransferResult(self.plan.total, time.perf_counter() - t0, wire_bytes=wire)
 
     def save_async(self, metadata: Optional[Dict] = None) -> PendingSave:
         """Checkpoint without stalling the training stream on PCIe.
@@ -558,9 +657,18 @@ class Checkpointer:
         self.last_save = res
         return res
 
-    def restore(self, strict: bool = True) -> TransferResult:
-        """Unpack + verify the current checkpoint into the bound tensors."""
+    def restore(self, strict: bool = True, stream_timeout: Optional[float] = None
+                ) -> TransferResult:
+        """Unpack + verify the current checkpoint into the bound tensors.  If a preempted
+        predecessor is still streaming a newer one into the region, restore that one behind
+        its progress (``stream_timeout`` s without progress -> :class:`CheckpointError`;
+        default ``TPI_STREAM_TIMEOUT`` or 30)."""
         self.wait_pending()
+        streaming = self._streaming()
+        if streaming is not None:
+            if stream_timeout is None:
+                stream_timeout = float(os.environ.get("TPI_STREAM_TIMEOUT", "30"))
+            return self._restore_streaming(*streaming, strict=strict, timeout=stream_timeout)
         active = self._active()
         if active is None:
             header = self.header()  # raises "no checkpoint" unless an incomplete one is there
@@ -591,6 +699,42 @@ class Checkpointer:
             res = TransferResult(self.plan.total, time.perf_counter() - t0, 0, bad, first,
                                  wire_bytes=nbytes)
         res.crc = int(header.get("crc32c", 0))
+        self.last_restore = res
+        if strict and res.bad_tiles:
+            raise CheckpointError("%d corrupt tile(s), first at %d" % (res.bad_tiles,
+                                                                      res.first_bad))
+        return res
+
+    def _restore_streaming(self, slot: _Slot, header: Dict, strict: bool,
+                           timeout: float) -> TransferResult:
+        self._check_compatible(header)
+        zipped = header.get("codec", "none") == "tpz1"
+        prog = slot.progress
+        if self.engine is not None:
+            import torch
+
+            from ..ops._loader import HipError
+
+            sig = torch.cuda.current_stream(self.device_index).cuda_stream
+            try:
+                res = self.engine.restore_stream(
+                    self.plan, self.region.addr + slot.base + self.stream_offset, slot.crcs,
+                    slot.csizes if zipped else None, prog.ctypes.data + 16, timeout, sig)
+            except HipError as error:  # stalled / failed writer: no usable checkpoint here
+                raise CheckpointError(str(error)) from error
+        else:  # host tensors: wait for the whole spill, then the ordinary restore
+            last, seen = time.monotonic(), -1
+            while int(prog[4]) != STREAM_COMPLETE:
+                if int(prog[4]) == STREAM_FAILED:
+                    raise CheckpointError("the streamed checkpoint failed in its writer")
+                if int(prog[2]) != seen:
+                    seen, last = int(prog[2]), time.monotonic()
+                elif time.monotonic() - last > timeout:
+                    raise CheckpointError("streamed checkpoint stalled (writer gone?)")
+                time.sleep(0.001)
+            return self.restore(strict)
+        res.crc = native().crc32c_combine_tiles_ptr(slot.crcs.ctypes.data, self.plan.ntiles,
+                                                     self.plan.tile_bytes, self.plan.total)
         self.last_restore = res
         if strict and res.bad_tiles:
             raise CheckpointError("%d corrupt tile(s), first at %d" % (res.bad_tiles,

@@ -122,7 +122,7 @@ _prefetch_lock = threading.Lock()
 
 
 def prefetch(path: str, device_index: Optional[int] = None, numa: bool = True,
-             window: int = PIN_WINDOW) -> bool:
+             window: int = PIN_WINDOW, cancel: Optional[threading.Event] = None) -> bool:
     """Start mapping and pinning an existing spill file in the background.
 
     A respawned rank calls this right after ``import torch``: the region is mapped at once and
@@ -140,6 +140,8 @@ def prefetch(path: str, device_index: Optional[int] = None, numa: bool = True,
     with _prefetch_lock:
         if path in _prefetched:
             return True
+        if cancel is not None and cancel.is_set():  # the owner moved on (see watch_prefetch)
+            return False
         node = -1
         if numa:
             import torch
@@ -156,6 +158,27 @@ def prefetch(path: str, device_index: Optional[int] = None, numa: bool = True,
             box["error"] = error
         _prefetched[path] = (None, box)
     return True
+
+
+def watch_prefetch(path: str, cancel: threading.Event, poll: float = 0.2) -> threading.Thread:
+    """:func:`prefetch` ``path`` as soon as it exists.  A hot standby starts with its rank,
+    before the rank has created its spill file; mapping and pinning the file well before any
+    preemption leaves the successor's restore nothing to wait for but the data.  Stops when
+    ``cancel`` is set."""
+    def run():
+        while not cancel.is_set():
+            try:
+                ready = os.path.getsize(path) > 0
+            except OSError:
+                ready = False
+            if ready:
+                prefetch(path, cancel=cancel)
+                return
+            cancel.wait(poll)
+
+    thread = threading.Thread(target=run, name="tpi-watch-prefetch", daemon=True)
+    thread.start()
+    return thread
 
 
 def adopt(path: str, size: int) -> Optional[HostRegion]:

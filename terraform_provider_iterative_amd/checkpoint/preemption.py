@@ -71,8 +71,10 @@ def _describe(res) -> List[str]:
             "%.3f s" % res.seconds, "%.1f GB/s" % res.gbps]
 
 
-def checkpoint_all(metadata: Optional[Dict] = None) -> List[float]:
-    """Save every registered checkpointer; returns per-checkpointer GB/s."""
+def checkpoint_all(metadata: Optional[Dict] = None, on_stream=None) -> List[float]:
+    """Save every registered checkpointer; returns per-checkpointer GB/s.  ``on_stream``
+    (single checkpointer only): stream the save to the successor (see
+    :meth:`Checkpointer.save`); called once the successor may start."""
     meta = dict(metadata or {})
     for cb in _callbacks:
         extra = cb()
@@ -80,7 +82,7 @@ def checkpoint_all(metadata: Optional[Dict] = None) -> List[float]:
             meta.update(extra)
     rates = []
     for ck in _registered:
-        res = ck.save(meta)
+        res = ck.save(meta, on_stream=on_stream if len(_registered) == 1 else None)
         rates.append(res.gbps)
         journal("checkpoint-saved", *_describe(res))
         path = _persist_paths.get(id(ck))
@@ -216,6 +218,15 @@ def _handoff_safe() -> bool:
     return True
 
 
+def _stream_handoff() -> bool:
+    """Release the successor when the spill *starts* (TPI_STREAM_HANDOFF, default on): it
+    restores each chunk as it lands.  Needs one registered checkpointer, a supervisor to tell,
+    and room for the successor's copy of the state next to ours (:func:`_handoff_safe`)."""
+    if os.environ.get("TPI_STREAM_HANDOFF", "1") in ("0", "false", "no"):
+        return False
+    return len(_registered) == 1 and bool(os.environ.get("TPI_NOTIFY_FD")) and _handoff_safe()
+
+
 def notify_released() -> bool:
     """Tell the supervisor the spill is complete (``TPI_NOTIFY_FD``), so it can respawn this
     rank now instead of after the exit; returns whether a notification was sent."""
@@ -249,10 +260,14 @@ def standby(prefetch_path: Optional[str] = None) -> bool:
     if os.environ.get("TPI_STANDBY") != "1":
         _notify(b"standby\n")
         return False
+    cancel = threading.Event()
     if prefetch_path:
-        from .host import prefetch
+        from .host import prefetch, watch_prefetch
 
-        prefetch(prefetch_path)
+        if not prefetch(prefetch_path):
+            # hot standby (started with the rank): the spill file appears later; map and pin
+            # it then, long before a preemption
+            watch_prefetch(prefetch_path, cancel)
     fd = int(os.environ.get("TPI_STANDBY_FD", "4"))
     while True:
         try:
@@ -260,6 +275,7 @@ def standby(prefetch_path: Optional[str] = None) -> bool:
             break
         except InterruptedError:
             continue
+    cancel.set()
     if not msg.startswith(b"go"):
         os._exit(0)  # discarded before activation
     os.close(fd)
@@ -297,13 +313,23 @@ def _handler(signum, frame):  # pragma: no cover - exercised in subprocess tests
     _fired.set()
     journal("preempt-signal", "signal %d" % signum)
     t0 = time.perf_counter()
+    released = []
+
+    def stream_started():
+        # the successor starts now and restores behind the spill (other PCIe direction)
+        if notify_released():
+            released.append(True)
+            journal("checkpoint-streaming", "successor may start")
+
     try:
-        rates = checkpoint_all({"reason": "preempted", "signal": signum})
+        stream = stream_started if _stream_handoff() else None
+        rates = checkpoint_all({"reason": "preempted", "signal": signum}, on_stream=stream)
         print("tpi: preemption checkpoint saved in %.3fs (%s GB/s)" % (
             time.perf_counter() - t0, ", ".join("%.1f" % r for r in rates)), flush=True)
         code = PREEMPTED_EXIT_CODE
-        if notify_released():
-            journal("checkpoint-released", "successor may start")
+        if released or notify_released():
+            if not released:
+                journal("checkpoint-released", "successor may start")
             _linger()
     except Exception as error:
         print("tpi: preemption checkpoint FAILED: %s" % error, file=sys.stderr, flush=True)
@@ -329,11 +355,8 @@ def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None) -> Op
     is raised.
     """
     failure: Optional[CheckpointError] = None
-    try:
-        header = checkpointer.header()
-    except CheckpointError:  # no checkpoint in the region (bad magic)
-        header = None
-    if header is not None and header.get("complete"):
+    header = checkpointer.latest()  # complete, or still streaming in from the predecessor
+    if header is not None:
         try:
             res = checkpointer.restore()
             journal("checkpoint-restored", "host region", *_describe(res))

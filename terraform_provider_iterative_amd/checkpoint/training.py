@@ -125,10 +125,10 @@ class TrainingState:
 
         meta = None
         try:
-            header = self.checkpointer.header()
-            if header.get("complete"):
+            header = self.checkpointer.latest()  # complete, or streaming in (preemption)
+            if header is not None:
                 meta = header.get("metadata", {})
-        except Exception:  # no checkpoint in the region
+        except Exception:  # unreadable region
             meta = None
         if meta is None and persist_path:
             import os

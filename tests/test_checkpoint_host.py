@@ -1,5 +1,6 @@
 """Checkpointer on CPU tensors (host C++ path): save/restore/persist/load/corruption."""
 import os
+import time
 
 import numpy as np
 import pytest
@@ -180,3 +181,82 @@ def test_resume_refuses_a_corrupt_region_instead_of_starting_fresh(tmp_path):
         f.write(b"\0" * 8)
     with Checkpointer(src, path=path, tile_bytes=4096) as ck:
         assert preemption.resume(ck) is None  # truly nothing saved: fresh start
+
+
+def _stream_pair(tmp_path, codec):
+    import torch
+
+    from terraform_provider_iterative_amd.checkpoint import Checkpointer
+
+    g = torch.Generator().manual_seed(3)
+    src = {"w": torch.randn(70000, generator=g), "b": torch.randn(33, 17, generator=g).t(),
+           "i": torch.arange(5000, dtype=torch.int64)}
+    dst = {"w": torch.zeros(70000), "b": torch.zeros(17, 33), "i": torch.zeros(5000,
+                                                                             dtype=torch.int64)}
+    path = str(tmp_path / "spill")
+    writer = Checkpointer(src, path=path, tile_bytes=4096, codec=codec)
+    reader_holder = {}
+
+    def make_reader():
+        reader_holder["ck"] = Checkpointer(dst, path=path, tile_bytes=4096)
+
+    return src, dst, writer, reader_holder, make_reader
+
+
+@pytest.mark.parametrize("codec", ["none", "tpz1"])
+def test_streamed_save_is_restored_by_a_successor(tmp_path, codec):
+    """Preemption hand-off: the successor sees the streaming header as soon as the save
+    starts and restores once the writer's progress says the data is there."""
+    import threading
+
+    import torch
+
+    src, dst, writer, holder, make_reader = _stream_pair(tmp_path, codec)
+    result = {}
+
+    def successor():
+        make_reader()
+        ck = holder["ck"]
+        header = ck.latest()
+        result["streaming"] = bool(header and header.get("streaming"))
+        result["meta"] = header["metadata"]
+        result["res"] = ck.restore(stream_timeout=10)
+
+    threads = []
+
+    def on_stream():  # the supervisor would start the successor now
+        t = threading.Thread(target=successor)
+        t.start()
+        threads.append(t)
+        time.sleep(0.2)  # let it find the header mid-save
+
+    writer.save({"step": 7}, on_stream=on_stream)
+    threads[0].join(30)
+    assert result["streaming"] and result["meta"]["step"] == 7
+    assert result["res"].bad_tiles == 0
+    for k in src:
+        assert torch.equal(dst[k], src[k]), k
+    # after the save the checkpoint is an ordinary complete one
+    assert holder["ck"].latest()["complete"] and holder["ck"]._streaming() is None
+    holder["ck"].close()
+    writer.close()
+
+
+def test_failed_streamed_save_fails_the_successor(tmp_path, monkeypatch):
+    from terraform_provider_iterative_amd.checkpoint import CheckpointError, Checkpointer
+
+    src, dst, writer, holder, make_reader = _stream_pair(tmp_path, "none")
+
+    def boom(*a, **k):
+        raise RuntimeError("device lost")
+
+    monkeypatch.setattr(writer, "_host_save", boom)
+    with pytest.raises(RuntimeError):
+        writer.save({"step": 1}, on_stream=lambda: None)
+    make_reader()
+    # the failed stream is not offered for restore
+    assert holder["ck"].latest() is None
+    with pytest.raises(CheckpointError):
+        holder["ck"].restore()
+    holder["ck"].close()
+    writer.close()

@@ -421,3 +421,88 @@ def test_rollback_from_hbm_snapshot():
         assert res.bad_tiles == 0 and res.wire_bytes == 0
         for k in ref:
             assert torch.equal(src[k], ref[k]), k
+
+
+@pytest.mark.parametrize("codec", ["none", "tpz1"])
+def test_streamed_restore_follows_the_writers_progress(codec, tmp_path):
+    """Preemption hand-off on the device path: a successor restores a checkpoint that is
+    still being published, chunk by chunk, and finishes only after the last chunk."""
+    import threading
+    import time
+
+    from terraform_provider_iterative_amd.checkpoint import Checkpointer
+    from terraform_provider_iterative_amd.checkpoint import checkpointer as ckmod
+
+    g = torch.Generator().manual_seed(5)
+    src = {"a": torch.randn(3 << 20, generator=g).to(torch.bfloat16).cuda(),
+           "b": torch.randn(1 << 20, generator=g).mul(1e-3).cuda(),
+           "t": torch.randn(640, 1000, generator=g).cuda().t()}
+    path = str(tmp_path / "spill")
+    kw = dict(tile_bytes=1 << 20, chunk_bytes=2 << 20, nbuf=2, codec=codec)
+    writer = Checkpointer(src, path=path, **kw)
+    words = np.zeros(2, dtype=np.uint64)  # the engine publishes here during this save
+    writer.engine.set_progress(words.ctypes.data)
+    res = writer.save({"step": 3})
+    writer.engine.set_progress(0)
+    assert int(words[0]) == writer.plan.ntiles and int(words[1]) == res.wire_bytes
+    # turn the complete checkpoint back into one "being streamed": header + progress block
+    slot = writer.slots[0]
+    header = writer.header()
+    header.update(complete=False, streaming=True)
+    writer._write_header(slot, header)
+    prog = slot.progress
+    prog[1], prog[2], prog[3], prog[4] = header["generation"], 0, 0, ckmod.STREAM_RUNNING
+    prog[0] = ckmod.PROGRESS_MAGIC
+    dst = {k: torch.zeros_like(v) for k, v in src.items()}
+    dst["t"] = torch.zeros(640, 1000, device="cuda").t()
+    reader = Checkpointer(dst, path=path, **kw)
+    assert reader.latest()["streaming"]
+    out = {}
+
+    def successor():
+        t0 = time.perf_counter()
+        out["res"] = reader.restore(stream_timeout=20)
+        out["s"] = time.perf_counter() - t0
+
+    th = threading.Thread(target=successor)
+    th.start()
+    per = writer.engine.chunk_bytes // writer.plan.tile_bytes
+    steps = 0
+    for tiles in range(per, writer.plan.ntiles + per, per):  # one chunk every 50 ms
+        time.sleep(0.05)
+        prog[2] = min(tiles, writer.plan.ntiles)
+        steps += 1
+    prog[4] = ckmod.STREAM_COMPLETE
+    th.join(60)
+    assert out["res"].bad_tiles == 0 and out["s"] >= 0.05 * (steps - 1)
+    torch.cuda.synchronize()
+    for k in src:
+        assert torch.equal(dst[k], src[k]), k
+    reader.close()
+    writer.close()
+
+
+def test_streamed_restore_gives_up_on_a_stalled_writer(tmp_path):
+    from terraform_provider_iterative_amd.checkpoint import CheckpointError, Checkpointer
+    from terraform_provider_iterative_amd.checkpoint import checkpointer as ckmod
+
+    src = {"a": torch.randn(1 << 20, device="cuda")}
+    path = str(tmp_path / "spill")
+    writer = Checkpointer(src, path=path, tile_bytes=1 << 20, chunk_bytes=1 << 20)
+    writer.save()
+    slot = writer.slots[0]
+    header = writer.header()
+    header.update(complete=False, streaming=True)
+    writer._write_header(slot, header)
+    prog = slot.progress
+    prog[1], prog[2], prog[4] = header["generation"], 0, ckmod.STREAM_RUNNING
+    prog[0] = ckmod.PROGRESS_MAGIC
+    reader = Checkpointer({"a": torch.zeros(1 << 20, device="cuda")}, path=path,
+                          tile_bytes=1 << 20, chunk_bytes=1 << 20)
+    with pytest.raises(CheckpointError, match="stalled"):
+        reader.restore(stream_timeout=0.3)
+    prog[4] = ckmod.STREAM_FAILED
+    with pytest.raises(CheckpointError):
+        reader.restore(stream_timeout=5)
+    reader.close()
+    writer.close()

@@ -88,14 +88,17 @@ def test_preempt_checkpoint_respawn_resume(cloud, how):
         assert "rank-preempted" in codes and "rank-released" not in codes
     else:  # early hand-off: respawned on "released", the old process reaped afterwards
         assert "rank-released" in codes and "rank-released-exit" in codes
-        assert "checkpoint-released" in codes
-        assert codes.index("rank-released") < codes.index("respawn")
-    # phase journal: start -> first output -> preempt -> saved -> respawn -> restored
+        # streamed hand-off (default): released when the spill starts, the successor
+        # restores behind it
+        assert "checkpoint-streaming" in codes and "checkpoint-released" not in codes
+        assert codes.index("checkpoint-streaming") < codes.index("rank-released") < \
+            codes.index("respawn")
+    # phase journal: start -> first output -> preempt -> saved / respawn -> restored
     for phase in ("rank-start", "rank-first-output", "preempt-signal", "checkpoint-saved",
                   "checkpoint-restored"):
         assert phase in codes, (phase, codes)
-    assert codes.index("checkpoint-saved") < codes.index("respawn") < \
-        codes.index("checkpoint-restored")
+    assert codes.index("checkpoint-saved") < codes.index("checkpoint-restored")
+    assert codes.index("respawn") < codes.index("checkpoint-restored")
     saved = [e for e in task.events() if e.code == "checkpoint-saved"][0]
     assert saved.description[0] == "rank 0" and saved.description[-1].endswith("GB/s")
     task.delete()
@@ -149,6 +152,32 @@ def test_warm_standby_takes_over(cloud, monkeypatch):
     assert "standby-discarded" not in codes
     starts = [e for e in events if e.code == "rank-start"]
     assert len(starts) == 2 and "warm standby" in starts[1].description
+    task.delete()
+
+
+def test_hot_standby_restores_behind_the_streamed_spill(cloud, monkeypatch):
+    """TPI_WARM_STANDBY=hot: the successor runs (imports done) before any preemption; the
+    preempted rank releases it when its spill *starts* and it resumes from the stream."""
+    monkeypatch.setenv("TPI_WARM_STANDBY", "hot")
+    script = STANDBY % {"python": sys.executable, "root": ROOT, "steps": 30}
+    spec = Task(environment=Environment(script=script, timeout=300,
+                                        variables=Variables({"TPI_TASK": "true"})))
+    task = backends.new(cloud, new_deterministic_identifier("preempt-hot"), spec)
+    task.create()
+    _wait_for(task, "step 3")
+    deadline = time.time() + 30
+    while time.time() < deadline and "standby-start" not in [e.code for e in task.events()]:
+        time.sleep(0.05)
+    task.preempt()
+    status = task.wait(90)
+    logs = task.logs()
+    assert status["succeeded"] == 1, (status, logs)
+    assert any("activated" in l and "final 30 30" in l for l in logs), logs
+    codes = [e.code for e in task.events()]
+    assert codes.index("standby-start") < codes.index("preempt-requested")
+    for code in ("standby-activated", "checkpoint-streaming", "rank-released", "respawn",
+                 "checkpoint-restored"):
+        assert code in codes, (code, codes)
     task.delete()
 
 
