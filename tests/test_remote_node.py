@@ -19,7 +19,7 @@ from terraform_provider_iterative_amd.utils.identifier import new_deterministic_
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 SCRIPT = """#!/bin/sh
-sleep 0.5
+sleep 3
 echo "rank $RANK says $GREETING_FROM_CLIENT"
 cat input.txt
 test -e skip.log && echo "skip.log leaked"
