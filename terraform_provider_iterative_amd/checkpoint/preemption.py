@@ -311,6 +311,11 @@ def _handler(signum, frame):  # pragma: no cover - exercised in subprocess tests
     if _fired.is_set():
         return
     _fired.set()
+    # The successor's "restored" reaches us as SIGUSR2 (see _linger).  With a streamed
+    # hand-off it can arrive while this save is still finishing (final header, persist); its
+    # default action would kill us mid-write, so it stays pending until _linger takes it.
+    if hasattr(signal, "pthread_sigmask"):
+        signal.pthread_sigmask(signal.SIG_BLOCK, [signal.SIGUSR2])
     journal("preempt-signal", "signal %d" % signum)
     t0 = time.perf_counter()
     released = []

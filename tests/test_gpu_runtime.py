@@ -196,3 +196,43 @@ def test_early_prefetched_region_is_adopted(tmp_path):
         assert ck.restore().bad_tiles == 0 and ck.header()["metadata"] == {"step": 5}
         torch.cuda.synchronize()
     assert torch.equal(dst["w"], ref["w"])
+
+
+def test_remote_node_mi355x_task_stages_and_runs_on_the_gpu(tmp_path, monkeypatch):
+    """``region = "host=..."`` with ``cloud = "mi355x"``: the workdir travels to the node,
+    its runtime stages it into HBM and the rank sees the placed GPU (fake ssh transport)."""
+    node_root = tmp_path / "node-state"
+    node_root.mkdir()
+    monkeypatch.setenv("FAKE_SSH_STATE_ROOT", str(node_root))
+    monkeypatch.setenv("TPI_SSH_COMMAND", "%s %s" % (sys.executable,
+                                                     os.path.join(ROOT, "tests", "fake_ssh.py")))
+    monkeypatch.setenv("TPI_REMOTE_PYTHON", sys.executable)
+    monkeypatch.delenv("TPI_MI355X_GPUS", raising=False)
+    work = tmp_path / "w"
+    work.mkdir()
+    payload = np.random.default_rng(1).integers(0, 256, 80 << 20, dtype=np.uint8)
+    (work / "data.bin").write_bytes(payload.tobytes())
+    (work / "run.py").write_text(
+        "import os, sys\nsys.path.insert(0, %r)\nimport torch\n"
+        "from terraform_provider_iterative_amd.runtime.stage import attach\n"
+        "t = attach().tensor('data.bin')\n"
+        "print('gpus', torch.cuda.device_count(), os.environ.get('HIP_VISIBLE_DEVICES'),\n"
+        "      'staged', t.device.type, int(t[:4096].sum()))\n" % ROOT)
+    script = "#!/bin/sh\nexec %s run.py\n" % sys.executable
+    spec = Task(size=Size(machine="m+mi355x"),
+                environment=Environment(script=script, directory=str(work), timeout=300,
+                                        variables=Variables({"TPI_STAGE": "hbm"})))
+    task = backends.new(Cloud(provider="mi355x", region="host=gpu-box"),
+                        new_deterministic_identifier("remote-gpu"), spec)
+    task.create()
+    deadline = time.time() + 240
+    while time.time() < deadline:
+        task.read()
+        if task.status().get("succeeded", 0) + task.status().get("failed", 0):
+            break
+        time.sleep(0.5)
+    log = "".join(task.logs())
+    assert task.status()["succeeded"] == 1, log
+    assert "gpus 1" in log and "staged cuda %d" % int(payload[:4096].sum()) in log, log
+    assert task.gpus() and (node_root / "mi355x").is_dir()
+    task.delete()
