@@ -6,6 +6,7 @@
 
 #include "filter.h"
 #include "../common/tpz.h"
+#include "fileio.h"
 #include "hostops.h"
 #include "transfer.h"
 
@@ -162,6 +163,26 @@ PYBIND11_MODULE(_tpi_native, m) {
                         &first);
     }
     return py::make_tuple(bad, first);
+  });
+  m.def("write_file_ptr", [](const std::string& path, uintptr_t src, uint64_t n, int threads,
+                            bool sync) {
+    std::string err;
+    {
+      py::gil_scoped_release nogil;
+      err = tpi::write_file(path, (const void*)src, n, threads, sync);
+    }
+    if (!err.empty()) throw std::runtime_error(err);
+  });
+  m.def("read_stream_ptr", [](const std::string& path, uintptr_t dst, uint64_t offset,
+                              uint64_t n, int threads, uint64_t chunk, uintptr_t words,
+                              uintptr_t tile_ends, uint64_t ntiles) {
+    std::string err;
+    {
+      py::gil_scoped_release nogil;
+      err = tpi::read_stream(path, (void*)dst, offset, n, threads, chunk, (uint64_t*)words,
+                             (const uint64_t*)tile_ends, ntiles);
+    }
+    if (!err.empty()) throw std::runtime_error(err);
   });
   m.def("resident_bytes", [](const std::string& path) {
     uint64_t size = 0;

@@ -51,6 +51,8 @@ from .host import HostRegion
 
 MAGIC = b"TPICKPT2"
 PREAMBLE = 32
+FILE_THREADS = 16        # persist / load: native pwrite/pread threads
+LOAD_CHUNK = 256 << 20   # load: bytes read (and published to the restore) per step
 PROGRESS_MAGIC = struct.unpack("<Q", b"TPIPROG1")[0]
 STREAM_RUNNING, STREAM_COMPLETE, STREAM_FAILED = 1, 2, 3
 MODES = {"sdma": 0, "direct": 1}
@@ -757,18 +759,20 @@ class Checkpointer:
             raise CheckpointError("nothing saved yet")
         slot, header = active
         tmp = path + ".tpi-partial"
-        data = self.region.array(slot.base, self.stream_offset + int(header["stream_bytes"]))
-        with open(tmp, "wb") as f:
-            f.write(memoryview(data))
-            f.flush()
-            os.fsync(f.fileno())
+        # parallel pwrite of the slot (native, GIL released) + fsync, then an atomic rename
+        native().write_file_ptr(tmp, self.region.addr + slot.base,
+                                self.stream_offset + int(header["stream_bytes"]),
+                                FILE_THREADS, True)
         os.replace(tmp, path)
         return path
 
     def load(self, path: str) -> TransferResult:
         """Read a persisted checkpoint file into the region (the slot a save would write, so
-        a bad file leaves the current checkpoint intact with ``slots=2``), then
-        :meth:`restore` it."""
+        a bad file leaves the current checkpoint intact with ``slots=2``) and restore it.
+
+        The stream section is read by parallel native readers in chunks that are published
+        like a streamed save's (progress block), so the device restore runs behind the file
+        read instead of after it."""
         self.wait_pending()
         slot, generation = self._target()
         with open(path, "rb") as f:
@@ -777,22 +781,52 @@ class Checkpointer:
             self._check_compatible(header)
             if not header.get("complete"):
                 raise CheckpointError("%s holds an incomplete checkpoint" % path)
-            self._invalidate(slot)
-            f.seek(self.entries_offset)
-            end = self.stream_offset + int(header["stream_bytes"])
-            dst = self.region.array(slot.base, end)
-            view = memoryview(dst)
-            off = self.entries_offset
-            while off < end:
-                n = f.readinto(view[off:off + (64 << 20)])
-                if not n:
-                    break
-                off += n
-        if off < end:
-            raise CheckpointError("%s is truncated (%d of %d bytes)" % (path, off, end))
-        header["generation"] = generation  # newest now; written last, like a save
-        self._write_header(slot, header)
-        return self.restore()
+            size = os.fstat(f.fileno()).st_size
+        stream_bytes = int(header["stream_bytes"])
+        end = self.stream_offset + stream_bytes
+        if size < end:
+            raise CheckpointError("%s is truncated (%d of %d bytes)" % (path, size, end))
+        self._invalidate(slot)
+        # entries + CRCs + blob sizes first (small), then the stream, streamed
+        native().read_stream_ptr(path, self.region.addr + slot.base + self.entries_offset,
+                                 self.entries_offset, self.stream_offset - self.entries_offset,
+                                 FILE_THREADS, 64 << 20, 0, 0, 0)
+        if header.get("codec", "none") == "tpz1":
+            tile_ends = np.cumsum(slot.csizes.astype(np.uint64), dtype=np.uint64)
+            if len(tile_ends) and int(tile_ends[-1]) != stream_bytes:
+                raise CheckpointError("%s: blob sizes do not add up to the stream" % path)
+        else:
+            tile_ends = np.minimum(np.arange(1, self.plan.ntiles + 1, dtype=np.uint64)
+                                   * np.uint64(self.plan.tile_bytes), np.uint64(self.plan.total))
+        header["generation"] = generation  # newest once complete; written last, like a save
+        prog = slot.progress
+        prog[1], prog[2], prog[3], prog[5] = generation, 0, 0, os.getpid()
+        prog[4] = STREAM_RUNNING
+        prog[0] = PROGRESS_MAGIC
+        self._write_header(slot, dict(header, complete=False, streaming=True))
+        failure: list = []
+
+        def read():
+            try:
+                native().read_stream_ptr(path, self.region.addr + slot.base + self.stream_offset,
+                                         self.stream_offset, stream_bytes, FILE_THREADS,
+                                         LOAD_CHUNK, prog.ctypes.data + 16,
+                                         tile_ends.ctypes.data, len(tile_ends))
+                self._write_header(slot, header)
+                prog[4] = STREAM_COMPLETE
+            except BaseException as error:  # the restore sees FAILED and raises
+                failure.append(error)
+                prog[4] = STREAM_FAILED
+
+        reader = threading.Thread(target=read, name="tpi-load", daemon=True)
+        reader.start()
+        try:
+            res = self.restore()
+        finally:
+            reader.join()
+        if failure:
+            raise CheckpointError("loading %s failed: %s" % (path, failure[0]))
+        return res
 
     def close(self) -> None:
         try:
