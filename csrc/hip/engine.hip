@@ -1265,7 +1265,12 @@ int tpi_restore_stream(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total
     const int b = (int)(k % e->nbuf);
     const uint64_t len = std::min(e->chunk, total - base);
     const uint64_t t0i = base / tile, nt = (len + tile - 1) / tile;
-    if (wait_published(words, t0i + nt, timeout_s)) return -1;
+    if (wait_published(words, t0i + nt, timeout_s)) {
+      // leave no copy or kernel of the chunks already issued running past this call
+      (void)hipStreamSynchronize(e->copy);
+      (void)hipStreamSynchronize(e->compute);
+      return -1;
+    }
     uint64_t cbeg = base, cend = base + len;
     if (zipped) {
       for (uint64_t i = t0i; i < t0i + nt; ++i) {
