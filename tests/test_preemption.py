@@ -181,6 +181,34 @@ def test_hot_standby_restores_behind_the_streamed_spill(cloud, monkeypatch):
     task.delete()
 
 
+def test_hot_standby_gang_of_two(cloud, monkeypatch):
+    """Two coupled ranks, each with a hot standby: preempting rank 1 takes the gang down,
+    both stream their spills, both standbys take over and finish from their own spill."""
+    monkeypatch.setenv("TPI_WARM_STANDBY", "hot")
+    script = STANDBY.replace('".spill")', '".spill-" + os.environ["RANK"])') % {
+        "python": sys.executable, "root": ROOT, "steps": 30}
+    spec = Task(parallelism=2,
+                environment=Environment(script=script, timeout=300,
+                                        variables=Variables({"TPI_TASK": "true"})))
+    task = backends.new(cloud, new_deterministic_identifier("preempt-hot-gang"), spec)
+    task.create()
+    _wait_for(task, "step 3")
+    deadline = time.time() + 30
+    while time.time() < deadline and \
+            sum(e.code == "standby-start" for e in task.events()) < 2:
+        time.sleep(0.05)
+    task.preempt(rank=1)
+    status = task.wait(120)
+    logs = task.logs()
+    assert status["succeeded"] == 2, (status, logs)
+    finished = [l for l in logs if "activated" in l and "final 30 30" in l]
+    assert len(finished) == 2, logs
+    codes = [e.code for e in task.events()]
+    assert codes.count("standby-activated") == 2, codes
+    assert codes.count("checkpoint-streaming") + codes.count("checkpoint-released") == 2, codes
+    task.delete()
+
+
 def test_unused_standby_is_discarded(cloud, monkeypatch):
     monkeypatch.setenv("TPI_WARM_STANDBY", "1")
     # stop arrives while the preempted rank is still releasing: its standby must not run
