@@ -72,7 +72,7 @@ def measure_workdir_fanout(nbytes: int, rank: int, world: int, device, barrier: 
     comm = TaskComm.from_group(device=device.index) if world > 1 else None
     out: Dict[str, dict] = {"bytes": total, "files": len(files)}
     try:
-        with Loader(device.index, chunk_bytes=64 << 20, nbuf=4, threads=8,
+        with Loader(device.index, chunk_bytes=64 << 20, nbuf=4, threads=16,
                     numa_node=numa_node) as loader:
             loader.load(workdir, files, 0, min(total, 256 << 20), image.data_ptr())  # warm
             for method in methods:
