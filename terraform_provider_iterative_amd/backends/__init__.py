@@ -21,8 +21,14 @@ class UnknownProviderError(ValueError):
 
 
 def _retarget(cloud: Cloud) -> Cloud:
+    """``TPI_REMOTE_AS=mi355x|local`` runs configurations written for a remote cloud on a
+    node runtime; with ``TPI_REMOTE_HOST=[user@]node`` on that node over SSH (the cloud's own
+    region names no node, so it is replaced by ``host=...``)."""
     target = os.environ.get("TPI_REMOTE_AS")
     if cloud.provider in REMOTE_PROVIDERS and target in NODE_PROVIDERS:
+        host = os.environ.get("TPI_REMOTE_HOST")
+        if host:
+            return replace(cloud, provider=target, region="host=" + host)
         return replace(cloud, provider=target)
     return cloud
 

@@ -5,7 +5,9 @@ naming them still parse (schemas, machine catalogs, region aliases are kept in
 ``models/``) but every operation fails with a diagnostic that names the replacement, rather
 than the reference's generic ``unknown provider`` error (``task/task.go:17-45``).
 ``TPI_REMOTE_AS=mi355x|local`` re-targets them onto a node provider instead (handy for
-running an unchanged ``main.tf`` written for ``cloud = "aws"`` on this node).
+running an unchanged ``main.tf`` written for ``cloud = "aws"`` on this node), and
+``TPI_REMOTE_HOST=[user@]node`` onto *another* node's runtime over SSH (``backends/ssh.py``):
+the reference's remote workflow with an existing MI355X node in place of a provisioned VM.
 """
 from __future__ import annotations
 
@@ -31,7 +33,8 @@ class RemoteProviderUnavailable(RuntimeError):
         super().__init__(
             "cloud %r is a remote provider; this framework runs tasks on the node it is "
             "installed on: use cloud = \"mi355x\" (GPUs) or cloud = \"local\" (CPU), or set "
-            "TPI_REMOTE_AS=mi355x to run %r configurations here" % (provider, provider))
+            "TPI_REMOTE_AS=mi355x to run %r configurations here (TPI_REMOTE_HOST=node: on "
+            "that node over SSH)" % (provider, provider))
 
 
 class RemoteTask(Task):

@@ -176,3 +176,18 @@ def test_leo_smoke_flow_on_a_remote_node(tmp_path, remote):
     assert (work / "output" / "new").read_text().strip() == new
     assert (work / "cache" / "old").read_text() == old
     assert not (remote / "local" / ident).exists()
+
+
+def test_remote_cloud_config_retargeted_to_a_remote_node(tmp_path, remote, monkeypatch):
+    """An unchanged ``cloud = "aws"`` definition runs on a remote MI355X node's runtime with
+    TPI_REMOTE_AS + TPI_REMOTE_HOST."""
+    monkeypatch.setenv("TPI_REMOTE_AS", "local")
+    monkeypatch.setenv("TPI_REMOTE_HOST", "node-c")
+    cloud = Cloud(provider="aws", region="us-east")
+    ident = new_deterministic_identifier("retarget-remote")
+    task = backends.new(cloud, ident, Task(environment=Environment(script="#!/bin/sh\necho hi\n")))
+    assert isinstance(task, RemoteNodeTask) and task.transport.host == "node-c"
+    task.create()
+    assert _wait(task)["succeeded"] == 1 and "hi" in "".join(task.logs())
+    assert (remote / "local" / ident.long()).is_dir()
+    task.delete()
