@@ -1329,6 +1329,88 @@ int tpi_restore_stream(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total
   return 0;
 }
 
+// ---- HBM-to-HBM hand-off (preemption on the same GPU) --------------------------------------
+// The preempted rank exports its tensors' allocations with HIP IPC; its successor -- a new
+// process on the same GPU -- opens them and moves the state device to device through the
+// pack / unpack kernels (CRC-verified), instead of waiting for the host spill.
+
+int tpi_ipc_export(const void* ptr, void* handle_out, uint64_t* offset_out,
+                   uint64_t* alloc_bytes_out) {
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  HIP_OK(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr));
+  hipIpcMemHandle_t h;
+  HIP_OK(hipIpcGetMemHandle(&h, (void*)base));
+  memcpy(handle_out, &h, sizeof(h));
+  *offset_out = (uint64_t)((const uint8_t*)ptr - (const uint8_t*)base);
+  *alloc_bytes_out = size;
+  return 0;
+}
+
+// Move tensors `src` -> `dst` (same plan, different pointers) on the device: per chunk, pack
+// src into a staging buffer (computing tile CRCs), then unpack + verify into dst.
+int tpi_copy_segments(tpi_engine* e, const tpi_seg* src, const tpi_seg* dst, int n,
+                      uint64_t total, uint64_t signal_stream, uint64_t* bad_tiles,
+                      tpi_stats* stats) {
+  Range range("tpi_copy_segments");
+  std::lock_guard<std::mutex> lk(e->mu);
+  auto t0 = std::chrono::steady_clock::now();
+  if (check_segments(src, n, total)) return -1;
+  if (prepare(e, dst, n, total)) return -1;  // dst -> d_segs
+  e->hash_valid = false;
+  tpi_seg* d_src = nullptr;
+  HIP_OK(hipMalloc(&d_src, (size_t)n * sizeof(tpi_seg)));
+  auto release = [&] { (void)hipFree(d_src); };
+  auto ok = [&](hipError_t err, const char* what) {
+    if (err == hipSuccess) return true;
+    fail(std::string(what) + ": " + hipGetErrorString(err));
+    return false;
+  };
+  const uint64_t tile = e->tile;
+  const uint32_t init_full = init_for(tile);
+  const uint32_t init_last = init_for(total % tile ? total % tile : tile);
+  unsigned long long bad_init[2] = {0ull, ~0ull}, bad[2] = {0ull, 0ull};
+  bool good = ok(hipMemcpyAsync(d_src, src, (size_t)n * sizeof(tpi_seg), hipMemcpyHostToDevice,
+                                e->compute), "upload source segments") &&
+              ok(hipMemcpyAsync(e->d_bad, bad_init, sizeof(bad_init), hipMemcpyHostToDevice,
+                                e->compute), "upload bad counter");
+  if (good && signal_stream != TPI_NO_STREAM) {  // dst tensors: after the caller's work on them
+    good = ok(hipEventRecord(e->ev_wait, (hipStream_t)signal_stream), "hipEventRecord") &&
+           ok(hipStreamWaitEvent(e->compute, e->ev_wait, 0), "hipStreamWaitEvent");
+  }
+  uint64_t nchunks = 0;
+  for (uint64_t base = 0, k = 0; good && base < total; base += e->chunk, ++k) {
+    const uint64_t len = std::min(e->chunk, total - base);
+    void* buf = e->staging[k % e->nbuf];
+    good = ok(tpi_launch_transposes(src, n, base, len, buf, 0, e->compute), "transpose in") &&
+           ok(tpi_launch_stream_crc(0, d_src, n, base, len, buf, tile, e->tables, e->d_crcs,
+                                    init_full, init_last, nullptr, 1, e->compute), "pack") &&
+           ok(tpi_launch_stream_crc(1, e->d_segs, n, base, len, buf, tile, e->tables,
+                                    e->d_crcs, init_full, init_last, e->d_bad, 1, e->compute),
+              "unpack") &&
+           ok(tpi_launch_transposes(dst, n, base, len, buf, 1, e->compute), "transpose out");
+    nchunks = k + 1;
+  }
+  if (good)
+    good = ok(hipMemcpyAsync(bad, e->d_bad, sizeof(bad), hipMemcpyDeviceToHost, e->compute),
+              "bad counter") &&
+           ok(hipEventRecord(e->ev_done, e->compute), "hipEventRecord");
+  if (good && signal_stream != TPI_NO_STREAM)
+    good = ok(hipStreamWaitEvent((hipStream_t)signal_stream, e->ev_done, 0), "hipStreamWaitEvent");
+  if (!ok(hipStreamSynchronize(e->compute), "hipStreamSynchronize")) good = false;
+  release();
+  if (!good) return -1;
+  *bad_tiles = bad[0];
+  if (stats) {
+    stats->copy_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    stats->pack_ms = 0;
+    stats->bytes = total;
+    stats->chunks = nchunks;
+  }
+  return 0;
+}
+
 int tpi_host_unregister(void* ptr) {
   HIP_OK(hipHostUnregister(ptr));
   return 0;

@@ -178,6 +178,17 @@ int tpi_restore_stream(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total
                        const void* host_src, const uint32_t* crcs, const uint32_t* csizes,
                        const uint64_t* words, double timeout_s, uint64_t signal_stream,
                        uint64_t* bad_tiles, int64_t* first_bad, tpi_stats* stats);
+// HBM-to-HBM hand-off between processes on one GPU.  tpi_ipc_export: IPC handle
+// (TPI_IPC_HANDLE_BYTES) of the allocation holding `ptr` -- e.g. inside a torch caching-
+// allocator segment -- and ptr's offset in it; the successor maps it with tpi_ipc_open.
+// tpi_copy_segments moves tensors described by `src` (e.g. a predecessor's, mapped over IPC)
+// into `dst` through the pack / unpack kernels, tile CRCs verified (`bad_tiles`); both plans
+// must describe the same stream.
+int tpi_ipc_export(const void* ptr, void* handle_out, uint64_t* offset_out,
+                   uint64_t* alloc_bytes_out);
+int tpi_copy_segments(tpi_engine* e, const tpi_seg* src, const tpi_seg* dst, int n,
+                      uint64_t total, uint64_t signal_stream, uint64_t* bad_tiles,
+                      tpi_stats* stats);
 int tpi_engine_set_host_region(tpi_engine* e, void* base, uint64_t bytes, uint64_t window,
                                tpi_pinner* pinner);
 // hipMemcpyAsync host -> device on `stream` (0 = legacy default stream).

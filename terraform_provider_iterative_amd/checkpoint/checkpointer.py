@@ -155,6 +155,17 @@ class DeviceEngine:
         return TransferResult(plan.total, time.perf_counter() - t0, int(st.chunks),
                               int(bad.value), int(first.value), wire_bytes=int(st.bytes))
 
+    def copy_segments(self, src: np.ndarray, plan: PackPlan, signal_stream: int) -> TransferResult:
+        st = _Stats()
+        bad = ctypes.c_uint64(0)
+        t0 = time.perf_counter()
+        rc = self.lib.tpi_copy_segments(self.handle, src.ctypes.data, plan.segs.ctypes.data,
+                                        len(plan.entries), plan.total, signal_stream,
+                                        ctypes.byref(bad), ctypes.byref(st))
+        self.lib.check(rc, "tpi_copy_segments")
+        return TransferResult(plan.total, time.perf_counter() - t0, int(st.chunks),
+                              int(bad.value), wire_bytes=0)
+
     def set_progress(self, words_addr: int) -> None:
         self.lib.check(self.lib.tpi_engine_set_progress(self.handle,
                                                         ctypes.c_void_p(words_addr or None)),
@@ -741,6 +752,113 @@ class Checkpointer:
         if strict and res.bad_tiles:
             raise CheckpointError("%d corrupt tile(s), first at %d" % (res.bad_tiles,
                                                                       res.first_bad))
+        return res
+
+    # -- HBM-to-HBM hand-off (preemption on the same GPU) --------------------------------------
+    def _hbm_manifest_path(self) -> Optional[str]:
+        return self.path + ".hbm" if self.path and self.engine is not None else None
+
+    def export_hbm(self) -> Optional[str]:
+        """Preempted rank: publish HIP IPC handles of the bound tensors next to the spill file
+        (``<path>.hbm``), so a successor on the same GPU can copy the state device to device
+        (:meth:`restore_hbm`) while this process is still spilling it to host memory.  The
+        caller must keep the tensors unchanged (and this process alive) until the successor
+        has restored -- the preemption handler does (it lingers until ``restored``)."""
+        manifest = self._hbm_manifest_path()
+        if manifest is None:
+            return None
+        import torch
+
+        torch.cuda.synchronize(self.device_index)  # no queued kernel may still write them
+        lib = hip()
+        allocations: Dict[bytes, int] = {}
+        handles, where = [], []
+        handle = ctypes.create_string_buffer(64)
+        for seg in self.plan.segs:
+            if int(seg["nbytes"]) == 0 or int(seg["ptr"]) == 0:
+                where.append(None)
+                continue
+            offset, size = ctypes.c_uint64(0), ctypes.c_uint64(0)
+            lib.check(lib.tpi_ipc_export(ctypes.c_void_p(int(seg["ptr"])), handle,
+                                         ctypes.byref(offset), ctypes.byref(size)),
+                      "tpi_ipc_export")
+            key = handle.raw
+            if key not in allocations:
+                allocations[key] = len(handles)
+                handles.append(key.hex())
+            where.append([allocations[key], int(offset.value)])
+        bus = ctypes.create_string_buffer(64)
+        lib.tpi_device_pci_bus_id(self.device_index, bus, 64)
+        doc = {"format": "tpi-hbm-1", "pid": os.getpid(), "device": bus.value.decode(),
+               "entries_sha256": self._entries_digest, "total": self.plan.total,
+               "tile_bytes": self.plan.tile_bytes, "allocations": handles, "where": where,
+               "segs": self.plan.segs.tobytes().hex(), "created": time.time()}
+        tmp = manifest + ".tmp"
+        with open(tmp, "w") as handle_file:
+            json.dump(doc, handle_file)
+        os.replace(tmp, manifest)
+        return manifest
+
+    def _hbm_doc(self) -> Optional[Dict]:
+        manifest = self._hbm_manifest_path()
+        if manifest is None or not os.path.exists(manifest):
+            return None
+        try:
+            with open(manifest) as f:
+                doc = json.load(f)
+        except (OSError, ValueError):
+            return None
+        if (doc.get("format") != "tpi-hbm-1" or doc.get("pid") == os.getpid()
+                or doc.get("entries_sha256") != self._entries_digest
+                or doc.get("total") != self.plan.total):
+            return None
+        try:
+            os.kill(int(doc["pid"]), 0)  # the exporting process must still hold the memory
+        except (OSError, ValueError):
+            return None
+        bus = ctypes.create_string_buffer(64)
+        hip().tpi_device_pci_bus_id(self.device_index, bus, 64)
+        if doc.get("device") != bus.value.decode():
+            return None  # another GPU: the host region is the way
+        return doc
+
+    def hbm_ready(self) -> bool:
+        """A live predecessor on this GPU exported its tensors for :meth:`restore_hbm`."""
+        return self._hbm_doc() is not None
+
+    def restore_hbm(self, strict: bool = True) -> TransferResult:
+        """Copy the state of a preempted predecessor on the same GPU straight from its HBM
+        (HIP IPC, pack + unpack kernels, every tile CRC-verified) into the bound tensors."""
+        doc = self._hbm_doc()
+        if doc is None:
+            raise CheckpointError("no HBM hand-off from a live predecessor on this GPU")
+        import torch
+
+        lib = hip()
+        bases = []
+        try:
+            for h in doc["allocations"]:
+                base = ctypes.c_void_p()
+                lib.check(lib.tpi_ipc_open(bytes.fromhex(h), self.device_index,
+                                           ctypes.byref(base)), "tpi_ipc_open")
+                bases.append(base.value)
+            src = np.frombuffer(bytes.fromhex(doc["segs"]), dtype=self.plan.segs.dtype).copy()
+            if len(src) != len(self.plan.segs):
+                raise CheckpointError("HBM hand-off describes a different tensor set")
+            for i, w in enumerate(doc["where"]):
+                src[i]["ptr"] = 0 if w is None else bases[w[0]] + w[1]
+            sig = torch.cuda.current_stream(self.device_index).cuda_stream
+            res = self.engine.copy_segments(src, self.plan, sig)
+        finally:
+            for base in bases:
+                lib.tpi_ipc_close(ctypes.c_void_p(base))
+        self.last_restore = res
+        if strict and res.bad_tiles:
+            raise CheckpointError("%d tile(s) differ after the HBM hand-off" % res.bad_tiles)
+        try:
+            os.remove(self._hbm_manifest_path())
+        except OSError:
+            pass
         return res
 
     def _check_compatible(self, header: Dict) -> None:

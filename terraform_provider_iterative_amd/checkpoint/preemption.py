@@ -82,6 +82,12 @@ def checkpoint_all(metadata: Optional[Dict] = None, on_stream=None) -> List[floa
             meta.update(extra)
     rates = []
     for ck in _registered:
+        if on_stream is not None and len(_registered) == 1 and _hbm_handoff():
+            try:  # the successor on this GPU copies our HBM while we spill to the host
+                if ck.export_hbm():
+                    journal("checkpoint-hbm-export", "successor may copy device to device")
+            except Exception as error:  # the host path still works
+                journal("checkpoint-hbm-export-failed", str(error))
         res = ck.save(meta, on_stream=on_stream if len(_registered) == 1 else None)
         rates.append(res.gbps)
         journal("checkpoint-saved", *_describe(res))
@@ -218,6 +224,11 @@ def _handoff_safe() -> bool:
     return True
 
 
+def _hbm_handoff() -> bool:
+    """Export the tensors for a device-to-device hand-off (TPI_HBM_HANDOFF, default on)."""
+    return os.environ.get("TPI_HBM_HANDOFF", "1") not in ("0", "false", "no")
+
+
 def _stream_handoff() -> bool:
     """Release the successor when the spill *starts* (TPI_STREAM_HANDOFF, default on): it
     restores each chunk as it lands.  Needs one registered checkpointer, a supervisor to tell,
@@ -336,6 +347,13 @@ def _handler(signum, frame):  # pragma: no cover - exercised in subprocess tests
             if not released:
                 journal("checkpoint-released", "successor may start")
             _linger()
+        for ck in _registered:  # an HBM hand-off nobody took is stale once we exit
+            manifest = ck._hbm_manifest_path()
+            if manifest and os.path.exists(manifest):
+                try:
+                    os.remove(manifest)
+                except OSError:
+                    pass
     except Exception as error:
         print("tpi: preemption checkpoint FAILED: %s" % error, file=sys.stderr, flush=True)
         code = 1
@@ -361,6 +379,14 @@ def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None) -> Op
     """
     failure: Optional[CheckpointError] = None
     header = checkpointer.latest()  # complete, or still streaming in from the predecessor
+    if header is not None and checkpointer.hbm_ready():
+        try:  # the predecessor on this GPU is alive and exported its tensors: copy from HBM
+            res = checkpointer.restore_hbm()
+            journal("checkpoint-restored", "HBM hand-off", *_describe(res))
+            notify_restored()
+            return header.get("metadata", {})
+        except Exception as error:  # fall back to the host region
+            journal("checkpoint-hbm-failed", str(error))
     if header is not None:
         try:
             res = checkpointer.restore()

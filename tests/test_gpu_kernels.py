@@ -506,3 +506,54 @@ def test_streamed_restore_gives_up_on_a_stalled_writer(tmp_path):
         reader.restore(stream_timeout=5)
     reader.close()
     writer.close()
+
+
+HBM_EXPORTER = r'''
+import sys, torch
+sys.path.insert(0, %(root)r)
+from terraform_provider_iterative_amd.checkpoint import Checkpointer
+g = torch.Generator(device="cuda").manual_seed(11)
+t = {"a": torch.randn(5 << 20, device="cuda", generator=g).to(torch.bfloat16),
+     "m": torch.randn(700, 900, device="cuda", generator=g).t(),
+     "s": torch.randn(3000, device="cuda", generator=g)[::3]}
+ck = Checkpointer(t, path=%(path)r, tile_bytes=1 << 20, chunk_bytes=4 << 20)
+print("exported", ck.export_hbm(), flush=True)
+sys.stdin.readline()  # hold the memory until the successor is done
+'''
+
+
+def test_hbm_handoff_copies_a_live_predecessors_tensors(tmp_path):
+    """Same-GPU hand-off: the predecessor exports IPC handles of its tensors; the successor
+    copies them device to device (pack + unpack kernels, CRC-verified) -- no host copy."""
+    import subprocess
+    import sys
+
+    root = __import__("os").path.dirname(__import__("os").path.dirname(__file__))
+    path = str(tmp_path / "spill")
+    child = subprocess.Popen([sys.executable, "-c", HBM_EXPORTER % {"root": root, "path": path}],
+                             stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+    try:
+        line = child.stdout.readline()
+        assert line.startswith("exported"), line
+        g = torch.Generator(device="cuda").manual_seed(11)
+        want = {"a": torch.randn(5 << 20, device="cuda", generator=g).to(torch.bfloat16),
+                "m": torch.randn(700, 900, device="cuda", generator=g).t(),
+                "s": torch.randn(3000, device="cuda", generator=g)[::3]}
+        dst = {"a": torch.zeros(5 << 20, device="cuda", dtype=torch.bfloat16),
+               "m": torch.zeros(700, 900, device="cuda").t(),
+               "s": torch.zeros(3000, device="cuda")[::3]}
+        from terraform_provider_iterative_amd.checkpoint import Checkpointer
+
+        ck = Checkpointer(dst, path=path, tile_bytes=1 << 20, chunk_bytes=4 << 20)
+        assert ck.hbm_ready()
+        res = ck.restore_hbm()
+        torch.cuda.synchronize()
+        assert res.bad_tiles == 0
+        for k in want:
+            assert torch.equal(dst[k], want[k]), k
+        assert not ck.hbm_ready()  # consumed
+        ck.close()
+    finally:
+        child.stdin.write("\n")
+        child.stdin.flush()
+        child.wait(60)
