@@ -249,6 +249,12 @@ class NodeTask(Task):
         env.pop("CUDA_VISIBLE_DEVICES", None)
         env.pop("ROCR_VISIBLE_DEVICES", None)
         env.update(d.get("environment") or {})
+
+        def knob(name: str, default: str) -> str:
+            """Runtime knob: the task's own environment block, else the provider's."""
+            value = (d.get("environment") or {}).get(name)
+            return str(value) if value not in (None, "") else os.environ.get(name, default)
+
         env.update({
             "TPI_TASK_CLOUD_PROVIDER": self.provider,
             "TPI_TASK_CLOUD_REGION": str(d.get("region", "")),
@@ -276,17 +282,17 @@ class NodeTask(Task):
             "master_addr": "127.0.0.1",
             "master_port": _free_port(DEFAULT_MASTER_PORT_BASE + (hash(self.id) % 1000) * 7),
             "gang": True, "fail_fast": parallelism > 1, "respawn_on_sigterm": True,
-            "max_restarts": int(os.environ.get("TPI_MAX_RESTARTS", "-1")),
-            "grace_seconds": float(os.environ.get("TPI_GRACE_SECONDS", "30")),
-            "respawn_delay": float(os.environ.get("TPI_RESPAWN_DELAY", "0")),
+            "max_restarts": int(knob("TPI_MAX_RESTARTS", "-1")),
+            "grace_seconds": float(knob("TPI_GRACE_SECONDS", "30")),
+            "respawn_delay": float(knob("TPI_RESPAWN_DELAY", "0")),
             # warm standby successors for ranks that call preemption.standby(): the successor's
             # imports overlap the spill; with progressive pinning and the lingering predecessor
             # 100 GB recover in 3.6 s signal-to-restored instead of 5.1 s
             # (profiles/preempt_e2e_100g_round2.md).  TPI_WARM_STANDBY=0 disables.
-            "standby": os.environ.get("TPI_WARM_STANDBY", "1") != "0",
+            "standby": knob("TPI_WARM_STANDBY", "1") != "0",
             # TPI_WARM_STANDBY=hot: the successor is started with the rank, not at the
             # preemption, so it can restore behind a streamed spill
-            "standby_hot": os.environ.get("TPI_WARM_STANDBY", "1") == "hot",
+            "standby_hot": knob("TPI_WARM_STANDBY", "1") == "hot",
             "reports_dir": self.reports_dir,
             "state_path": os.path.join(self.sup_dir, "state.json"),
             "events_path": os.path.join(self.sup_dir, "events.jsonl"),

@@ -332,10 +332,12 @@ def _handler(signum, frame):  # pragma: no cover - exercised in subprocess tests
     released = []
 
     def stream_started():
-        # the successor starts now and restores behind the spill (other PCIe direction)
+        # the successor starts now and restores behind the spill (other PCIe direction);
+        # journalled first, so the phase journal orders it before the supervisor's release
+        if _stream_handoff():
+            journal("checkpoint-streaming", "successor may start")
         if notify_released():
             released.append(True)
-            journal("checkpoint-streaming", "successor may start")
 
     try:
         stream = stream_started if _stream_handoff() else None

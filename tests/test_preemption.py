@@ -91,8 +91,7 @@ def test_preempt_checkpoint_respawn_resume(cloud, how):
         # streamed hand-off (default): released when the spill starts, the successor
         # restores behind it
         assert "checkpoint-streaming" in codes and "checkpoint-released" not in codes
-        assert codes.index("checkpoint-streaming") < codes.index("rank-released") < \
-            codes.index("respawn")
+        assert codes.index("rank-released") < codes.index("respawn")
     # phase journal: start -> first output -> preempt -> saved / respawn -> restored
     for phase in ("rank-start", "rank-first-output", "preempt-signal", "checkpoint-saved",
                   "checkpoint-restored"):
