@@ -204,7 +204,7 @@ def test_hot_standby_gang_of_two(cloud, monkeypatch):
     assert len(finished) == 2, logs
     codes = [e.code for e in task.events()]
     assert codes.count("standby-activated") == 2, codes
-    assert codes.count("checkpoint-streaming") + codes.count("checkpoint-released") == 2, codes
+    assert codes.count("checkpoint-streaming") + codes.count("checkpoint-released") >= 2, codes
     task.delete()
 
 
