@@ -85,7 +85,7 @@ def measure_first_log_latency(timeout: float = 60.0, cloud: Optional[str] = None
             os.makedirs(work)
             with open(os.path.join(work, "main.tf"), "w") as handle:
                 handle.write(MAIN_TF % {"tag": "%d%d" % (os.getpid(), i), "cloud": cloud,
-                                        "machine": machine})
+                                        "machine": machine, "parallelism": parallelism})
             env = dict(os.environ)
             env["TPI_STATE_ROOT"] = os.path.join(base, "state")
             env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")

@@ -81,3 +81,15 @@ def test_bench_refuses_a_world_that_disagrees_with_gpus(tmp_path):
                          env=env)
     assert out.returncode != 0
     assert "disagree" in out.stderr
+
+
+def test_first_log_latency_probe_reports_every_rank(tmp_path, monkeypatch):
+    # The headline's apply->first-log probe renders main.tf with parallelism = N; a missing
+    # template key once turned every bench's first_log_latency_s into null.
+    monkeypatch.setenv("TMPDIR", str(tmp_path))
+    from terraform_provider_iterative_amd.bench_latency import measure_first_log_latency
+
+    out = measure_first_log_latency(timeout=30, cloud="local", repeats=1, parallelism=2)
+    assert out["parallelism"] == 2 and out["samples"] == 1
+    assert out["cli_s"] is not None and out["api_s"] is not None
+    assert out["cli_all_s"] is not None and out["cli_all_s"] >= out["cli_s"]
