@@ -73,6 +73,19 @@ static inline void tpi_crc_tables_init(tpi_crc_tables* t) {
 }
 
 // Standard CRC32C of a whole message from its raw (zero-init, no xorout) CRC and length.
+// Bank-column layout of the same tables for the CRC-only kernel (kernels.hip k_crc_tiles):
+// 256 rows of 64 dwords; dword c (< 32) of row v is slice[c & 15][v], dword 32 + c is
+// row[c & 3][v].  A row is 256 B, so the LDS bank of an entry is its column whatever v is.
+#define TPI_CRC_COLS_WORDS (256 * 64)
+
+static inline void tpi_crc_cols_init(const tpi_crc_tables* t, uint32_t* cols) {
+  for (int v = 0; v < 256; ++v)
+    for (int c = 0; c < 32; ++c) {
+      cols[v * 64 + c] = t->slice[c & 15][v];
+      cols[v * 64 + 32 + c] = t->row[c & 3][v];
+    }
+}
+
 static inline uint32_t tpi_crc32c_finish(uint32_t raw, uint64_t len, const uint32_t* x2n) {
   return raw ^ tpi_multmodp(tpi_x8nmodp(len, x2n), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
 }

@@ -97,7 +97,9 @@ const tpi_crc_tables& host_tables() {
   return t;
 }
 
-// Device copies of the CRC tables, one per device (lazily created, never freed).
+// Device copies of the CRC tables, one per device (lazily created, never freed).  The
+// bank-column layout (TPI_CRC_COLS_WORDS dwords, tpi_crc_cols_init) follows the struct in
+// the same allocation: the CRC-only kernel reads it at `tables + 1`.
 std::mutex g_tab_mu;
 std::vector<tpi_crc_tables*> g_dev_tables;
 
@@ -105,9 +107,13 @@ int device_tables(int dev, tpi_crc_tables** out) {
   std::lock_guard<std::mutex> lk(g_tab_mu);
   if ((int)g_dev_tables.size() <= dev) g_dev_tables.resize(dev + 1, nullptr);
   if (!g_dev_tables[dev]) {
+    static_assert(sizeof(tpi_crc_tables) % 16 == 0, "column tables must stay 16-B aligned");
+    std::vector<uint8_t> img(sizeof(tpi_crc_tables) + TPI_CRC_COLS_WORDS * 4);
+    memcpy(img.data(), &host_tables(), sizeof(tpi_crc_tables));
+    tpi_crc_cols_init(&host_tables(), (uint32_t*)(img.data() + sizeof(tpi_crc_tables)));
     tpi_crc_tables* d = nullptr;
-    HIP_OK(hipMalloc(&d, sizeof(tpi_crc_tables)));
-    HIP_OK(hipMemcpy(d, &host_tables(), sizeof(tpi_crc_tables), hipMemcpyHostToDevice));
+    HIP_OK(hipMalloc(&d, img.size()));
+    HIP_OK(hipMemcpy(d, img.data(), img.size(), hipMemcpyHostToDevice));
     g_dev_tables[dev] = d;
   }
   *out = g_dev_tables[dev];

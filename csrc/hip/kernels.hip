@@ -3,7 +3,8 @@
 //  k_stream_crc<MODE>  one 256-thread workgroup per tile of the packed stream.
 //     MODE_PACK    gather tensor payloads (contiguous or strided) -> packed buffer
 //     MODE_UNPACK  packed buffer -> scatter into tensors, verify tile CRC
-//     MODE_CRC     CRC only (device buffer integrity digests)
+//     MODE_CRC     CRC only (device buffer integrity digests); launched as k_crc_tiles,
+//                  the bank-conflict-free column-table variant of the same math
 //   Every lane owns the 16-byte words at row*4096 + lane*16 of its tile, so each row is one
 //   fully coalesced 4 KiB workgroup access (dwordx4 per lane).  The CRC32C of the tile is
 //   computed without serialising lanes: lane l folds its own word stream with Horner's rule
@@ -515,6 +516,144 @@ __global__ __launch_bounds__(WG) void k_stream_crc(TileArgs a) {
   }
 }
 
+// ---- CRC-only tiles: bank-conflict-free column tables ---------------------------------------
+//
+// MODE_CRC of k_stream_crc was bound by LDS bank conflicts (profiles/crc_lds_round2.md): a
+// lookup's index is a data byte, so the 32 lanes of a ds_read_b32 group hit random banks and
+// a group costs ~3.5 cycles.  k_crc_tiles reads the column layout of the same tables
+// (crc32c.h tpi_crc_cols_init: 256 rows x 256 B, every table copy in ONE bank column):
+//   * at unrolled step j of a word, lane l uses column (j + l) mod 32 -- a permutation of the
+//     32 banks over each lane group -- i.e. slice table (j + l) mod 16;
+//   * each lane first rotates its 16-byte word left by (l mod 16) bytes (8 v_cndmask + 4
+//     v_alignbyte on lane-constant masks), so step j always needs byte 15 - j;
+//   * the LDS byte address (data byte) << 8 | (column << 2) is one v_perm_b32 of the data
+//     dword and a register packing four of the lane's columns; the row shift picks the
+//     accumulator byte with a lane-constant perm selector and the row columns (+128 B).
+// Every lookup is conflict-free at 1 VALU + 1 xor, as many as the production layout.  512
+// threads per workgroup (two tiles, one per half) share the 64 KiB of tables: 16 waves per
+// CU at ~110 VGPRs.  Grid-stride over tile pairs, tables staged once per workgroup.
+// 8 GB of 1 MiB tiles on MI355X: 4.30 -> 6.63 TB/s (scripts/exp/crc_cf.hip, same math).
+
+#define CRC_WG 512
+
+struct ColLane {
+  bool m1, m2;          // rotate the word by one / two dwords
+  uint32_t s;           // then by s bytes (v_alignbyte)
+  uint32_t colpack[4];  // byte i of colpack[k]: ((4k + i + l) mod 32) * 4
+  uint32_t selR[4];     // row step j: byte0 <- colpack[0] byte j, byte1 <- acc byte (j + l) & 3
+};
+
+__device__ static inline ColLane col_lane(int lane) {
+  ColLane m;
+  const int l32 = lane & 31, r = lane & 15;
+  const int q2 = ((r + 3) >> 2) & 3;
+  m.m1 = q2 & 1;
+  m.m2 = q2 & 2;
+  m.s = (uint32_t)((4 - (r & 3)) & 3);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c |= (uint32_t)(((4 * k + i + l32) & 31) * 4) << (8 * i);
+    m.colpack[k] = c;
+    m.selR[k] = 0x0C0C0000u | ((4u + (uint32_t)((k + l32) & 3)) << 8) | (uint32_t)k;
+  }
+  return m;
+}
+
+__device__ static inline uint32_t col_at(const uint32_t* t, uint32_t byte_off) {
+  return *(const uint32_t*)((const char*)t + byte_off);
+}
+
+__device__ static inline uint32_t raw16_col(const uint32_t* t, const ColLane& m, u32x4 w) {
+  const uint32_t t0 = m.m1 ? w.w : w.x, t1 = m.m1 ? w.x : w.y, t2 = m.m1 ? w.y : w.z,
+                 t3 = m.m1 ? w.z : w.w;
+  const uint32_t x0 = m.m2 ? t2 : t0, x1 = m.m2 ? t3 : t1, x2 = m.m2 ? t0 : t2,
+                 x3 = m.m2 ? t1 : t3;
+  uint32_t R[4];
+  R[0] = __builtin_amdgcn_alignbyte(x1, x0, m.s);
+  R[1] = __builtin_amdgcn_alignbyte(x2, x1, m.s);
+  R[2] = __builtin_amdgcn_alignbyte(x3, x2, m.s);
+  R[3] = __builtin_amdgcn_alignbyte(x0, x3, m.s);
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int pos = 15 - j;
+    const uint32_t sel = 0x0C0C0000u | ((4u + (uint32_t)(pos & 3)) << 8) | (uint32_t)(j & 3);
+    c ^= col_at(t, __builtin_amdgcn_perm(R[pos >> 2], m.colpack[j >> 2], sel));
+  }
+  return c;
+}
+
+__device__ static inline uint32_t shift_row_col(const uint32_t* t, const ColLane& m, uint32_t a) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) c ^= col_at(t + 32, __builtin_amdgcn_perm(a, m.colpack[0], m.selR[j]));
+  return c;
+}
+
+__global__ __launch_bounds__(CRC_WG) void k_crc_tiles(TileArgs a) {
+  __shared__ uint32_t lds[TPI_CRC_COLS_WORDS + 2 * (WG / 64)];  // static: no base add per lookup
+  uint32_t* s_red = lds + TPI_CRC_COLS_WORDS;
+  const int tid = threadIdx.x, lane = tid & (WG - 1), half = tid / WG;
+  {
+    const u32x4* src = (const u32x4*)(a.tables + 1);  // column layout follows the struct
+    u32x4* dst = (u32x4*)lds;
+    for (int i = tid; i < TPI_CRC_COLS_WORDS / 4; i += CRC_WG) dst[i] = src[i];
+  }
+  const ColLane m = col_lane(lane);
+  __syncthreads();
+  const uint64_t ntiles = (a.len + a.tile_bytes - 1) / a.tile_bytes;
+  for (uint64_t pair = blockIdx.x; pair * 2 < ntiles; pair += gridDim.x) {
+    const uint64_t t = pair * 2 + half;
+    uint32_t contrib = 0;
+    uint64_t tile_len = 0;
+    if (t < ntiles) {
+      const uint64_t off = t * a.tile_bytes;
+      tile_len = umin64(a.tile_bytes, a.len - off);
+      const uint8_t* tbuf = a.buf + off;
+      uint32_t acc = 0;
+      uint64_t last_end = 0, row = 0;
+      const uint64_t nrows = (tile_len + TPI_ROW_BYTES - 1) / TPI_ROW_BYTES;
+      const uint64_t full_rows = tile_len / TPI_ROW_BYTES;
+      for (; row + UNROLL <= full_rows; row += UNROLL) {
+        u32x4 w[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+          w[u] = __builtin_nontemporal_load(
+              (const u32x4*)(tbuf + (row + u) * TPI_ROW_BYTES + lane * 16));
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) acc = shift_row_col(lds, m, acc) ^ raw16_col(lds, m, w[u]);
+        last_end = (row + UNROLL - 1) * TPI_ROW_BYTES + lane * 16 + 16;
+      }
+      for (; row < nrows; ++row) {  // remainder rows, possibly partial
+        const uint64_t rel = row * TPI_ROW_BYTES + lane * 16;
+        if (rel < tile_len) {
+          const u32x4 w = __builtin_nontemporal_load((const u32x4*)(tbuf + rel));
+          acc = shift_row_col(lds, m, acc) ^ raw16_col(lds, m, w);
+          last_end = rel + 16;
+        }
+      }
+      if (last_end) {
+        const uint32_t k = (tile_len % TPI_ROW_BYTES == 0)
+                               ? a.tables->lane_shift[lane]
+                               : tpi_x8nmodp(tile_len - last_end, a.tables->x2n);
+        contrib = tpi_multmodp(k, acc);
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) contrib ^= __shfl_xor(contrib, o, 64);
+    __syncthreads();  // s_red reuse across pairs
+    if ((tid & 63) == 0) s_red[tid >> 6] = contrib;
+    __syncthreads();
+    if (lane == 0 && t < ntiles) {
+      const uint32_t* r = s_red + (WG / 64) * half;
+      const uint32_t init = (tile_len == a.tile_bytes) ? a.init_full : a.init_last;
+      a.crcs[a.stream_base / a.tile_bytes + t] = r[0] ^ r[1] ^ r[2] ^ r[3] ^ init ^ 0xFFFFFFFFu;
+    }
+  }
+}
+
 // ---- striped XXH64 shard hash ----------------------------------------------------------------
 
 __global__ __launch_bounds__(WG) void k_shard_hash(const uint8_t* __restrict__ data,
@@ -687,7 +826,17 @@ extern "C" hipError_t tpi_launch_stream_crc(int mode, const tpi_seg* segs, int n
     case MODE_UNPACK:
       hipLaunchKernelGGL(k_stream_crc<MODE_UNPACK>, grid, block, 0, stream, a);
       break;
-    default: hipLaunchKernelGGL(k_stream_crc<MODE_CRC>, grid, block, 0, stream, a); break;
+    default: {
+      // CRC only: column-table kernel, two tiles per workgroup, grid-stride over the pairs
+      // with two workgroups per CU resident (64 KiB LDS each).
+      int dev = 0, cus = 256;
+      if (hipGetDevice(&dev) == hipSuccess)
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      const uint64_t pairs = (ntiles + 1) / 2;
+      const unsigned g = (unsigned)(pairs < (uint64_t)cus * 2 ? pairs : (uint64_t)cus * 2);
+      hipLaunchKernelGGL(k_crc_tiles, dim3(g), dim3(CRC_WG), 0, stream, a);
+      break;
+    }
   }
   return hipGetLastError();
 }

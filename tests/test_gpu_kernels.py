@@ -24,7 +24,9 @@ def _rand_bytes(n, seed):
 
 @pytest.mark.parametrize("n,tile", [(16, 4096), (4096, 4096), (4096 * 5 + 48, 4096),
                                     (3 * (1 << 20), 1 << 20), ((1 << 20) + 4096 * 3 + 32, 1 << 20),
-                                    (8192 * 7, 8192)])
+                                    (8192 * 7, 8192),
+                                    # > 2 workgroups per CU of tile pairs: the grid-stride loop
+                                    (4096 * 2101 + 16, 4096)])
 def test_crc32c_tiles_device_matches_host(n, tile):
     data = _rand_bytes(n, n)
     dev = torch.from_numpy(data).cuda()
