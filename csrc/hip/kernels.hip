@@ -595,7 +595,10 @@ __device__ static inline uint32_t shift_row_col(const uint32_t* t, const ColLane
 __global__ __launch_bounds__(CRC_WG) void k_crc_tiles(TileArgs a) {
   __shared__ uint32_t lds[TPI_CRC_COLS_WORDS + 2 * (WG / 64)];  // static: no base add per lookup
   uint32_t* s_red = lds + TPI_CRC_COLS_WORDS;
-  const int tid = threadIdx.x, lane = tid & (WG - 1), half = tid / WG;
+  const int tid = threadIdx.x, lane = tid & (WG - 1);
+  // wave-uniform, and made scalar: tile geometry and row loops then run on SGPRs instead
+  // of a divergent VGPR loop (5.5 -> 6.x TB/s)
+  const int half = __builtin_amdgcn_readfirstlane(tid) / WG;
   {
     const u32x4* src = (const u32x4*)(a.tables + 1);  // column layout follows the struct
     u32x4* dst = (u32x4*)lds;
@@ -829,9 +832,17 @@ extern "C" hipError_t tpi_launch_stream_crc(int mode, const tpi_seg* segs, int n
     default: {
       // CRC only: column-table kernel, two tiles per workgroup, grid-stride over the pairs
       // with two workgroups per CU resident (64 KiB LDS each).
+      static int cu_count[64];  // per device, queried once (the attribute query is not free)
       int dev = 0, cus = 256;
-      if (hipGetDevice(&dev) == hipSuccess)
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+        if (!__atomic_load_n(&cu_count[dev], __ATOMIC_RELAXED)) {
+          int c = 0;
+          if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+              c > 0)
+            __atomic_store_n(&cu_count[dev], c, __ATOMIC_RELAXED);
+        }
+        if (cu_count[dev]) cus = cu_count[dev];
+      }
       const uint64_t pairs = (ntiles + 1) / 2;
       const unsigned g = (unsigned)(pairs < (uint64_t)cus * 2 ? pairs : (uint64_t)cus * 2);
       hipLaunchKernelGGL(k_crc_tiles, dim3(g), dim3(CRC_WG), 0, stream, a);

@@ -21,6 +21,8 @@
 //   ./crc_cf [GB]           (GPU: variants vs the production layout, bit-exact check)
 #include <hip/hip_runtime.h>
 
+#include <dlfcn.h>
+
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -29,6 +31,7 @@
 #include <vector>
 
 #include "../../csrc/common/crc32c.h"
+
 
 #define CK(x)                                                                   \
   do {                                                                          \
@@ -381,6 +384,16 @@ __global__ __launch_bounds__(WGT) void k_crc_pm(const uint8_t* __restrict__ buf,
   }
 }
 
+__global__ void k_fill(uint64_t* p, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t z = i * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    p[i] = z ^ (z >> 31);
+  }
+}
+
 // ---- host ------------------------------------------------------------------------------------
 
 static uint32_t crc_bitwise(const uint8_t* p, size_t n) {
@@ -500,10 +513,16 @@ int main(int argc, char** argv) {
   uint8_t* d;
   CK(hipMalloc(&d, n));
   std::vector<uint8_t> h(tile * 2);
-  srand(7);
-  for (auto& x : h) x = (uint8_t)rand();
-  for (uint64_t off = 0; off < n; off += h.size())
-    CK(hipMemcpy(d + off, h.data(), std::min<uint64_t>(h.size(), n - off), hipMemcpyHostToDevice));
+  if (getenv("CRC_CF_PATTERN")) {  // a 2-tile pattern repeated (the first measurements)
+    srand(7);
+    for (auto& x : h) x = (uint8_t)rand();
+    for (uint64_t off = 0; off < n; off += h.size())
+      CK(hipMemcpy(d + off, h.data(), std::min<uint64_t>(h.size(), n - off), hipMemcpyHostToDevice));
+  } else {  // every byte distinct-random (splitmix64 of the word index)
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, (uint64_t*)d, n / 8);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(h.data(), d, h.size(), hipMemcpyDeviceToHost));
+  }
   uint32_t* dcrc;
   CK(hipMalloc(&dcrc, (n / tile) * 4));
   const uint32_t want0 = crc_bitwise(h.data(), tile), want1 = crc_bitwise(h.data() + tile, tile);
@@ -545,6 +564,29 @@ int main(int argc, char** argv) {
   V(16, 4, 3)
   V(32, 8, 4)
   V(16, 8, 6)
+  // The production entry point (libtpi_hip.so tpi_crc32c_tiles -> k_crc_tiles), same buffer.
+  if (void* lib = dlopen("terraform_provider_iterative_amd/_lib/libtpi_hip.so", RTLD_NOW)) {
+    typedef int (*fn_t)(const void*, uint64_t, uint64_t, uint32_t*, uint64_t);
+    fn_t fn = (fn_t)dlsym(lib, "tpi_crc32c_tiles");
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    fn(d, n, tile, dcrc, 0);
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(a, 0));
+    for (int i = 0; i < 10; ++i) fn(d, n, tile, dcrc, 0);
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    got.assign(n / tile, 0);
+    CK(hipMemcpy(got.data(), dcrc, got.size() * 4, hipMemcpyDeviceToHost));
+    printf("%-30s %7.1f GB/s%s\n", "libtpi_hip tpi_crc32c_tiles", (double)n * 10 / (ms * 1e-3) / 1e9,
+           got == ref ? "" : "  MISMATCH");
+    ok = ok && got == ref;
+  } else {
+    printf("libtpi_hip.so not loaded: %s\n", dlerror());
+  }
   printf("%s\n", ok ? "all variants match" : "MISMATCH");
   return ok ? 0 : 1;
 }
