@@ -244,7 +244,9 @@ def main(argv=None):
     latency = None
     if rank == 0 and not args.no_latency:
         # an iterative_task with parallelism = N (one GPU per rank), like the job measured
-        latency = first_log_latency(parallelism=world)
+        # (one GPU per rank: a rehearsal with more ranks than GPUs probes with what exists)
+        gpus = torch.cuda.device_count() if on_gpu else world
+        latency = first_log_latency(parallelism=max(1, min(world, gpus)))
 
     from terraform_provider_iterative_amd.checkpoint import Checkpointer
 

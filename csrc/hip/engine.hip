@@ -40,6 +40,12 @@ extern "C" hipError_t tpi_launch_stream_crc(int mode, const tpi_seg* segs, int n
                                             uint32_t* crcs, uint32_t init_full,
                                             uint32_t init_last, unsigned long long* bad,
                                             int staged, hipStream_t stream);
+extern "C" hipError_t tpi_launch_stream_copy(const tpi_seg* src, const tpi_seg* dst, int nseg,
+                                             uint64_t stream_base, uint64_t len,
+                                             uint64_t tile_bytes, const tpi_crc_tables* tables,
+                                             uint32_t* crcs, uint32_t init_full,
+                                             uint32_t init_last, unsigned long long* bad,
+                                             hipStream_t stream);
 extern "C" hipError_t tpi_launch_transposes(const tpi_seg* host_segs, int nseg, uint64_t base,
                                             uint64_t len, void* buf, int dir,
                                             hipStream_t stream);
@@ -1353,8 +1359,12 @@ int tpi_ipc_export(const void* ptr, void* handle_out, uint64_t* offset_out,
   return 0;
 }
 
-// Move tensors `src` -> `dst` (same plan, different pointers) on the device: per chunk, pack
-// src into a staging buffer (computing tile CRCs), then unpack + verify into dst.
+// Move tensors `src` -> `dst` (same plan, different pointers) on the device.  Default: per
+// chunk, one fused pass copies tensor to tensor and records the tile CRCs of what it read
+// (MODE_COPY), then a read-back pass checks dst against them (MODE_VERIFY): 3 x the state in
+// HBM traffic.
+// TPI_HANDOFF_COPY=staged (or segments whose stream layouts differ) takes the older route:
+// pack src into a staging buffer, then unpack + verify into dst (4 x the traffic).
 int tpi_copy_segments(tpi_engine* e, const tpi_seg* src, const tpi_seg* dst, int n,
                       uint64_t total, uint64_t signal_stream, uint64_t* bad_tiles,
                       tpi_stats* stats) {
@@ -1384,8 +1394,24 @@ int tpi_copy_segments(tpi_engine* e, const tpi_seg* src, const tpi_seg* dst, int
     good = ok(hipEventRecord(e->ev_wait, (hipStream_t)signal_stream), "hipEventRecord") &&
            ok(hipStreamWaitEvent(e->compute, e->ev_wait, 0), "hipStreamWaitEvent");
   }
+  bool fused = true;
+  for (int i = 0; i < n && fused; ++i)
+    fused = src[i].off == dst[i].off && src[i].nbytes == dst[i].nbytes;
+  if (const char* m = getenv("TPI_HANDOFF_COPY")) fused = fused && strcmp(m, "staged") != 0;
   uint64_t nchunks = 0;
-  for (uint64_t base = 0, k = 0; good && base < total; base += e->chunk, ++k) {
+  // No staging buffer bounds the fused route's spans: 4 GiB (4096 one-MiB tiles, 16
+  // workgroups per CU) keeps the chip full, where a 256 MB chunk is one workgroup per CU.
+  const uint64_t span = std::max<uint64_t>(e->chunk, ((4ull << 30) / tile) * tile);
+  for (uint64_t base = 0, k = 0; good && fused && base < total; base += span, ++k) {
+    const uint64_t len = std::min(span, total - base);
+    good = ok(tpi_launch_stream_copy(d_src, e->d_segs, n, base, len, tile, e->tables, e->d_crcs,
+                                     init_full, init_last, nullptr, e->compute), "copy") &&
+           ok(tpi_launch_stream_copy(e->d_segs, nullptr, n, base, len, tile, e->tables,
+                                     e->d_crcs, init_full, init_last, e->d_bad, e->compute),
+              "verify");
+    nchunks = k + 1;
+  }
+  for (uint64_t base = 0, k = 0; good && !fused && base < total; base += e->chunk, ++k) {
     const uint64_t len = std::min(e->chunk, total - base);
     void* buf = e->staging[k % e->nbuf];
     good = ok(tpi_launch_transposes(src, n, base, len, buf, 0, e->compute), "transpose in") &&

@@ -5,6 +5,9 @@
 //     MODE_UNPACK  packed buffer -> scatter into tensors, verify tile CRC
 //     MODE_CRC     CRC only (device buffer integrity digests); launched as k_crc_tiles,
 //                  the bank-conflict-free column-table variant of the same math
+//     MODE_COPY    tensors -> tensors (same stream layout, other pointers) + tile CRCs, with
+//                  no stream buffer in between (HBM-to-HBM preemption hand-off)
+//     MODE_VERIFY  gather tensors, verify tile CRCs (the hand-off's read-back check)
 //   Every lane owns the 16-byte words at row*4096 + lane*16 of its tile, so each row is one
 //   fully coalesced 4 KiB workgroup access (dwordx4 per lane).  The CRC32C of the tile is
 //   computed without serialising lanes: lane l folds its own word stream with Horner's rule
@@ -34,7 +37,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ static inline uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 
-enum { MODE_PACK = 0, MODE_UNPACK = 1, MODE_CRC = 2 };
+enum { MODE_PACK = 0, MODE_UNPACK = 1, MODE_CRC = 2, MODE_COPY = 3, MODE_VERIFY = 4 };
 #define WG 256
 #define UNROLL 8
 #define LDS_WORDS (16 * 256 + 4 * 256 + WG)
@@ -382,6 +385,7 @@ struct TileArgs {
   const uint32_t* list;     // optional: workgroup i handles stream tile list[i] (sparse pack)
   uint64_t total;           // stream length (needed with `list`)
   int staged;               // TRANSPOSE segments are moved by k_transpose (see gather16)
+  const tpi_seg* dsegs;     // MODE_COPY: destination segments (same off/nbytes as segs)
 };
 
 // Stream geometry of this workgroup's tile: (global tile, stream offset, length, buffer).
@@ -427,8 +431,10 @@ __global__ __launch_bounds__(WG) void k_stream_crc(TileArgs a) {
   const uint64_t gbase = geom.gbase;  // packed-stream offset
   uint8_t* tbuf = geom.buf;
 
-  SegCursor cur;
+  SegCursor cur, dcur;
   if (MODE != MODE_CRC) seg_load(a.segs, a.nseg, seg_find(a.segs, a.nseg, gbase + lane * 16), cur);
+  if (MODE == MODE_COPY)
+    seg_load(a.dsegs, a.nseg, seg_find(a.dsegs, a.nseg, gbase + lane * 16), dcur);
   __syncthreads();
 
   uint32_t acc = 0;
@@ -449,6 +455,9 @@ __global__ __launch_bounds__(WG) void k_stream_crc(TileArgs a) {
         kept |= (cur.kind == TPI_SEG_TRANSPOSE && gbase + rel + 16 <= cur.off + cur.nbytes ? 1u
                                                                                       : 0u)
                 << u;
+      } else if (MODE == MODE_COPY || MODE == MODE_VERIFY) {
+        advance(a.segs, a.nseg, gbase + rel, cur);
+        w[u] = gather16(a.segs, cur, gbase + rel, nullptr, false);
       } else {
         w[u] = __builtin_nontemporal_load((const u32x4*)(tbuf + rel));
       }
@@ -463,6 +472,9 @@ __global__ __launch_bounds__(WG) void k_stream_crc(TileArgs a) {
       } else if (MODE == MODE_UNPACK) {
         advance(a.segs, a.nseg, gbase + rel, cur);
         scatter16(a.segs, cur, gbase + rel, w[u], a.staged);
+      } else if (MODE == MODE_COPY) {
+        advance(a.dsegs, a.nseg, gbase + rel, dcur);
+        scatter16(a.dsegs, dcur, gbase + rel, w[u], false);
       }
       acc = shift_row(s_row, acc) ^ raw16(s_slice, w[u]);
     }
@@ -476,6 +488,13 @@ __global__ __launch_bounds__(WG) void k_stream_crc(TileArgs a) {
         advance(a.segs, a.nseg, gbase + rel, cur);
         w = gather16(a.segs, cur, gbase + rel, tbuf + rel, a.staged);
         __builtin_nontemporal_store(w, (u32x4*)(tbuf + rel));
+      } else if (MODE == MODE_COPY || MODE == MODE_VERIFY) {
+        advance(a.segs, a.nseg, gbase + rel, cur);
+        w = gather16(a.segs, cur, gbase + rel, nullptr, false);
+        if (MODE == MODE_COPY) {
+          advance(a.dsegs, a.nseg, gbase + rel, dcur);
+          scatter16(a.dsegs, dcur, gbase + rel, w, false);
+        }
       } else {
         w = __builtin_nontemporal_load((const u32x4*)(tbuf + rel));
         if (MODE == MODE_UNPACK) {
@@ -505,7 +524,7 @@ __global__ __launch_bounds__(WG) void k_stream_crc(TileArgs a) {
     const uint32_t init = (tile_len == a.tile_bytes) ? a.init_full : a.init_last;
     const uint32_t crc = raw ^ init ^ 0xFFFFFFFFu;
     const uint64_t gtile = geom.gtile;
-    if (MODE == MODE_UNPACK) {
+    if (MODE == MODE_UNPACK || MODE == MODE_VERIFY) {
       if (crc != a.crcs[gtile]) {
         atomicAdd(&a.bad[0], 1ull);
         atomicMin(&a.bad[1], (unsigned long long)gtile);
@@ -822,6 +841,7 @@ extern "C" hipError_t tpi_launch_stream_crc(int mode, const tpi_seg* segs, int n
   a.list = nullptr;
   a.total = 0;
   a.staged = staged;
+  a.dsegs = nullptr;
   const uint64_t ntiles = (len + tile_bytes - 1) / tile_bytes;
   dim3 grid((unsigned)ntiles), block(WG);
   switch (mode) {
@@ -849,6 +869,39 @@ extern "C" hipError_t tpi_launch_stream_crc(int mode, const tpi_seg* segs, int n
       break;
     }
   }
+  return hipGetLastError();
+}
+
+// MODE_COPY (dst != nullptr: src tensors -> dst tensors + tile CRCs into `crcs`) or
+// MODE_VERIFY (dst == nullptr: gather `src`, count tiles whose CRC differs from `crcs`) over
+// stream bytes [stream_base, stream_base + len).  No stream buffer; TRANSPOSE segments take
+// the element-wise path.
+extern "C" hipError_t tpi_launch_stream_copy(const tpi_seg* src, const tpi_seg* dst, int nseg,
+                                             uint64_t stream_base, uint64_t len,
+                                             uint64_t tile_bytes, const tpi_crc_tables* tables,
+                                             uint32_t* crcs, uint32_t init_full,
+                                             uint32_t init_last, unsigned long long* bad,
+                                             hipStream_t stream) {
+  if (len == 0) return hipSuccess;
+  TileArgs a;
+  a.segs = src;
+  a.nseg = nseg;
+  a.stream_base = stream_base;
+  a.len = len;
+  a.buf = nullptr;
+  a.tile_bytes = tile_bytes;
+  a.tables = tables;
+  a.crcs = crcs;
+  a.init_full = init_full;
+  a.init_last = init_last;
+  a.bad = bad;
+  a.list = nullptr;
+  a.total = 0;
+  a.staged = 0;
+  a.dsegs = dst;
+  const dim3 grid((unsigned)((len + tile_bytes - 1) / tile_bytes)), block(WG);
+  if (dst) hipLaunchKernelGGL(k_stream_crc<MODE_COPY>, grid, block, 0, stream, a);
+  else hipLaunchKernelGGL(k_stream_crc<MODE_VERIFY>, grid, block, 0, stream, a);
   return hipGetLastError();
 }
 
@@ -883,6 +936,7 @@ extern "C" hipError_t tpi_launch_pack_list(const tpi_seg* segs, int nseg, uint64
   a.init_last = init_last;
   a.bad = nullptr;
   a.list = list;
+  a.dsegs = nullptr;
   a.total = total;
   a.staged = 0;
   hipLaunchKernelGGL(k_stream_crc<MODE_PACK>, dim3(n), dim3(WG), 0, stream, a);

@@ -41,11 +41,14 @@ resource "iterative_task" "latency" {
 
 
 def _first_log(state_root: str, timeout: float, t0: float, poll: float = 0.0005,
-               count: int = 1) -> Optional[float]:
-    """Seconds from ``t0`` until ``count`` ranks' logs (``reports/task-*``) hold a line."""
+               count: int = 1, proc: Optional[subprocess.Popen] = None) -> Optional[float]:
+    """Seconds from ``t0`` until ``count`` ranks' logs (``reports/task-*``) hold a line;
+    None at the timeout, or at once when ``proc`` (the apply) has failed."""
     pattern = os.path.join(state_root, "*", "*", "reports", "task-*")
     deadline = t0 + timeout
     while time.perf_counter() < deadline:
+        if proc is not None and proc.poll() not in (None, 0):
+            return None
         seen = 0
         for path in glob.glob(pattern):
             try:
@@ -93,8 +96,8 @@ def measure_first_log_latency(timeout: float = 60.0, cloud: Optional[str] = None
             proc = subprocess.Popen([sys.executable, os.path.join(ROOT, "bin", "tpi"), "apply",
                                      "-auto-approve"], cwd=work, env=env,
                                     stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
-            latency = _first_log(env["TPI_STATE_ROOT"], timeout, t0)
-            every = _first_log(env["TPI_STATE_ROOT"], timeout, t0, count=parallelism)
+            latency = _first_log(env["TPI_STATE_ROOT"], timeout, t0, proc=proc)
+            every = _first_log(env["TPI_STATE_ROOT"], timeout, t0, count=parallelism, proc=proc)
             proc.wait(timeout=timeout)
             if latency is not None:
                 cli.append(latency)
@@ -117,8 +120,11 @@ def measure_first_log_latency(timeout: float = 60.0, cloud: Optional[str] = None
                     "script": "#!/bin/sh\necho first log line\n"})
                 t1 = time.perf_counter()
                 result = resources.task_create(data)
-                lat = _first_log(os.environ["TPI_STATE_ROOT"], timeout, t1)
-                every = _first_log(os.environ["TPI_STATE_ROOT"], timeout, t1, count=parallelism)
+                created = bool(result.id) and not any(
+                    d.severity == "error" for d in result.diagnostics)
+                wait = timeout if created else 0.0  # a refused create logs nothing
+                lat = _first_log(os.environ["TPI_STATE_ROOT"], wait, t1)
+                every = _first_log(os.environ["TPI_STATE_ROOT"], wait, t1, count=parallelism)
                 if lat is not None:
                     api.append(lat)
                 if every is not None:

@@ -508,6 +508,8 @@ def _dispatch(args, verbose: bool) -> int:
         if not destroy:
             engine.outputs(state)
             state.save(state_path)
+        if not ok:  # like terraform: the errors above, no completion summary
+            return 1
         if destroy:
             print("\nDestroy complete! Resources: %d destroyed." % destroyed)
         else:
@@ -515,7 +517,7 @@ def _dispatch(args, verbose: bool) -> int:
                 added, changed, destroyed))
             for k, v in (state.data.get("outputs") or {}).items():
                 print("%s = %s" % (k, "<sensitive>" if v.get("sensitive") else json.dumps(v["value"])))
-        return 0 if ok else 1
+        return 0
 
 
 if __name__ == "__main__":

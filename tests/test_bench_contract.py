@@ -93,3 +93,21 @@ def test_first_log_latency_probe_reports_every_rank(tmp_path, monkeypatch):
     assert out["parallelism"] == 2 and out["samples"] == 1
     assert out["cli_s"] is not None and out["api_s"] is not None
     assert out["cli_all_s"] is not None and out["cli_all_s"] >= out["cli_s"]
+
+
+def test_first_log_latency_probe_gives_up_when_apply_fails(tmp_path, monkeypatch):
+    # a failing apply (here: more GPUs than the node has) must not hold the bench for the
+    # probe's whole timeout
+    monkeypatch.setenv("TMPDIR", str(tmp_path))
+    import time
+
+    from terraform_provider_iterative_amd import bench_latency
+
+    t0 = time.perf_counter()
+    try:
+        out = bench_latency.measure_first_log_latency(timeout=60, cloud="mi355x", repeats=1,
+                                                      parallelism=64)
+        assert out["cli_s"] is None
+    except Exception:
+        pass  # the in-process create refuses too; the bench catches that
+    assert time.perf_counter() - t0 < 30

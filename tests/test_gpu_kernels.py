@@ -524,11 +524,17 @@ sys.stdin.readline()  # hold the memory until the successor is done
 '''
 
 
-def test_hbm_handoff_copies_a_live_predecessors_tensors(tmp_path):
+@pytest.mark.parametrize("route", ["fused", "staged"])
+def test_hbm_handoff_copies_a_live_predecessors_tensors(tmp_path, monkeypatch, route):
     """Same-GPU hand-off: the predecessor exports IPC handles of its tensors; the successor
-    copies them device to device (pack + unpack kernels, CRC-verified) -- no host copy."""
+    copies them device to device, CRC-verified, with no host copy.  The default route is the
+    fused tensor-to-tensor copy plus a read-back verify; TPI_HANDOFF_COPY=staged selects pack +
+    unpack through a staging buffer.  Transposed and strided views take the element-wise path."""
     import subprocess
     import sys
+
+    if route == "staged":
+        monkeypatch.setenv("TPI_HANDOFF_COPY", "staged")
 
     root = __import__("os").path.dirname(__import__("os").path.dirname(__file__))
     path = str(tmp_path / "spill")
