@@ -71,8 +71,9 @@ if resuming:
     ok = meta is not None and meta.get("digests") == digests()
     print("restored %%d bytes in %%.3f s, verified %%s, warm standby %%s, activation -> restored "
           "%%.3f s (HBM state %%.3f, host region map+register %%.3f after it); process start -> "
-          "import done %%.3f s" %% (ck.plan.total, t1 - t0, ok, activated, t1 - t_active,
-                                  t_alloc - t_active, t_map - t_alloc, t_import - t_start),
+          "import done %%.3f s; Checkpointer %%s" %% (ck.plan.total, t1 - t0, ok, activated,
+                                  t1 - t_active, t_alloc - t_active, t_map - t_alloc,
+                                  t_import - t_start, ck.init_times),
           flush=True)
     ck.close()
     os.remove(spill)

@@ -1168,13 +1168,13 @@ tpi_pinner* tpi_host_pin_start(void* base, uint64_t bytes, uint64_t window, int 
   p->threads = std::max(1, threads);
   p->device = device;
   p->toucher = std::thread([p] {
-    const uint64_t page = 4096;
+    constexpr uint64_t page = 4096;
     for (uint64_t w = 0; w < p->bytes && !p->stop.load(); w += p->window) {
       const uint64_t end = std::min(p->bytes, w + p->window);
       const uint64_t per = ((end - w) / p->threads + page - 1) / page * page;
       std::vector<std::thread> pool;
       for (int t = 0; t < p->threads; ++t)
-        pool.emplace_back([p, w, end, per, t, page] {
+        pool.emplace_back([p, w, end, per, t] {
           const uint64_t b = w + (uint64_t)t * per, e = std::min(end, b + per);
           volatile const uint8_t* q = p->base;
           uint8_t sink = 0;

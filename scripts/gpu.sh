@@ -19,6 +19,7 @@
 #   preempt      bench/bench_preempt.py --gb 100 (config 4 end to end)
 #   preempt-standby  the same with a warm standby successor (TPI_WARM_STANDBY=1)
 #   preempt-hot  hot standby (started with the rank) restoring behind the streamed spill
+#   handoff      bench/bench_handoff.py --gb 16 (same-GPU HBM hand-off alone, per copy route)
 #   async        bench/bench_async.py --gb 100
 #   concurrent   bench/bench_concurrent.py (config 5)
 #   rehearse     bench.py at 2 and 4 ranks sharing the one GPU (gloo control plane)
@@ -62,6 +63,8 @@ run_job() {
                        > "$OUT/preempt-standby.json" 2> "$OUT/preempt-standby.log" ;;
     preempt-hot) timeout -k 10 900 python bench/bench_preempt.py --gb 100 --hot $extra \
                    > "$OUT/preempt-hot.json" 2> "$OUT/preempt-hot.log" ;;
+    handoff) timeout -k 10 600 python bench/bench_handoff.py $extra \
+               > "$OUT/handoff.json" 2> "$OUT/handoff.log" ;;
     async) timeout -k 10 900 python bench/bench_async.py --gb 100 $extra \
              > "$OUT/async.json" 2> "$OUT/async.log" ;;
     concurrent) timeout -k 10 600 python bench/bench_concurrent.py $extra \

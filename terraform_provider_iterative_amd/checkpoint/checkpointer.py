@@ -308,6 +308,7 @@ class Checkpointer:
                  chunk_bytes: int = 256 << 20, nbuf: int = 3, mode: str = "sdma",
                  numa: bool = True, populate: bool = True, codec: str = "none",
                  slots: int = 1):
+        t0 = time.perf_counter()
         self.plan = PackPlan.from_tensors(tensors, tile_bytes)
         self.path = path
         self.mode = MODES[mode]
@@ -338,7 +339,9 @@ class Checkpointer:
                 node = ctypes.c_int(-1)
                 if hip().tpi_device_numa_node(self.device_index, ctypes.byref(node)) == 0:
                     numa_node = node.value
+            t1 = time.perf_counter()
             self.engine = DeviceEngine(self.device_index, chunk_bytes, nbuf, tile_bytes)
+        t2 = time.perf_counter()
         adopted = host.adopt(path, self.size) if path and self.plan.on_device else None
         if adopted is not None and adopted.pinner and self.mode != MODES["sdma"]:
             adopted.close()  # the direct (zero-copy kernel) path needs one registration
@@ -351,6 +354,11 @@ class Checkpointer:
                                              self.region.size, self.region.window,
                                              self.region.pinner)
         self.slots = [_Slot(self, i, i * self.slot_bytes) for i in range(slots)]
+        t3 = time.perf_counter()
+        # where construction time goes (seconds): plan+layout, device engine, host region
+        self.init_times = {"plan": round((t1 if self.engine else t2) - t0, 4),
+                           "engine": round(t2 - t1, 4) if self.engine else 0.0,
+                           "region": round(t3 - t2, 4)}
         self.saves = 0
         self._snap = self._snap_crcs = None  # HBM snapshot of save_async
         self._pending: Optional[PendingSave] = None
