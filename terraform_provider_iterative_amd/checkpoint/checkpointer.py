@@ -38,7 +38,7 @@ import struct
 import threading
 import time
 from dataclasses import dataclass
-from typing import Any, Dict, Mapping, Optional, Sequence, Tuple, Union
+from typing import Any, Dict, List, Mapping, Optional, Sequence, Tuple, Union
 
 import numpy as np
 
@@ -233,6 +233,39 @@ class DeviceEngine:
             pass
 
 
+# Engines created ahead of the Checkpointer that takes them (prewarm_engine).
+_engine_pool: Dict[Tuple[int, int, int, int], List[DeviceEngine]] = {}
+_engine_pool_lock = threading.Lock()
+
+
+def prewarm_engine(device_index: Optional[int] = None, chunk_bytes: int = 256 << 20,
+                   nbuf: int = 3, tile_bytes: int = 1 << 20) -> bool:
+    """Create a device engine now for the next :class:`Checkpointer` with these parameters.
+
+    Engine creation (streams, HBM staging chunks, pinned bounce buffers, SDMA binding) takes
+    ~0.1 s on MI355X.  A warm standby calls this before it blocks (:func:`preemption.standby`),
+    so after its activation the Checkpointer starts without it and the HBM hand-off begins
+    ~0.1 s earlier.  Returns False when no engine could be made (no GPU, no library)."""
+    try:
+        if device_index is None:
+            import torch
+
+            device_index = torch.cuda.current_device()
+        engine = DeviceEngine(device_index, chunk_bytes, nbuf, tile_bytes)
+    except Exception:
+        return False
+    with _engine_pool_lock:
+        _engine_pool.setdefault((device_index, chunk_bytes, nbuf, tile_bytes), []).append(engine)
+    return True
+
+
+def _take_engine(device_index: int, chunk_bytes: int, nbuf: int,
+                 tile_bytes: int) -> Optional[DeviceEngine]:
+    with _engine_pool_lock:
+        pool = _engine_pool.get((device_index, chunk_bytes, nbuf, tile_bytes))
+        return pool.pop() if pool else None
+
+
 def _layout(header_cap: int, entries_len: int, ntiles: int, total: int, tile_bytes: int):
     entries_offset = align_up(PREAMBLE + header_cap, 4096)
     crc_offset = align_up(entries_offset + entries_len, 4096)
@@ -340,7 +373,8 @@ class Checkpointer:
                 if hip().tpi_device_numa_node(self.device_index, ctypes.byref(node)) == 0:
                     numa_node = node.value
             t1 = time.perf_counter()
-            self.engine = DeviceEngine(self.device_index, chunk_bytes, nbuf, tile_bytes)
+            self.engine = (_take_engine(self.device_index, chunk_bytes, nbuf, tile_bytes)
+                           or DeviceEngine(self.device_index, chunk_bytes, nbuf, tile_bytes))
         t2 = time.perf_counter()
         adopted = host.adopt(path, self.size) if path and self.plan.on_device else None
         if adopted is not None and adopted.pinner and self.mode != MODES["sdma"]:
