@@ -185,6 +185,8 @@ def main():
             result["signal_to_restored_s"] = round(t_restored - (t_sig or t_preempt), 3)
             if t_saved:
                 result["saved_to_restored_s"] = round(t_restored - t_saved, 3)
+        if t_sig:  # every journal phase after the signal, seconds from it
+            result["timeline"] = [[c, round(t - t_sig, 4), d] for c, t, d in events if t >= t_sig]
         result["verified"] = any("verified True" in l for l in logs)
         result["ok"] = bool(status.get("succeeded") == 1 and result["verified"])
     finally:

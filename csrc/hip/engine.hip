@@ -1346,6 +1346,15 @@ int tpi_restore_stream(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total
 // process on the same GPU -- opens them and moves the state device to device through the
 // pack / unpack kernels (CRC-verified), instead of waiting for the host spill.
 
+int tpi_mem_range(const void* ptr, uint64_t* base_out, uint64_t* alloc_bytes_out) {
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  HIP_OK(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr));
+  *base_out = (uint64_t)(uintptr_t)base;
+  *alloc_bytes_out = size;
+  return 0;
+}
+
 int tpi_ipc_export(const void* ptr, void* handle_out, uint64_t* offset_out,
                    uint64_t* alloc_bytes_out) {
   hipDeviceptr_t base = nullptr;

@@ -184,6 +184,9 @@ int tpi_restore_stream(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total
 // tpi_copy_segments moves tensors described by `src` (e.g. a predecessor's, mapped over IPC)
 // into `dst` through the pack / unpack kernels, tile CRCs verified (`bad_tiles`); both plans
 // must describe the same stream.
+// Base address and size of the device allocation holding ptr (exporters call
+// tpi_ipc_export once per allocation, not once per tensor).
+int tpi_mem_range(const void* ptr, uint64_t* base_out, uint64_t* alloc_bytes_out);
 int tpi_ipc_export(const void* ptr, void* handle_out, uint64_t* offset_out,
                    uint64_t* alloc_bytes_out);
 int tpi_copy_segments(tpi_engine* e, const tpi_seg* src, const tpi_seg* dst, int n,

@@ -186,6 +186,7 @@ struct Rank {
   bool standby_capable = false;  // announced "standby" (calls preemption.standby())
   int hot_spawns = 0;            // hot standbys started for this incarnation
   int gofd = -1;                 // standby only: write end of its activation pipe
+  double hold_until = 0;  // a resuming incarnation: no new hot standby until it restored
 };
 
 struct Spec {
@@ -707,6 +708,7 @@ class Supervisor {
     r.started = now();
     r.first_output = false;
     r.released = false;
+    r.hold_until = (!standby && r.restarts > 0) ? r.started + kStandbyHold : 0;
     event(standby ? "standby-start" : "rank-start",
           {"rank " + std::to_string(r.index), "pid " + std::to_string(pid), "machine " + r.uuid,
            "gpus " + (r.gpus.empty() ? "-" : r.gpus), "restart " + std::to_string(r.restarts)});
@@ -729,10 +731,16 @@ class Supervisor {
   // that has already imported its framework and initialised the GPU, so on preemption it is
   // activated the moment the old rank releases -- with a streamed spill, while the spill is
   // still running.  At most two per incarnation (a standby that keeps dying is not retried).
+  //
+  // A successor that is restoring does not get its own standby yet: starting one (interpreter,
+  // framework import, GPU context, engine, spill mapping) competes with the restore for CPU
+  // and GPU.  It comes after the successor reports "restored", or kStandbyHold seconds.
+  static constexpr double kStandbyHold = 10.0;
   void keep_hot_standbys() {
+    const double t = now();
     for (auto& r : ranks_) {
       if (r.state != Rank::RUNNING || r.pid <= 0 || !r.standby_capable || r.term_at > 0 ||
-          standby_[r.index].pid > 0 || r.hot_spawns >= 2)
+          standby_[r.index].pid > 0 || r.hot_spawns >= 2 || t < r.hold_until)
         continue;
       ++r.hot_spawns;
       spawn_standby(r);
@@ -786,6 +794,7 @@ class Supervisor {
     r.exit_code = -1;
     r.exit_signal = 0;
     r.state = Rank::RUNNING;
+    r.hold_until = now() + kStandbyHold;
     sb = Rank();
     event("rank-start", {"rank " + std::to_string(r.index), "pid " + std::to_string(r.pid),
                          "machine " + r.uuid, "gpus " + (r.gpus.empty() ? "-" : r.gpus),
@@ -847,7 +856,10 @@ class Supervisor {
         const std::string msg(buf, (size_t)n);
         if (msg.find("released") != std::string::npos) got = true;
         if (msg.find("standby") != std::string::npos) r.standby_capable = true;
-        if (msg.find("restored") != std::string::npos) release_predecessors(r.index);
+        if (msg.find("restored") != std::string::npos) {
+          release_predecessors(r.index);
+          r.hold_until = 0;  // its hot standby may start now
+        }
         continue;
       }
       if (n == 0) {

@@ -813,22 +813,26 @@ class Checkpointer:
 
         torch.cuda.synchronize(self.device_index)  # no queued kernel may still write them
         lib = hip()
-        allocations: Dict[bytes, int] = {}
+        allocations: Dict[int, int] = {}  # allocation base -> index in `handles`
         handles, where = [], []
         handle = ctypes.create_string_buffer(64)
+        base, size, offset = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
         for seg in self.plan.segs:
-            if int(seg["nbytes"]) == 0 or int(seg["ptr"]) == 0:
+            ptr = int(seg["ptr"])
+            if int(seg["nbytes"]) == 0 or ptr == 0:
                 where.append(None)
                 continue
-            offset, size = ctypes.c_uint64(0), ctypes.c_uint64(0)
-            lib.check(lib.tpi_ipc_export(ctypes.c_void_p(int(seg["ptr"])), handle,
-                                         ctypes.byref(offset), ctypes.byref(size)),
-                      "tpi_ipc_export")
-            key = handle.raw
+            # one IPC handle per allocation (hipIpcGetMemHandle is the slow call; tensors
+            # of one caching-allocator segment share it)
+            lib.check(lib.tpi_mem_range(ctypes.c_void_p(ptr), ctypes.byref(base),
+                                        ctypes.byref(size)), "tpi_mem_range")
+            key = int(base.value)
             if key not in allocations:
+                lib.check(lib.tpi_ipc_export(ctypes.c_void_p(ptr), handle, ctypes.byref(offset),
+                                             ctypes.byref(size)), "tpi_ipc_export")
                 allocations[key] = len(handles)
-                handles.append(key.hex())
-            where.append([allocations[key], int(offset.value)])
+                handles.append(handle.raw.hex())
+            where.append([allocations[key], ptr - key])
         bus = ctypes.create_string_buffer(64)
         lib.tpi_device_pci_bus_id(self.device_index, bus, 64)
         doc = {"format": "tpi-hbm-1", "pid": os.getpid(), "device": bus.value.decode(),

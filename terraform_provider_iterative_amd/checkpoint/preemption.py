@@ -76,16 +76,21 @@ def checkpoint_all(metadata: Optional[Dict] = None, on_stream=None) -> List[floa
     (single checkpointer only): stream the save to the successor (see
     :meth:`Checkpointer.save`); called once the successor may start."""
     meta = dict(metadata or {})
+    t0 = time.perf_counter()
     for cb in _callbacks:
         extra = cb()
         if extra:
             meta.update(extra)
+    t_cb = time.perf_counter() - t0
     rates = []
     for ck in _registered:
         if on_stream is not None and len(_registered) == 1 and _hbm_handoff():
             try:  # the successor on this GPU copies our HBM while we spill to the host
+                t1 = time.perf_counter()
                 if ck.export_hbm():
-                    journal("checkpoint-hbm-export", "successor may copy device to device")
+                    journal("checkpoint-hbm-export", "successor may copy device to device",
+                            "callbacks %.3f s" % t_cb,
+                            "export %.3f s" % (time.perf_counter() - t1))
             except Exception as error:  # the host path still works
                 journal("checkpoint-hbm-export-failed", str(error))
         res = ck.save(meta, on_stream=on_stream if len(_registered) == 1 else None)

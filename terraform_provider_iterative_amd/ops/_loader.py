@@ -71,6 +71,7 @@ class HipLib:
             "tpi_engine_d2h_engine": (c.c_uint32, [vp]),
             "tpi_engine_set_progress": (i32, [vp, vp]),
             "tpi_ipc_export": (i32, [vp, vp, c.POINTER(u64), c.POINTER(u64)]),
+            "tpi_mem_range": (i32, [vp, c.POINTER(u64), c.POINTER(u64)]),
             "tpi_copy_segments": (i32, [vp, vp, vp, i32, u64, u64, c.POINTER(u64), vp]),
             "tpi_restore_stream": (i32, [vp, vp, i32, u64, vp, vp, vp, vp, c.c_double, u64,
                                          c.POINTER(u64), c.POINTER(i64), vp]),

@@ -177,6 +177,9 @@ def test_hot_standby_restores_behind_the_streamed_spill(cloud, monkeypatch):
     for code in ("standby-activated", "checkpoint-streaming", "rank-released", "respawn",
                  "checkpoint-restored"):
         assert code in codes, (code, codes)
+    # the successor's own hot standby waits until it restored (no start-up next to a restore)
+    starts = [i for i, c in enumerate(codes) if c == "standby-start"]
+    assert all(i > codes.index("checkpoint-restored") for i in starts[1:]), codes
     task.delete()
 
 
