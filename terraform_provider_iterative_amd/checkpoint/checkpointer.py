@@ -881,13 +881,27 @@ class Checkpointer:
         import torch
 
         lib = hip()
-        bases = []
+        bases: List[Optional[int]] = [None] * len(doc["allocations"])
+        t0 = time.perf_counter()
+
+        def open_one(i: int) -> None:
+            base = ctypes.c_void_p()
+            lib.check(lib.tpi_ipc_open(bytes.fromhex(doc["allocations"][i]), self.device_index,
+                                       ctypes.byref(base)), "tpi_ipc_open")
+            bases[i] = base.value
+
         try:
-            for h in doc["allocations"]:
-                base = ctypes.c_void_p()
-                lib.check(lib.tpi_ipc_open(bytes.fromhex(h), self.device_index,
-                                           ctypes.byref(base)), "tpi_ipc_open")
-                bases.append(base.value)
+            # one mapping per predecessor allocation (a model's state is hundreds of them);
+            # the opens are independent driver calls, so 8 threads overlap them
+            if len(bases) > 8:
+                from concurrent.futures import ThreadPoolExecutor
+
+                with ThreadPoolExecutor(8) as pool:
+                    list(pool.map(open_one, range(len(bases))))
+            else:
+                for i in range(len(bases)):
+                    open_one(i)
+            self.hbm_open_s = time.perf_counter() - t0
             src = np.frombuffer(bytes.fromhex(doc["segs"]), dtype=self.plan.segs.dtype).copy()
             if len(src) != len(self.plan.segs):
                 raise CheckpointError("HBM hand-off describes a different tensor set")
@@ -897,7 +911,8 @@ class Checkpointer:
             res = self.engine.copy_segments(src, self.plan, sig)
         finally:
             for base in bases:
-                lib.tpi_ipc_close(ctypes.c_void_p(base))
+                if base is not None:
+                    lib.tpi_ipc_close(ctypes.c_void_p(base))
         self.last_restore = res
         if strict and res.bad_tiles:
             raise CheckpointError("%d tile(s) differ after the HBM hand-off" % res.bad_tiles)

@@ -404,7 +404,8 @@ def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None) -> Op
     if header is not None and checkpointer.hbm_ready():
         try:  # the predecessor on this GPU is alive and exported its tensors: copy from HBM
             res = checkpointer.restore_hbm()
-            journal("checkpoint-restored", "HBM hand-off", *_describe(res))
+            journal("checkpoint-restored", "HBM hand-off", *_describe(res),
+                    "ipc open %.3f s" % getattr(checkpointer, "hbm_open_s", 0.0))
             notify_restored()
             return header.get("metadata", {})
         except Exception as error:  # fall back to the host region
