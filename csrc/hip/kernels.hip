@@ -611,9 +611,6 @@ __device__ static inline uint32_t shift_row_col(const uint32_t* t, const ColLane
   return c;
 }
 
-// MODE_CRC: CRC of the stream buffer `a.buf` into `a.crcs`.  MODE_VERIFY: gather the words from
-// the segments `a.segs` (the HBM hand-off's read-back) and count tiles whose CRC differs.
-template <int MODE>
 __global__ __launch_bounds__(CRC_WG) void k_crc_tiles(TileArgs a) {
   __shared__ uint32_t lds[TPI_CRC_COLS_WORDS + 2 * (WG / 64)];  // static: no base add per lookup
   uint32_t* s_red = lds + TPI_CRC_COLS_WORDS;
@@ -636,18 +633,7 @@ __global__ __launch_bounds__(CRC_WG) void k_crc_tiles(TileArgs a) {
     if (t < ntiles) {
       const uint64_t off = t * a.tile_bytes;
       tile_len = umin64(a.tile_bytes, a.len - off);
-      const uint8_t* tbuf = MODE == MODE_CRC ? a.buf + off : nullptr;
-      const uint64_t gbase = a.stream_base + off;
-      SegCursor cur;
-      if (MODE == MODE_VERIFY)
-        seg_load(a.segs, a.nseg, seg_find(a.segs, a.nseg, gbase + lane * 16), cur);
-      auto load = [&](uint64_t rel) -> u32x4 {
-        if (MODE == MODE_VERIFY) {
-          advance(a.segs, a.nseg, gbase + rel, cur);
-          return gather16(a.segs, cur, gbase + rel, nullptr, false);
-        }
-        return __builtin_nontemporal_load((const u32x4*)(tbuf + rel));
-      };
+      const uint8_t* tbuf = a.buf + off;
       uint32_t acc = 0;
       uint64_t last_end = 0, row = 0;
       const uint64_t nrows = (tile_len + TPI_ROW_BYTES - 1) / TPI_ROW_BYTES;
@@ -655,7 +641,9 @@ __global__ __launch_bounds__(CRC_WG) void k_crc_tiles(TileArgs a) {
       for (; row + UNROLL <= full_rows; row += UNROLL) {
         u32x4 w[UNROLL];
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) w[u] = load((row + u) * TPI_ROW_BYTES + lane * 16);
+        for (int u = 0; u < UNROLL; ++u)
+          w[u] = __builtin_nontemporal_load(
+              (const u32x4*)(tbuf + (row + u) * TPI_ROW_BYTES + lane * 16));
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) acc = shift_row_col(lds, m, acc) ^ raw16_col(lds, m, w[u]);
         last_end = (row + UNROLL - 1) * TPI_ROW_BYTES + lane * 16 + 16;
@@ -663,7 +651,7 @@ __global__ __launch_bounds__(CRC_WG) void k_crc_tiles(TileArgs a) {
       for (; row < nrows; ++row) {  // remainder rows, possibly partial
         const uint64_t rel = row * TPI_ROW_BYTES + lane * 16;
         if (rel < tile_len) {
-          const u32x4 w = load(rel);
+          const u32x4 w = __builtin_nontemporal_load((const u32x4*)(tbuf + rel));
           acc = shift_row_col(lds, m, acc) ^ raw16_col(lds, m, w);
           last_end = rel + 16;
         }
@@ -683,16 +671,7 @@ __global__ __launch_bounds__(CRC_WG) void k_crc_tiles(TileArgs a) {
     if (lane == 0 && t < ntiles) {
       const uint32_t* r = s_red + (WG / 64) * half;
       const uint32_t init = (tile_len == a.tile_bytes) ? a.init_full : a.init_last;
-      const uint32_t crc = r[0] ^ r[1] ^ r[2] ^ r[3] ^ init ^ 0xFFFFFFFFu;
-      const uint64_t gtile = a.stream_base / a.tile_bytes + t;
-      if (MODE == MODE_VERIFY) {
-        if (crc != a.crcs[gtile]) {
-          atomicAdd(&a.bad[0], 1ull);
-          atomicMin(&a.bad[1], (unsigned long long)gtile);
-        }
-      } else {
-        a.crcs[gtile] = crc;
-      }
+      a.crcs[a.stream_base / a.tile_bytes + t] = r[0] ^ r[1] ^ r[2] ^ r[3] ^ init ^ 0xFFFFFFFFu;
     }
   }
 }
@@ -840,24 +819,6 @@ __global__ __launch_bounds__(256) void k_dirty_tiles(const uint64_t* __restrict_
 
 // ---- launch helpers (used by engine.hip) -----------------------------------------------------
 
-// k_crc_tiles: two tiles per workgroup, grid-stride over the pairs with two workgroups per CU
-// resident (64 KiB LDS each).
-static unsigned crc_tiles_grid(uint64_t ntiles) {
-  static int cu_count[64];  // per device, queried once (the attribute query is not free)
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
-    if (!__atomic_load_n(&cu_count[dev], __ATOMIC_RELAXED)) {
-      int c = 0;
-      if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-          c > 0)
-        __atomic_store_n(&cu_count[dev], c, __ATOMIC_RELAXED);
-    }
-    if (cu_count[dev]) cus = cu_count[dev];
-  }
-  const uint64_t pairs = (ntiles + 1) / 2;
-  return (unsigned)(pairs < (uint64_t)cus * 2 ? pairs : (uint64_t)cus * 2);
-}
-
 extern "C" hipError_t tpi_launch_stream_crc(int mode, const tpi_seg* segs, int nseg,
                                             uint64_t stream_base, uint64_t len, void* buf,
                                             uint64_t tile_bytes, const tpi_crc_tables* tables,
@@ -888,10 +849,25 @@ extern "C" hipError_t tpi_launch_stream_crc(int mode, const tpi_seg* segs, int n
     case MODE_UNPACK:
       hipLaunchKernelGGL(k_stream_crc<MODE_UNPACK>, grid, block, 0, stream, a);
       break;
-    default:  // CRC only: the column-table kernel
-      hipLaunchKernelGGL(k_crc_tiles<MODE_CRC>, dim3(crc_tiles_grid(ntiles)), dim3(CRC_WG), 0,
-                         stream, a);
+    default: {
+      // CRC only: column-table kernel, two tiles per workgroup, grid-stride over the pairs
+      // with two workgroups per CU resident (64 KiB LDS each).
+      static int cu_count[64];  // per device, queried once (the attribute query is not free)
+      int dev = 0, cus = 256;
+      if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+        if (!__atomic_load_n(&cu_count[dev], __ATOMIC_RELAXED)) {
+          int c = 0;
+          if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+              c > 0)
+            __atomic_store_n(&cu_count[dev], c, __ATOMIC_RELAXED);
+        }
+        if (cu_count[dev]) cus = cu_count[dev];
+      }
+      const uint64_t pairs = (ntiles + 1) / 2;
+      const unsigned g = (unsigned)(pairs < (uint64_t)cus * 2 ? pairs : (uint64_t)cus * 2);
+      hipLaunchKernelGGL(k_crc_tiles, dim3(g), dim3(CRC_WG), 0, stream, a);
       break;
+    }
   }
   return hipGetLastError();
 }
@@ -923,12 +899,9 @@ extern "C" hipError_t tpi_launch_stream_copy(const tpi_seg* src, const tpi_seg* 
   a.total = 0;
   a.staged = 0;
   a.dsegs = dst;
-  const uint64_t ntiles = (len + tile_bytes - 1) / tile_bytes;
-  if (dst)
-    hipLaunchKernelGGL(k_stream_crc<MODE_COPY>, dim3((unsigned)ntiles), dim3(WG), 0, stream, a);
-  else  // read-back verify: read-only, on the conflict-free column tables
-    hipLaunchKernelGGL(k_crc_tiles<MODE_VERIFY>, dim3(crc_tiles_grid(ntiles)), dim3(CRC_WG), 0,
-                       stream, a);
+  const dim3 grid((unsigned)((len + tile_bytes - 1) / tile_bytes)), block(WG);
+  if (dst) hipLaunchKernelGGL(k_stream_crc<MODE_COPY>, grid, block, 0, stream, a);
+  else hipLaunchKernelGGL(k_stream_crc<MODE_VERIFY>, grid, block, 0, stream, a);
   return hipGetLastError();
 }
 
