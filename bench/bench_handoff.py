@@ -114,6 +114,9 @@ def main():
         except OSError:
             pass
         child.wait(60)
+        import shutil
+
+        shutil.rmtree(tmp, ignore_errors=True)  # the spill region file is state-sized
     print(json.dumps(out))
 
 
