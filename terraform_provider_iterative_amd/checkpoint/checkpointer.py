@@ -874,7 +874,8 @@ class Checkpointer:
 
     def restore_hbm(self, strict: bool = True) -> TransferResult:
         """Copy the state of a preempted predecessor on the same GPU straight from its HBM
-        (HIP IPC, pack + unpack kernels, every tile CRC-verified) into the bound tensors."""
+        (HIP IPC; one fused copy pass + a read-back verify, every tile CRC-checked) into the
+        bound tensors."""
         doc = self._hbm_doc()
         if doc is None:
             raise CheckpointError("no HBM hand-off from a live predecessor on this GPU")
@@ -890,17 +891,25 @@ class Checkpointer:
                                        ctypes.byref(base)), "tpi_ipc_open")
             bases[i] = base.value
 
-        try:
+        def close_one(i: int) -> None:
+            if bases[i] is not None:
+                lib.tpi_ipc_close(ctypes.c_void_p(bases[i]))
+                bases[i] = None
+
+        def each(fn) -> None:
             # one mapping per predecessor allocation (a model's state is hundreds of them);
-            # the opens are independent driver calls, so 8 threads overlap them
+            # opens and closes are independent driver calls, so 8 threads overlap them
             if len(bases) > 8:
                 from concurrent.futures import ThreadPoolExecutor
 
                 with ThreadPoolExecutor(8) as pool:
-                    list(pool.map(open_one, range(len(bases))))
+                    list(pool.map(fn, range(len(bases))))
             else:
                 for i in range(len(bases)):
-                    open_one(i)
+                    fn(i)
+
+        try:
+            each(open_one)
             self.hbm_open_s = time.perf_counter() - t0
             src = np.frombuffer(bytes.fromhex(doc["segs"]), dtype=self.plan.segs.dtype).copy()
             if len(src) != len(self.plan.segs):
@@ -910,9 +919,9 @@ class Checkpointer:
             sig = torch.cuda.current_stream(self.device_index).cuda_stream
             res = self.engine.copy_segments(src, self.plan, sig)
         finally:
-            for base in bases:
-                if base is not None:
-                    lib.tpi_ipc_close(ctypes.c_void_p(base))
+            t1 = time.perf_counter()
+            each(close_one)
+            self.hbm_close_s = time.perf_counter() - t1
         self.last_restore = res
         if strict and res.bad_tiles:
             raise CheckpointError("%d tile(s) differ after the HBM hand-off" % res.bad_tiles)

@@ -405,7 +405,8 @@ def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None) -> Op
         try:  # the predecessor on this GPU is alive and exported its tensors: copy from HBM
             res = checkpointer.restore_hbm()
             journal("checkpoint-restored", "HBM hand-off", *_describe(res),
-                    "ipc open %.3f s" % getattr(checkpointer, "hbm_open_s", 0.0))
+                    "ipc open %.3f s" % getattr(checkpointer, "hbm_open_s", 0.0),
+                    "ipc close %.3f s" % getattr(checkpointer, "hbm_close_s", 0.0))
             notify_restored()
             return header.get("metadata", {})
         except Exception as error:  # fall back to the host region
