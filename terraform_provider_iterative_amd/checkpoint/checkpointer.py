@@ -261,9 +261,17 @@ def prewarm_engine(device_index: Optional[int] = None, chunk_bytes: int = 256 <<
 
 def _take_engine(device_index: int, chunk_bytes: int, nbuf: int,
                  tile_bytes: int) -> Optional[DeviceEngine]:
+    """The prewarmed engine for these parameters, if any.  Prewarmed engines of the device that
+    do not match are released: their staging chunks and pinned buffers would otherwise stay
+    allocated for the life of the process."""
     with _engine_pool_lock:
         pool = _engine_pool.get((device_index, chunk_bytes, nbuf, tile_bytes))
-        return pool.pop() if pool else None
+        engine = pool.pop() if pool else None
+        stale = [k for k in _engine_pool if k[0] == device_index]
+        unused = [e for k in stale for e in _engine_pool.pop(k)]
+    for other in unused:
+        other.close()
+    return engine
 
 
 def _layout(header_cap: int, entries_len: int, ntiles: int, total: int, tile_bytes: int):

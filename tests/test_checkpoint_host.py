@@ -260,3 +260,26 @@ def test_failed_streamed_save_fails_the_successor(tmp_path, monkeypatch):
         holder["ck"].restore()
     holder["ck"].close()
     writer.close()
+
+
+def test_engine_pool_hands_out_the_matching_engine_and_releases_the_rest(monkeypatch):
+    # prewarm_engine's pool, with stand-in engines (no GPU): the first Checkpointer on a device
+    # takes the engine with its parameters; the device's other prewarmed engines are closed
+    from terraform_provider_iterative_amd.checkpoint import checkpointer as ckmod
+
+    class FakeEngine:
+        def __init__(self):
+            self.closed = False
+
+        def close(self):
+            self.closed = True
+
+    monkeypatch.setattr(ckmod, "_engine_pool", {})
+    match, other, elsewhere = FakeEngine(), FakeEngine(), FakeEngine()
+    ckmod._engine_pool[(0, 256 << 20, 3, 1 << 20)] = [match]
+    ckmod._engine_pool[(0, 64 << 20, 2, 1 << 20)] = [other]
+    ckmod._engine_pool[(1, 256 << 20, 3, 1 << 20)] = [elsewhere]
+    assert ckmod._take_engine(0, 256 << 20, 3, 1 << 20) is match
+    assert other.closed and not match.closed and not elsewhere.closed
+    assert list(ckmod._engine_pool) == [(1, 256 << 20, 3, 1 << 20)]
+    assert ckmod._take_engine(0, 256 << 20, 3, 1 << 20) is None
