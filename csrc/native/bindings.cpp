@@ -4,6 +4,7 @@
 
 #include <stdexcept>
 
+#include "ctl.h"
 #include "filter.h"
 #include "../common/tpz.h"
 #include "fileio.h"
@@ -190,6 +191,27 @@ PYBIND11_MODULE(_tpi_native, m) {
     const int64_t r = tpi::resident_bytes(path.c_str(), &size, &tmpfs);
     return py::make_tuple(r, size, (bool)tmpfs);
   });
+  // step-boundary agreement block (ctl.h); `base` is the address of a shared mapping
+  m.def("ctl_bytes", &tpi::ctl::bytes);
+  m.def("ctl_init", [](uintptr_t base, int world) { tpi::ctl::init((void*)base, world); });
+  m.def("ctl_valid", [](uintptr_t base, int world) {
+    return tpi::ctl::valid((const void*)base, world);
+  });
+  m.def("ctl_arrive", [](uintptr_t base, int rank, uint64_t ordinal) {
+    uint64_t preempt = 0, periodic = 0;
+    tpi::ctl::arrive((void*)base, rank, ordinal, &preempt, &periodic);
+    return py::make_tuple(preempt, periodic);
+  });
+  m.def("ctl_propose_preempt", [](uintptr_t base, int world, int self) {
+    return tpi::ctl::propose_preempt((void*)base, world, self);
+  });
+  m.def("ctl_propose_periodic", [](uintptr_t base, int world, int self) {
+    return tpi::ctl::propose_periodic((void*)base, world, self);
+  });
+  m.def("ctl_ordinal", [](uintptr_t base, int rank) {
+    return tpi::ctl::ordinal_of((const void*)base, rank);
+  });
+
   m.def("tpz_bound", [](uint64_t len) { return tpz_bound(len); });
   m.def("tpz_meta_bytes", [](uint64_t ntiles) { return tpz_meta_bytes(ntiles); });
   m.def("tpz_encode_ptr", [](uintptr_t src, uint64_t total, uint64_t tile, uintptr_t dst,

@@ -39,6 +39,7 @@
 // supervisor/events.jsonl journal.
 #include <errno.h>
 #include <fcntl.h>
+#include <netinet/in.h>
 #include <poll.h>
 #include <sched.h>
 #include <signal.h>
@@ -577,6 +578,9 @@ class Supervisor {
     add("TPI_RESTART_COUNT", std::to_string(r.restarts));
     add("TPI_EVENTS_FILE", s_.events_path);  // ranks journal checkpoint phases here
     add("TPI_NOTIFY_FD", "3");                 // "released": spill done, respawn may start
+    // SIGTERM -> SIGKILL window: a preempted rank saves at its next step boundary and falls
+    // back to an immediate save after half of it (checkpoint/preemption.py)
+    add("TPI_GRACE_SECONDS", std::to_string(s_.grace));
     if (staged_) add("TPI_HBM_WORKDIR", s_.stager_manifest);  // runtime/stage.py attach()
     if (s_.deadline > 0) {
       add("TPI_DEADLINE", std::to_string((long long)s_.deadline));
@@ -767,8 +771,9 @@ class Supervisor {
   bool activate_standby(Rank& r) {
     Rank& sb = standby_[r.index];
     if (sb.pid <= 0) return false;
-    const char go[] = "go\n";
-    const bool sent = sb.gofd >= 0 && write(sb.gofd, go, 3) == 3;
+    // the rendezvous port of this incarnation (the standby was spawned with the previous one)
+    const std::string go = "go port=" + std::to_string(s_.master_port) + "\n";
+    const bool sent = sb.gofd >= 0 && write(sb.gofd, go.data(), go.size()) == (ssize_t)go.size();
     if (sb.gofd >= 0) close(sb.gofd);
     sb.gofd = -1;
     if (!sent) {
@@ -966,6 +971,7 @@ class Supervisor {
     if (respawn_at_ <= 0 || t < respawn_at_ || stop_ || timed_out_) return;
     if (s_.gang && running() > 0) return;  // wait for the whole gang to go down
     respawn_at_ = 0;
+    if (s_.gang && s_.parallelism > 1) next_master_port();
     for (auto& r : ranks_)
       if (r.state == Rank::PREEMPTED) {
         if (s_.max_restarts >= 0 && r.restarts >= s_.max_restarts) {
@@ -981,6 +987,28 @@ class Supervisor {
                           "restart " + std::to_string(r.restarts)});
         if (!activate_standby(r)) spawn(r);
       }
+  }
+
+  // A fresh rendezvous port for every gang incarnation: a predecessor that lingers after its
+  // spill (early hand-off) may still hold the old one -- rank 0's TCPStore listens on it.
+  void next_master_port() {
+    for (int i = 1; i <= 256; ++i) {
+      int port = s_.master_port + i;
+      if (port > 65000) port = 20000 + port % 1000;
+      int fd = socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+      struct sockaddr_in a;
+      memset(&a, 0, sizeof(a));
+      a.sin_family = AF_INET;
+      a.sin_port = htons((uint16_t)port);
+      a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+      const bool free_port = fd >= 0 && bind(fd, (struct sockaddr*)&a, sizeof(a)) == 0;
+      if (fd >= 0) close(fd);
+      if (free_port) {
+        s_.master_port = port;
+        event("rendezvous", {"master port " + std::to_string(port)});
+        return;
+      }
+    }
   }
 
   void handle_signals() {

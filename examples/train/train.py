@@ -4,8 +4,9 @@
 * stages the task workdir into HBM (rank 0 reads, RCCL fans out to the other ranks),
 * trains a small random-init transformer-style MLP in bf16 on synthetic tokens (DDP over
   RCCL when ``WORLD_SIZE > 1``),
-* checkpoints model + optimizer state to host DRAM on SIGTERM (preemption) and resumes from
-  it when respawned, persisting to the task's storage at the end.
+* checkpoints model + optimizer state to host DRAM on SIGTERM (preemption) at the next step
+  boundary (``state.step``) -- all ranks at the same step -- and resumes from it when
+  respawned, persisting to the task's storage at the end.
 
 Environment (set by the supervisor): RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT,
 HIP_VISIBLE_DEVICES, TPI_DATA_DIRECTORY, TPI_MACHINE_IDENTITY.
@@ -132,7 +133,9 @@ def main():
         t_ck = time.perf_counter()
         if args.ckpt_every and (step + 1) % args.ckpt_every == 0:
             state.save_async({"step": step + 1})  # HBM snapshot; the PCIe spill runs behind
-        elif not preemption.tick({"step": step + 1}):  # every TPI_SYNC_INTERVAL s (default 10)
+        # step boundary: a SIGTERM that arrived during this step is saved here (every rank at
+        # the same step); periodic checkpoints every TPI_SYNC_INTERVAL s (default 10)
+        elif not state.step(step + 1):
             continue
         if device.type == "cuda":
             torch.cuda.current_stream().synchronize()

@@ -30,6 +30,7 @@ from __future__ import annotations
 import json
 import logging
 import os
+import re
 import shlex
 import subprocess
 import tarfile
@@ -68,13 +69,21 @@ def _node_region(region: str) -> str:
     return ",".join(keep)
 
 
+_HOST = re.compile(r"^(?:[A-Za-z0-9._][A-Za-z0-9._-]*@)?(?:[A-Za-z0-9_][A-Za-z0-9._-]*|\[[0-9A-Fa-f:.]+\])$")
+
+
 class Transport:
     """One command per operation through ``TPI_SSH_COMMAND <host> <remote command>``."""
 
     def __init__(self, cloud: Cloud):
         sel = parse_region_selectors(cloud.region)
         self.host = sel["host"]
+        # the host goes into ssh's argv: "-oProxyCommand=..." would be parsed as an option
+        if not _HOST.match(self.host or ""):
+            raise ValueError("region host %r is not [user@]hostname" % self.host)
         self.port = sel.get("port")
+        if self.port is not None and not str(self.port).isdigit():
+            raise ValueError("region port %r is not a number" % self.port)
         self.state_root = sel.get("root", "")
         self.provider = cloud.provider
         self.region = _node_region(cloud.region)

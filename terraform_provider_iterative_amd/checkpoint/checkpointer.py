@@ -283,6 +283,27 @@ def _layout(header_cap: int, entries_len: int, ntiles: int, total: int, tile_byt
     return entries_offset, crc_offset, csize_offset, stream_offset, stream_offset + capacity
 
 
+def _writer_alive(pid: int) -> bool:
+    """Is the process that published a streamed save still running (zombies count as gone)?
+    Our own pid is alive (``load()`` streams from a reader thread of this process)."""
+    if pid <= 0:
+        return False
+    if pid == os.getpid():
+        return True
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        return True
+    try:
+        with open("/proc/%d/stat" % pid) as f:
+            state = f.read().rsplit(")", 1)[1].split()[0]
+        return state not in ("Z", "X")
+    except (OSError, IndexError):
+        return True
+
+
 class PendingSave:
     """An asynchronous save in flight (:meth:`Checkpointer.save_async`)."""
 
@@ -427,7 +448,9 @@ class Checkpointer:
 
     def _streaming(self) -> Optional[Tuple[_Slot, Dict]]:
         """A slot a streamed save is writing (or has just finished) that is newer than the
-        newest complete checkpoint: what a preempted rank's successor restores."""
+        newest complete checkpoint: what a preempted rank's successor restores.  A slot still
+        marked running whose writer process is gone (SIGKILLed past the grace period, OOM) is
+        no stream: waiting on it would only time out."""
         active = self._active()
         floor = active[1].get("generation", 0) if active else 0
         best = None
@@ -441,10 +464,28 @@ class Checkpointer:
                     and int(prog[0]) == PROGRESS_MAGIC
                     and int(prog[1]) == header.get("generation")
                     and int(prog[4]) in (STREAM_RUNNING, STREAM_COMPLETE)
+                    and (int(prog[4]) == STREAM_COMPLETE or _writer_alive(int(prog[5])))
                     and header.get("generation", 0) > floor
                     and (best is None or header["generation"] > best[1]["generation"])):
                 best = (slot, header)
         return best
+
+    def candidates(self) -> List[Dict]:
+        """Every restorable copy in the region, newest first: ``{"generation", "metadata",
+        "streaming"}`` (a streamed save in flight, then the complete slots).  Ranks that must
+        resume the same step pick a common one (:meth:`TrainingState.resume_consistent`)."""
+        out = []
+        streaming = self._streaming()
+        if streaming is not None:
+            out.append({"generation": streaming[1].get("generation", 0), "streaming": True,
+                        "metadata": streaming[1].get("metadata", {})})
+        for slot in self.slots:
+            header = self._slot_header(slot)
+            if header is not None:
+                out.append({"generation": header.get("generation", 0), "streaming": False,
+                            "metadata": header.get("metadata", {})})
+        out.sort(key=lambda c: -c["generation"])
+        return out
 
     def latest(self) -> Optional[Dict]:
         """Header of the newest restorable checkpoint -- complete, or being streamed by a
@@ -720,19 +761,26 @@ class Checkpointer:
         self.last_save = res
         return res
 
-    def restore(self, strict: bool = True, stream_timeout: Optional[float] = None
-                ) -> TransferResult:
+    def restore(self, strict: bool = True, stream_timeout: Optional[float] = None,
+                generation: Optional[int] = None) -> TransferResult:
         """Unpack + verify the current checkpoint into the bound tensors.  If a preempted
         predecessor is still streaming a newer one into the region, restore that one behind
         its progress (``stream_timeout`` s without progress -> :class:`CheckpointError`;
-        default ``TPI_STREAM_TIMEOUT`` or 30)."""
+        default ``TPI_STREAM_TIMEOUT`` or 30).  ``generation`` picks a specific copy (one of
+        :meth:`candidates`) instead of the newest."""
         self.wait_pending()
         streaming = self._streaming()
-        if streaming is not None:
+        if streaming is not None and generation in (None, streaming[1].get("generation")):
             if stream_timeout is None:
                 stream_timeout = float(os.environ.get("TPI_STREAM_TIMEOUT", "30"))
             return self._restore_streaming(*streaming, strict=strict, timeout=stream_timeout)
         active = self._active()
+        if generation is not None:
+            active = next(((s, h) for s in self.slots
+                           for h in [self._slot_header(s)]
+                           if h is not None and h.get("generation") == generation), None)
+            if active is None:
+                raise CheckpointError("no complete checkpoint of generation %d" % generation)
         if active is None:
             header = self.header()  # raises "no checkpoint" unless an incomplete one is there
             raise CheckpointError("checkpoint incomplete (save was interrupted)")

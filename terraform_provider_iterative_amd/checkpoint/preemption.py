@@ -6,12 +6,33 @@ shutting down writes no status and gets respawned with the workdir restored from
 a rank that installed :func:`install` checkpoints its registered tensors to host memory (and
 optionally the storage root) and exits with :data:`PREEMPTED_EXIT_CODE`, and its successor
 calls :func:`resume` to restore them.
+
+**Where the save happens.**  The reference leaves consistency to the user script, which
+resumes from files it wrote at its own points (``README.md:88-101``).  A tensor checkpoint
+taken at whatever bytecode a signal interrupts can be torn: weights already updated by
+``opt.step()`` next to the old step counter, or half of AdamW's ``_foreach`` moment updates.
+So the signal handler only *records* the request; the save runs at the next **step boundary**
+-- :func:`step` (or :func:`tick`), called by the training loop where the registered tensors
+are consistent -- and every rank of a job saves the same boundary (:mod:`.agreement`: one
+shared cache line per rank, no per-step collective).
+
+* The signal is seen even while the main thread is blocked in C (a collective, a device
+  sync): CPython's C-level handler writes it to a wakeup pipe that a watcher thread reads
+  (``signal.set_wakeup_fd``), so the request, its journal line and its deadline do not wait
+  for the interpreter.
+* A script that never calls :func:`step`/:func:`tick` keeps the old behaviour (save in the
+  handler, journalled ``consistency signal``).
+* A rank that reaches no boundary within ``TPI_PREEMPT_FALLBACK_SECONDS`` (default half of
+  the supervisor's grace period ``TPI_GRACE_SECONDS``) is saved by the watcher thread anyway,
+  journalled ``preempt-torn-risk`` and marked ``consistency torn-risk`` in the metadata, which
+  :meth:`TrainingState.resume_consistent` refuses by default.
 """
 from __future__ import annotations
 
 import json
 import logging
 import os
+import select
 import signal
 import sys
 import threading
@@ -28,7 +49,18 @@ _registered: List[Checkpointer] = []
 _persist_paths: Dict[int, str] = {}
 _callbacks: List[Callable[[], Optional[Dict]]] = []
 _installed = False
-_fired = threading.Event()
+_signals: tuple = (signal.SIGTERM,)
+
+_requested = threading.Event()   # a preemption signal arrived
+_fired = threading.Event()       # the preemption save started (at most one per process)
+_usr2 = threading.Event()        # the successor restored: a lingering predecessor may exit
+_save_lock = threading.Lock()
+_note_lock = threading.Lock()
+_signal_info: Dict[str, float] = {}
+_boundary_seen = False           # the loop calls step()/tick(): saves wait for a boundary
+_last_step: Optional[int] = None  # user step of the last boundary
+_agreement = None
+_wakeup_r: Optional[int] = None
 
 
 def register(checkpointer: Checkpointer, persist_path: Optional[str] = None) -> None:
@@ -38,11 +70,16 @@ def register(checkpointer: Checkpointer, persist_path: Optional[str] = None) -> 
 
 
 def on_preempt(callback: Callable[[], Optional[Dict]]) -> None:
-    """Callback run before the save; may return metadata (e.g. ``{"step": n}``)."""
+    """Callback run before every save (preemption or periodic); may return metadata."""
     _callbacks.append(callback)
 
 
 def preempted() -> bool:
+    """A preemption was requested (the rank will save at its next step boundary)."""
+    return _requested.is_set()
+
+
+def saving() -> bool:
     return _fired.is_set()
 
 
@@ -71,16 +108,22 @@ def _describe(res) -> List[str]:
             "%.3f s" % res.seconds, "%.1f GB/s" % res.gbps]
 
 
-def checkpoint_all(metadata: Optional[Dict] = None, on_stream=None) -> List[float]:
-    """Save every registered checkpointer; returns per-checkpointer GB/s.  ``on_stream``
-    (single checkpointer only): stream the save to the successor (see
-    :meth:`Checkpointer.save`); called once the successor may start."""
-    meta = dict(metadata or {})
-    t0 = time.perf_counter()
+def _collect_metadata(base: Dict) -> Dict:
+    meta = dict(base)
     for cb in _callbacks:
         extra = cb()
         if extra:
             meta.update(extra)
+    return meta
+
+
+def checkpoint_all(metadata: Optional[Dict] = None, on_stream=None) -> List[float]:
+    """Save every registered checkpointer; returns per-checkpointer GB/s.  ``on_stream``
+    (single checkpointer only): stream the save to the successor (see
+    :meth:`Checkpointer.save`); called once the successor may start."""
+    t0 = time.perf_counter()
+    meta = _collect_metadata({})
+    meta.update(metadata or {})
     t_cb = time.perf_counter() - t0
     rates = []
     for ck in _registered:
@@ -110,11 +153,12 @@ def checkpoint_all(metadata: Optional[Dict] = None, on_stream=None) -> List[floa
 
 _tick_last: Optional[float] = None
 _tick_pending: Dict[int, object] = {}  # id(checkpointer) -> PendingSave of the last tick
+_slots_warned = False
 
 
 def sync_interval() -> float:
     """Seconds between periodic checkpoints (``TPI_SYNC_INTERVAL``, default 10 as in the
-    reference; 0 or less disables :func:`tick`)."""
+    reference; 0 or less disables the cadence)."""
     try:
         return float(os.environ.get("TPI_SYNC_INTERVAL", "10"))
     except ValueError:
@@ -139,29 +183,43 @@ def _collect_finished() -> bool:
     return not running
 
 
-def _agree(due: bool) -> bool:
-    """Ranks of one job checkpoint the same step: with ``torch.distributed`` initialised the
-    decision is the minimum over ranks (one 4-byte all-reduce per call; every rank must call
-    :func:`tick` at the same steps)."""
-    dist = sys.modules.get("torch.distributed")
-    if dist is None or not dist.is_available() or not dist.is_initialized() or \
-            dist.get_world_size() < 2:
-        return due
-    import torch
+def _periodic_save(step_no: Optional[int], metadata: Optional[Dict]) -> None:
+    global _slots_warned
+    meta = _collect_metadata({"reason": "periodic", "consistency": "boundary"})
+    if step_no is not None:
+        meta["step"] = step_no
+    meta.update(metadata or {})
+    mode = os.environ.get("TPI_SYNC_MODE", "async")
+    for ck in _registered:
+        if len(ck.slots) == 1 and not _slots_warned:
+            _slots_warned = True  # the spill overwrites the one copy: a crash mid-spill loses it
+            journal("checkpoint-sync-warning", "slots=1: each periodic spill invalidates the "
+                    "only copy while it runs; Checkpointer(slots=2) keeps the previous one")
+        if mode == "sync":
+            t0 = time.perf_counter()
+            res = ck.sync(meta)
+            journal("checkpoint-synced", "incremental", "%d dirty tiles" % res.dirty_tiles,
+                    *_describe(res), "%.1f ms" % ((time.perf_counter() - t0) * 1e3))
+        else:
+            _tick_pending[id(ck)] = ck.save_async(meta)
+    _collect_finished()  # host tensors save synchronously: journal them now
 
-    device = "cpu"
-    if dist.get_backend() == "nccl":
-        device = torch.device("cuda", torch.cuda.current_device())
-    flag = torch.tensor([1 if due else 0], dtype=torch.int32, device=device)
-    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-    return bool(flag.item())
 
+def step(step: Optional[int] = None, metadata: Optional[Dict] = None,
+         force: bool = False) -> bool:
+    """Step-boundary hook: call it where the registered tensors are consistent (after the
+    optimizer step *and* the step counter update), at the same points on every rank.
 
-def tick(metadata: Optional[Dict] = None, force: bool = False) -> bool:
-    """Periodic checkpoint hook: call it at a step boundary (where the registered tensors are
-    consistent).  Every :func:`sync_interval` seconds it checkpoints every registered
-    :class:`Checkpointer` into its host region, so a rank that dies without a SIGTERM (OOM,
-    crash, SIGKILL after the grace period) still leaves a recent checkpoint behind.
+    * A pending preemption is saved here -- on every rank at the same boundary -- and the
+      process exits (this call does not return then).
+    * Every :func:`sync_interval` seconds (rank 0's clock decides for the job) it takes a
+      periodic checkpoint of every registered :class:`Checkpointer`, so a rank that dies
+      without a SIGTERM (OOM, crash, SIGKILL after the grace period) still leaves a recent
+      checkpoint behind.  ``force=True`` checkpoints now (every rank must pass it at the same
+      boundary).
+
+    ``step`` (the loop's own counter) is recorded in every save's metadata.  Returns True when
+    this call took a periodic checkpoint.
 
     ``TPI_SYNC_MODE``:
       ``async`` (default)  HBM snapshot + background spill (:meth:`Checkpointer.save_async`):
@@ -171,44 +229,44 @@ def tick(metadata: Optional[Dict] = None, force: bool = False) -> bool:
       ``sync``             incremental (:meth:`Checkpointer.sync`): only tiles whose device
                            digest changed since the last tick cross PCIe -- cheapest for mostly
                            frozen state (fine-tuning adapters, embeddings); blocks the caller.
-
-    The first call arms the timer.  Returns True when this call checkpointed.  Each completed
-    checkpoint is journalled (``checkpoint-synced``) with its bytes, wire bytes and time.  In a
-    multi-rank job all ranks decide together (:func:`_agree`), so they checkpoint the same step
-    and :meth:`TrainingState.resume_consistent` finds it on every rank.
     """
-    global _tick_last
-    if _fired.is_set() or not _registered:
-        return False
+    global _boundary_seen, _last_step, _agreement, _tick_last
+    _boundary_seen = True
+    if step is not None:
+        _last_step = step
+    elif metadata and isinstance(metadata.get("step"), int):
+        _last_step = metadata["step"]
+    if _fired.is_set():  # a fallback save is running in the watcher: stop touching tensors
+        threading.Event().wait()
+    if _agreement is None:
+        from . import agreement
+
+        _agreement = agreement.create()
     now = time.monotonic()
     idle = _collect_finished()
-    if _tick_last is None and not force:
-        _tick_last = now
-        return False
     interval = sync_interval()
-    if interval <= 0 and not force:
-        return False
-    due = idle and (force or now - _tick_last >= interval)
-    if not _agree(due):
-        return False
-    meta = {"reason": "periodic"}
-    for cb in _callbacks:
-        extra = cb()
-        if extra:
-            meta.update(extra)
-    meta.update(metadata or {})
-    mode = os.environ.get("TPI_SYNC_MODE", "async")
-    for ck in _registered:
-        if mode == "sync":
-            t0 = time.perf_counter()
-            res = ck.sync(meta)
-            journal("checkpoint-synced", "incremental", "%d dirty tiles" % res.dirty_tiles,
-                    *_describe(res), "%.1f ms" % ((time.perf_counter() - t0) * 1e3))
-        else:
-            _tick_pending[id(ck)] = ck.save_async(meta)
-    _tick_last = now
-    _collect_finished()  # host tensors save synchronously: journal them now
-    return True
+    due = False
+    if _registered and _tick_last is None and not force:
+        _tick_last = now  # the first call arms the timer
+    elif _registered and (force or (interval > 0 and idle and now - _tick_last >= interval)):
+        due = True
+    shared = _agreement.kind == "shm"
+    preempt_here, periodic_here = _agreement.arrive(_requested.is_set(),
+                                                    due and not force)
+    if preempt_here:
+        _boundary_save()  # does not return
+    if shared and _agreement.proposed:
+        _tick_last = now  # rank 0 chose the next periodic boundary: the interval restarts
+    if force or periodic_here:
+        _periodic_save(_last_step, metadata)
+        _tick_last = now
+        return True
+    return False
+
+
+def tick(metadata: Optional[Dict] = None, force: bool = False) -> bool:
+    """:func:`step` with the step number (if any) taken from ``metadata["step"]``."""
+    return step(None, metadata, force)
 
 
 def _handoff_safe() -> bool:
@@ -297,7 +355,7 @@ def standby(prefetch_path: Optional[str] = None) -> bool:
     fd = int(os.environ.get("TPI_STANDBY_FD", "4"))
     while True:
         try:
-            msg = os.read(fd, 16)
+            msg = os.read(fd, 64)
             break
         except InterruptedError:
             continue
@@ -305,6 +363,9 @@ def standby(prefetch_path: Optional[str] = None) -> bool:
     if not msg.startswith(b"go"):
         os._exit(0)  # discarded before activation
     os.close(fd)
+    for word in msg.split():  # "go port=N": this incarnation's rendezvous port
+        if word.startswith(b"port="):
+            os.environ["MASTER_PORT"] = word[5:].decode()
     os.environ.pop("TPI_STANDBY", None)
     journal("standby-activated")
     _notify(b"standby\n")  # the activated process can itself be succeeded by a standby
@@ -313,18 +374,18 @@ def standby(prefetch_path: Optional[str] = None) -> bool:
 
 def _linger() -> None:
     """After an early hand-off, stay alive (host region still pinned) until the supervisor
-    says the successor restored (SIGUSR2) or ``TPI_LINGER_SECONDS`` (default 20) pass: the
-    kernel's unpinning of a 100 GB region on exit (~1.4 s) would otherwise run during the
-    successor's restore and halve its DMA rate (profiles/preempt_e2e_100g_round1.md)."""
+    says the successor restored (SIGUSR2, seen through :data:`_usr2`) or
+    ``TPI_LINGER_SECONDS`` (default 20) pass: the kernel's unpinning of a 100 GB region on exit
+    (~1.4 s) would otherwise run during the successor's restore and halve its DMA rate
+    (profiles/preempt_e2e_100g_round1.md)."""
     try:
         timeout = float(os.environ.get("TPI_LINGER_SECONDS", "20"))
     except ValueError:
         timeout = 20.0
-    if timeout <= 0 or not hasattr(signal, "sigtimedwait"):
+    if timeout <= 0:
         return
     sys.stdout.flush()
-    signal.pthread_sigmask(signal.SIG_BLOCK, [signal.SIGUSR2])
-    got = signal.sigtimedwait([signal.SIGUSR2], timeout)
+    got = _usr2.wait(timeout)
     journal("predecessor-exit", "successor restored" if got else "linger timeout")
 
 
@@ -333,32 +394,73 @@ def notify_restored() -> bool:
     return _notify(b"restored\n")
 
 
-def _handler(signum, frame):  # pragma: no cover - exercised in subprocess tests
-    if _fired.is_set():
+def fallback_seconds() -> float:
+    """How long a requested preemption waits for a step boundary before the watcher saves
+    anyway (``TPI_PREEMPT_FALLBACK_SECONDS``; default half of ``TPI_GRACE_SECONDS``, the
+    supervisor's SIGTERM -> SIGKILL window, itself 30 s by default)."""
+    try:
+        return float(os.environ["TPI_PREEMPT_FALLBACK_SECONDS"])
+    except (KeyError, ValueError):
+        pass
+    try:
+        grace = float(os.environ.get("TPI_GRACE_SECONDS", "30"))
+    except ValueError:
+        grace = 30.0
+    return max(0.5 * grace, 0.1)
+
+
+def _boundary_mode() -> bool:
+    """Does a preemption wait for the next step boundary?  ``TPI_PREEMPT_AT``: ``auto``
+    (default: yes once the loop has called :func:`step`/:func:`tick`), ``boundary`` (always),
+    ``signal`` (never: save in the handler, the pre-boundary behaviour)."""
+    at = os.environ.get("TPI_PREEMPT_AT", "auto")
+    if at == "signal":
+        return False
+    return at == "boundary" or _boundary_seen
+
+
+def _note_signal(signum: int) -> bool:
+    """Record a preemption request once (handler or watcher, whichever runs first)."""
+    with _note_lock:
+        if _requested.is_set():
+            return False
+        _signal_info["signum"] = signum
+        _signal_info["time"] = time.time()
+        _signal_info["mono"] = time.monotonic()
+        _requested.set()
+    journal("preempt-signal", "signal %d" % signum,
+            "save at the next step boundary" if _boundary_mode() else "save now (no step hook)")
+    return True
+
+
+def _save_and_exit(consistency: str, ordinal: Optional[int] = None) -> None:
+    """Run the preemption save once and exit; returns only if another thread is saving."""
+    if not _save_lock.acquire(blocking=False):
         return
     _fired.set()
-    # The successor's "restored" reaches us as SIGUSR2 (see _linger).  With a streamed
-    # hand-off it can arrive while this save is still finishing (final header, persist); its
-    # default action would kill us mid-write, so it stays pending until _linger takes it.
-    if hasattr(signal, "pthread_sigmask"):
-        signal.pthread_sigmask(signal.SIG_BLOCK, [signal.SIGUSR2])
-    journal("preempt-signal", "signal %d" % signum)
+    signum = int(_signal_info.get("signum", signal.SIGTERM))
     t0 = time.perf_counter()
     released = []
+    stream_ok = False
 
     def stream_started():
         # the successor starts now and restores behind the spill (other PCIe direction);
         # journalled first, so the phase journal orders it before the supervisor's release
-        if _stream_handoff():
+        if stream_ok:
             journal("checkpoint-streaming", "successor may start")
         if notify_released():
             released.append(True)
 
+    meta = {"reason": "preempted", "signal": signum, "consistency": consistency}
+    if _last_step is not None:
+        meta["step"] = _last_step
+    if ordinal is not None:
+        meta["boundary"] = ordinal
     try:
         t_safe = time.perf_counter()
-        stream = stream_started if _stream_handoff() else None
+        stream_ok = _stream_handoff()  # evaluated once: one device-memory query
         _phase["handoff-check"] = time.perf_counter() - t_safe
-        rates = checkpoint_all({"reason": "preempted", "signal": signum}, on_stream=stream)
+        rates = checkpoint_all(meta, on_stream=stream_started if stream_ok else None)
         print("tpi: preemption checkpoint saved in %.3fs (%s GB/s)" % (
             time.perf_counter() - t0, ", ".join("%.1f" % r for r in rates)), flush=True)
         code = PREEMPTED_EXIT_CODE
@@ -380,28 +482,111 @@ def _handler(signum, frame):  # pragma: no cover - exercised in subprocess tests
     os._exit(code)
 
 
+def _boundary_save() -> None:
+    ordinal = getattr(_agreement, "ordinal", None)
+    waited = time.monotonic() - _signal_info.get("mono", time.monotonic())
+    desc = ["boundary %s" % ordinal, "waited %.3f s" % waited]
+    if _last_step is not None:
+        desc.insert(1, "step %d" % _last_step)
+    journal("preempt-boundary", *desc)
+    _save_and_exit("boundary", ordinal)
+    threading.Event().wait()  # the watcher's fallback save owns the process now
+
+
+def _on_signal(signum, frame):  # pragma: no cover - exercised in subprocess tests
+    _note_signal(signum)
+    if not _boundary_mode() and not _fired.is_set():
+        _save_and_exit("signal")  # no step hook in this script: save where it stands
+
+
+def _on_usr2(signum, frame):  # pragma: no cover - exercised in subprocess tests
+    _usr2.set()
+
+
+def _watch(rfd: int) -> None:
+    """Watcher thread: sees signals through the wakeup pipe even while the main thread is
+    blocked in C, and saves anyway when no step boundary comes in time."""
+    preempt_signals = {int(s) for s in _signals}
+    while True:
+        timeout = None
+        if _requested.is_set() and not _fired.is_set():
+            timeout = max(0.0, _signal_info["mono"] + fallback_seconds() - time.monotonic())
+        try:
+            ready, _, _ = select.select([rfd], [], [], timeout)
+        except InterruptedError:
+            continue
+        if not ready:
+            if _fired.is_set():
+                continue
+            journal("preempt-torn-risk", "no step boundary within %.1f s" % fallback_seconds(),
+                    "last step %s" % _last_step)
+            _save_and_exit("torn-risk" if _boundary_mode() else "signal")
+            continue
+        try:
+            data = os.read(rfd, 64)
+        except (BlockingIOError, InterruptedError):
+            continue
+        if not data:
+            return
+        for signum in data:
+            if signum == signal.SIGUSR2:
+                _usr2.set()
+            elif signum in preempt_signals:
+                _note_signal(signum)
+
+
 def install(signals=(signal.SIGTERM,)) -> None:
-    global _installed
+    """Arm preemption handling (call from the main thread).  SIGTERM records a request (saved
+    at the next :func:`step`, or at once in a script that never calls it); SIGUSR2 from the
+    supervisor lets a lingering predecessor exit."""
+    global _installed, _signals, _wakeup_r
+    _signals = tuple(signals)
     for sig in signals:
-        signal.signal(sig, _handler)
+        signal.signal(sig, _on_signal)
+    signal.signal(signal.SIGUSR2, _on_usr2)
+    if _wakeup_r is None:
+        r, w = os.pipe()
+        os.set_blocking(w, False)
+        try:
+            signal.set_wakeup_fd(w, warn_on_full_buffer=False)
+        except ValueError:  # not the main thread: the Python handlers still work
+            os.close(r)
+            os.close(w)
+        else:
+            _wakeup_r = r
+            threading.Thread(target=_watch, args=(r,), name="tpi-preempt-watch",
+                             daemon=True).start()
     _installed = True
     # The hand-off check's first device-memory query costs ~0.1 s on MI355X (measured in the
     # handler: signal -> HBM export 0.11 s); pay it now, not after the signal.
     _handoff_safe()
 
 
-def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None) -> Optional[Dict]:
+def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None,
+           generation: Optional[int] = None) -> Optional[Dict]:
     """Restore from the host region (or ``persist_path``) if a complete checkpoint exists.
 
     Returns the checkpoint metadata, or ``None`` for a fresh start -- only when there is no
     complete checkpoint anywhere.  A checkpoint that exists but fails verification (corrupt
     tiles) has already been partly unpacked into the tensors, so it never turns into a fresh
     start: the persisted copy is tried next, and if that fails too :class:`CheckpointError`
-    is raised.
+    is raised.  ``generation``: restore that copy of the region (see
+    :meth:`Checkpointer.candidates`) rather than the newest.
     """
     failure: Optional[CheckpointError] = None
     header = checkpointer.latest()  # complete, or still streaming in from the predecessor
-    if header is not None and checkpointer.hbm_ready():
+    newest = header
+    if generation is not None:
+        header = next(({"generation": c["generation"], "metadata": c["metadata"]}
+                       for c in checkpointer.candidates() if c["generation"] == generation),
+                      None)
+        if header is None:
+            raise CheckpointError("no checkpoint of generation %d in the region" % generation)
+    meta = (header or {}).get("metadata", {})
+    if meta.get("consistency") in ("torn-risk", "signal"):
+        journal("checkpoint-torn-risk", "restoring a save taken at %s" % meta["consistency"],
+                "step %s" % meta.get("step"))
+    if header is not None and header is newest and checkpointer.hbm_ready():
         try:  # the predecessor on this GPU is alive and exported its tensors: copy from HBM
             res = checkpointer.restore_hbm()
             journal("checkpoint-restored", "HBM hand-off", *_describe(res),
@@ -413,7 +598,7 @@ def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None) -> Op
             journal("checkpoint-hbm-failed", str(error))
     if header is not None:
         try:
-            res = checkpointer.restore()
+            res = checkpointer.restore(generation=generation)
             journal("checkpoint-restored", "host region", *_describe(res))
             notify_restored()
             return header.get("metadata", {})

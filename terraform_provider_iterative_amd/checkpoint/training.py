@@ -12,6 +12,7 @@ had to re-read its own files after a spot respawn (README.md:93-101).
 """
 from __future__ import annotations
 
+import json
 from typing import Any, Dict, Optional, Tuple
 
 from . import preemption
@@ -74,8 +75,17 @@ def _decode_into(t, blob: Dict[str, Any]) -> None:
         t.copy_(src.to(t.device))
 
 
+TORN = ("torn-risk", "signal")  # saves not taken at a step boundary
+
+
 class TrainingState:
-    """Checkpointer over a model + optimizer (see module docstring)."""
+    """Checkpointer over a model + optimizer (see module docstring).
+
+    The training loop reports each finished step with :meth:`step` (after ``opt.step()`` and
+    whatever else makes up the step): that is where a preemption is saved -- on every rank at
+    the same boundary -- and where periodic checkpoints are taken.  Every save records the step
+    number in its metadata (``"step"``), so :meth:`resume_consistent` compares real steps.
+    """
 
     def __init__(self, model, optimizer=None, extra: Optional[Dict[str, Any]] = None,
                  path: Optional[str] = None, device=None, **checkpointer_kwargs):
@@ -84,18 +94,36 @@ class TrainingState:
             raise ValueError("nothing to checkpoint on the model's device")
         self.checkpointer = Checkpointer(tensors, path=path, **checkpointer_kwargs)
         self.path = path
+        self.step_value: Optional[int] = None  # last step reported (or restored)
 
     def host_metadata(self) -> Dict[str, Any]:
         return {"host_tensors": {k: _encode(t) for k, t in self.host.items()}}
 
+    def _metadata(self, metadata: Optional[Dict] = None) -> Dict[str, Any]:
+        meta: Dict[str, Any] = {}
+        if self.step_value is not None:
+            meta["step"] = self.step_value
+        meta.update(metadata or {})
+        if isinstance(meta.get("step"), int):
+            self.step_value = meta["step"]
+        meta.update(self.host_metadata())
+        return meta
+
+    def step(self, step: int, metadata: Optional[Dict] = None, force: bool = False) -> bool:
+        """The loop finished step ``step``: save a pending preemption here (does not return
+        then), or take a periodic checkpoint when one is due (:func:`.preemption.step`).
+        Returns True when a periodic checkpoint was taken."""
+        self.step_value = int(step)
+        return preemption.step(self.step_value, metadata, force)
+
     def save(self, metadata: Optional[Dict] = None):
-        return self.checkpointer.save({**(metadata or {}), **self.host_metadata()})
+        return self.checkpointer.save(self._metadata(metadata))
 
     def save_async(self, metadata: Optional[Dict] = None):
         """Periodic checkpoint that stalls the training stream only for the HBM snapshot;
         host-side tensors are captured now, with the snapshot (see
         :meth:`Checkpointer.save_async`)."""
-        return self.checkpointer.save_async({**(metadata or {}), **self.host_metadata()})
+        return self.checkpointer.save_async(self._metadata(metadata))
 
     def restore_host(self, metadata: Dict) -> None:
         blobs = metadata.get("host_tensors", {})
@@ -111,26 +139,26 @@ class TrainingState:
         meta = preemption.resume(self.checkpointer, persist_path)
         if meta is not None:
             self.restore_host(meta)
+            if isinstance(meta.get("step"), int):
+                self.step_value = meta["step"]
         return meta
 
-    def resume_consistent(self, persist_path: Optional[str] = None, group=None,
-                          key: str = "step") -> Optional[Dict]:
-        """:meth:`resume` for data/tensor-parallel ranks: all ranks resume from checkpoints of
-        the same ``metadata[key]`` or none does.  A rank whose save did not complete (killed
-        during the spill) would otherwise restart from an older step than its peers; here the
-        group agrees first (``all_gather_object``) and falls back to a fresh start together.
-        Call on every rank of ``group`` (default: the world) after ``init_process_group``.
-        """
-        import torch.distributed as dist
-
-        meta = None
+    def _candidates(self, persist_path: Optional[str], key: str,
+                    allow_torn: bool) -> Dict[Any, Tuple[str, Optional[int]]]:
+        """``{step: (source, generation)}`` of this rank's restorable copies: the region's
+        (a streamed save in flight, both slots) and the persisted file; newest copy per step."""
+        out: Dict[Any, Tuple[str, Optional[int]]] = {}
         try:
-            header = self.checkpointer.latest()  # complete, or streaming in (preemption)
-            if header is not None:
-                meta = header.get("metadata", {})
+            cands = self.checkpointer.candidates()
         except Exception:  # unreadable region
-            meta = None
-        if meta is None and persist_path:
+            cands = []
+        for cand in cands:  # newest first
+            meta = cand["metadata"]
+            value = meta.get(key)
+            if value is None or (meta.get("consistency") in TORN and not allow_torn):
+                continue
+            out.setdefault(value, ("region", cand["generation"]))
+        if persist_path:
             import os
 
             from .checkpointer import describe_checkpoint
@@ -138,19 +166,60 @@ class TrainingState:
             if os.path.exists(persist_path):
                 try:
                     info = describe_checkpoint(persist_path, entries=False)
-                    meta = info.get("metadata", {}) if info.get("complete") else None
                 except Exception:
-                    meta = None
-        mine = None if meta is None else meta.get(key, True)
-        seen = [None] * dist.get_world_size(group)
-        dist.all_gather_object(seen, mine, group=group)
-        if any(v is None for v in seen) or len(set(map(repr, seen))) != 1:
-            return None  # disagreement: everybody starts fresh
-        # The headers agree, but a rank's data may still fail verification; then its tensors
-        # hold a partial unpack, so every rank aborts together rather than diverging.
+                    info = {}
+                meta = info.get("metadata", {}) if info.get("complete") else {}
+                value = meta.get(key)
+                if value is not None and (meta.get("consistency") not in TORN or allow_torn):
+                    out.setdefault(value, ("persist", None))
+        return out
+
+    def resume_consistent(self, persist_path: Optional[str] = None, group=None,
+                          key: str = "step", allow_torn: bool = False) -> Optional[Dict]:
+        """:meth:`resume` for data/tensor-parallel ranks: every rank resumes from a checkpoint
+        of the same ``metadata[key]`` (the step), or none does.
+
+        Each rank lists the steps it can restore -- a streamed save in flight, both slots of a
+        ``slots=2`` region, the persisted file -- and the group (``all_gather_object``) picks
+        the newest step that every rank holds.  So a rank whose last save did not complete
+        (killed during the spill) makes the gang fall back to the previous common step instead
+        of diverging.  Saves not taken at a step boundary (``consistency`` ``torn-risk`` /
+        ``signal``: see :mod:`.preemption`) are refused unless ``allow_torn``; so are saves
+        without ``metadata[key]``.  Returns None (fresh start everywhere) when no step is
+        common.  Call on every rank of ``group`` (default: the world) after
+        ``init_process_group``.
+        """
+        import torch.distributed as dist
+
+        mine = self._candidates(persist_path, key, allow_torn)
+        seen: list = [None] * dist.get_world_size(group)
+        dist.all_gather_object(seen, sorted(mine, key=repr), group=group)
+        common = set(seen[0] or [])
+        for other in seen[1:]:
+            common &= set(other or [])
+        if not common:
+            if any(seen):
+                preemption.journal("checkpoint-disagreement", "no step common to every rank",
+                                   "steps per rank %s" % json.dumps(seen)[:400])
+            return None  # everybody starts fresh
+        chosen = max(common)
+        source, generation = mine[chosen]
+        # Every rank restores that step; a rank's data may still fail verification.  Then its
+        # tensors hold a partial unpack, so every rank aborts together rather than diverging.
         error: Optional[BaseException] = None
+        restored = None
         try:
-            restored = self.resume(persist_path)
+            if source == "region":
+                restored = preemption.resume(self.checkpointer, None, generation)
+            else:
+                res = self.checkpointer.load(persist_path)
+                preemption.journal("checkpoint-restored", persist_path,
+                                   "%.1f GB/s" % res.gbps)
+                restored = self.checkpointer.header().get("metadata", {})
+            if restored is not None:
+                self.restore_host(restored)
+                self.step_value = restored.get(key) if isinstance(restored.get(key), int) \
+                    else self.step_value
         except Exception as exc:  # CheckpointError, I/O errors
             error, restored = exc, None
         ok = [None] * dist.get_world_size(group)
@@ -160,13 +229,14 @@ class TrainingState:
 
             bad = [r for r, v in enumerate(ok) if not v]
             raise CheckpointError("ranks %s could not restore step %r: %s" % (
-                bad, mine, error or "restored on another rank only")) from error
+                bad, chosen, error or "restored on another rank only")) from error
         return restored
 
     def install(self, persist_path: Optional[str] = None) -> None:
-        """Checkpoint on SIGTERM (then exit 143 so the supervisor respawns the rank)."""
+        """Checkpoint on SIGTERM (at the next :meth:`step`; then exit 143 so the supervisor
+        respawns the rank)."""
         preemption.register(self.checkpointer, persist_path)
-        preemption.on_preempt(self.host_metadata)
+        preemption.on_preempt(lambda: self._metadata(None))
         preemption.install()
 
     def close(self) -> None:

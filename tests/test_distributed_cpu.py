@@ -162,11 +162,12 @@ def test_resume_consistent_aborts_every_rank_when_one_restore_fails(tmp_path):
         assert results[rank].startswith("aborted") and "[1]" in results[rank], results[rank]
 
 
-def _tick_worker(rank, world, port, root, results):
-    """Periodic checkpoints in a 2-rank job: rank 1's clock is not due at the first check,
-    so neither rank checkpoints; at the next check both do, at the same step."""
+def _tick_worker(rank, world, port, root, results, agreement):
+    """Periodic checkpoints in a coupled job (an all-reduce per step, like DDP): rank 0's
+    clock proposes, every rank checkpoints at the same steps; rank 1 runs slower per step."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TPI_SYNC_INTERVAL="0.2",
-                      TPI_EVENTS_FILE=os.path.join(root, "events.jsonl"), RANK=str(rank))
+                      TPI_EVENTS_FILE=os.path.join(root, "events.jsonl"), RANK=str(rank),
+                      TPI_AGREEMENT=agreement)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import time
@@ -174,29 +175,37 @@ def _tick_worker(rank, world, port, root, results):
         from terraform_provider_iterative_amd.checkpoint import Checkpointer, preemption
 
         state = {"w": torch.zeros(2048)}
-        ck = Checkpointer(state, path=os.path.join(root, "rank%d" % rank), tile_bytes=4096)
+        ck = Checkpointer(state, path=os.path.join(root, "rank%d" % rank), tile_bytes=4096,
+                          slots=2)
         preemption.register(ck)
-        decisions = [preemption.tick()]  # arms the timer on every rank
-        time.sleep(0.25 if rank == 0 else 0.0)
-        state["w"].fill_(1)
-        decisions.append(preemption.tick({"step": 1}))  # rank 1 not due yet -> nobody
-        time.sleep(0.25)
-        state["w"].fill_(2)
-        decisions.append(preemption.tick({"step": 2}))  # both due
+        saved_at = []
+        for i in range(1, 25):
+            grad = torch.ones(4)
+            dist.all_reduce(grad)
+            state["w"].fill_(i)
+            time.sleep(0.02 if rank == 0 else 0.035)
+            if preemption.step(i):
+                saved_at.append(i)
         ck.wait_pending()
-        results[rank] = (decisions, ck.header()["metadata"].get("step"))
+        results[rank] = (saved_at, ck.header()["metadata"].get("step"),
+                         preemption._agreement.kind)
         ck.close()
     finally:
         dist.destroy_process_group()
 
 
-def test_periodic_tick_is_collective(tmp_path):
+@pytest.mark.parametrize("agreement", ["auto", "collective"])
+def test_periodic_tick_is_collective(tmp_path, agreement):
     manager = mp.Manager()
     results = manager.dict()
-    mp.spawn(_tick_worker, args=(2, _free_port(), str(tmp_path), results), nprocs=2)
+    mp.spawn(_tick_worker, args=(2, _free_port(), str(tmp_path), results, agreement),
+             nprocs=2)
+    saved0, last0, kind = results[0]
+    assert kind == ("shm" if agreement == "auto" else "collective")
+    assert len(saved0) >= 2, saved0
     for rank in range(2):
-        decisions, step = results[rank]
-        assert decisions == [False, False, True], (rank, decisions)
-        assert step == 2
+        saved, last, _ = results[rank]
+        assert saved == saved0, (rank, saved, saved0)
+        assert last == saved0[-1]
     lines = (tmp_path / "events.jsonl").read_text().splitlines()
-    assert sum('"checkpoint-synced"' in l for l in lines) == 2
+    assert sum('"checkpoint-synced"' in l for l in lines) == 2 * len(saved0)

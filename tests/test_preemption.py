@@ -92,6 +92,12 @@ def test_preempt_checkpoint_respawn_resume(cloud, how):
         # restores behind it
         assert "checkpoint-streaming" in codes and "checkpoint-released" not in codes
         assert codes.index("rank-released") < codes.index("respawn")
+        # the supervisor's SIGUSR2 ("successor restored") ends the predecessor's linger; it
+        # must not kill it: the spill finishes (checkpoint-saved) and the exit is 143
+        exits = [e for e in task.events() if e.code == "rank-released-exit"]
+        assert exits and exits[0].description[-1] == "code 143", exits[0].description
+        assert "predecessor-exit" in codes
+        assert codes.index("checkpoint-saved") < codes.index("rank-released-exit")
     # phase journal: start -> first output -> preempt -> saved / respawn -> restored
     for phase in ("rank-start", "rank-first-output", "preempt-signal", "checkpoint-saved",
                   "checkpoint-restored"):
@@ -260,6 +266,9 @@ def fresh_preemption(monkeypatch):
     monkeypatch.setattr(preemption, "_callbacks", [])
     monkeypatch.setattr(preemption, "_tick_pending", {})
     monkeypatch.setattr(preemption, "_tick_last", None)
+    monkeypatch.setattr(preemption, "_agreement", None)
+    monkeypatch.setattr(preemption, "_boundary_seen", False)
+    monkeypatch.setattr(preemption, "_last_step", None)
     return preemption
 
 

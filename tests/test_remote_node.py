@@ -191,3 +191,12 @@ def test_remote_cloud_config_retargeted_to_a_remote_node(tmp_path, remote, monke
     assert _wait(task)["succeeded"] == 1 and "hi" in "".join(task.logs())
     assert (remote / "local" / ident.long()).is_dir()
     task.delete()
+
+
+@pytest.mark.parametrize("region", ["host=-oProxyCommand=touch_x", "host=user@-p",
+                                    "host=n1,port=22;rm"])
+def test_remote_host_cannot_inject_ssh_options(region):
+    from terraform_provider_iterative_amd.backends.ssh import Transport
+
+    with pytest.raises(ValueError):
+        Transport(Cloud(provider="local", region=region))
