@@ -6,8 +6,10 @@ resource walk (4 creates in flight at once).
 Reports, as one JSON line:
 
 * ``create_s`` / ``first_log_s`` per task (from the moment all creates were issued);
-* that the four GPU sets are disjoint and cover the node, and that a fifth task is refused
-  with a placement error (and how fast);
+* that the four GPU sets -- and the four tasks' reserved core sets -- are disjoint and cover
+  the node, and that a fifth task is queued (``create`` returns, ``leo read`` says queued, like
+  a scaling group without capacity) and starts as soon as GPUs are released
+  (``queued_start_s``: last group exit -> the fifth task's first log);
 * ``all_succeeded_s``: wall time until every supervisor exited with ``succeeded``;
 * ``reuse_s``: time from the last supervisor exit until an 8-GPU task is placed on the
   released GPUs without any ``delete`` in between (lease auto-cleanup);
@@ -56,28 +58,33 @@ def run(tasks: int = 4, gpus_per_task: int = 2, sleep: float = 1.0,
 
     need = tasks * gpus_per_task
     physical = len(discover())
-    saved = os.environ.get("TPI_MI355X_GPUS")
+    keys = ("TPI_MI355X_GPUS", "TPI_NODE_CPUS", "TPI_NODE_MEMORY_MB")
+    saved = {k: os.environ.get(k) for k in keys}
     if torch_job and physical < need:
         raise SystemExit("--torch needs %d GPUs, found %d" % (need, physical))
+    logical = physical < need or saved["TPI_MI355X_GPUS"] is not None
     if physical < need:
         os.environ["TPI_MI355X_GPUS"] = ",".join(str(i) for i in range(need))
+    if logical:  # logical slots stand for an 8-GPU node: its cores and DRAM too
+        os.environ.setdefault("TPI_NODE_CPUS", "0-%d" % (16 * need - 1))
+        os.environ.setdefault("TPI_NODE_MEMORY_MB", str(256000 * need))
     try:
-        return _run(tasks, gpus_per_task, sleep, need, physical, torch_job)
+        return _run(tasks, gpus_per_task, sleep, need, physical, torch_job, logical)
     finally:  # repeats must see the node again, not this run's logical slots
-        if saved is None:
-            os.environ.pop("TPI_MI355X_GPUS", None)
-        else:
-            os.environ["TPI_MI355X_GPUS"] = saved
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
 def _run(tasks: int, gpus_per_task: int, sleep: float, need: int, physical: int,
-         torch_job: bool) -> dict:
+         torch_job: bool, logical: bool) -> dict:
     from terraform_provider_iterative_amd import backends
     from terraform_provider_iterative_amd.models.cloud import (Cloud, Credentials,
                                                                NodeCredentials)
     from terraform_provider_iterative_amd.models.values import (Environment, Size, Task,
                                                                 Variables)
-    from terraform_provider_iterative_amd.parallel.placement import PlacementError
     from terraform_provider_iterative_amd.utils.identifier import new_deterministic_identifier
 
     state = tempfile.mkdtemp(prefix="tpi-concurrent-")
@@ -105,17 +112,24 @@ def _run(tasks: int, gpus_per_task: int, sleep: float, need: int, physical: int,
     sets = [sorted(t.gpus()) for t in group]
     disjoint = len(set().union(*map(set, sets))) == need and all(len(s) == gpus_per_task
                                                                  for s in sets)
+    cpu_sets = [sorted(c for cs in (t._definition().get("allocation") or {}).get("rank_cpus")
+                       or [] for c in cs) for t in group]
+    cpus_disjoint = sum(map(len, cpu_sets)) == len(set().union(*map(set, cpu_sets))) > 0
     extra = make("conc-extra-%d" % os.getpid(), 1, SCRIPT % 0)
     t1 = time.perf_counter()
-    try:
-        extra.create()
-        refused, refuse_s = False, None
-    except PlacementError:
-        refused, refuse_s = True, time.perf_counter() - t1
-    extra.delete()
+    extra.create()
+    queue_s = time.perf_counter() - t1
+    queued = (extra.status() == {"running": 0, "succeeded": 0, "failed": 0}
+              and not extra.gpus() and extra.supervisor_running())
     statuses = [t.wait(60.0) for t in group]
     t_done = time.perf_counter()
     all_ok = all(s.get("succeeded") == 1 for s in statuses)
+    try:
+        queued_start_s = _first_log(extra, t_done, 30.0)
+    except TimeoutError:
+        queued_start_s = None
+    extra_ok = extra.wait(30.0).get("succeeded") == 1
+    extra.delete()
     again = make("conc-after-%d" % os.getpid(), need, SCRIPT % 0)
     again.create()
     reuse_s = time.perf_counter() - t_done
@@ -130,12 +144,14 @@ def _run(tasks: int, gpus_per_task: int, sleep: float, need: int, physical: int,
     return {
         "config": "%d concurrent %d-GPU iterative_task resources on one node (placement + "
                   "auto-cleanup)" % (tasks, gpus_per_task),
-        "gpus": {"physical": physical, "slots": need,
-                 "logical_slots": physical < need},
+        "gpus": {"physical": physical, "slots": need, "logical_slots": logical},
         "create_s": [round(created[i], 4) for i in range(tasks)],
         "first_log_s": [round(x, 4) for x in first],
         "gpu_sets": sets, "disjoint": disjoint,
-        "fifth_refused": refused, "refuse_s": None if refuse_s is None else round(refuse_s, 4),
+        "cpu_sets": [_span(c) for c in cpu_sets], "cpus_disjoint": cpus_disjoint,
+        "fifth_queued": queued, "queue_create_s": round(queue_s, 4),
+        "queued_start_s": None if queued_start_s is None else round(queued_start_s, 4),
+        "fifth_succeeded": extra_ok,
         "all_succeeded": all_ok, "all_succeeded_s": round(t_done - t0, 3),
         "task_sleep_s": sleep,
         "reuse_s": round(reuse_s, 4), "reused_all_gpus": reused,
@@ -143,6 +159,10 @@ def _run(tasks: int, gpus_per_task: int, sleep: float, need: int, physical: int,
         "torch_job": torch_job,
         "torch_devices": devices,
     }
+
+
+def _span(cpus) -> str:
+    return "%d-%d" % (cpus[0], cpus[-1]) if cpus else "-"
 
 
 def _devices(logs) -> int:
@@ -168,7 +188,8 @@ def main() -> int:
     out["repeats"] = len(runs)
     out["median_first_log_s"] = sorted(max(r["first_log_s"]) for r in runs)[len(runs) // 2]
     out["median_reuse_s"] = sorted(r["reuse_s"] for r in runs)[len(runs) // 2]
-    out["ok"] = all(r["disjoint"] and r["fifth_refused"] and r["all_succeeded"]
+    out["ok"] = all(r["disjoint"] and r["cpus_disjoint"] and r["fifth_queued"]
+                    and r["fifth_succeeded"] and r["all_succeeded"]
                     and r["reused_all_gpus"] and (not r["torch_job"] or
                                                   r["torch_devices"] == [args.gpus_per_task]
                                                   * args.tasks) for r in runs)

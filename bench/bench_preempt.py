@@ -50,6 +50,7 @@ t_active = time.time()
 resuming = os.path.exists(spill)
 if resuming and %(prefetch)r:
     prefetch(spill)  # map + pin the spill while the model state is being allocated
+t_prefetch = time.time()
 tensors = synthetic_checkpoint(nbytes, 8192, dev, fill=not resuming)
 torch.cuda.synchronize()
 t_alloc = time.time()
@@ -70,9 +71,10 @@ if resuming:
     t1 = time.time()
     ok = meta is not None and meta.get("digests") == digests()
     print("restored %%d bytes in %%.3f s, verified %%s, warm standby %%s, activation -> restored "
-          "%%.3f s (HBM state %%.3f, host region map+register %%.3f after it); process start -> "
-          "import done %%.3f s; Checkpointer %%s" %% (ck.plan.total, t1 - t0, ok, activated,
-                                  t1 - t_active, t_alloc - t_active, t_map - t_alloc,
+          "%%.3f s (prefetch %%.3f, HBM state %%.3f, host region map+register %%.3f after it); "
+          "process start -> import done %%.3f s; Checkpointer %%s" %% (
+              ck.plan.total, t1 - t0, ok, activated, t1 - t_active, t_prefetch - t_active,
+              t_alloc - t_prefetch, t_map - t_alloc,
                                   t_import - t_start, ck.init_times),
           flush=True)
     ck.close()
@@ -85,9 +87,10 @@ preemption.install()
 print("ready %%d bytes in HBM" %% ck.plan.total, flush=True)
 step = 0
 while True:  # a "training loop" whose steps leave the state consistent at every boundary
-    time.sleep(0.002)
+    time.sleep(%(step_s)r)
     step += 1
-    preemption.step(step)  # a SIGTERM is saved here, at most one step after it arrived
+    if %(boundary)r:
+        preemption.step(step)  # a SIGTERM is saved here, at most one step after it arrived
 '''
 
 
@@ -110,6 +113,10 @@ def main():
     p.add_argument("--early-prefetch", action="store_true",
                    help="successor maps + pins the spill before importing torch (measured "
                         "slower on MI355X: the pinning stalls the import)")
+    p.add_argument("--step-seconds", type=float, default=0.002,
+                   help="duration of the rank's (idle) training step")
+    p.add_argument("--signal-mode", action="store_true",
+                   help="the rank never calls preemption.step(): save in the signal handler")
     args = p.parse_args()
     if args.hot:
         args.standby = True
@@ -127,7 +134,8 @@ def main():
                   credentials=Credentials(node=NodeCredentials(state_root=state)))
     script = RANK % {"python": sys.executable, "root": ROOT, "spill": spill, "gb": args.gb,
                      "codec": args.codec, "prefetch": not args.no_prefetch,
-                     "early": args.early_prefetch, "standby": args.standby}
+                     "early": args.early_prefetch, "standby": args.standby,
+                     "step_s": args.step_seconds, "boundary": not args.signal_mode}
     # the ranks' runtime knobs travel as task variables (the rank environment is the task's)
     rank_env = {"TPI_TASK": "true", "TPI_STREAM_HANDOFF": "0" if args.no_stream else "1"}
     for knob in ("TPI_D2H_ENGINE", "TPI_STREAM_TIMEOUT", "TPI_LINGER_SECONDS",
@@ -142,7 +150,9 @@ def main():
                         "DRAM->restore (1 x MI355X, iterative_task)" % args.gb,
               "codec": args.codec, "spill": spill, "prefetch": not args.no_prefetch,
               "early_prefetch": args.early_prefetch, "standby": args.standby,
-              "hot_standby": args.hot, "stream_handoff": not args.no_stream}
+              "hot_standby": args.hot, "stream_handoff": not args.no_stream,
+              "save_at": "signal" if args.signal_mode else "step boundary",
+              "step_seconds": args.step_seconds}
     os.environ["TPI_WARM_STANDBY"] = "hot" if args.hot else ("1" if args.standby else "0")
     try:
         task.create()

@@ -50,6 +50,8 @@
 #include <sys/signalfd.h>
 #include <sys/socket.h>
 #include <sys/un.h>
+#include <dirent.h>
+#include <ftw.h>
 #include <sys/stat.h>
 #include <sys/time.h>
 #include <sys/types.h>
@@ -152,7 +154,7 @@ const char* signame(int sig) {
   }
 }
 
-enum class TermReason { NONE, STOP, PREEMPT, TIMEOUT, FAILFAST };
+enum class TermReason { NONE, STOP, PREEMPT, TIMEOUT, FAILFAST, REQUEUE, OOM, DISK };
 
 // --daemon: the launching parent blocks on this pipe until the ranks are spawned and the
 // first state.json is on disk, so "create returned" implies "supervisor visible".
@@ -212,6 +214,14 @@ struct Spec {
   std::vector<std::string> stager_argv;
   std::string stager_manifest, stager_log, stager_gpus;
   double stager_timeout = 600;
+  // machine-type limits (resource_job.go:112-118 turns cpu/memory/disk into pod limits):
+  // host memory per rank (its process group; 0 = none) and the task's workdir size
+  uint64_t rank_memory_kb = 0;
+  uint64_t disk_limit_bytes = 0;
+  double memory_interval = 1.0, disk_interval = 10.0;
+  // spot reclaim: after `requeue` the task goes back to the node queue through this command
+  std::vector<std::string> requeue_argv;
+  int restart_base = 0;  // restarts of earlier supervisors of this task (requeued incarnations)
 };
 
 Spec load_spec(const std::string& path) {
@@ -257,6 +267,13 @@ Spec load_spec(const std::string& path) {
   s.stager_log = st["log"].str(s.task_dir + "/supervisor/stager.log");
   s.stager_gpus = st["gpus"].str();
   s.stager_timeout = st["timeout"].num(600);
+  const Value& lim = v["limits"];
+  s.rank_memory_kb = (uint64_t)lim["rank_memory_mb"].num(0) * 1024;
+  s.disk_limit_bytes = (uint64_t)(lim["disk_gb"].num(0) * 1e9);
+  s.memory_interval = lim["memory_interval"].num(1.0);
+  s.disk_interval = lim["disk_interval"].num(10.0);
+  for (auto& a : v["requeue_argv"].a) s.requeue_argv.push_back(a.str());
+  s.restart_base = (int)v["restart_base"].num(0);
   if (s.workdir.empty() || s.script.empty()) throw std::runtime_error("spec needs workdir+script");
   return s;
 }
@@ -271,7 +288,9 @@ class Supervisor {
     for (int i = 0; i < s_.parallelism; ++i) {
       ranks_[i].index = i;
       ranks_[i].gpus = s_.rank_gpus[i];
+      ranks_[i].restarts = s_.restart_base;
     }
+    total_restarts_ = s_.restart_base;
   }
 
   int run() {
@@ -312,6 +331,7 @@ class Supervisor {
       check_deadline(t);
       check_grace(t);
       check_respawn(t);
+      check_limits(t);
       if (all_finished()) break;
       double timeout = 2.0;
       if (s_.deadline > 0 && !timed_out_) timeout = std::min(timeout, s_.deadline - t);
@@ -320,6 +340,8 @@ class Supervisor {
           if (r.pid > 0 && r.term_at > 0 && !r.killed)
             timeout = std::min(timeout, r.term_at + s_.grace - t);
       if (respawn_at_ > 0) timeout = std::min(timeout, respawn_at_ - t);
+      if (s_.rank_memory_kb) timeout = std::min(timeout, next_memory_check_ - t);
+      if (s_.disk_limit_bytes) timeout = std::min(timeout, next_disk_check_ - t);
       timeout = std::max(timeout, 0.0);
       std::vector<struct pollfd> pfds;
       pfds.push_back({sfd_, POLLIN, 0});
@@ -371,6 +393,104 @@ class Supervisor {
   int total_restarts_ = 0;
   pid_t stager_pid_ = -1;
   bool staged_ = false;
+  bool requeue_ = false;  // reclaimed (spot): ranks go down, the task goes back to the queue
+  double next_memory_check_ = 0, next_disk_check_ = 0;
+
+  // ---- machine-type limits -------------------------------------------------------------------
+  // Host memory of a process group: proportional set size (shared pages split between their
+  // users, so a spill region mapped by two processes is not counted twice), VmRSS fallback.
+  static uint64_t group_memory_kb(pid_t pgid) {
+    uint64_t total = 0;
+    DIR* d = opendir("/proc");
+    if (!d) return 0;
+    while (struct dirent* e = readdir(d)) {
+      char* end = nullptr;
+      long pid = strtol(e->d_name, &end, 10);
+      if (!end || *end || pid <= 0) continue;
+      std::string stat;
+      try {
+        stat = read_file("/proc/" + std::to_string(pid) + "/stat");
+      } catch (...) {
+        continue;
+      }
+      size_t rp = stat.rfind(')');
+      if (rp == std::string::npos) continue;
+      std::istringstream fields(stat.substr(rp + 2));
+      std::string state;
+      long ppid = 0, pgrp = 0;
+      fields >> state >> ppid >> pgrp;
+      if (pgrp != (long)pgid) continue;
+      uint64_t kb = 0;
+      for (const char* file : {"/smaps_rollup", "/status"}) {
+        std::ifstream in("/proc/" + std::to_string(pid) + file);
+        std::string key;
+        uint64_t value;
+        const std::string want = file[1] == 's' && file[2] == 'm' ? "Pss:" : "VmRSS:";
+        while (in >> key) {
+          if (key == want && in >> value) {
+            kb = value;
+            break;
+          }
+          in.ignore(1 << 20, '\n');
+        }
+        if (kb) break;
+      }
+      total += kb;
+    }
+    closedir(d);
+    return total;
+  }
+
+  static thread_local uint64_t du_total_;
+  static int du_visit(const char*, const struct stat* st, int type, struct FTW*) {
+    if (type == FTW_F) du_total_ += (uint64_t)st->st_blocks * 512;
+    return 0;
+  }
+  uint64_t workdir_bytes() {
+    du_total_ = 0;
+    nftw(s_.workdir.c_str(), du_visit, 32, FTW_PHYS | FTW_MOUNT);
+    return du_total_;
+  }
+
+  void check_limits(double t) {
+    if (s_.rank_memory_kb && t >= next_memory_check_) {
+      next_memory_check_ = t + s_.memory_interval;
+      for (auto& r : ranks_) {
+        if (r.state != Rank::RUNNING || r.pid <= 0 || r.killed) continue;
+        const uint64_t kb = group_memory_kb(r.pid);
+        if (kb <= s_.rank_memory_kb) continue;
+        // like a container OOM kill: no grace, the rank fails (no respawn)
+        r.reason = TermReason::OOM;
+        if (r.term_at == 0) r.term_at = t;
+        kill(-r.pid, SIGKILL);
+        kill(r.pid, SIGKILL);
+        r.killed = true;
+        event("rank-oom-killed", {"rank " + std::to_string(r.index),
+                                  "memory " + std::to_string(kb / 1024) + " MB",
+                                  "limit " + std::to_string(s_.rank_memory_kb / 1024) + " MB"});
+      }
+    }
+    if (s_.disk_limit_bytes && t >= next_disk_check_ && !stop_) {
+      next_disk_check_ = t + s_.disk_interval;
+      const uint64_t used = workdir_bytes();
+      if (used > s_.disk_limit_bytes) {
+        // ephemeral-storage eviction: every rank is terminated and fails
+        event("disk-limit", {"workdir " + std::to_string(used / 1000000) + " MB",
+                             "limit " + std::to_string(s_.disk_limit_bytes / 1000000) + " MB"});
+        for (int i = 0; i < s_.parallelism; ++i) discard_standby(i, "disk limit");
+        for (auto& r : ranks_)
+          if (r.state == Rank::RUNNING) terminate(r, TermReason::DISK);
+        respawn_at_ = 0;
+        for (auto& r : ranks_)
+          if (r.state == Rank::PREEMPTED || r.state == Rank::PENDING) {
+            write_status(r, "disk-limit", "", "killed");
+            r.state = Rank::DONE;
+          }
+        disk_exceeded_ = true;
+      }
+    }
+  }
+  bool disk_exceeded_ = false;
 
   // ---- workdir stager ----------------------------------------------------------------------
   void stage() {
@@ -875,6 +995,10 @@ class Supervisor {
       }
       break;
     }
+    if (got && r.pid > 0 && r.reason == TermReason::REQUEUE) {
+      kill(r.pid, SIGUSR2);  // nobody restores from this GPU: end its linger now
+      return false;
+    }
     if (!got || r.pid <= 0 || r.state != Rank::RUNNING || stop_ || timed_out_) return false;
     if (!(r.reason == TermReason::PREEMPT ||
           (r.reason == TermReason::NONE && s_.respawn_on_sigterm)))
@@ -932,7 +1056,9 @@ class Supervisor {
 
   void terminate(Rank& r, TermReason why) {
     if (r.pid <= 0 || r.state != Rank::RUNNING) return;
-    if (r.reason == TermReason::NONE || why == TermReason::STOP) r.reason = why;
+    if (r.reason == TermReason::NONE || why == TermReason::STOP || why == TermReason::DISK ||
+        (why == TermReason::REQUEUE && r.reason == TermReason::PREEMPT))
+      r.reason = why;
     if (r.term_at == 0) {
       r.term_at = now();
       kill(-r.pid, SIGTERM);
@@ -968,7 +1094,9 @@ class Supervisor {
   }
 
   void check_respawn(double t) {
-    if (respawn_at_ <= 0 || t < respawn_at_ || stop_ || timed_out_) return;
+    if (respawn_at_ <= 0 || t < respawn_at_ || stop_ || timed_out_ || requeue_ ||
+        disk_exceeded_)
+      return;
     if (s_.gang && running() > 0) return;  // wait for the whole gang to go down
     respawn_at_ = 0;
     if (s_.gang && s_.parallelism > 1) next_master_port();
@@ -1058,6 +1186,30 @@ class Supervisor {
     return true;
   }
 
+  // Spot reclaim (an on-demand task needs this task's GPUs): every rank is preempted --
+  // checkpointed as usual -- but not respawned here; once the gang is down the reservation is
+  // released and the task goes back to the node queue (requeue_argv), to resume wherever it
+  // is placed next (resource_auto_scaling_group.go:51-106: a reclaimed spot instance is
+  // replaced when capacity returns).
+  bool request_requeue(const std::string& source) {
+    if (stop_ || timed_out_ || s_.requeue_argv.empty()) return false;
+    if (requeue_) return true;
+    requeue_ = true;
+    respawn_at_ = 0;
+    event("requeue-requested", {source});
+    for (int i = 0; i < s_.parallelism; ++i) discard_standby(i, "requeue");
+    for (auto& r : ranks_) {
+      if (r.state == Rank::RUNNING) {
+        terminate(r, TermReason::REQUEUE);
+      } else if (r.state == Rank::PREEMPTED || r.state == Rank::PENDING) {
+        r.state = Rank::DONE;  // between preemption and respawn: resumes after the queue
+        r.reason = TermReason::REQUEUE;
+      }
+    }
+    dirty_ = true;
+    return true;
+  }
+
   // ---- control socket --------------------------------------------------------------------
   // sun_path holds 108 bytes and task directories can be longer, so bind/connect go through
   // /proc/self/fd/<dirfd>/<name> (the client in backends/node.py does the same).
@@ -1135,6 +1287,10 @@ class Supervisor {
       } else if (req == "stop") {
         request_stop("control socket");
         reply = "{\"ok\": true}\n";
+      } else if (req == "requeue" || req.compare(0, 8, "requeue ") == 0) {
+        const bool ok = request_requeue(req.size() > 8 ? req.substr(8) : "control socket");
+        reply = ok ? "{\"ok\": true}\n"
+                   : "{\"ok\": false, \"error\": \"task cannot be requeued\"}\n";
       } else {
         reply = "{\"ok\": false, \"error\": " + quote("unknown command: " + req) + "}\n";
       }
@@ -1211,6 +1367,22 @@ class Supervisor {
       event("rank-timeout", desc);
       return;
     }
+    if (r.reason == TermReason::OOM || r.reason == TermReason::DISK) {
+      const bool oom = r.reason == TermReason::OOM;
+      discard_standby(r.index, oom ? "memory limit" : "disk limit");
+      r.state = Rank::DONE;
+      write_status(r, oom ? "oom" : "disk-limit", code_s, status_s);
+      event(oom ? "rank-oom" : "rank-disk-limit", desc);
+      if (oom && s_.fail_fast)
+        for (auto& o : ranks_)
+          if (o.state == Rank::RUNNING) terminate(o, TermReason::FAILFAST);
+      return;
+    }
+    if (r.reason == TermReason::REQUEUE && !(WIFEXITED(st) && code == 0)) {
+      r.state = Rank::DONE;  // no status: the task is not over, it waits for capacity again
+      event("rank-requeued", desc);
+      return;
+    }
     bool preempted = r.reason == TermReason::PREEMPT ||
                      (s_.respawn_on_sigterm && r.reason == TermReason::NONE &&
                       ((signaled && sig == SIGTERM) || code == 143));
@@ -1271,12 +1443,56 @@ class Supervisor {
     stop_stager();
     for (auto& l : s_.leases) unlink(l.c_str());
     close_control();
-    event("supervisor-exit", {stop_ ? "stopped" : "all ranks finished"});
-    write_state("stopped");
+    bool requeued = false;
+    if (requeue_ && !stop_ && !timed_out_) {
+      bool pending = false;  // a rank that has not finished on its own
+      for (auto& r : ranks_)
+        if (r.reason == TermReason::REQUEUE && !(r.exit_signal == 0 && r.exit_code == 0))
+          pending = true;
+      if (pending) requeued = spawn_requeue();
+    }
+    event("supervisor-exit", {requeued ? "requeued" : stop_ ? "stopped" : "all ranks finished"});
+    if (!requeued) write_state("stopped");
     signal_ready();
     return 0;
   }
+
+  // Detached (own session) child that puts the task back into the node queue; it owns
+  // state.json from here on (phase "queued").
+  bool spawn_requeue() {
+    write_state("requeued");
+    pid_t pid = fork();
+    if (pid < 0) {
+      event("requeue-failed", {strerror(errno)});
+      return false;
+    }
+    if (pid == 0) {
+      setsid();
+      if (fork() != 0) _exit(0);  // the grandchild is reparented: no zombie, no pdeathsig
+      sigset_t none;
+      sigemptyset(&none);
+      sigprocmask(SIG_SETMASK, &none, nullptr);
+      for (int sig : {SIGCHLD, SIGTERM, SIGINT, SIGHUP, SIGUSR1, SIGUSR2, SIGPIPE})
+        signal(sig, SIG_DFL);
+      int devnull = open("/dev/null", O_RDWR);
+      if (devnull >= 0) {
+        dup2(devnull, 0);
+        dup2(devnull, 1);
+      }
+      std::vector<char*> argv;
+      for (auto& a : s_.requeue_argv) argv.push_back(const_cast<char*>(a.c_str()));
+      argv.push_back(nullptr);
+      execv(argv[0], argv.data());
+      _exit(127);
+    }
+    int st = 0;
+    waitpid(pid, &st, 0);
+    event("requeued", {"waiting for capacity"});
+    return true;
+  }
 };
+
+thread_local uint64_t Supervisor::du_total_ = 0;
 
 }  // namespace
 

@@ -21,6 +21,7 @@ import os
 import signal
 import socket
 import subprocess
+import sys
 import time
 from typing import Dict, List, Optional
 
@@ -29,7 +30,8 @@ from ..models.cloud import PROVIDER_LOCAL, PROVIDER_MI355X, Cloud, parse_region_
 from ..models.machine_types import MachineType, parse_node_machine
 from ..models.values import (STATUS_RUNNING, Event, NotFoundError, NotImplementedErr,
                              RemoteStorage, Task as TaskSpec, new_status)
-from ..parallel.placement import Placement, PlacementError, numa_cpus, pid_alive
+from ..parallel.placement import (Allocation, Placement, PlacementBusy, PlacementError,
+                                  Request, node_cpus, pid_alive)
 from ..storage import transfer as storage
 from ..utils.identifier import Identifier, parse_identifier
 from ..utils.steps import Step, StepTiming, run_steps
@@ -45,6 +47,41 @@ PASSTHROUGH_PREFIXES = ("LC_", "HSA_", "HIP_", "ROCR_", "ROCM_", "NCCL_", "RCCL_
                         "AMD_", "MIOPEN_", "TORCH_", "PYTORCH_")
 
 DEFAULT_MASTER_PORT_BASE = 29500
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+class Queued(Exception):
+    """Placement could not reserve the machine now: the task waits in the node queue."""
+
+
+def control_socket(sup_dir: str, command: str, timeout: float = 2.0) -> Optional[Dict]:
+    """One request on a supervisor's control socket (``<sup_dir>/control.sock``); the reply as
+    a dict, or None when no supervisor is listening.  The path is reached through
+    ``/proc/self/fd`` because AF_UNIX paths are limited to 108 bytes (the supervisor binds
+    the same way)."""
+    try:
+        dfd = os.open(sup_dir, os.O_RDONLY | os.O_DIRECTORY)
+    except OSError:
+        return None
+    try:
+        with socket.socket(socket.AF_UNIX, socket.SOCK_STREAM) as sock:
+            sock.settimeout(timeout)
+            sock.connect("/proc/self/fd/%d/control.sock" % dfd)
+            sock.sendall(command.encode() + b"\n")
+            chunks = []
+            while True:
+                data = sock.recv(65536)
+                if not data:
+                    break
+                chunks.append(data)
+    except OSError:
+        return None
+    finally:
+        os.close(dfd)
+    try:
+        return json.loads(b"".join(chunks).decode() or "null")
+    except ValueError:
+        return None
 
 
 def _now() -> float:
@@ -124,37 +161,34 @@ class NodeTask(Task):
 
     def control(self, command: str, timeout: float = 2.0) -> Optional[Dict]:
         """One request on the supervisor's control socket (``supervisor/control.sock``:
-        ``ping``, ``state``, ``preempt``, ``stop``); the reply as a dict, or None when no
-        supervisor is listening.  The path is reached through ``/proc/self/fd`` because
-        AF_UNIX paths are limited to 108 bytes (the supervisor binds the same way)."""
-        try:
-            dfd = os.open(self.sup_dir, os.O_RDONLY | os.O_DIRECTORY)
-        except OSError:
-            return None
-        try:
-            with socket.socket(socket.AF_UNIX, socket.SOCK_STREAM) as sock:
-                sock.settimeout(timeout)
-                sock.connect("/proc/self/fd/%d/control.sock" % dfd)
-                sock.sendall(command.encode() + b"\n")
-                chunks = []
-                while True:
-                    data = sock.recv(65536)
-                    if not data:
-                        break
-                    chunks.append(data)
-        except OSError:
-            return None
-        finally:
-            os.close(dfd)
-        try:
-            return json.loads(b"".join(chunks).decode() or "null")
-        except ValueError:
-            return None
+        ``ping``, ``state``, ``preempt``, ``preempt <rank>``, ``requeue``, ``stop``)."""
+        return control_socket(self.sup_dir, command, timeout)
 
     def supervisor_running(self) -> bool:
+        """A supervisor, or the queue waiter of a queued task, is alive (the task is not
+        over).  A supervisor that just handed its task back to the queue counts until the
+        waiter has taken over state.json."""
         state = self._state()
         pid = int(state.get("pid", 0) or 0)
+        if state.get("phase") == "requeued":
+            return _now() - float(state.get("heartbeat", 0) or 0) < 30.0
         return bool(pid) and state.get("phase") != "stopped" and pid_alive(pid)
+
+    @classmethod
+    def from_root(cls, root: str) -> "NodeTask":
+        """The task stored at ``<state_root>/<provider>/<id>`` (queue waiter, agents)."""
+        from ..models.cloud import Credentials, NodeCredentials
+        from ..models.values import Environment, Size
+
+        saved = _read_json(os.path.join(root, "task.json")) or {}
+        state_root = os.path.dirname(os.path.dirname(os.path.abspath(root)))
+        cloud = Cloud(provider=saved.get("provider", PROVIDER_LOCAL),
+                      region=saved.get("region", "") or "",
+                      credentials=Credentials(node=NodeCredentials(state_root=state_root)))
+        spec = TaskSpec(size=Size(machine=saved.get("machine") or "m"),
+                        parallelism=saved.get("parallelism", 1),
+                        environment=Environment(timeout=saved.get("timeout") or 0))
+        return cls(cloud, parse_identifier(saved.get("id") or os.path.basename(root)), spec)
 
     def _machine(self) -> MachineType:
         if self.machine is None:
@@ -206,35 +240,108 @@ class NodeTask(Task):
     def _create_storage(self) -> None:
         for d in (self.root, self.reports_dir, self.sup_dir):
             os.makedirs(d, exist_ok=True)
+        try:
+            os.remove(self._stop_marker())
+        except FileNotFoundError:
+            pass
         os.makedirs(self.data_dir, exist_ok=True)
         if self._saved is None:
             self._saved = self._definition()
             _write_json(self.task_file, self._saved)
             self._event("created", "task %s" % self.id)
 
+    def _knob(self, name: str, default: str) -> str:
+        """Runtime knob: the task's own environment block, else the provider's."""
+        value = (self._definition().get("environment") or {}).get(name)
+        return str(value) if value not in (None, "") else os.environ.get(name, default)
+
+    def resource_mode(self) -> str:
+        """``reserve``: the machine type's cores and memory are reserved on the node next to
+        the GPUs (disjoint core sets, memory admission; a task that does not fit is queued) --
+        the default for ``mi355x``.  ``limit``: they are only limits (affinity capped to
+        ``cpus`` cores, the memory limit enforced), like the k8s Job's limits without requests
+        (``resource_job.go:107-118``) -- the default for ``local``.  ``TPI_RESOURCE_MODE``."""
+        default = "reserve" if self.provider == PROVIDER_MI355X else "limit"
+        mode = self._knob("TPI_RESOURCE_MODE", default)
+        return mode if mode in ("reserve", "limit") else default
+
+    def spot(self) -> bool:
+        """``spot >= 0`` (``values.go:17-22``: 0 auto, > 0 max price): reclaimable."""
+        try:
+            return float(self._definition().get("spot", -1)) >= 0
+        except (TypeError, ValueError):
+            return False
+
+    def _request(self) -> Optional[Request]:
+        d = self._definition()
+        machine = self._machine()
+        gpus = machine.gpus if self.provider == PROVIDER_MI355X else 0
+        reserve = self.resource_mode() == "reserve"
+        if not gpus and not reserve:
+            return None
+        selectors = parse_region_selectors(self.cloud.region)
+        return Request(task=self.id, parallelism=d["parallelism"], gpus_per_rank=gpus,
+                       cpus_per_rank=machine.cpus if reserve else 0,
+                       memory_mb_per_rank=machine.memory_mb if reserve else 0,
+                       spot=self.spot(), task_dir=self.root,
+                       gpu_filter=_index_list(selectors["gpus"]) if "gpus" in selectors else None,
+                       numa=int(selectors["numa"]) if "numa" in selectors else None)
+
     def _place(self) -> None:
+        """Reserve the task's machine(s) on this node; raises :class:`Queued` when they are
+        busy (``TPI_PLACEMENT_QUEUE=0``: fail instead, the pre-queue behaviour)."""
         definition = self._definition()
-        gpus_per = self._machine().gpus
-        total = gpus_per * definition["parallelism"]
-        if self.provider != PROVIDER_MI355X or total == 0:
+        req = self._request()
+        if req is None:
             definition["gpus"] = []
-        else:
-            selectors = parse_region_selectors(self.cloud.region)
-            placement = self.placement
-            if "gpus" in selectors:  # explicit pinning, e.g. region = "gpus=2-3"
-                wanted = _index_list(selectors["gpus"])
-                placement.gpus = [g for g in placement.gpus if g.index in wanted]
-            if "numa" in selectors:
-                placement.gpus = [g for g in placement.gpus
-                                  if str(g.numa_node) == selectors["numa"]]
-            try:
-                gpus = placement.allocate(self.id, total, task_dir=self.root)
-            except PlacementError as error:
-                raise PlacementError("%s: %s" % (self.id, error)) from None
-            definition["gpus"] = [g.index for g in gpus]
-            definition["gpu_info"] = [g.to_json() for g in gpus]
-            self._event("placed", "gpus " + ",".join(str(g.index) for g in gpus))
+            _write_json(self.task_file, definition)
+            return
+        placement = self.placement
+        try:
+            alloc = placement.reserve(req)
+        except PlacementBusy as busy:
+            if self._knob("TPI_PLACEMENT_QUEUE", "1") == "0":
+                raise PlacementError("%s: %s" % (self.id, busy)) from None
+            placement.enqueue(req, reason=str(busy))
+            self._event("queued", str(busy), "spot" if req.spot else "on-demand",
+                        "position %d" % placement.position(self.id))
+            self._reclaim(placement, req)
+            raise Queued(str(busy)) from None
+        except PlacementError as error:
+            raise PlacementError("%s: %s" % (self.id, error)) from None
+        self._apply(definition, alloc, placement)
+
+    def _apply(self, definition: Dict, alloc: Allocation, placement: Placement) -> None:
+        by_index = {g.index: g for g in placement.gpus}
+        definition["gpus"] = list(alloc.gpus)
+        definition["gpu_info"] = [by_index[g].to_json() for g in alloc.gpus if g in by_index]
+        definition["allocation"] = alloc.to_json()
         _write_json(self.task_file, definition)
+        desc = ["gpus " + (",".join(str(g) for g in alloc.gpus) or "-")]
+        if any(alloc.rank_cpus):
+            desc.append("cpus " + " | ".join(_ranges(c) for c in alloc.rank_cpus))
+        if alloc.memory_mb:
+            desc.append("memory %d MB" % alloc.memory_mb)
+        if alloc.spot:
+            desc.append("spot")
+        self._event("placed", *(desc + alloc.notes))
+
+    def _reclaim(self, placement: Placement, req: Request) -> List[str]:
+        """On-demand task that does not fit: requeue the spot tasks whose resources make it
+        fit (they checkpoint, release and wait for capacity again)."""
+        if req.spot or placement.position(self.id) != 0:
+            return []
+        out = []
+        for victim in placement.victims(req):
+            task_dir = victim.get("task_dir") or ""
+            reply = control_socket(os.path.join(task_dir, "supervisor"),
+                                   "requeue reclaimed by %s" % self.id)
+            if reply and reply.get("ok"):
+                placement.mark_requeueing(victim["task"])
+                self._event("reclaim", "spot task %s" % victim["task"],
+                            "gpus " + ",".join(str(g) for g in victim.get("gpus") or []))
+                out.append(victim["task"])
+        return out
 
     def _spec_json(self) -> Dict:
         d = self._definition()
@@ -262,14 +369,12 @@ class NodeTask(Task):
         })
         visible = ",".join(str(g) for g in gpus)
         numa = [g.get("numa_node", -1) for g in d.get("gpu_info") or []]
+        alloc = d.get("allocation") or {}
         ranks = []
         for r in range(parallelism):
             mine = list(range(r * per, (r + 1) * per)) if per else []
-            # affinity: the cores of the socket the rank's first GPU hangs off
-            node = numa[mine[0]] if mine and mine[0] < len(numa) else -1
-            cpus = numa_cpus(node) if os.environ.get("TPI_NUMA_PIN", "1") != "0" else []
             ranks.append({"gpus": visible, "rank_gpus": ",".join(str(i) for i in mine),
-                          "cpus": cpus})
+                          "cpus": self._rank_cpus(r, alloc)})
         if gpus:
             env["TPI_VISIBLE_GPUS"] = visible
         script_path = os.path.join(self.sup_dir, "script")
@@ -296,8 +401,50 @@ class NodeTask(Task):
             "reports_dir": self.reports_dir,
             "state_path": os.path.join(self.sup_dir, "state.json"),
             "events_path": os.path.join(self.sup_dir, "events.jsonl"),
-            "leases": [self.placement.lease_path(g) for g in gpus],
+            "leases": [self.placement.lease_path(g) for g in gpus] +
+                      ([self.placement.alloc_path(self.id)] if alloc else []),
+            "limits": self._limits(alloc),
+            "requeue_argv": self._waiter_argv(),
         }
+
+    def _rank_cpus(self, rank: int, alloc: Dict) -> List[int]:
+        """Affinity of rank ``rank``: its reserved cores (``reserve`` mode), else -- a limit
+        only -- ``machine.cpus`` cores of this node, a different window per rank
+        (``TPI_NUMA_PIN=0``: no affinity)."""
+        if self._knob("TPI_NUMA_PIN", "1") == "0":
+            return []
+        rank_cpus = alloc.get("rank_cpus") or []
+        if rank < len(rank_cpus) and rank_cpus[rank]:
+            return list(rank_cpus[rank])
+        cores = node_cpus()
+        want = self._machine().cpus
+        if not cores or want <= 0 or want >= len(cores):
+            return []
+        start = (rank * want + (sum(map(ord, self.id)) % len(cores))) % len(cores)
+        return sorted(cores[(start + i) % len(cores)] for i in range(want))
+
+    def _limits(self, alloc: Dict) -> Dict:
+        """Machine-type limits the supervisor enforces (``resource_job.go:112-118``: k8s turns
+        them into pod limits): host memory per rank and the task's ``disk_size``
+        (``TPI_ENFORCE_LIMITS=0`` disables)."""
+        if self._knob("TPI_ENFORCE_LIMITS", "1") == "0":
+            return {}
+        memory = int(alloc.get("memory_mb_per_rank") or 0) or self._machine().memory_mb
+        out = {"rank_memory_mb": memory}
+        try:
+            disk = float(self._definition().get("disk_size", -1) or -1)
+        except (TypeError, ValueError):
+            disk = -1
+        if disk > 0:
+            out["disk_gb"] = disk
+        limit_mb = self._knob("TPI_DISK_LIMIT_MB", "")  # finer than disk_size's GB
+        if limit_mb:
+            out["disk_gb"] = float(limit_mb) / 1000.0
+        try:
+            out["disk_interval"] = float(self._knob("TPI_DISK_CHECK_INTERVAL", "10"))
+        except ValueError:
+            pass
+        return out
 
     def _stager(self, d: Dict, per: int, visible: str, numa: List[int]) -> Optional[Dict]:
         """The supervisor's ``stager`` entry when the workdir goes to HBM before the ranks
@@ -338,15 +485,106 @@ class NodeTask(Task):
     # -- Task interface -------------------------------------------------------------------------
     def create(self) -> None:
         log.info("Creating resources...")
+        queued: List[str] = []
+
+        def place():
+            try:
+                self._place()
+            except Queued as why:
+                queued.append(str(why))
+
+        def start():
+            if queued:
+                self._spawn_waiter()
+            else:
+                self.start()
+
         steps = [Step("Validating machine...", self._validate),
                  Step("Creating storage...", self._create_storage),
-                 Step("Placing task...", self._place),
+                 Step("Placing task...", place),
                  Step("Writing machine script...", self._write_script)]
         if self.spec.environment.directory:
             steps.append(Step("Uploading Directory...", self.push))
-        steps.append(Step("Starting task...", self.start))
+        steps.append(Step("Starting task...", start))
         run_steps(steps, self.timings)
-        log.info("Creation completed")
+        log.info("Creation completed" + (" (queued: %s)" % queued[0] if queued else ""))
+
+    # -- the node queue -----------------------------------------------------------------------
+    def _waiter_argv(self) -> List[str]:
+        code = ("import sys; sys.path.insert(0, %r); "
+                "from terraform_provider_iterative_amd.parallel.scheduler import main; "
+                "sys.exit(main([%r]))" % (ROOT, self.root))
+        return [sys.executable, "-c", code]
+
+    def _spawn_waiter(self) -> int:
+        """Start the detached process that waits for this task's turn, then starts it."""
+        logfile = open(os.path.join(self.sup_dir, "queue.log"), "ab")
+        try:
+            proc = subprocess.Popen(self._waiter_argv(), stdin=subprocess.DEVNULL,
+                                    stdout=logfile, stderr=logfile, close_fds=True,
+                                    cwd=self.root, start_new_session=True)
+        finally:
+            logfile.close()
+        self._write_queue_state(proc.pid)
+        return proc.pid
+
+    def _write_queue_state(self, pid: int, phase: str = "queued") -> None:
+        state = self._state()
+        _write_json(os.path.join(self.sup_dir, "state.json"), {
+            "pid": pid, "task_id": self.id, "phase": phase, "running": 0, "ranks": [],
+            "restarts": int(state.get("restarts", 0) or 0), "heartbeat": _now()})
+
+    def run_queued(self, poll: float = 0.1) -> int:
+        """The waiter (:mod:`..parallel.scheduler`): hold this task's place in the queue until
+        its machine can be reserved, reclaiming spot capacity when it is the on-demand head,
+        then start the supervisor.  SIGTERM (``leo stop`` / ``delete``) leaves the queue."""
+        stopping: List[bool] = []
+        signal.signal(signal.SIGTERM, lambda *_: stopping.append(True))
+        if os.path.exists(self._stop_marker()):
+            stopping.append(True)
+        else:
+            self._write_queue_state(os.getpid())
+        placement = self.placement
+        req = self._request()
+        requeued = self._was_running()
+        if req is None:  # nothing to wait for
+            self.start(restart_base=self._restarts() + requeued, force=True)
+            return 0
+        placement.enqueue(req, waiter_pid=os.getpid(),
+                          reason="requeued" if requeued else "busy")
+        if requeued:  # a reclaimed spot task: back in the queue, resumes when placed again
+            self._event("queued", "requeued", "spot" if req.spot else "on-demand",
+                        "position %d" % placement.position(self.id))
+        t0 = _now()
+        while not stopping:
+            if os.path.exists(self._stop_marker()):
+                break
+            try:
+                alloc = placement.reserve(req)
+            except PlacementBusy:
+                if not req.spot:
+                    self._reclaim(placement, req)
+                time.sleep(poll)
+                continue
+            except PlacementError as error:
+                placement.dequeue(self.id)
+                self._event("placement-failed", str(error))
+                self._write_queue_state(0, "stopped")
+                return 1
+            self._event("dequeued", "waited %.3f s" % (_now() - t0))
+            self._apply(self._definition(), alloc, placement)
+            self.start(restart_base=self._restarts() + requeued, force=True)
+            return 0
+        placement.dequeue(self.id)
+        self._event("stop-requested", "queued task left the queue")
+        self._write_queue_state(0, "stopped")
+        return 0
+
+    def _restarts(self) -> int:
+        return int(self._state().get("restarts", 0) or 0)
+
+    def _was_running(self) -> bool:
+        return any(e.code == "rank-start" for e in self.events())
 
     def read(self) -> None:
         if not os.path.isdir(self.root):
@@ -407,10 +645,11 @@ class NodeTask(Task):
         if os.path.isdir(self.root):
             storage.native().remove_tree(self.root)
 
-    def start(self) -> None:
-        if self.supervisor_running():
+    def start(self, restart_base: int = 0, force: bool = False) -> None:
+        if not force and self.supervisor_running():
             return
         spec = self._spec_json()
+        spec["restart_base"] = restart_base
         spec_path = os.path.join(self.sup_dir, "spec.json")
         _write_json(spec_path, spec)
         # TPI_SUPERVISOR_BIN: an alternative build (e.g. the ASan/UBSan one of the tests)
@@ -434,6 +673,24 @@ class NodeTask(Task):
     def stop(self, wait: float = 60.0) -> None:
         state = self._state()
         pid = int(state.get("pid", 0) or 0)
+        if state.get("phase") in ("queued", "requeued"):
+            # the queue waiter (or the one a requeueing supervisor is about to start) sees
+            # the marker and leaves the queue; a waiter that is gone is cleaned up here
+            with open(self._stop_marker(), "w"):
+                pass
+            deadline = _now() + wait
+            while _now() < deadline and self.supervisor_running():
+                pid = int(self._state().get("pid", 0) or 0)
+                if pid and self._state().get("phase") == "queued":
+                    try:
+                        os.kill(pid, signal.SIGTERM)
+                    except ProcessLookupError:
+                        pass
+                time.sleep(0.02)
+            self.placement.dequeue(self.id)
+            if self._state().get("phase") in ("queued", "requeued"):
+                self._write_queue_state(0, "stopped")
+            return
         if not pid or not pid_alive(pid) or state.get("phase") == "stopped":
             return
         if not (self.control("stop") or {}).get("ok"):
@@ -444,6 +701,9 @@ class NodeTask(Task):
         deadline = _now() + wait
         while _now() < deadline and pid_alive(pid):
             time.sleep(0.02)
+
+    def _stop_marker(self) -> str:
+        return os.path.join(self.sup_dir, "stop-requested")
 
     def preempt(self, rank: Optional[int] = None) -> None:
         """Fault injection: preempt every rank, or only ``rank`` (its gang follows when the
@@ -545,6 +805,22 @@ class NodeTask(Task):
                 break
             time.sleep(poll)
         return self.status()
+
+
+def _ranges(cpus: List[int]) -> str:
+    """``[0,1,2,5]`` -> ``"0-2,5"``."""
+    out, start, prev = [], None, None
+    for c in sorted(cpus):
+        if start is None:
+            start = prev = c
+        elif c == prev + 1:
+            prev = c
+        else:
+            out.append(str(start) if start == prev else "%d-%d" % (start, prev))
+            start = prev = c
+    if start is not None:
+        out.append(str(start) if start == prev else "%d-%d" % (start, prev))
+    return ",".join(out) or "-"
 
 
 def _index_list(spec: str) -> List[int]:

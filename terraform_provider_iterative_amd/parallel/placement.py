@@ -111,7 +111,71 @@ def discover(environ=None) -> List[GPU]:
 
 
 class PlacementError(RuntimeError):
-    pass
+    """The request can never be placed on this node (more GPUs than it has, ...)."""
+
+
+class PlacementBusy(PlacementError):
+    """The node could run the request, but not now: the task waits in the queue."""
+
+
+def node_cpus(environ=None) -> List[int]:
+    """Cores tasks may be given: ``TPI_NODE_CPUS`` (``0-15,32-47``) or this process's
+    affinity mask (a container's cpuset, not the host's core count)."""
+    environ = os.environ if environ is None else environ
+    spec = environ.get("TPI_NODE_CPUS")
+    if spec:
+        return _cpulist(spec)
+    if hasattr(os, "sched_getaffinity"):
+        return sorted(os.sched_getaffinity(0))
+    return list(range(os.cpu_count() or 1))
+
+
+def node_memory_mb(environ=None) -> int:
+    """Host memory tasks may reserve: ``TPI_NODE_MEMORY_MB``, else ``TPI_MEMORY_FRACTION``
+    (default 0.9) of MemTotal."""
+    environ = os.environ if environ is None else environ
+    if environ.get("TPI_NODE_MEMORY_MB"):
+        return int(float(environ["TPI_NODE_MEMORY_MB"]))
+    total_kb = 0
+    for line in _read("/proc/meminfo").splitlines():
+        if line.startswith("MemTotal:"):
+            total_kb = int(line.split()[1])
+    fraction = float(environ.get("TPI_MEMORY_FRACTION", "0.9"))
+    return int(total_kb / 1024 * fraction)
+
+
+@record
+class Request:
+    """What a task asks the node for: ``parallelism`` ranks, each with ``gpus_per_rank`` GPUs,
+    ``cpus_per_rank`` cores and ``memory_mb_per_rank`` of host memory (the machine type is
+    per machine, and a rank is a machine: ``resource_job.go:107-140`` gives each of the Job's
+    ``parallelism`` pods the machine's limits).  ``spot``: reclaimable capacity."""
+    task: str
+    parallelism: int = 1
+    gpus_per_rank: int = 0
+    cpus_per_rank: int = 0
+    memory_mb_per_rank: int = 0
+    spot: bool = False
+    task_dir: str = ""
+    gpu_filter: Optional[List[int]] = None  # region "gpus=" / "numa=" selectors
+    numa: Optional[int] = None
+
+
+@record
+class Allocation:
+    task: str
+    gpus: List[int] = field(default_factory=list)
+    rank_cpus: List[List[int]] = field(default_factory=list)
+    memory_mb: int = 0                      # whole task
+    memory_mb_per_rank: int = 0
+    spot: bool = False
+    notes: List[str] = field(default_factory=list)  # clamped requests etc.
+
+    def to_json(self) -> dict:
+        return {"task": self.task, "gpus": list(self.gpus),
+                "rank_cpus": [list(c) for c in self.rank_cpus], "memory_mb": self.memory_mb,
+                "memory_mb_per_rank": self.memory_mb_per_rank, "spot": self.spot,
+                "notes": list(self.notes)}
 
 
 class Placement:
@@ -244,7 +308,279 @@ class Placement:
                     n += 1
                 except FileNotFoundError:
                     pass
+            for path in (self.alloc_path(task_id), self.queue_path(task_id)):
+                try:
+                    os.unlink(path)
+                except FileNotFoundError:
+                    pass
             return n
+
+    # -- whole-machine reservations: GPUs + cores + host memory, a queue, spot preemption ----
+    #
+    # The reference's scaling group keeps ``desired = parallelism`` until the cloud has the
+    # capacity (resource_auto_scaling_group.go:51-106,188-199), and its consumers show the
+    # task as ``queued`` meanwhile (cmd/leo/read/read.go:164-176).  On one node the capacity
+    # is this node's GPUs, cores and DRAM: a task that does not fit waits in a queue (on-demand
+    # before spot, then first come first served), and an on-demand task may reclaim the
+    # resources of ``spot >= 0`` tasks, which are checkpointed and re-queued.
+
+    def alloc_path(self, task_id: str) -> str:
+        return os.path.join(self.root, "tasks", task_id + ".json")
+
+    def queue_path(self, task_id: str) -> str:
+        return os.path.join(self.root, "queue", task_id + ".json")
+
+    def _load_dir(self, sub: str) -> Dict[str, dict]:
+        out: Dict[str, dict] = {}
+        base = os.path.join(self.root, sub)
+        try:
+            names = os.listdir(base)
+        except OSError:
+            return out
+        for name in names:
+            if not name.endswith(".json"):
+                continue
+            try:
+                out[name[:-5]] = json.loads(_read(os.path.join(base, name)) or "null") or {}
+            except ValueError:
+                continue
+        return out
+
+    def allocations(self) -> Dict[str, dict]:
+        """Live reservations by task id (stale ones -- task gone, supervisor dead past the
+        grace period -- are dropped)."""
+        out = {}
+        for task, alloc in self._load_dir("tasks").items():
+            if self._alive(alloc):
+                out[task] = alloc
+            else:
+                try:
+                    os.unlink(self.alloc_path(task))
+                except FileNotFoundError:
+                    pass
+        return out
+
+    def queue(self) -> List[dict]:
+        """Live queue entries, in service order: on-demand before spot, then FIFO."""
+        live = []
+        for task, entry in self._load_dir("queue").items():
+            pid = int(entry.get("waiter_pid", 0) or 0)
+            fresh = time.time() - float(entry.get("enqueued", 0)) < self.LEASE_GRACE
+            if (pid and _pid_alive(pid)) or (not pid and fresh):
+                live.append(entry)
+            else:
+                try:
+                    os.unlink(self.queue_path(task))
+                except FileNotFoundError:
+                    pass
+        return sorted(live, key=lambda e: (int(e.get("priority", 1)), e.get("enqueued", 0)))
+
+    def enqueue(self, req: "Request", waiter_pid: int = 0, reason: str = "") -> dict:
+        with self._locked():
+            old = _read(self.queue_path(req.task))
+            entry = json.loads(old) if old else {}
+            entry.update({"task": req.task, "task_dir": req.task_dir, "request": _req_json(req),
+                          "priority": 1 if req.spot else 0, "reason": reason})
+            entry.setdefault("enqueued", time.time())
+            if waiter_pid:
+                entry["waiter_pid"] = waiter_pid
+            os.makedirs(os.path.dirname(self.queue_path(req.task)), exist_ok=True)
+            tmp = self.queue_path(req.task) + ".tmp"
+            with open(tmp, "w") as handle:
+                json.dump(entry, handle)
+            os.replace(tmp, self.queue_path(req.task))
+            return entry
+
+    def dequeue(self, task_id: str) -> None:
+        with self._locked():
+            try:
+                os.unlink(self.queue_path(task_id))
+            except FileNotFoundError:
+                pass
+
+    def position(self, task_id: str) -> int:
+        """0-based place of ``task_id`` in the queue, -1 if not queued."""
+        for i, entry in enumerate(self.queue()):
+            if entry.get("task") == task_id:
+                return i
+        return -1
+
+    def reserve(self, req: "Request") -> "Allocation":
+        """Reserve GPUs, cores and memory for every rank of ``req`` atomically.
+
+        Idempotent (an existing reservation is returned).  Raises :class:`PlacementError` when
+        the node can never hold the request and :class:`PlacementBusy` when it cannot right
+        now -- including when a task queued ahead of it is waiting for the same node."""
+        with self._locked():
+            existing = self._load_dir("tasks").get(req.task)
+            if existing and existing.get("gpus") is not None:
+                return _alloc_from(existing)
+            pool = self._pool(req)
+            need = req.gpus_per_rank * req.parallelism
+            if need > len(pool):
+                raise PlacementError("task needs %d GPUs; %d match on this node"
+                                     % (need, len(pool)))
+            ahead = self._ahead(req)
+            if ahead:
+                raise PlacementBusy("queued behind %s" % ", ".join(ahead[:3]))
+            allocs = self.allocations()
+            free = [g for g in self._free_locked() if g in pool]
+            if len(free) < need:
+                raise PlacementBusy("not enough free GPUs: need %d, free %d (held by %s)" % (
+                    need, len(free), ", ".join(sorted(allocs)) or "-"))
+            chosen = sorted(self._choose(free, need, True), key=lambda g: g.index)
+            alloc = Allocation(task=req.task, gpus=[g.index for g in chosen], spot=req.spot)
+            self._reserve_cpus(req, chosen, allocs, alloc)
+            self._reserve_memory(req, allocs, alloc)
+            now = time.time()
+            for gpu in chosen:
+                tmp = self.lease_path(gpu.index) + ".tmp"
+                with open(tmp, "w") as handle:
+                    json.dump({"task": req.task, "task_dir": req.task_dir, "created": now,
+                               "creator_pid": os.getpid(), "gpu": gpu.index,
+                               "spot": req.spot}, handle)
+                os.replace(tmp, self.lease_path(gpu.index))
+            record = dict(alloc.to_json(), task_dir=req.task_dir, created=now,
+                          creator_pid=os.getpid())
+            os.makedirs(os.path.dirname(self.alloc_path(req.task)), exist_ok=True)
+            tmp = self.alloc_path(req.task) + ".tmp"
+            with open(tmp, "w") as handle:
+                json.dump(record, handle)
+            os.replace(tmp, self.alloc_path(req.task))
+            try:
+                os.unlink(self.queue_path(req.task))
+            except FileNotFoundError:
+                pass
+            return alloc
+
+    def _pool(self, req: "Request") -> List[GPU]:
+        pool = list(self.gpus)
+        if req.gpu_filter is not None:
+            pool = [g for g in pool if g.index in req.gpu_filter]
+        if req.numa is not None:
+            pool = [g for g in pool if g.numa_node == req.numa]
+        return pool
+
+    def _ahead(self, req: "Request") -> List[str]:
+        """Queued tasks that must be served before ``req``."""
+        mine = None
+        entries = self.queue()
+        for entry in entries:
+            if entry.get("task") == req.task:
+                mine = (int(entry.get("priority", 1)), entry.get("enqueued", 0))
+        if mine is None:  # not queued yet: behind everyone of its priority or better
+            mine = (1 if req.spot else 0, float("inf"))
+        return [e["task"] for e in entries if e.get("task") != req.task and
+                (int(e.get("priority", 1)), e.get("enqueued", 0)) < mine]
+
+    def _reserve_cpus(self, req: "Request", gpus: List[GPU], allocs: Dict[str, dict],
+                      alloc: "Allocation") -> None:
+        if req.cpus_per_rank <= 0:
+            alloc.rank_cpus = [[] for _ in range(req.parallelism)]
+            return
+        cores = node_cpus()
+        per = min(req.cpus_per_rank, max(1, len(cores) // req.parallelism))
+        if per < req.cpus_per_rank:
+            alloc.notes.append("cpus clamped to %d per rank (node has %d cores)"
+                               % (per, len(cores)))
+        used = {c for a in allocs.values() for cs in a.get("rank_cpus") or [] for c in cs}
+        free = [c for c in cores if c not in used]
+        if len(free) < per * req.parallelism:
+            raise PlacementBusy("not enough free cores: need %d x %d, free %d"
+                                % (req.parallelism, per, len(free)))
+        taken: set = set()
+        out = []
+        for r in range(req.parallelism):
+            mine = gpus[r * req.gpus_per_rank:(r + 1) * req.gpus_per_rank]
+            local = {c for g in mine for c in g.cpus}
+            # the cores of the socket the rank's GPUs hang off first, then any
+            order = [c for c in free if c in local and c not in taken] + \
+                    [c for c in free if c not in local and c not in taken]
+            pick = sorted(order[:per])
+            taken.update(pick)
+            out.append(pick)
+        alloc.rank_cpus = out
+
+    def _reserve_memory(self, req: "Request", allocs: Dict[str, dict],
+                        alloc: "Allocation") -> None:
+        if req.memory_mb_per_rank <= 0:
+            return
+        budget = node_memory_mb()
+        per = min(req.memory_mb_per_rank, max(1, budget // req.parallelism))
+        if per < req.memory_mb_per_rank:
+            alloc.notes.append("memory clamped to %d MB per rank (node budget %d MB)"
+                               % (per, budget))
+        used = sum(int(a.get("memory_mb", 0) or 0) for a in allocs.values())
+        if used + per * req.parallelism > budget:
+            raise PlacementBusy("not enough host memory: need %d MB, free %d of %d MB"
+                                % (per * req.parallelism, budget - used, budget))
+        alloc.memory_mb_per_rank = per
+        alloc.memory_mb = per * req.parallelism
+
+    def victims(self, req: "Request") -> List[dict]:
+        """Spot reservations an on-demand ``req`` would reclaim to fit now: the fewest tasks
+        (largest first) whose GPUs, cores and memory, added to what is free, cover it."""
+        if req.spot:
+            return []
+        with self._locked():
+            allocs = self.allocations()
+            pool = self._pool(req)
+            free_gpus = {g.index for g in self._free_locked() if g in pool}
+            need_gpus = req.gpus_per_rank * req.parallelism
+            cores = node_cpus()
+            used_cores = {c for a in allocs.values() for cs in a.get("rank_cpus") or []
+                          for c in cs}
+            per_cpu = min(req.cpus_per_rank, max(1, len(cores) // req.parallelism)) \
+                if req.cpus_per_rank > 0 else 0
+            free_cores = len(set(cores) - used_cores)
+            budget = node_memory_mb()
+            per_mem = min(req.memory_mb_per_rank, max(1, budget // req.parallelism)) \
+                if req.memory_mb_per_rank > 0 else 0
+            free_mem = budget - sum(int(a.get("memory_mb", 0) or 0) for a in allocs.values())
+            spot = [a for a in allocs.values() if a.get("spot") and not a.get("requeueing")]
+            spot.sort(key=lambda a: (-len(a.get("gpus") or []), -int(a.get("memory_mb", 0))))
+            chosen: List[dict] = []
+
+            def fits() -> bool:
+                return (len(free_gpus) >= need_gpus and free_cores >= per_cpu * req.parallelism
+                        and free_mem >= per_mem * req.parallelism)
+
+            for a in spot:
+                if fits():
+                    break
+                chosen.append(a)
+                free_gpus.update(g for g in a.get("gpus") or [] if any(p.index == g for p in pool))
+                free_cores += sum(len(cs) for cs in a.get("rank_cpus") or [])
+                free_mem += int(a.get("memory_mb", 0) or 0)
+            return chosen if chosen and fits() else []
+
+    def mark_requeueing(self, task_id: str) -> None:
+        """A reclaimed spot task keeps its reservation until its ranks are down."""
+        with self._locked():
+            raw = _read(self.alloc_path(task_id))
+            if not raw:
+                return
+            alloc = json.loads(raw)
+            alloc["requeueing"] = time.time()
+            tmp = self.alloc_path(task_id) + ".tmp"
+            with open(tmp, "w") as handle:
+                json.dump(alloc, handle)
+            os.replace(tmp, self.alloc_path(task_id))
+
+
+def _req_json(req: "Request") -> dict:
+    return {"task": req.task, "parallelism": req.parallelism,
+            "gpus_per_rank": req.gpus_per_rank, "cpus_per_rank": req.cpus_per_rank,
+            "memory_mb_per_rank": req.memory_mb_per_rank, "spot": req.spot,
+            "task_dir": req.task_dir, "gpu_filter": req.gpu_filter, "numa": req.numa}
+
+
+def _alloc_from(data: dict) -> "Allocation":
+    return Allocation(task=data.get("task", ""), gpus=list(data.get("gpus") or []),
+                      rank_cpus=[list(c) for c in data.get("rank_cpus") or []],
+                      memory_mb=int(data.get("memory_mb", 0) or 0),
+                      memory_mb_per_rank=int(data.get("memory_mb_per_rank", 0) or 0),
+                      spot=bool(data.get("spot")), notes=list(data.get("notes") or []))
 
 
 def numa_cpus(node: int) -> List[int]:

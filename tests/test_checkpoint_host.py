@@ -283,3 +283,45 @@ def test_engine_pool_hands_out_the_matching_engine_and_releases_the_rest(monkeyp
     assert other.closed and not match.closed and not elsewhere.closed
     assert list(ckmod._engine_pool) == [(1, 256 << 20, 3, 1 << 20)]
     assert ckmod._take_engine(0, 256 << 20, 3, 1 << 20) is None
+
+
+@pytest.mark.parametrize("slots", [1, 2])
+def test_stream_of_a_dead_writer_is_not_waited_for(tmp_path, slots):
+    """A slot left 'streaming' by a writer that died (SIGKILL after the grace period, OOM) is
+    no checkpoint: resume must not stall TPI_STREAM_TIMEOUT on it and must fall back to the
+    older copy (slots=2) or a fresh start (slots=1)."""
+    import subprocess
+    import sys
+
+    from terraform_provider_iterative_amd.checkpoint import checkpointer as ckmod, preemption
+
+    dead = subprocess.Popen([sys.executable, "-c", "pass"])
+    dead.wait()
+    state = {"w": torch.arange(5000, dtype=torch.float32)}
+    path = str(tmp_path / "spill")
+    ck = Checkpointer(state, path=path, tile_bytes=4096, slots=slots)
+    ck.save({"step": 1})
+    state["w"].add_(1)
+    ck.save({"step": 2}) if slots == 2 else None
+    slot, generation = ck._target()  # the slot the next save would write
+    ck._invalidate(slot)
+    header = ck._header(False, 0, {"step": 3}, "none", None, generation)
+    header["streaming"] = True
+    ck._write_header(slot, header)
+    prog = slot.progress
+    prog[1], prog[2], prog[3], prog[5] = generation, 0, 0, dead.pid
+    prog[4] = ckmod.STREAM_RUNNING
+    prog[0] = ckmod.PROGRESS_MAGIC
+    fresh = {"w": torch.zeros(5000)}
+    ck2 = Checkpointer(fresh, path=path, tile_bytes=4096, slots=slots)
+    t0 = time.monotonic()
+    meta = preemption.resume(ck2)
+    assert time.monotonic() - t0 < 5
+    if slots == 2:
+        assert meta["step"] == 2 and torch.equal(fresh["w"], state["w"])
+    else:
+        assert meta is None
+    prog[5] = os.getpid()  # the same slot with a live writer is a stream in flight
+    assert ck2.latest()["metadata"]["step"] == 3
+    ck2.close()
+    ck.close()

@@ -1,4 +1,5 @@
 """HIP kernels vs host references (run on an MI355X: ``pytest -m gpu``)."""
+import os
 import numpy as np
 import pytest
 import torch
@@ -454,6 +455,7 @@ def test_streamed_restore_follows_the_writers_progress(codec, tmp_path):
     writer._write_header(slot, header)
     prog = slot.progress
     prog[1], prog[2], prog[3], prog[4] = header["generation"], 0, 0, ckmod.STREAM_RUNNING
+    prog[5] = os.getpid()  # a live writer
     prog[0] = ckmod.PROGRESS_MAGIC
     dst = {k: torch.zeros_like(v) for k, v in src.items()}
     dst["t"] = torch.zeros(640, 1000, device="cuda").t()
@@ -498,6 +500,7 @@ def test_streamed_restore_gives_up_on_a_stalled_writer(tmp_path):
     writer._write_header(slot, header)
     prog = slot.progress
     prog[1], prog[2], prog[4] = header["generation"], 0, ckmod.STREAM_RUNNING
+    prog[5] = os.getpid()  # alive, but never makes progress
     prog[0] = ckmod.PROGRESS_MAGIC
     reader = Checkpointer({"a": torch.zeros(1 << 20, device="cuda")}, path=path,
                           tile_bytes=1 << 20, chunk_bytes=1 << 20)

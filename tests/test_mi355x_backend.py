@@ -19,7 +19,10 @@ from terraform_provider_iterative_amd.utils.identifier import new_deterministic_
 
 @pytest.fixture()
 def cloud(tmp_path, monkeypatch):
+    # an 8-GPU MI355X node: 8 GPUs, 128 cores, 2 TB of reservable host memory
     monkeypatch.setenv("TPI_MI355X_GPUS", "0,1,2,3,4,5,6,7")
+    monkeypatch.setenv("TPI_NODE_CPUS", "0-127")
+    monkeypatch.setenv("TPI_NODE_MEMORY_MB", "2000000")
     return Cloud(provider="mi355x",
                  credentials=Credentials(node=NodeCredentials(state_root=str(tmp_path / "st"))))
 
@@ -72,12 +75,18 @@ def test_four_concurrent_two_gpu_tasks(cloud):
     sets = [set(t.gpus()) for t in tasks]
     assert all(len(s) == 2 for s in sets)
     assert len(set().union(*sets)) == 8  # disjoint
+    # a fifth task does not fit: it is queued (create succeeds, like a scaling group
+    # without capacity) and starts when a GPU frees up
     extra = _task(cloud, "conc-extra", "#!/bin/sh\necho hi\n", machine="m+mi355x")
-    with pytest.raises(PlacementError):
-        extra.create()
-    extra.delete()
+    extra.create()
+    assert extra.status() == {"running": 0, "succeeded": 0, "failed": 0}  # leo read: queued
+    assert extra.supervisor_running() and not extra.gpus()
     for t in tasks:
         assert t.wait(30)["succeeded"] == 1
+    assert extra.wait(30)["succeeded"] == 1
+    codes = [e.code for e in extra.events()]
+    assert codes.index("queued") < codes.index("dequeued") < codes.index("placed")
+    extra.delete()
     # auto-cleanup: all GPUs free again, a new task fits
     again = _task(cloud, "after", "#!/bin/sh\necho ok\n", machine="xl+mi355x")
     again.create()
@@ -193,6 +202,7 @@ def test_bench_concurrent_config5(monkeypatch, tmp_path):
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     out = mod.run(tasks=4, gpus_per_task=2, sleep=0.2)
-    assert out["disjoint"] and out["fifth_refused"] and out["all_succeeded"]
+    assert out["disjoint"] and out["cpus_disjoint"] and out["all_succeeded"]
+    assert out["fifth_queued"] and out["fifth_succeeded"] and out["queued_start_s"] < 5
     assert out["reused_all_gpus"]
     assert len(out["first_log_s"]) == 4
