@@ -214,6 +214,9 @@ struct Spec {
   std::vector<std::string> stager_argv;
   std::string stager_manifest, stager_log, stager_gpus;
   double stager_timeout = 600;
+  // false (default): ranks start while the stager loads (attach() waits for the manifest),
+  // so staging is off the first-log path; true: ranks start once the workdir is in HBM
+  bool stage_before_ranks = false;
   // machine-type limits (resource_job.go:112-118 turns cpu/memory/disk into pod limits):
   // host memory per rank (its process group; 0 = none) and the task's workdir size
   uint64_t rank_memory_kb = 0;
@@ -267,6 +270,7 @@ Spec load_spec(const std::string& path) {
   s.stager_log = st["log"].str(s.task_dir + "/supervisor/stager.log");
   s.stager_gpus = st["gpus"].str();
   s.stager_timeout = st["timeout"].num(600);
+  s.stage_before_ranks = st["before_ranks"].boolean(false);
   const Value& lim = v["limits"];
   s.rank_memory_kb = (uint64_t)lim["rank_memory_mb"].num(0) * 1024;
   s.disk_limit_bytes = (uint64_t)(lim["disk_gb"].num(0) * 1e9);
@@ -315,11 +319,16 @@ class Supervisor {
       return finish();
     }
     if (!s_.stager_argv.empty()) {
-      // like the reference's restore before the task service starts (tpl:89): the workdir is
-      // in HBM before any rank runs; create returns at once ("staging" = the VM booting)
-      write_state("staging");
-      signal_ready();
-      stage();
+      // The reference restores the workdir before the task service starts (tpl:89).  Here the
+      // stager loads it while the ranks start (their imports overlap the H2D), and attach()
+      // blocks until the manifest lands; "before_ranks" keeps the strict order.
+      if (s_.stage_before_ranks) {
+        write_state("staging");
+        signal_ready();
+        stage();
+      } else {
+        start_stager();
+      }
     }
     for (auto& r : ranks_)
       if (r.state == Rank::PENDING) spawn(r);
@@ -342,6 +351,7 @@ class Supervisor {
       if (respawn_at_ > 0) timeout = std::min(timeout, respawn_at_ - t);
       if (s_.rank_memory_kb) timeout = std::min(timeout, next_memory_check_ - t);
       if (s_.disk_limit_bytes) timeout = std::min(timeout, next_disk_check_ - t);
+      if (stager_fd_ >= 0) timeout = std::min(timeout, stager_deadline_ - t);
       timeout = std::max(timeout, 0.0);
       std::vector<struct pollfd> pfds;
       pfds.push_back({sfd_, POLLIN, 0});
@@ -359,6 +369,8 @@ class Supervisor {
         }
       size_t nrank_fds = pfds.size();
       if (ctl_fd_ >= 0) pfds.push_back({ctl_fd_, POLLIN, 0});
+      const size_t stager_slot = pfds.size();
+      if (stager_fd_ >= 0) pfds.push_back({stager_fd_, POLLIN, 0});
       int rc = poll(pfds.data(), pfds.size(), (int)(timeout * 1000) + 1);
       if (rc < 0 && errno != EINTR) break;
       bool released = false;
@@ -370,7 +382,12 @@ class Supervisor {
       if (released) handoff_released();
       if (s_.standby_hot) keep_hot_standbys();
       if (pfds[0].revents & POLLIN) handle_signals();
-      if (nrank_fds < pfds.size() && (pfds[nrank_fds].revents & POLLIN)) handle_control();
+      if (ctl_fd_ >= 0 && nrank_fds < pfds.size() && (pfds[nrank_fds].revents & POLLIN))
+        handle_control();
+      if (stager_fd_ >= 0 && stager_slot < pfds.size() &&
+          (pfds[stager_slot].revents & (POLLIN | POLLHUP | POLLERR)))
+        read_stager();
+      if (stager_fd_ >= 0 && now() >= stager_deadline_) stage_failed("timed out");
       if (dirty_ || now() - last_state > 5) {
         write_state();
         last_state = now();
@@ -493,11 +510,64 @@ class Supervisor {
   bool disk_exceeded_ = false;
 
   // ---- workdir stager ----------------------------------------------------------------------
+  int stager_fd_ = -1;            // the stager's stdout ("staged ..." line), while staging
+  double stager_deadline_ = 0;
+  std::string stager_out_;
+
+  // Blocking variant ("before_ranks"): start the stager and wait for "staged".
   void stage() {
+    if (!start_stager()) return;
+    while (!stop_ && stager_fd_ >= 0) {
+      const double left = stager_deadline_ - now();
+      if (left <= 0) {
+        stage_failed("timed out");
+        break;
+      }
+      struct pollfd pf[3] = {{stager_fd_, POLLIN, 0}, {sfd_, POLLIN, 0}, {ctl_fd_, POLLIN, 0}};
+      int rc = poll(pf, ctl_fd_ >= 0 ? 3 : 2, (int)(std::min(left, 1.0) * 1000) + 1);
+      if (rc < 0 && errno != EINTR) break;
+      if (pf[0].revents & (POLLIN | POLLHUP | POLLERR)) read_stager();
+      if (pf[1].revents & POLLIN) handle_signals();
+      if (ctl_fd_ >= 0 && (pf[2].revents & POLLIN)) handle_control();
+    }
+    if (!staged_ && stager_fd_ >= 0) stage_failed("stopped");
+  }
+
+  // The stager's stdout: "staged <stats>" once every copy is in HBM and verified.
+  void read_stager() {
+    char buf[4096];
+    ssize_t n = read(stager_fd_, buf, sizeof(buf));
+    if (n < 0 && (errno == EAGAIN || errno == EINTR)) return;
+    if (n <= 0) {  // EOF: the stager died before staging finished
+      stage_failed("stager exited");
+      return;
+    }
+    stager_out_.append(buf, (size_t)n);
+    size_t nl = stager_out_.find('\n');
+    if (nl != std::string::npos && stager_out_.compare(0, 7, "staged ") == 0) {
+      staged_ = true;
+      event("workdir-staged", {"manifest " + s_.stager_manifest, stager_out_.substr(7, nl - 7)});
+      close(stager_fd_);
+      stager_fd_ = -1;
+    }
+  }
+
+  // Ranks blocked in attach() see "<manifest>.failed" and raise instead of timing out.
+  void stage_failed(const std::string& why) {
+    if (stager_fd_ >= 0) close(stager_fd_);
+    stager_fd_ = -1;
+    event("stage-failed", {stop_ ? "stopped" : why, "see " + s_.stager_log});
+    atomic_write(s_.stager_manifest + ".failed", why + " (see " + s_.stager_log + ")\n");
+    stop_stager();
+  }
+
+  bool start_stager() {
+    unlink(s_.stager_manifest.c_str());  // a previous incarnation's
+    unlink((s_.stager_manifest + ".failed").c_str());
     int p[2];
     if (pipe2(p, O_CLOEXEC)) {
-      event("stage-failed", {std::string("pipe: ") + strerror(errno)});
-      return;
+      stage_failed(std::string("pipe: ") + strerror(errno));
+      return false;
     }
     int logfd = open(s_.stager_log.c_str(), O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
     std::vector<std::string> env;
@@ -535,42 +605,16 @@ class Supervisor {
     if (logfd >= 0) close(logfd);
     if (pid < 0) {
       close(p[0]);
-      event("stage-failed", {std::string("fork: ") + strerror(errno)});
-      return;
+      stage_failed(std::string("fork: ") + strerror(errno));
+      return false;
     }
     stager_pid_ = pid;
+    stager_fd_ = p[0];
+    fcntl(stager_fd_, F_SETFL, fcntl(stager_fd_, F_GETFL) | O_NONBLOCK);
+    stager_deadline_ = now() + s_.stager_timeout;
+    stager_out_.clear();
     event("stager-start", {"pid " + std::to_string(pid)});
-    std::string out, why = "stager exited";
-    const double until = now() + s_.stager_timeout;
-    while (!stop_) {
-      const double left = until - now();
-      if (left <= 0) {
-        why = "timed out";
-        break;
-      }
-      struct pollfd pf[3] = {{p[0], POLLIN, 0}, {sfd_, POLLIN, 0}, {ctl_fd_, POLLIN, 0}};
-      int rc = poll(pf, ctl_fd_ >= 0 ? 3 : 2, (int)(std::min(left, 1.0) * 1000) + 1);
-      if (rc < 0 && errno != EINTR) break;
-      if (pf[0].revents & (POLLIN | POLLHUP | POLLERR)) {
-        char buf[4096];
-        ssize_t n = read(p[0], buf, sizeof(buf));
-        if (n <= 0) break;  // EOF: the stager died before staging finished
-        out.append(buf, (size_t)n);
-        size_t nl = out.find('\n');
-        if (nl != std::string::npos && out.compare(0, 7, "staged ") == 0) {
-          staged_ = true;
-          event("workdir-staged", {"manifest " + s_.stager_manifest, out.substr(7, nl - 7)});
-          break;
-        }
-      }
-      if (pf[1].revents & POLLIN) handle_signals();
-      if (ctl_fd_ >= 0 && (pf[2].revents & POLLIN)) handle_control();
-    }
-    close(p[0]);
-    if (!staged_) {
-      event("stage-failed", {stop_ ? "stopped" : why, "see " + s_.stager_log});
-      stop_stager();
-    }
+    return true;
   }
 
   // SIGTERM (the stager writes dirty shards back first), then SIGKILL after the grace period.
@@ -701,7 +745,9 @@ class Supervisor {
     // SIGTERM -> SIGKILL window: a preempted rank saves at its next step boundary and falls
     // back to an immediate save after half of it (checkpoint/preemption.py)
     add("TPI_GRACE_SECONDS", std::to_string(s_.grace));
-    if (staged_) add("TPI_HBM_WORKDIR", s_.stager_manifest);  // runtime/stage.py attach()
+    // runtime/stage.py attach(): maps the rank's copy, waiting for the manifest if the stager
+    // is still loading
+    if (staged_ || stager_fd_ >= 0) add("TPI_HBM_WORKDIR", s_.stager_manifest);
     if (s_.deadline > 0) {
       add("TPI_DEADLINE", std::to_string((long long)s_.deadline));
       add("TPI_REMAINING_RUN_TIME", std::to_string((long long)(s_.deadline - now())));

@@ -8,7 +8,9 @@ on every rank's GPU (sharded H2D over every GPU's own PCIe link + one in-place R
 all-gather over xGMI), verified by the shard-hash kernel, and the stager stays up to write
 dirty shards back on the reference's cadence.  Ranks start with ``TPI_HBM_WORKDIR`` naming
 the stager's manifest and map their copy zero-copy with :func:`attach` -- no user code is
-needed for the staging itself.
+needed for the staging itself.  The ranks start while the stager is still loading (their
+interpreter and framework start-up overlaps the H2D copies, and the first log line does not
+wait for the workdir); :func:`attach` blocks until the manifest lands.
 
 Knobs (task ``environment`` or the provider's environment):
 
@@ -24,6 +26,8 @@ Knobs (task ``environment`` or the provider's environment):
                            MI355X stages at 39 GB/s with 8, 50 GB/s with 16 -- the PCIe-bound
                            H2D then sets the pace; profiles/config2_stager_threads_round2.json)
 ``TPI_STAGE_CHUNK_BYTES``  pinned ring chunk (default 64 MiB; 256 MiB was slower: 32 GB/s)
+``TPI_STAGE_WAIT``         ``1``: start the ranks only once the workdir is staged (default ``0``)
+``TPI_HBM_WORKDIR_TIMEOUT`` how long :func:`attach` waits for the stager (default 600 s)
 =========================  =====================================================================
 """
 from __future__ import annotations
@@ -110,7 +114,8 @@ def plan(root: str, sup_dir: str, devices: Sequence[int], numa: Sequence[int],
         _build.build_stager()
     return {"argv": [binary, path], "manifest": manifest,
             "log": os.path.join(sup_dir, "stager.log"),
-            "timeout": float(_env(environ, "TPI_STAGE_TIMEOUT", "600"))}
+            "timeout": float(_env(environ, "TPI_STAGE_TIMEOUT", "600")),
+            "before_ranks": _env(environ, "TPI_STAGE_WAIT", "0") not in ("0", "false", "no")}
 
 
 # ---- rank side --------------------------------------------------------------------------------
@@ -199,14 +204,39 @@ class HbmWorkdir:
             self._mapping = None
 
 
-def attach(manifest: Optional[str] = None, rank: Optional[int] = None) -> HbmWorkdir:
-    """Map this rank's copy of the staged workdir (``$TPI_HBM_WORKDIR``)."""
+def wait_staged(path: str, timeout: Optional[float] = None) -> float:
+    """Block until the stager published ``path`` (seconds waited).  Raises RuntimeError when
+    the supervisor marked staging failed (``<path>.failed``) and TimeoutError after
+    ``timeout`` (default ``TPI_HBM_WORKDIR_TIMEOUT`` or 600 s)."""
+    import time
+
+    if timeout is None:
+        timeout = float(os.environ.get("TPI_HBM_WORKDIR_TIMEOUT", "600"))
+    t0 = time.monotonic()
+    delay = 0.0005
+    while not os.path.exists(path):
+        if os.path.exists(path + ".failed"):
+            with open(path + ".failed") as handle:
+                raise RuntimeError("workdir staging failed: %s" % handle.read().strip())
+        if time.monotonic() - t0 > timeout:
+            raise TimeoutError("workdir not staged after %.0f s (%s)" % (timeout, path))
+        time.sleep(delay)
+        delay = min(delay * 2, 0.005)
+    return time.monotonic() - t0
+
+
+def attach(manifest: Optional[str] = None, rank: Optional[int] = None,
+           timeout: Optional[float] = None) -> HbmWorkdir:
+    """Map this rank's copy of the staged workdir (``$TPI_HBM_WORKDIR``), waiting for the
+    stager if it is still loading (:func:`wait_staged`)."""
     path = manifest or os.environ.get("TPI_HBM_WORKDIR")
     if not path:
         raise RuntimeError("no staged workdir: TPI_HBM_WORKDIR is not set (TPI_STAGE=off, "
                            "a small workdir, or staging failed -- see events.jsonl)")
+    waited = wait_staged(path, timeout)
     with open(path) as handle:
         data = json.load(handle)
+    data.setdefault("stats", {})["attach_wait_s"] = round(waited, 4)
     rank = int(os.environ.get("RANK", "0")) if rank is None else rank
     entry = data["ranks"][rank]
     if data.get("host"):

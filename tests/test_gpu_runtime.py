@@ -236,3 +236,65 @@ def test_remote_node_mi355x_task_stages_and_runs_on_the_gpu(tmp_path, monkeypatc
     assert "gpus 1" in log and "staged cuda %d" % int(payload[:4096].sum()) in log, log
     assert task.gpus() and (node_root / "mi355x").is_dir()
     task.delete()
+
+
+SPOT_GPU = r'''#!%(python)s
+import os, sys, time
+sys.path.insert(0, %(root)r)
+import torch
+from terraform_provider_iterative_amd.checkpoint import Checkpointer, preemption
+dev = torch.device("cuda", 0)
+g = torch.Generator(device=dev).manual_seed(3)
+state = {"w": torch.zeros(64 << 20, device=dev), "noise": torch.randn(1 << 20, device=dev, generator=g)}
+ck = Checkpointer(state, path=os.path.join(os.environ["TPI_DATA_DIRECTORY"], ".spill"))
+meta = preemption.resume(ck)
+start = (meta or {}).get("step", 0)
+print("start", start, "gpu", os.environ.get("HIP_VISIBLE_DEVICES"), flush=True)
+preemption.register(ck)
+preemption.install()
+for step in range(start, 60):
+    state["w"].add_(1)
+    torch.cuda.synchronize()
+    time.sleep(0.03)
+    preemption.step(step + 1)
+print("final", int(state["w"][0].item()), int(state["w"][-1].item()), flush=True)
+'''
+
+
+def test_on_demand_task_reclaims_a_spot_task_on_the_gpu(cloud):
+    """Spot semantics on one MI355X: the spot task holds the GPU, an on-demand task arrives,
+    queues, reclaims it (the spot task checkpoints 256 MB of HBM state at a step boundary and
+    goes back to the queue), runs a bf16 matmul, and the spot task resumes afterwards."""
+    spot_spec = Task(size=Size(machine="m+mi355x"), spot=0,
+                     environment=Environment(script=SPOT_GPU % {"python": sys.executable,
+                                                                "root": ROOT},
+                                             timeout=600, variables=Variables({"TPI_TASK": "true"})))
+    spot = backends.new(cloud, new_deterministic_identifier("gpu-spot"), spot_spec)
+    spot.create()
+    deadline = time.time() + 300
+    while time.time() < deadline and "start 0" not in "".join(spot.logs()):
+        time.sleep(0.1)
+    assert "start 0" in "".join(spot.logs()), spot.logs()
+    time.sleep(0.5)
+    od_script = ("#!%s\nimport torch\nx = torch.randn(4096, 4096, device='cuda', "
+                 "dtype=torch.bfloat16)\nprint('on-demand', float((x @ x).float().abs().mean()), "
+                 "flush=True)\n" % sys.executable)
+    od = backends.new(cloud, new_deterministic_identifier("gpu-ondemand"),
+                      Task(size=Size(machine="m+mi355x"),
+                           environment=Environment(script=od_script, timeout=600,
+                                                   variables=Variables({"TPI_TASK": "true"}))))
+    od.create()
+    assert od.wait(300)["succeeded"] == 1, od.logs()
+    assert spot.wait(300)["succeeded"] == 1, spot.logs()
+    logs = spot.logs()
+    assert len(logs) == 2, logs
+    resumed = int(logs[1].split("start ")[1].split()[0])
+    assert 0 < resumed < 60 and "final 60 60" in logs[1], logs
+    codes = [e.code for e in spot.events()]
+    for code in ("requeue-requested", "preempt-boundary", "checkpoint-saved", "requeued",
+                 "dequeued", "checkpoint-restored"):
+        assert code in codes, (code, codes)
+    od_codes = [e.code for e in od.events()]
+    assert od_codes.index("queued") < od_codes.index("reclaim") < od_codes.index("placed")
+    od.delete()
+    spot.delete()

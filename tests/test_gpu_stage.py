@@ -103,7 +103,7 @@ def test_task_workdir_staged_in_hbm_and_written_back(tmp_path, monkeypatch):
     assert "attached cuda" in logs and "True" in logs
     events = task.events()
     codes = [e.code for e in events]
-    assert "workdir-staged" in codes and codes.index("workdir-staged") < codes.index("rank-start")
+    assert "workdir-staged" in codes  # the rank starts while staging runs; attach() waits
     manifest = json.load(open(os.path.join(task.sup_dir, "stage-manifest.json")))
     assert manifest["stats"]["verified"] is True and manifest["ranks"][0]["ipc"]
     data = open(os.path.join(task.data_dir, "a.bin"), "rb").read()

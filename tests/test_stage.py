@@ -79,6 +79,7 @@ def test_mode_selection():
 ATTACH = """#!/bin/sh
 exec python3 - <<'EOF'
 import os, hashlib
+print("rank up", os.environ["RANK"], flush=True)  # before the workdir is needed
 from terraform_provider_iterative_amd.runtime.stage import attach
 w = attach()
 root = os.environ["TPI_DATA_DIRECTORY"]
@@ -98,8 +99,15 @@ EOF
 
 
 @pytest.mark.parametrize("method", ["sharded", "broadcast", "independent"])
-def test_host_mode_stage_attach_and_write_back(cloud, tmp_path, method):
+def test_host_mode_stage_attach_and_write_back(cloud, tmp_path, method, monkeypatch):
     work, sizes = _workdir(tmp_path)
+    # a stager that takes 1.5 s to start: the ranks' first lines must not wait for it
+    from terraform_provider_iterative_amd import _build
+
+    slow = tmp_path / "slow-stager"
+    slow.write_text("#!/bin/sh\nsleep 1.5\nexec %s \"$@\"\n" % _build.build_stager())
+    slow.chmod(0o755)
+    monkeypatch.setenv("TPI_STAGER_BIN", str(slow))
     task = _task(cloud, "stage-" + method, ATTACH, work, parallelism=3,
                  env={"TPI_STAGE": "host", "TPI_STAGE_METHOD": method,
                       "TPI_SYNC_INTERVAL": "0.2"})
@@ -108,9 +116,13 @@ def test_host_mode_stage_attach_and_write_back(cloud, tmp_path, method):
     logs = "\n".join(task.logs())
     assert status["succeeded"] == 3, (logs, open(os.path.join(task.sup_dir, "stager.log")).read())
     assert logs.count("attached rank") == 3 and "True" in logs
-    codes = [e.code for e in task.events()]
+    events = task.events()
+    codes = [e.code for e in events]
     assert "workdir-staged" in codes and "stager-exit" in codes
-    assert codes.index("workdir-staged") < codes.index("rank-start")
+    # staging is off the first-log path: every rank started and logged before it finished
+    staged_at = [e.time for e in events if e.code == "workdir-staged"][0]
+    first = [e.time for e in events if e.code == "rank-first-output"]
+    assert len(first) == 3 and max(first) < staged_at, (first, staged_at)
     # rank 0 changed 3 bytes of a.bin in its copy: exactly that shard went back to the file
     data = open(os.path.join(task.data_dir, "a.bin"), "rb").read()
     assert data[:3] == b"XYZ" and len(data) == sizes["a.bin"]
@@ -121,14 +133,23 @@ def test_host_mode_stage_attach_and_write_back(cloud, tmp_path, method):
     task.delete()
 
 
-def test_stage_failure_falls_back_to_the_host_workdir(cloud, tmp_path, monkeypatch):
+def test_stage_failure_is_reported_to_attach(cloud, tmp_path, monkeypatch):
+    """A stager that dies: attach() raises at once (no timeout wait) and the rank can fall
+    back to the host workdir."""
     work, _ = _workdir(tmp_path)
     monkeypatch.setenv("TPI_STAGER_BIN", "/bin/false")
-    task = _task(cloud, "stage-fail", "#!/bin/sh\necho \"hbm=[$TPI_HBM_WORKDIR]\"\n", work,
-                 parallelism=1, env={"TPI_STAGE": "host"})
+    script = ("#!/bin/sh\nexec python3 - <<'EOF'\nimport os, time\n"
+              "from terraform_provider_iterative_amd.runtime.stage import attach\n"
+              "t0 = time.time()\ntry:\n    attach(timeout=60)\nexcept RuntimeError as e:\n"
+              "    print('fallback after %.1f s:' % (time.time() - t0), e)\n"
+              "print(len(open(os.path.join(os.environ['TPI_DATA_DIRECTORY'], 'a.bin'), 'rb')"
+              ".read()))\nEOF\n")
+    task = _task(cloud, "stage-fail", script, work, parallelism=1, env={"TPI_STAGE": "host"})
     task.create()
     assert task.wait(30)["succeeded"] == 1
-    assert "hbm=[]" in task.logs()[0]
+    log = task.logs()[0]
+    assert "fallback after" in log and "workdir staging failed" in log, log
+    assert float(log.split("fallback after ")[1].split()[0]) < 10
     assert "stage-failed" in [e.code for e in task.events()]
     task.delete()
 
@@ -140,12 +161,13 @@ def test_stop_while_staging(cloud, tmp_path, monkeypatch):
     slow.chmod(0o755)
     monkeypatch.setenv("TPI_STAGER_BIN", str(slow))
     monkeypatch.setenv("TPI_GRACE_SECONDS", "1")
-    task = _task(cloud, "stage-stop", "#!/bin/sh\necho never\n", work, parallelism=1,
-                 env={"TPI_STAGE": "host"})
+    script = ("#!/bin/sh\nexec python3 -c 'from terraform_provider_iterative_amd.runtime."
+              "stage import attach; attach(); print(\"never\")'\n")
+    task = _task(cloud, "stage-stop", script, work, parallelism=1, env={"TPI_STAGE": "host"})
     t0 = time.time()
     task.create()  # returns while staging
     assert time.time() - t0 < 10
-    assert task.status()["running"] == 0
+    assert task.status()["running"] == 1  # the rank runs, blocked in attach()
     task.stop(wait=30)
     assert not task.supervisor_running()
     assert time.time() - t0 < 20
