@@ -329,31 +329,58 @@ int tpi_loader_load(tpi_loader* L, const tpi_file* files, uint64_t nfiles, uint6
   return rc;
 }
 
+// Write-back: image ranges -> files.  Device images go through the pinned ring: the D2H of
+// the next nbuf-1 chunks is in flight on the copy stream while the pool writes the current
+// one, so the PCIe leg and the file writes overlap (the mirror of tpi_loader_load).
 int tpi_loader_store(tpi_loader* L, const tpi_file* files, uint64_t nfiles,
                      const uint64_t* ranges, uint64_t nranges, const void* src,
                      tpi_stats* stats) {
   roctxRangePushA("tpi_loader_store");
   auto t0 = std::chrono::steady_clock::now();
   uint64_t bytes = 0, chunks = 0;
+  struct Piece {
+    uint64_t a, b;
+  };
+  std::vector<Piece> pieces;  // every chunk of every range, in order
+  for (uint64_t r = 0; r < nranges; ++r)
+    for (uint64_t a = ranges[2 * r]; a < ranges[2 * r + 1]; a += L->chunk)
+      pieces.push_back({a, std::min(ranges[2 * r + 1], a + L->chunk)});
   int rc = [&]() -> int {
-    if (L->device >= 0) TPI_HIP(hipSetDevice(L->device));
-    for (uint64_t r = 0; r < nranges; ++r) {
-      const uint64_t lo = ranges[2 * r], hi = ranges[2 * r + 1];
-      for (uint64_t a = lo; a < hi; a += L->chunk) {
-        const uint64_t b = std::min(hi, a + L->chunk);
-        const uint8_t* host = (const uint8_t*)src + a;
-        if (L->device >= 0) {
-          TPI_HIP(hipMemcpyAsync(L->ring[0], (const uint8_t*)src + a, b - a,
-                                 hipMemcpyDeviceToHost, L->stream));
-          TPI_HIP(hipStreamSynchronize(L->stream));
-          host = L->ring[0];
-        }
-        std::string err = parallel_ranges(*L->pool, a, b, [&](uint64_t x, uint64_t y) {
-          return write_range(files, nfiles, x, y, host + (x - a));
-        });
-        if (!err.empty()) return tpi_fail(err);
-        bytes += b - a;
-        ++chunks;
+    auto write = [&](const Piece& p, const uint8_t* host) -> int {
+      std::string err = parallel_ranges(*L->pool, p.a, p.b, [&](uint64_t x, uint64_t y) {
+        return write_range(files, nfiles, x, y, host + (x - p.a));
+      });
+      if (!err.empty()) return tpi_fail(err);
+      bytes += p.b - p.a;
+      ++chunks;
+      return 0;
+    };
+    if (L->device < 0) {
+      for (auto& p : pieces)
+        if (write(p, (const uint8_t*)src + p.a)) return -1;
+      return 0;
+    }
+    TPI_HIP(hipSetDevice(L->device));
+    const size_t depth = (size_t)L->nbuf;
+    size_t issued = 0;
+    auto issue = [&](size_t k) -> int {
+      const int slot = (int)(k % depth);
+      TPI_HIP(hipMemcpyAsync(L->ring[slot], (const uint8_t*)src + pieces[k].a,
+                             pieces[k].b - pieces[k].a, hipMemcpyDeviceToHost, L->stream));
+      TPI_HIP(hipEventRecord(L->ev[slot], L->stream));
+      return 0;
+    };
+    for (size_t k = 0; k < pieces.size(); ++k) {
+      // keep up to nbuf - 1 copies ahead of the chunk being written (its slot stays busy)
+      while (issued < pieces.size() && issued < k + depth - 1 + (depth == 1)) {
+        if (issue(issued)) return -1;
+        ++issued;
+      }
+      const int slot = (int)(k % depth);
+      TPI_HIP(hipEventSynchronize(L->ev[slot]));
+      if (write(pieces[k], L->ring[slot])) {
+        (void)hipStreamSynchronize(L->stream);  // no copy may land in a ring we give up
+        return -1;
       }
     }
     return 0;
@@ -453,15 +480,26 @@ tpi_comm* tpi_comm_init_rank(const uint8_t* id_bytes, int nranks, int rank, int 
 }
 
 int tpi_comm_init_all(int ndev, const int* devices, tpi_comm** out) {
+  for (int i = 0; i < ndev; ++i) out[i] = nullptr;
   std::vector<ncclComm_t> raw(ndev, nullptr);
   TPI_NCCL(ncclCommInitAll(raw.data(), ndev, devices));
   for (int i = 0; i < ndev; ++i) {
     out[i] = new tpi_comm();
     out[i]->comm = raw[i];
+    raw[i] = nullptr;  // owned by out[i] now
     out[i]->device = devices[i];
     out[i]->rank = i;
     out[i]->nranks = ndev;
-    if (comm_stream(out[i])) return -1;
+    if (comm_stream(out[i])) {
+      // a partial set is useless (every collective needs all ranks): release all of it
+      const std::string why = tpi_last_error();
+      for (int j = 0; j < ndev; ++j) {
+        tpi_comm_destroy(out[j]);
+        out[j] = nullptr;
+        if (raw[j]) (void)ncclCommDestroy(raw[j]);
+      }
+      return tpi_fail("task communicator stream: " + why);
+    }
   }
   return 0;
 }

@@ -188,32 +188,70 @@ class Stager {
     publish();
   }
 
-  // Digest rank 0's copy and write the shards that changed since the last sync back to the
-  // files.  Returns the number of dirty shards.
+  // Digest every rank's copy and write the shards that changed since the last sync back to
+  // the files, each from the rank that changed it (the reference's 10 s loop syncs each
+  // machine's own workdir, tpl:118-124).  A shard two ranks changed differently is written
+  // from the lowest of them and reported as a conflict.  Returns the number of dirty shards.
   uint64_t sync(const char* why) {
     auto t0 = std::chrono::steady_clock::now();
-    std::vector<uint64_t> cur = digests(0);
-    std::vector<uint64_t> ranges;
-    uint64_t dirty = 0;
-    for (uint64_t i = 0; i < cur.size(); ++i) {
-      if (i < base_.size() && cur[i] == base_[i]) continue;
+    std::vector<std::vector<uint64_t>> cur(n_);
+    {
+      std::vector<std::thread> th;
+      for (int i = 0; i < n_; ++i) th.emplace_back([&, i] { cur[i] = digests(i); });
+      for (auto& t : th) t.join();
+    }
+    std::vector<std::vector<uint64_t>> ranges(n_);
+    uint64_t dirty = 0, conflicts = 0;
+    std::vector<uint64_t> per_rank(n_, 0);
+    const uint64_t nshards = cur[0].size();
+    for (uint64_t k = 0; k < nshards; ++k) {
+      int writer = -1;
+      for (int i = 0; i < n_; ++i) {
+        if (k < bases_[i].size() && cur[i][k] == bases_[i][k]) continue;
+        if (writer < 0) writer = i;
+        else if (cur[i][k] != cur[writer][k]) ++conflicts;
+      }
+      if (writer < 0) continue;
       ++dirty;
-      const uint64_t lo = i * s_.shard_bytes, hi = std::min(s_.total, lo + s_.shard_bytes);
-      if (!ranges.empty() && ranges.back() == lo) ranges.back() = hi;
+      ++per_rank[writer];
+      const uint64_t lo = k * s_.shard_bytes, hi = std::min(s_.total, lo + s_.shard_bytes);
+      auto& r = ranges[writer];
+      if (!r.empty() && r.back() == lo) r.back() = hi;
       else {
-        ranges.push_back(lo);
-        ranges.push_back(hi);
+        r.push_back(lo);
+        r.push_back(hi);
       }
     }
-    tpi_stats st = {};
-    if (dirty && s_.writeback)
-      check(tpi_loader_store(loaders_[0], s_.files.data(), s_.files.size(), ranges.data(),
-                             ranges.size() / 2, image_[0], &st),
-            "write-back");
-    if (dirty) base_ = cur;
+    std::vector<tpi_stats> st(n_);
+    if (dirty && s_.writeback) {
+      std::vector<std::thread> th;
+      std::vector<std::string> errs(n_);
+      for (int i = 0; i < n_; ++i)
+        if (!ranges[i].empty())
+          th.emplace_back([&, i] {
+            st[i] = tpi_stats{};
+            if (tpi_loader_store(loaders_[i], s_.files.data(), s_.files.size(), ranges[i].data(),
+                                 ranges[i].size() / 2, image_[i], &st[i]))
+              errs[i] = tpi_last_error();
+          });
+      for (auto& t : th) t.join();
+      for (auto& e : errs)
+        if (!e.empty()) die("write-back: " + e);
+    }
+    bases_ = cur;
+    uint64_t bytes = 0;
+    for (auto& x : st) bytes += x.bytes;
+    std::string who;
+    for (int i = 0; i < n_; ++i)
+      if (per_rank[i]) who += (who.empty() ? "" : ",") + std::to_string(i) + ":" +
+                              std::to_string(per_rank[i]);
     event(s_, "workdir-sync", {why, "dirty_shards " + std::to_string(dirty),
-                               "bytes " + std::to_string(st.bytes),
+                               "bytes " + std::to_string(bytes),
+                               "ranks " + (who.empty() ? std::string("-") : who),
                                "ms " + std::to_string(ms_since(t0))});
+    if (conflicts)
+      event(s_, "workdir-sync-conflict", {std::to_string(conflicts) + " shard(s) changed "
+                                          "differently by several ranks; lowest rank written"});
     return dirty;
   }
 
@@ -240,7 +278,8 @@ class Stager {
   std::vector<void*> image_;
   std::vector<tpi_loader*> loaders_;
   std::vector<tpi_comm*> comms_;
-  std::vector<uint64_t> base_;  // digests of rank 0's copy as last synced
+  std::vector<uint64_t> base_;                 // digests of the staged image (every copy)
+  std::vector<std::vector<uint64_t>> bases_;   // per rank: digests of its copy as last synced
   double alloc_ms_ = 0, load_ms_ = 0, read_ms_ = 0, fanout_ms_ = 0, comm_ms_ = 0,
          verify_ms_ = 0;
   bool verified_ = false;
@@ -367,6 +406,7 @@ class Stager {
     for (int i = 1; i < n_ && s_.verify; ++i) verified_ = verified_ && digests(i) == base_;
     verify_ms_ = ms_since(t0);
     if (!verified_) die("fan-out verification failed: GPU copies differ");
+    bases_.assign(n_, base_);
   }
 
   void publish() {

@@ -40,6 +40,11 @@ def main():
     p.add_argument("--ckpt-every", type=int, default=0,
                    help="asynchronous checkpoint every N steps (0: only on SIGTERM/exit)")
     args = p.parse_args()
+    # first log line before the framework import (~0.5-1.5 s): the task is visibly running
+    # while torch loads and the runtime stages the workdir (attach() waits for it below)
+    log("rank %s/%s starting (machine %s)" % (os.environ.get("RANK", "0"),
+                                             os.environ.get("WORLD_SIZE", "1"),
+                                             os.environ.get("TPI_MACHINE_IDENTITY", "-")))
 
     import torch
     import torch.distributed as dist

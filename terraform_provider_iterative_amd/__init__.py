@@ -9,8 +9,9 @@ Layers (see docs/ARCHITECTURE.md):
   iterative_cml_runner) over ``models`` (values, schemas, machine types)
 * backends       ``backends.node`` (cloud = "local" | "mi355x") and ``backends.remote``
 * node runtime   ``csrc/supervisor`` (native rank supervisor), ``parallel.placement``
-  (GPU leases), ``storage`` (rclone-compatible sync, native walker)
-* data plane     ``ops`` + ``checkpoint`` + ``runtime.workdir`` + ``parallel.broadcast``:
+  (reservations of GPUs, cores and memory; the node queue; spot reclaim),
+  ``parallel.scheduler`` (queue waiter), ``storage`` (rclone-compatible sync, native walker)
+* data plane     ``ops`` + ``checkpoint`` + ``runtime`` (stager, workdir) + ``parallel.comm``:
   hand-written CDNA4 HIP kernels (CRC32C tiles, XXH64 shard hashes, pack/unpack),
   pinned-host checkpoint pipeline, HBM workdir staging, RCCL fan-out over xGMI
 """

@@ -55,11 +55,22 @@ def measure_workdir_fanout(nbytes: int, rank: int, world: int, device, barrier: 
 
     workdir = workdir or os.path.join(os.environ.get("TMPDIR", "/tmp"),
                                       "tpi-fanout-%s" % os.environ.get("MASTER_PORT", "0"))
+    requested = nbytes
+    if rank == 0:  # a small TMPDIR shrinks the workdir instead of failing the measurement
+        parent = os.path.dirname(os.path.abspath(workdir))
+        try:
+            free = shutil.disk_usage(parent).free
+        except OSError:
+            free = 0
+        nbytes = int(min(nbytes, max(0, 0.4 * free)))
+    nbytes = int(allmax(float(nbytes) if rank == 0 else 0.0))
+    if nbytes < (64 << 20):
+        raise RuntimeError("no room for a synthetic workdir under %s" % workdir)
     err = None
     if rank == 0:
         try:
             write_workdir(workdir, nbytes)
-        except OSError as error:  # e.g. a small TMPDIR: every rank must learn it, no deadlock
+        except OSError as error:  # every rank must learn it, no deadlock
             err = error
             shutil.rmtree(workdir, ignore_errors=True)
     barrier()
@@ -70,7 +81,8 @@ def measure_workdir_fanout(nbytes: int, rank: int, world: int, device, barrier: 
     total = (size + quantum - 1) // quantum * quantum
     image = torch.empty(total, dtype=torch.uint8, device=device)
     comm = TaskComm.from_group(device=device.index) if world > 1 else None
-    out: Dict[str, dict] = {"bytes": total, "files": len(files)}
+    out: Dict[str, dict] = {"bytes": total, "files": len(files),
+                            "requested_bytes": requested}
     try:
         with Loader(device.index, chunk_bytes=64 << 20, nbuf=4, threads=16,
                     numa_node=numa_node) as loader:

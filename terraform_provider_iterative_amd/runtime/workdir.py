@@ -10,7 +10,8 @@
    the next registration overlap; everything else goes through the native loader
    (``runtime/stage.py`` ``Loader``: pread workers into a NUMA-local pinned ring, H2D of
    chunk k overlapping the reads of chunk k+1; 51 GB/s for 10 GB on MI355X),
-3. fans the buffer out to every rank over xGMI (:mod:`..parallel.broadcast`),
+3. fans the buffer out to every rank over xGMI with the RCCL task communicator
+   (:class:`..parallel.comm.TaskComm`, the runtime stager's own data plane),
 4. optionally verifies the copy with the device shard-hash kernel on every rank.
 
 Each file is then a zero-copy ``uint8`` view (``StagedWorkdir.tensor(path)``); the digests
@@ -32,6 +33,7 @@ from ..storage.transfer import make_filter, transfer_rules
 log = logging.getLogger("tpi.workdir")
 
 ALIGN = 4096
+FANOUT_METHODS = ("sharded", "broadcast", "independent")
 ZERO_COPY_MIN = 64 << 20  # files at least this large are DMA'd from their page-cache pages
 
 
@@ -291,7 +293,19 @@ def stage_workdir(root: Optional[str] = None, device=None, exclude: Optional[Lis
                   group=None, src: int = 0, method: str = "auto", verify: bool = True,
                   chunk_bytes: int = 256 << 20, threads: int = 16,
                   zero_copy_min: int = ZERO_COPY_MIN) -> StagedWorkdir:
-    """Stage ``root`` (default ``$TPI_DATA_DIRECTORY`` or cwd) into HBM on every rank."""
+    """Stage ``root`` (default ``$TPI_DATA_DIRECTORY`` or cwd) into HBM on every rank.
+
+    The library path for scripts that stage themselves (``TPI_STAGE=off`` tasks, or no
+    runtime stager); it uses the stager's own data plane -- the native loader and the RCCL
+    task communicator (:class:`..parallel.comm.TaskComm`) -- with ``torch.distributed`` only
+    carrying the file list and the digests:
+
+    * ``sharded`` (``auto`` on GPUs): rank i loads the i-th 1/N of the image over its own
+      PCIe link, then one in-place all-gather over xGMI;
+    * ``broadcast``: rank ``src`` loads everything, then an RCCL broadcast;
+    * ``independent`` (``auto`` on CPUs): every rank loads its own copy -- the reference's
+      pattern, each machine running its own ``rclone copy`` (``machine-script.sh.tpl:89``).
+    """
     import torch
 
     root = root or os.environ.get("TPI_DATA_DIRECTORY") or os.getcwd()
@@ -307,30 +321,61 @@ def stage_workdir(root: Optional[str] = None, device=None, exclude: Optional[Lis
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
             else torch.device("cpu")
+    device = torch.device(device)
+    on_gpu = device.type == "cuda"
+    if method == "auto":
+        method = "sharded" if on_gpu else "independent"
+    if method not in FANOUT_METHODS:
+        raise ValueError("method must be one of %s" % (FANOUT_METHODS,))
+    if not on_gpu:
+        method = "independent"  # host images: every rank reads the node's files itself
     if rank == src:
-        files, total = manifest(root, exclude)
-        meta = [[(f.path, f.offset, f.size, f.mtime_ns) for f in files], total]
+        files, size = manifest(root, exclude)
+        meta = [[(f.path, f.offset, f.size, f.mtime_ns) for f in files], size]
     else:
         meta = [None, None]
     if world > 1:
         dist.broadcast_object_list(meta, src=src, group=group)
     files = [FileEntry(*m) for m in meta[0]]
-    total = int(meta[1])
-    # on the device the source rank's load writes every byte (gaps included) and receivers
-    # get the broadcast; the host path reads straight into the buffer, so gaps start zeroed
-    alloc = torch.empty if torch.device(device).type == "cuda" else torch.zeros
+    size = int(meta[1])
+    # the sharded all-gather needs equal shards: pad the image to a multiple of world pages
+    quantum = ALIGN * max(1, world)
+    total = (size + quantum - 1) // quantum * quantum if world > 1 and on_gpu else size
+    alloc = torch.zeros if not on_gpu or method == "sharded" else torch.empty
     buffer = alloc(total, dtype=torch.uint8, device=device)
-    stats: Dict[str, float] = {"bytes": total, "files": len(files)}
-    if rank == src:
+    stats: Dict[str, float] = {"bytes": total, "files": len(files), "method": method}  # type: ignore
+    t0 = time.perf_counter()
+    if world == 1 or method == "independent":
         load = load_into(root, files, total, buffer, chunk_bytes, threads, zero_copy_min)
-        stats["load_s"] = load["seconds"]
         stats["read_s"] = load["read_s"]
         stats["zero_copy_files"] = load.get("zero_copy_files", 0)
-    if world > 1:
-        from ..parallel.broadcast import broadcast_buffer, choose_method
+    else:
+        from ..parallel.comm import TaskComm
+        from .stage import Loader
 
-        stats["broadcast_s"] = broadcast_buffer(buffer, src, group, method)
-        stats["broadcast_method"] = choose_method(world, method)  # type: ignore[assignment]
+        entries = [(f.path, f.offset, f.size) for f in files]
+        torch.cuda.current_stream(device).synchronize()  # the zeroed buffer, before the DMA
+        comm = TaskComm.from_group(group, device=device.index)
+        try:
+            with Loader(device.index, chunk_bytes=min(chunk_bytes, 64 << 20), nbuf=4,
+                        threads=threads, numa_node=_numa(device.index)) as loader:
+                if method == "sharded":
+                    shard = total // world
+                    lo, hi = rank * shard, min(size, (rank + 1) * shard)
+                    if lo < hi:
+                        stats["read_s"] = loader.load(root, entries, lo, hi,
+                                                      buffer.data_ptr())["read_ms"] / 1e3
+                    stats["load_s"] = time.perf_counter() - t0
+                    comm.allgather_inplace(buffer, shard)
+                else:
+                    if rank == src:
+                        stats["read_s"] = loader.load(root, entries, 0, size,
+                                                      buffer.data_ptr())["read_ms"] / 1e3
+                    stats["load_s"] = time.perf_counter() - t0
+                    comm.broadcast(buffer, total, root=src)
+        finally:
+            comm.close()
+    stats["stage_s"] = time.perf_counter() - t0
     staged = StagedWorkdir(root, files, buffer, stats)
     if total:  # baseline of sync(): what was staged
         base = staged.digest()

@@ -111,3 +111,27 @@ def test_first_log_latency_probe_gives_up_when_apply_fails(tmp_path, monkeypatch
     except Exception:
         pass  # the in-process create refuses too; the bench catches that
     assert time.perf_counter() - t0 < 30
+
+
+def test_eight_rank_rehearsal_finishes_inside_the_watchdog(tmp_path):
+    """The driver's N=8 launch (torch.distributed.run --nproc-per-node 8) rehearsed on CPU:
+    every side measurement finishes (no watchdog note) and rank 0 prints one line."""
+    import time
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "8", "--device", "cpu", "--total-gb",
+           "0.04", "--steps", "2", "--warmup", "1", "--no-latency", "--hidden", "256",
+           "--side-timeout", "120"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    t0 = time.time()
+    out = subprocess.run(cmd, cwd=str(tmp_path), capture_output=True, text=True, timeout=400,
+                         env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["config"]["parallelism"] == "shard8"
+    assert d["restore_verified"] is True
+    assert "stall_ms" in d["save_async"] and "GBps" in d["raw_GBps"], d
+    assert time.time() - t0 < 120 + 60

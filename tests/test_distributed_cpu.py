@@ -18,14 +18,8 @@ def _worker(rank, world, port, root, results, method):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from terraform_provider_iterative_amd.parallel.broadcast import broadcast_buffer
         from terraform_provider_iterative_amd.runtime.workdir import stage_workdir
 
-        n = 100003
-        buf = torch.arange(n, dtype=torch.int64).to(torch.uint8) if rank == 0 else \
-            torch.zeros(n, dtype=torch.uint8)
-        broadcast_buffer(buf, src=0, method=method)
-        ok_buf = bool(torch.equal(buf, torch.arange(n, dtype=torch.int64).to(torch.uint8)))
         staged = stage_workdir(root, device=torch.device("cpu"), method=method,
                                exclude=["skip.bin"])
         names = sorted(f.path for f in staged.files)
@@ -34,15 +28,18 @@ def _worker(rank, world, port, root, results, method):
         expect = torch.from_numpy(
             __import__("numpy").frombuffer(open(os.path.join(root, "sub/big.bin"), "rb").read(),
                                            dtype="uint8").copy())
-        results[rank] = (ok_buf, names, a, bool(torch.equal(big, expect)),
-                         staged.stats.get("verified"))
+        results[rank] = (names, a, bool(torch.equal(big, expect)),
+                         staged.stats.get("verified"), staged.stats.get("method"))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,method", [(2, "broadcast"), (4, "scatter_allgather"),
-                                          (3, "auto")])
-def test_stage_and_broadcast(tmp_path, world, method):
+@pytest.mark.parametrize("world,method", [(2, "broadcast"), (4, "sharded"), (3, "auto")])
+def test_stage_workdir_on_cpu_ranks(tmp_path, world, method):
+    """The library staging path with gloo ranks on CPU: host images are read by every rank
+    (the GPU schedules -- sharded all-gather, broadcast -- run the RCCL task communicator and
+    are covered by tests/test_gpu_stage.py); the file list comes from rank 0 and the copies
+    are verified by digest."""
     root = tmp_path / "wd"
     (root / "sub").mkdir(parents=True)
     (root / "a.txt").write_bytes(b"hello workdir")
@@ -54,11 +51,10 @@ def test_stage_and_broadcast(tmp_path, world, method):
     mp.spawn(_worker, args=(world, _free_port(), str(root), results, method), nprocs=world)
     assert len(results) == world
     for rank in range(world):
-        ok_buf, names, a, big_ok, verified = results[rank]
-        assert ok_buf, rank
+        names, a, big_ok, verified, used = results[rank]
         assert names == ["a.txt", "sub/big.bin"]
         assert a == b"hello workdir" and big_ok
-        assert verified in (True, None)
+        assert verified is True and used == "independent"
 
 
 def test_write_back(tmp_path):

@@ -195,3 +195,57 @@ def test_loader_host_image_roundtrip(tmp_path):
         image[5:8] = [1, 2, 3]
         loader.store(str(work), files, [(0, 4096)], image.ctypes.data)
     assert (work / "a.bin").read_bytes()[5:8] == b"\x01\x02\x03"
+
+
+EIGHT = """#!/bin/sh
+exec python3 - <<'EOF'
+import glob, os, time
+import torch
+from terraform_provider_iterative_amd.runtime.stage import attach
+w = attach()
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+root = os.environ["TPI_DATA_DIRECTORY"]
+for rel in w.paths():
+    assert bytes(w.tensor(rel).numpy()) == open(os.path.join(root, rel), "rb").read(), rel
+flag = os.path.join(os.environ["TPI_TASK_DIRECTORY"], "verified-%d" % rank)
+open(flag, "w").close()
+while len(glob.glob(os.path.join(os.environ["TPI_TASK_DIRECTORY"], "verified-*"))) < world:
+    time.sleep(0.01)
+# every rank changes its own file in its own copy; ranks 0 and 1 also change c.bin differently
+w.tensor("f%d.bin" % rank)[:4] = torch.tensor(list(b"R%03d" % rank), dtype=torch.uint8)
+if rank < 2:
+    w.tensor("c.bin")[:2] = torch.tensor(list(b"C%d" % rank), dtype=torch.uint8)
+print("changed", rank, flush=True)
+EOF
+"""
+
+
+@pytest.mark.parametrize("method", ["sharded", "broadcast", "independent"])
+def test_eight_rank_write_back_takes_every_ranks_changes(cloud, tmp_path, method):
+    """Host-mode rehearsal of an 8-GPU task: 8 copies staged by all three methods; every
+    rank's changes reach the files (not only rank 0's), conflicts are reported."""
+    work = tmp_path / "work8"
+    work.mkdir()
+    rng = __import__("numpy").random.default_rng(8)
+    for r in range(8):
+        (work / ("f%d.bin" % r)).write_bytes(rng.integers(0, 256, (1 << 20) + 333,
+                                                          dtype="uint8").tobytes())
+    (work / "c.bin").write_bytes(b"c" * 5000)
+    task = _task(cloud, "stage8-" + method, EIGHT, work, parallelism=8,
+                 env={"TPI_STAGE": "host", "TPI_STAGE_METHOD": method,
+                      "TPI_SYNC_INTERVAL": "30", "TPI_RESOURCE_MODE": "limit"})
+    task.create()
+    status = task.wait(120)
+    logs = "\n".join(task.logs())
+    assert status["succeeded"] == 8, (logs, open(os.path.join(task.sup_dir, "stager.log")).read())
+    for r in range(8):
+        data = open(os.path.join(task.data_dir, "f%d.bin" % r), "rb").read()
+        assert data[:4] == b"R%03d" % r, (r, data[:4])
+        assert data[4:] == (work / ("f%d.bin" % r)).read_bytes()[4:]
+    assert open(os.path.join(task.data_dir, "c.bin"), "rb").read()[:2] == b"C0"
+    events = task.events()
+    final = [e for e in events if e.code == "workdir-sync" and "final" in e.description][-1]
+    # c.bin shares shard 0 with the head of f0.bin: 8 dirty shards, one of them in conflict
+    assert "dirty_shards 8" in final.description, final.description
+    assert any(e.code == "workdir-sync-conflict" for e in events)
+    task.delete()
