@@ -128,6 +128,11 @@ def main():
                                                                 Variables)
     from terraform_provider_iterative_amd.utils.identifier import new_random_identifier
 
+    need = args.gb * 1e9 * 1.02
+    free = shutil.disk_usage(args.spill_dir).free
+    if free < need:  # a tmpfs that cannot hold the spill would SIGBUS the rank mid-save
+        raise SystemExit("need %.0f GB free in %s for the spill, have %.0f"
+                         % (need / 1e9, args.spill_dir, free / 1e9))
     state = tempfile.mkdtemp(prefix="tpi-preempt-")
     spill = os.path.join(args.spill_dir, "tpi-preempt-%d.spill" % os.getpid())
     cloud = Cloud(provider="mi355x",
@@ -139,7 +144,7 @@ def main():
     # the ranks' runtime knobs travel as task variables (the rank environment is the task's)
     rank_env = {"TPI_TASK": "true", "TPI_STREAM_HANDOFF": "0" if args.no_stream else "1"}
     for knob in ("TPI_D2H_ENGINE", "TPI_STREAM_TIMEOUT", "TPI_LINGER_SECONDS",
-                 "TPI_HBM_HANDOFF"):
+                 "TPI_HBM_HANDOFF", "TPI_RELEASE_HBM"):
         if os.environ.get(knob):
             rank_env[knob] = os.environ[knob]
     spec = Task(size=Size(machine="m+mi355x"),
@@ -152,6 +157,7 @@ def main():
               "early_prefetch": args.early_prefetch, "standby": args.standby,
               "hot_standby": args.hot, "stream_handoff": not args.no_stream,
               "save_at": "signal" if args.signal_mode else "step boundary",
+              "release_hbm": os.environ.get("TPI_RELEASE_HBM", "1") != "0",
               "step_seconds": args.step_seconds}
     os.environ["TPI_WARM_STANDBY"] = "hot" if args.hot else ("1" if args.standby else "0")
     try:

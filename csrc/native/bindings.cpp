@@ -81,6 +81,7 @@ PYBIND11_MODULE(_tpi_native, m) {
         d["dirs"] = s.dirs;
         d["skipped"] = s.skipped;
         d["skipped_bytes"] = s.skipped_bytes;
+        d["cloned"] = s.cloned;
         d["seconds"] = s.seconds;
         return d;
       },

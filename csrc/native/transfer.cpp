@@ -3,6 +3,8 @@
 #include <dirent.h>
 #include <errno.h>
 #include <fcntl.h>
+#include <linux/fs.h>
+#include <sys/ioctl.h>
 #include <string.h>
 #include <sys/stat.h>
 #include <sys/types.h>
@@ -89,6 +91,7 @@ struct FileJob {
   int in_fd = -1, out_fd = -1;
   std::atomic<int> pieces_left{0};
   std::atomic<bool> failed{false};
+  bool cloned = false;  // FICLONE shared the extents: no pieces to copy
   std::string error;
   std::mutex mu;
 };
@@ -203,12 +206,16 @@ TransferStats copy_dir(const std::string& src, const std::string& dst, const Fil
       close(j->in_fd);
       throw std::runtime_error("open " + j->tmp + ": " + strerror(errno));
     }
-    if (e.size && ftruncate(j->out_fd, (off_t)e.size)) {
+    // A copy-on-write clone (XFS reflink, btrfs) shares the extents: the push of a
+    // multi-GB workdir becomes a metadata operation.  Elsewhere: parallel byte copies.
+    const bool cloned = j->cloned = e.size && ioctl(j->out_fd, FICLONE, j->in_fd) == 0;
+    if (!cloned && e.size && ftruncate(j->out_fd, (off_t)e.size)) {
       close(j->in_fd);
       close(j->out_fd);
       throw std::runtime_error("ftruncate " + j->tmp + ": " + strerror(errno));
     }
-    uint64_t n = e.size ? (e.size + piece_bytes - 1) / piece_bytes : 0;
+    uint64_t n = e.size && !cloned ? (e.size + piece_bytes - 1) / piece_bytes : 0;
+    if (cloned) stats.cloned++;
     j->pieces_left = (int)n;
     for (uint64_t k = 0; k < n; ++k)
       pieces.push_back({j.get(), k * piece_bytes, std::min(piece_bytes, e.size - k * piece_bytes)});
@@ -241,7 +248,7 @@ TransferStats copy_dir(const std::string& src, const std::string& dst, const Fil
   for (auto& t : pool) t.join();
   std::string first_error;
   for (auto& j : jobs) {
-    if (j->size == 0) finish_job(j.get());  // empty files have no pieces
+    if (j->size == 0 || j->cloned) finish_job(j.get());  // no pieces: finish here
     if (j->failed && first_error.empty()) first_error = j->error;
   }
   if (!first_error.empty()) throw std::runtime_error(first_error);

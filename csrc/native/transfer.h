@@ -23,6 +23,7 @@ struct Entry {
 
 struct TransferStats {
   uint64_t files = 0, bytes = 0, dirs = 0, skipped = 0, skipped_bytes = 0;
+  uint64_t cloned = 0;  // files whose extents were shared (reflink) instead of copied
   double seconds = 0;
 };
 

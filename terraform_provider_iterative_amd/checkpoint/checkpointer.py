@@ -1072,6 +1072,25 @@ class Checkpointer:
             raise CheckpointError("loading %s failed: %s" % (path, failure[0]))
         return res
 
+    def release_device(self) -> int:
+        """A preempted rank after its save: free the HBM this checkpointer and its bound
+        tensors hold -- engine staging chunks, the async snapshot, and the storages of every
+        bound tensor (which the model shares: they are unusable afterwards) -- keeping the
+        host region (and its pinning) for the successor.  Returns the bytes released."""
+        freed = 0
+        self._snap = self._snap_crcs = None
+        for slot in self.slots:
+            slot.digests = None
+        if self.engine is not None:
+            self.engine.close()
+            self.engine = None
+        for t in getattr(self.plan, "_bound", []):
+            if getattr(t, "is_cuda", False):
+                storage = t.untyped_storage()
+                freed += storage.nbytes()
+                storage.resize_(0)
+        return freed
+
     def close(self) -> None:
         try:
             self.wait_pending()

@@ -354,3 +354,65 @@ def _ctl_rank(path, rank, world, q):
             break
         time.sleep(rng.random() * 0.002 * (rank + 1))  # skewed step times
     q.put((rank, target, ordinal))
+
+
+BIG_STATE = r'''#!%(python)s
+import os, sys, threading, time
+sys.path.insert(0, %(root)r)
+import torch
+from terraform_provider_iterative_amd.checkpoint import Checkpointer, preemption
+# A rank whose state is too big for two copies in HBM: until it has released its device
+# memory there is no room for a successor (simulated: the hand-off check follows the flag).
+released = threading.Event()
+def fake_release():
+    released.set()
+    return 150 * 10**9
+preemption._release_device_memory = fake_release
+preemption._handoff_safe = released.is_set
+state = {"w": torch.zeros(5000, dtype=torch.float64)}
+ck = Checkpointer(state, path=os.path.join(os.environ["TPI_DATA_DIRECTORY"], ".spill"),
+                  tile_bytes=4096)
+meta = preemption.resume(ck)
+start = (meta or {}).get("step", 0)
+print("start", start, flush=True)
+preemption.register(ck)
+preemption.install()
+for step in range(start, 40):
+    state["w"] += 1
+    time.sleep(0.05)
+    preemption.step(step + 1)
+print("final", int(state["w"][0]), flush=True)
+'''
+
+
+def test_big_state_rank_releases_hbm_before_the_hand_off(cloud):
+    """State > half of HBM (no room for the successor's copy next to ours): the rank saves
+    at the boundary, frees its device memory, then releases the successor while its host
+    region stays pinned, and exits only after the successor restored -- instead of making
+    the successor wait for its full exit."""
+    spec = Task(environment=Environment(
+        script=BIG_STATE % {"python": sys.executable, "root": ROOT}, timeout=300,
+        variables=Variables({"TPI_TASK": "true"})))
+    task = backends.new(cloud, new_deterministic_identifier("big-state"), spec)
+    task.create()
+    deadline = time.time() + 60
+    while time.time() < deadline and "start 0" not in "".join(task.logs()):
+        time.sleep(0.05)
+    time.sleep(0.3)
+    task.preempt()
+    status = task.wait(90)
+    logs = task.logs()
+    assert status["succeeded"] == 1, (status, logs)
+    assert "final 40" in logs[1], logs
+    events = task.events()
+    codes = [e.code for e in events]
+    # saved (not streamed: no room) -> HBM freed -> released -> successor restores -> exit
+    assert "checkpoint-streaming" not in codes, codes
+    order = ["checkpoint-saved", "device-memory-released", "checkpoint-released",
+             "rank-released", "respawn", "checkpoint-restored", "predecessor-exit",
+             "rank-released-exit"]
+    idx = [codes.index(c) for c in order]
+    assert idx == sorted(idx), list(zip(order, idx))
+    exits = [e for e in events if e.code == "rank-released-exit"]
+    assert exits[0].description[-1] == "code 143"
+    task.delete()
