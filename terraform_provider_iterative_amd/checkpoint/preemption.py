@@ -634,9 +634,27 @@ def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None,
         try:  # the predecessor on this GPU is alive and exported its tensors: copy from HBM
             res = checkpointer.restore_hbm()
             journal("checkpoint-restored", "HBM hand-off", *_describe(res),
-                    "ipc open %.3f s" % getattr(checkpointer, "hbm_open_s", 0.0),
-                    "ipc close %.3f s" % getattr(checkpointer, "hbm_close_s", 0.0))
+                    "ipc open %.3f s" % getattr(checkpointer, "hbm_open_s", 0.0))
             notify_restored()
+
+            def behind():  # after "restored": the unmapping, then the host copy's durability
+                checkpointer.wait_hbm_close()
+                journal("hbm-handoff-closed",
+                        "ipc close %.3f s" % getattr(checkpointer, "hbm_close_s", 0.0))
+                t0 = time.perf_counter()
+                done = checkpointer.wait_stream(timeout=float(os.environ.get(
+                    "TPI_DURABLE_TIMEOUT", "600")))
+                if done is False:  # resumed from HBM, but the predecessor's spill failed
+                    journal("checkpoint-not-durable", "the predecessor's host copy failed; "
+                            "no host checkpoint until this rank saves")
+                    print("tpi: WARNING: resumed from the predecessor's HBM, but its host "
+                          "spill failed: no durable checkpoint until the next save",
+                          file=sys.stderr, flush=True)
+                else:
+                    journal("checkpoint-durable", "host copy complete %.3f s after restore"
+                            % (time.perf_counter() - t0))
+
+            threading.Thread(target=behind, name="tpi-handoff-durability", daemon=True).start()
             return header.get("metadata", {})
         except Exception as error:  # fall back to the host region
             journal("checkpoint-hbm-failed", str(error))

@@ -325,3 +325,31 @@ def test_stream_of_a_dead_writer_is_not_waited_for(tmp_path, slots):
     assert ck2.latest()["metadata"]["step"] == 3
     ck2.close()
     ck.close()
+
+
+def test_save_waits_for_a_predecessors_stream_into_the_same_slot(tmp_path):
+    """After an HBM hand-off the successor runs while its predecessor still spills into the
+    shared host region: the successor's first save must not overwrite that slot mid-write."""
+    import threading
+
+    from terraform_provider_iterative_amd.checkpoint import checkpointer as ckmod
+
+    state = {"w": torch.arange(5000, dtype=torch.float32)}
+    path = str(tmp_path / "spill")
+    ck = Checkpointer(state, path=path, tile_bytes=4096)
+    ck.save({"step": 1})
+    prog = ck.slots[0].progress
+    prog[1], prog[5] = ck.header()["generation"], os.getppid()  # a live foreign writer
+    prog[4] = ckmod.STREAM_RUNNING
+    prog[0] = ckmod.PROGRESS_MAGIC
+    threading.Timer(0.4, lambda: prog.__setitem__(4, ckmod.STREAM_COMPLETE)).start()
+    t0 = time.monotonic()
+    ck.save({"step": 2})
+    assert time.monotonic() - t0 >= 0.35
+    assert ck.header()["metadata"]["step"] == 2
+    # a writer that died mid-stream: no wait, reported as not completed
+    prog[5], prog[4], prog[0] = 2 ** 22 + 12345, ckmod.STREAM_RUNNING, ckmod.PROGRESS_MAGIC
+    assert ck.wait_stream(timeout=5) is False
+    prog[4] = ckmod.STREAM_COMPLETE
+    assert ck.wait_stream() is None
+    ck.close()
