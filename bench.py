@@ -9,6 +9,12 @@ encode] -> pinned host DRAM over PCIe, side-stream pipeline) + restore (host -> 
 verify every tile's CRC32C, scatter).  The codec is lossless; ``value`` counts checkpoint
 (tensor) bytes, the JSON also reports the compressed bytes that crossed PCIe.
 
+The restore is the one a preempted rank's successor runs (config 4's streamed hand-off, the
+runtime default): it restores the checkpoint *being* saved into the successor's own tensors,
+chunk by chunk as the save publishes them, over the other direction of the PCIe link.  Both
+are complete and verified inside every step; ``--no-overlap`` restores only after the save
+(into the saved tensors), and the JSON also carries that sequential rate (``sequential``).
+
 Synthetic state (random, no dataset/checkpoint available): bf16 parameters ~ N(0, 0.02),
 fp32 exp_avg ~ N(0, 1e-3), fp32 exp_avg_sq ~ N(0, 1e-3)^2 -- value distributions of a
 trained AdamW state (an untrained one would be all-zero moments, which compress ~1000x).
@@ -65,6 +71,10 @@ def parse_args(argv=None):
     p.add_argument("--side-timeout", type=float, default=300.0,
                    help="seconds the untimed side measurements may take before rank 0 prints "
                         "the headline without them")
+    p.add_argument("--no-overlap", action="store_true",
+                   help="restore after the save instead of streaming behind it")
+    p.add_argument("--spill-dir", default="/dev/shm",
+                   help="where the host region lives (shared by saver and restorer)")
     p.add_argument("--device", choices=("cuda", "cpu"), default="cuda",
                    help="cpu: rehearse the multi-rank control flow on CPU tensors over gloo "
                         "(tests; not a measurement of the MI355X path)")
@@ -251,14 +261,55 @@ def main(argv=None):
     from terraform_provider_iterative_amd.checkpoint import Checkpointer
 
     per_rank = int(args.total_gb * 1e9 / world)
+    overlap = not args.no_overlap
+    spill_dir = args.spill_dir if os.path.isdir(args.spill_dir) else None
+    import tempfile
+
+    spill_path = os.path.join(spill_dir or tempfile.gettempdir(), "tpi-bench-%s-%d-r%d.spill" % (
+        os.environ.get("MASTER_PORT", "0"), os.getpid(), rank))
     t_setup = time.perf_counter()
     tensors = synthetic_checkpoint(per_rank, args.hidden, device)
     sync()
-    ck = Checkpointer(tensors, tile_bytes=int(args.tile_mb * (1 << 20)),
-                      chunk_bytes=int(args.chunk_mb * (1 << 20)), nbuf=args.nbuf, mode=args.mode,
-                      codec=args.codec)
+    ck_kw = dict(tile_bytes=int(args.tile_mb * (1 << 20)), chunk_bytes=int(args.chunk_mb * (1 << 20)),
+                 nbuf=args.nbuf, mode=args.mode, codec=args.codec)
+    ck = Checkpointer(tensors, path=spill_path, **ck_kw)
+    successor = ck_in = None
+    if overlap:  # the successor's tensors, restored from the same host region
+        successor = synthetic_checkpoint(per_rank, args.hidden, device, fill=False)
+        sync()
+        ck_in = Checkpointer(successor, path=spill_path, **ck_kw)
+    try:  # both mappings hold the pages; no name left behind even if the process dies
+        os.remove(spill_path)
+    except OSError:
+        pass
     setup_s = time.perf_counter() - t_setup
     barrier()
+
+    def save_restore(meta):
+        """One step: (wire bytes, save s, restore s, restore result)."""
+        a = time.perf_counter()
+        if not overlap:
+            wire = ck.save(meta).wire_bytes
+            b = time.perf_counter()
+            res = ck.restore()
+            return wire, b - a, time.perf_counter() - b, res
+        box = {}
+
+        def restorer():
+            try:
+                box["res"] = ck_in.restore()
+            except BaseException as error:  # surfaced below
+                box["error"] = error
+            box["t"] = time.perf_counter()
+
+        thread = threading.Thread(target=restorer, name="bench-restore")
+        # the restore starts once the save has published its streaming header
+        wire = ck.save(meta, on_stream=thread.start).wire_bytes
+        b = time.perf_counter()
+        thread.join()
+        if "error" in box:
+            raise box["error"]
+        return wire, b - a, box["t"] - a, box["res"]
 
     def progress(msg: str) -> None:  # stderr heartbeat: long (profiled) runs are not silent
         if rank == 0:
@@ -266,8 +317,7 @@ def main(argv=None):
 
     progress("setup %.1f s (%d bytes per rank)" % (setup_s, per_rank))
     for i in range(args.warmup):
-        ck.save({"warmup": True})
-        ck.restore()
+        save_restore({"warmup": True})
         progress("warmup %d/%d" % (i + 1, args.warmup))
     barrier()
 
@@ -275,16 +325,16 @@ def main(argv=None):
     wire = 0
     t0 = time.perf_counter()
     for step in range(args.steps):
-        a = time.perf_counter()
-        wire = ck.save({"step": step}).wire_bytes
-        b = time.perf_counter()
-        res = ck.restore()
-        c = time.perf_counter()
+        if overlap and successor is not None:
+            # the successor's tensors must really be rewritten by every step's restore
+            for t in list(successor.values())[:2]:
+                t.zero_()
+        wire, s_s, r_s, res = save_restore({"step": step})
         if res.bad_tiles:
             raise SystemExit("bench: %d corrupt tiles after restore" % res.bad_tiles)
-        save_s += b - a
-        restore_s += c - b
-        progress("step %d/%d save %.3f s restore %.3f s" % (step + 1, args.steps, b - a, c - b))
+        save_s += s_s
+        restore_s += r_s
+        progress("step %d/%d save %.3f s restore %.3f s" % (step + 1, args.steps, s_s, r_s))
     barrier()
     elapsed = time.perf_counter() - t0
 
@@ -292,19 +342,27 @@ def main(argv=None):
     if args.verify:  # outside the timed region: prove the restore really rewrote HBM
         from terraform_provider_iterative_amd import ops
 
-        names = list(tensors)[:3]
-
-        def digest(n):
-            out = ops.shard_hash(tensors[n].view(-1).view(torch.uint8))
+        def digest(d, n):
+            out = ops.shard_hash(d[n].view(-1).view(torch.uint8))
             return out.cpu().tolist() if hasattr(out, "cpu") else out.tolist()
 
-        before = [digest(n) for n in names]
-        for n in names:
-            tensors[n].zero_()
-        ck.restore()
-        sync()
-        after = [digest(n) for n in names]
-        verified = before == after
+        if overlap:  # every tensor of the successor equals the saved state
+            sync()
+            verified = all(digest(successor, n) == digest(tensors, n) for n in tensors)
+        else:
+            names = list(tensors)[:3]
+            before = [digest(tensors, n) for n in names]
+            for n in names:
+                tensors[n].zero_()
+            ck.restore()
+            sync()
+            verified = before == [digest(tensors, n) for n in names]
+    if ck_in is not None:  # the side measurements need the HBM back
+        ck_in.close()
+        ck_in = None
+        successor = None
+        if on_gpu:
+            torch.cuda.empty_cache()
 
     elapsed = allmax(elapsed)
     save_max, restore_max = allmax(save_s), allmax(restore_s)
@@ -337,6 +395,7 @@ def main(argv=None):
                        "tensors_per_rank": len(tensors)},
             "save_GBps": round(total * args.steps / save_max / 1e9, 3),
             "restore_GBps": round(total * args.steps / restore_max / 1e9, 3),
+            "restore_streams_behind_save": overlap,
             "per_gpu_save_GBps": round(ck.plan.total * args.steps / save_max / 1e9, 3),
             "per_gpu_restore_GBps": round(ck.plan.total * args.steps / restore_max / 1e9, 3),
             "wire_bytes_per_step": wire_total,
@@ -346,6 +405,7 @@ def main(argv=None):
             "first_log_latency": latency,
             "workdir_broadcast": None,
             "raw_GBps": None,
+            "sequential": None,
             "rank0_cpu_affinity": len(pinned_cpus) if pinned_cpus else None,
             "restore_verified": verified,
             "save_async": None,
@@ -359,7 +419,7 @@ def main(argv=None):
     def emit(note=None):
         if out is not None and printed.acquire(blocking=False):  # exactly one line
             if note:
-                for key in ("save_async", "raw_GBps", "workdir_broadcast"):
+                for key in ("save_async", "raw_GBps", "workdir_broadcast", "sequential"):
                     if out[key] is None:
                         out[key] = {"error": note}
             print(json.dumps(out), flush=True)
@@ -423,6 +483,30 @@ def main(argv=None):
                 "save_GBps": round(total / rs / 1e9, 3),
                 "restore_GBps": round(total / rr / 1e9, 3)})
 
+    sequential = None
+    if overlap:  # untimed: the same step with the restore after the save (into the saved tensors)
+        err, ss, rr = None, 0.0, 0.0
+        try:
+            barrier()
+            a = time.perf_counter()
+            ck.save({"sequential": True})
+            sync()
+            ss = time.perf_counter() - a
+            a = time.perf_counter()
+            res = ck.restore()
+            sync()
+            rr = time.perf_counter() - a
+            if res.bad_tiles:
+                err = "%d corrupt tiles" % res.bad_tiles
+        except Exception as error:
+            err = repr(error)
+        failed = allmax(1.0 if err else 0.0)
+        ss, rr = allmax(ss), allmax(rr)
+        sequential = ({"error": err or "failed on another rank"} if failed else
+                      {"GBps": round(2 * total / (ss + rr) / 1e9, 3),
+                       "save_GBps": round(total / ss / 1e9, 3),
+                       "restore_GBps": round(total / rr / 1e9, 3)})
+
     fanout = None
     # configs 2/3: workdir -> HBM on every rank (untimed; RCCL needs one GPU per rank)
     if args.broadcast_gb > 0 and on_gpu and (world == 1 or backend == "nccl"):
@@ -444,6 +528,7 @@ def main(argv=None):
         out["save_async"] = async_stall
         out["raw_GBps"] = raw
         out["workdir_broadcast"] = fanout
+        out["sequential"] = sequential
     emit()
     ck.close()
     if world > 1:
