@@ -11,6 +11,7 @@
 // chunk, byte-plane encode into staging[b], D2H only the compressed bytes (and the inverse).
 // Incremental sync (tpi_sync): per-tile digests from the tensors, pack + D2H of dirty tiles.
 #include <errno.h>
+#include <signal.h>
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
@@ -356,13 +357,39 @@ int publish_chunk(tpi_engine* e, const std::vector<ChunkMark>& marks, uint64_t j
 // Streaming hand-off, restore side: block until the writer has published `tiles` tiles.
 // Fails when the writer reports failure (words[2] == 3, the progress block's state word) or
 // makes no progress for `timeout_s` (it died).
+// Is the process that publishes a streamed save (progress word 3) still running?  Zombies
+// count as gone: a SIGKILLed predecessor is not reaped at once.
+bool writer_alive(uint64_t pid) {
+  if (pid == 0 || pid == (uint64_t)getpid()) return true;
+  if (kill((pid_t)pid, 0) != 0 && errno == ESRCH) return false;
+  char path[64];
+  snprintf(path, sizeof(path), "/proc/%llu/stat", (unsigned long long)pid);
+  FILE* f = fopen(path, "r");
+  if (!f) return true;  // no /proc: trust kill()
+  char buf[512];
+  const size_t n = fread(buf, 1, sizeof(buf) - 1, f);
+  fclose(f);
+  buf[n] = 0;
+  const char* rp = strrchr(buf, ')');
+  return !(rp && rp[1] == ' ' && (rp[2] == 'Z' || rp[2] == 'X'));
+}
+
 int wait_published(const uint64_t* words, uint64_t tiles, double timeout_s) {
   uint64_t seen = __atomic_load_n(&words[0], __ATOMIC_ACQUIRE);
   auto last = std::chrono::steady_clock::now();
+  auto last_check = last;
   while (seen < tiles) {
     if (__atomic_load_n(&words[2], __ATOMIC_ACQUIRE) == 3)  // the writer reported a failure
       return fail("the streamed checkpoint failed in its writer");
     std::this_thread::sleep_for(std::chrono::microseconds(50));
+    const auto now = std::chrono::steady_clock::now();
+    if (std::chrono::duration<double>(now - last_check).count() > 0.02) {
+      last_check = now;
+      if (__atomic_load_n(&words[0], __ATOMIC_ACQUIRE) < tiles &&
+          __atomic_load_n(&words[2], __ATOMIC_ACQUIRE) != 2 &&
+          !writer_alive(__atomic_load_n(&words[3], __ATOMIC_ACQUIRE)))
+        return fail("the streamed checkpoint's writer exited before finishing it");
+    }
     const uint64_t now_tiles = __atomic_load_n(&words[0], __ATOMIC_ACQUIRE);
     if (now_tiles != seen) {
       seen = now_tiles;

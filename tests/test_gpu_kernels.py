@@ -509,6 +509,20 @@ def test_streamed_restore_gives_up_on_a_stalled_writer(tmp_path):
     prog[4] = ckmod.STREAM_FAILED
     with pytest.raises(CheckpointError):
         reader.restore(stream_timeout=5)
+    # the writer dies while the successor waits for its chunks: the native wait notices the
+    # exit within ~20 ms instead of sitting out the timeout
+    import subprocess
+    import sys
+    import threading
+    import time
+
+    child = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(0.5)"])
+    prog[4], prog[5] = ckmod.STREAM_RUNNING, child.pid
+    threading.Thread(target=child.wait, daemon=True).start()  # reaped: no zombie
+    t0 = time.monotonic()
+    with pytest.raises(CheckpointError, match="exited"):
+        reader._restore_streaming(reader.slots[0], header, strict=True, timeout=30)
+    assert time.monotonic() - t0 < 5
     reader.close()
     writer.close()
 
