@@ -414,9 +414,12 @@ class Supervisor {
   double next_memory_check_ = 0, next_disk_check_ = 0;
 
   // ---- machine-type limits -------------------------------------------------------------------
-  // Host memory of a process group: proportional set size (shared pages split between their
-  // users, so a spill region mapped by two processes is not counted twice), VmRSS fallback.
+  // Host memory of a process group: the resident set of each member (/proc/<pid>/statm, O(1)
+  // per process from the kernel's counters -- smaps_rollup's proportional set size would walk
+  // the page tables of a 100 GB pinned spill on every sample and stall this event loop).
+  // Pages shared inside the group (forked workers) count once per member.
   static uint64_t group_memory_kb(pid_t pgid) {
+    static const uint64_t page_kb = (uint64_t)sysconf(_SC_PAGESIZE) / 1024;
     uint64_t total = 0;
     DIR* d = opendir("/proc");
     if (!d) return 0;
@@ -424,35 +427,29 @@ class Supervisor {
       char* end = nullptr;
       long pid = strtol(e->d_name, &end, 10);
       if (!end || *end || pid <= 0) continue;
-      std::string stat;
-      try {
-        stat = read_file("/proc/" + std::to_string(pid) + "/stat");
-      } catch (...) {
+      char path[64], buf[512];
+      snprintf(path, sizeof(path), "/proc/%ld/stat", pid);
+      int fd = open(path, O_RDONLY | O_CLOEXEC);
+      if (fd < 0) continue;
+      ssize_t n = read(fd, buf, sizeof(buf) - 1);
+      close(fd);
+      if (n <= 0) continue;
+      buf[n] = 0;
+      const char* rp = strrchr(buf, ')');
+      long pgrp = 0;
+      char state = 0;
+      long ppid = 0;
+      if (!rp || sscanf(rp + 1, " %c %ld %ld", &state, &ppid, &pgrp) != 3 || pgrp != (long)pgid)
         continue;
-      }
-      size_t rp = stat.rfind(')');
-      if (rp == std::string::npos) continue;
-      std::istringstream fields(stat.substr(rp + 2));
-      std::string state;
-      long ppid = 0, pgrp = 0;
-      fields >> state >> ppid >> pgrp;
-      if (pgrp != (long)pgid) continue;
-      uint64_t kb = 0;
-      for (const char* file : {"/smaps_rollup", "/status"}) {
-        std::ifstream in("/proc/" + std::to_string(pid) + file);
-        std::string key;
-        uint64_t value;
-        const std::string want = file[1] == 's' && file[2] == 'm' ? "Pss:" : "VmRSS:";
-        while (in >> key) {
-          if (key == want && in >> value) {
-            kb = value;
-            break;
-          }
-          in.ignore(1 << 20, '\n');
-        }
-        if (kb) break;
-      }
-      total += kb;
+      snprintf(path, sizeof(path), "/proc/%ld/statm", pid);
+      fd = open(path, O_RDONLY | O_CLOEXEC);
+      if (fd < 0) continue;
+      n = read(fd, buf, sizeof(buf) - 1);
+      close(fd);
+      if (n <= 0) continue;
+      buf[n] = 0;
+      unsigned long long size = 0, resident = 0;
+      if (sscanf(buf, "%llu %llu", &size, &resident) == 2) total += resident * page_kb;
     }
     closedir(d);
     return total;
