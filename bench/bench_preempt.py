@@ -76,6 +76,9 @@ if resuming:
               t_alloc - t_prefetch, t_map - t_alloc,
                                   t_import - t_start, ck.init_times),
           flush=True)
+    # the predecessor is still spilling behind the HBM hand-off: wait for the host copy, so
+    # the journal shows when this resumed state became durable (checkpoint-durable)
+    ck.wait_stream(timeout=600)
     ck.close()
     os.remove(spill)
     sys.exit(0 if ok else 3)
@@ -206,6 +209,11 @@ def main():
                 result["saved_to_restored_s"] = round(t_restored - t_saved, 3)
         if t_sig:  # every journal phase after the signal, seconds from it
             result["timeline"] = [[c, round(t - t_sig, 4), d] for c, t, d in events if t >= t_sig]
+        t_durable, _ = first("checkpoint-durable", t_restored or 0.0)
+        if t_durable and t_sig:  # host copy of the resumed state complete (HBM hand-off)
+            result["signal_to_durable_s"] = round(t_durable - t_sig, 3)
+        result["durability"] = next((c for c, _, _ in events if c in (
+            "checkpoint-durable", "checkpoint-not-durable", "checkpoint-durability-unknown")), None)
         result["verified"] = any("verified True" in l for l in logs)
         result["ok"] = bool(status.get("succeeded") == 1 and result["verified"])
     finally:

@@ -427,6 +427,10 @@ class Checkpointer:
         self._pending: Optional[PendingSave] = None
         self.last_save: Optional[TransferResult] = None
         self.last_restore: Optional[TransferResult] = None
+        # close() stops wait_stream() pollers and joins the threads that watch this region
+        # (the hand-off's durability watcher) before the region is unmapped under them
+        self._closing = threading.Event()
+        self._watchers: List[threading.Thread] = []
 
     # -- slots -------------------------------------------------------------------------------
     def _slot_header(self, slot: _Slot) -> Optional[Dict]:
@@ -499,7 +503,8 @@ class Checkpointer:
     def wait_stream(self, timeout: Optional[float] = None) -> Optional[bool]:
         """Wait until a streamed save by *another* live process (a preempted predecessor
         spilling behind an HBM hand-off) has finished writing this region.  Returns True when
-        it completed, False when it failed (or its writer died), None when there was none.
+        it completed, False when it failed (or its writer died), None when there was none or
+        this checkpointer is being closed.
         Every save / load calls it first: a save must not overwrite a slot that is still
         being written, and must not drop the only host copy before it exists."""
         if timeout is None:
@@ -507,6 +512,8 @@ class Checkpointer:
         deadline = time.monotonic() + timeout
         seen = None
         while True:
+            if self._closing.is_set():
+                return None
             foreign = None
             for slot in self.slots:
                 prog = slot.progress
@@ -1137,7 +1144,24 @@ class Checkpointer:
             closer.join()
             self._hbm_closer = None
 
+    def watch(self, fn, name: str) -> threading.Thread:
+        """Run ``fn`` on a daemon thread that :meth:`close` joins before unmapping the
+        region (``fn`` may poll the region through :meth:`wait_stream`)."""
+        thread = threading.Thread(target=fn, name=name, daemon=True)
+        self._watchers.append(thread)
+        thread.start()
+        return thread
+
+    @property
+    def closing(self) -> bool:
+        return self._closing.is_set()
+
     def close(self) -> None:
+        self._closing.set()
+        for thread in self._watchers:
+            if thread is not threading.current_thread():
+                thread.join()
+        self._watchers = []
         self.wait_hbm_close()
         try:
             self.wait_pending()

@@ -650,11 +650,14 @@ def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None,
                     print("tpi: WARNING: resumed from the predecessor's HBM, but its host "
                           "spill failed: no durable checkpoint until the next save",
                           file=sys.stderr, flush=True)
+                elif done is None and checkpointer.closing:
+                    journal("checkpoint-durability-unknown", "the checkpointer was closed "
+                            "before the predecessor's host copy finished")
                 else:
                     journal("checkpoint-durable", "host copy complete %.3f s after restore"
                             % (time.perf_counter() - t0))
 
-            threading.Thread(target=behind, name="tpi-handoff-durability", daemon=True).start()
+            checkpointer.watch(behind, "tpi-handoff-durability")
             return header.get("metadata", {})
         except Exception as error:  # fall back to the host region
             journal("checkpoint-hbm-failed", str(error))

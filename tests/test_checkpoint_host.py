@@ -353,3 +353,26 @@ def test_save_waits_for_a_predecessors_stream_into_the_same_slot(tmp_path):
     prog[4] = ckmod.STREAM_COMPLETE
     assert ck.wait_stream() is None
     ck.close()
+
+
+def test_close_stops_and_joins_a_durability_watcher(tmp_path):
+    """A successor that closes its checkpointer while the hand-off's durability watcher still
+    waits on the predecessor's spill: close() stops the wait (None, not a false 'failed') and
+    joins the watcher before the region is unmapped under it."""
+    from terraform_provider_iterative_amd.checkpoint import checkpointer as ckmod
+
+    state = {"w": torch.arange(5000, dtype=torch.float32)}
+    ck = Checkpointer(state, path=str(tmp_path / "spill"), tile_bytes=4096)
+    ck.save({"step": 1})
+    prog = ck.slots[0].progress
+    prog[1], prog[5] = ck.header()["generation"], os.getppid()  # a live foreign writer
+    prog[4] = ckmod.STREAM_RUNNING
+    prog[0] = ckmod.PROGRESS_MAGIC
+    seen = []
+    watcher = ck.watch(lambda: seen.append(ck.wait_stream(timeout=60)), "test-watcher")
+    time.sleep(0.1)
+    assert watcher.is_alive()
+    t0 = time.monotonic()
+    ck.close()
+    assert time.monotonic() - t0 < 2
+    assert not watcher.is_alive() and seen == [None]
