@@ -512,8 +512,6 @@ class Checkpointer:
         deadline = time.monotonic() + timeout
         seen = None
         while True:
-            if self._closing.is_set():
-                return None
             foreign = None
             for slot in self.slots:
                 prog = slot.progress
@@ -524,6 +522,8 @@ class Checkpointer:
                 if seen is None:
                     return None
                 return int(seen.progress[4]) == STREAM_COMPLETE
+            if self._closing.is_set():  # (the outcome above wins over a close racing it)
+                return None
             seen = foreign
             if not _writer_alive(int(foreign.progress[5])) or time.monotonic() > deadline:
                 return False
