@@ -500,6 +500,11 @@ class Checkpointer:
         active = self._active()
         return active[1] if active else None
 
+    def durable(self, generation: int) -> bool:
+        """Does the region hold a complete copy of ``generation`` (or a newer one)?"""
+        active = self._active()
+        return active is not None and active[1].get("generation", 0) >= generation
+
     def wait_stream(self, timeout: Optional[float] = None) -> Optional[bool]:
         """Wait until a streamed save by *another* live process (a preempted predecessor
         spilling behind an HBM hand-off) has finished writing this region.  Returns True when

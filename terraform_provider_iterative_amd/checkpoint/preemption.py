@@ -644,6 +644,11 @@ def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None,
                 t0 = time.perf_counter()
                 done = checkpointer.wait_stream(timeout=float(os.environ.get(
                     "TPI_DURABLE_TIMEOUT", "600")))
+                if done is None:  # no spill running (any more): is the restored copy there?
+                    if checkpointer.durable(header.get("generation", 0)):
+                        done = True
+                    elif not checkpointer.closing:
+                        done = False
                 if done is False:  # resumed from HBM, but the predecessor's spill failed
                     journal("checkpoint-not-durable", "the predecessor's host copy failed; "
                             "no host checkpoint until this rank saves")

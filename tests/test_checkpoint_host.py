@@ -376,3 +376,15 @@ def test_close_stops_and_joins_a_durability_watcher(tmp_path):
     ck.close()
     assert time.monotonic() - t0 < 2
     assert not watcher.is_alive() and seen == [None]
+
+
+def test_durable_reports_a_complete_copy_of_a_generation(tmp_path):
+    state = {"w": torch.arange(5000, dtype=torch.float32)}
+    ck = Checkpointer(state, path=str(tmp_path / "spill"), tile_bytes=4096, slots=2)
+    assert not ck.durable(1)
+    ck.save({"step": 1})
+    gen = ck.header()["generation"]
+    assert ck.durable(gen) and not ck.durable(gen + 1)
+    ck.save({"step": 2})
+    assert ck.durable(gen) and ck.durable(gen + 1)
+    ck.close()
