@@ -1,0 +1,149 @@
+// Experiment: both directions of the PCIe link at once, with the finish time of each direction
+// measured on its own (sdma_copy.cpp's "bidir" line reports only the slower one).  The
+// overlapped bench (save streaming out while a restore streams back in) reaches ~63 GB/s out
+// and ~45-50 in (raw, TPZ1 0.80 on the wire); this isolates the link from the pipeline.
+//
+//   hipcc -O2 -std=c++17 scripts/exp/duplex.cpp -lhsa-runtime64 -o scripts/exp/duplex
+//   ./duplex [GiB]
+#include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+#include <sys/mman.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#define HIPCK(x)                                                \
+  do {                                                          \
+    hipError_t e_ = (x);                                        \
+    if (e_ != hipSuccess) {                                     \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));   \
+      exit(1);                                                  \
+    }                                                           \
+  } while (0)
+#define HSACK(x)                                                \
+  do {                                                          \
+    if ((x) != HSA_STATUS_SUCCESS) {                            \
+      fprintf(stderr, "%s failed\n", #x);                       \
+      exit(1);                                                  \
+    }                                                           \
+  } while (0)
+
+struct Agents {
+  uint32_t bdf = 0;
+  hsa_agent_t gpu{}, cpu{};
+  bool found = false;
+};
+
+static hsa_status_t find_gpu(hsa_agent_t a, void* data) {
+  Agents* g = (Agents*)data;
+  hsa_device_type_t t;
+  hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t);
+  if (t != HSA_DEVICE_TYPE_GPU) return HSA_STATUS_SUCCESS;
+  uint32_t bdf = 0;
+  hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
+  if (bdf == g->bdf) {
+    g->gpu = a;
+    hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_NEAREST_CPU, &g->cpu);
+    g->found = true;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+static double now() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+static void* pinned(size_t n, int fill) {
+  void* p = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (p == MAP_FAILED) exit(1);
+  madvise(p, n, MADV_HUGEPAGE);
+  memset(p, fill, n);
+  HIPCK(hipHostRegister(p, n, hipHostRegisterMapped | hipHostRegisterPortable));
+  return p;
+}
+
+int main(int argc, char** argv) {
+  const double gib = argc > 1 ? atof(argv[1]) : 2.0;
+  const size_t n = (size_t)(gib * (1ull << 30));
+  const size_t chunk = 256ull << 20;
+  HIPCK(hipSetDevice(0));
+  hipDeviceProp_t p;
+  HIPCK(hipGetDeviceProperties(&p, 0));
+  Agents ag;
+  ag.bdf = (uint32_t)((p.pciBusID << 8) | (p.pciDeviceID << 3));
+  HSACK(hsa_init());
+  HSACK(hsa_iterate_agents(find_gpu, &ag));
+  if (!ag.found) return 1;
+  void *dev_out, *dev_in;
+  HIPCK(hipMalloc(&dev_out, n));
+  HIPCK(hipMalloc(&dev_in, n));
+  HIPCK(hipMemset(dev_out, 7, n));
+  void* host_out = pinned(n, 1);
+  void* host_in = pinned(n, 3);
+  void *hd_out, *hd_in;
+  HIPCK(hipHostGetDevicePointer(&hd_out, host_out, 0));
+  HIPCK(hipHostGetDevicePointer(&hd_in, host_in, 0));
+  hipStream_t s;
+  HIPCK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  hipEvent_t ev;
+  HIPCK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  hsa_signal_t so, si;
+  HSACK(hsa_signal_create(1, 0, nullptr, &so));
+  HSACK(hsa_signal_create(1, 0, nullptr, &si));
+  const size_t nch = (n + chunk - 1) / chunk;
+
+  // out: D2H on SDMA engine `de` (0 = none); in: H2D on SDMA engine `he`, or via
+  // hipMemcpyAsync when he == 0 (what the restore uses), or none when he < 0.
+  auto run = [&](uint32_t de, int he, const char* label) {
+    double to_sum = 0, ti_sum = 0;
+    const int reps = 4;
+    for (int r = -1; r < reps; ++r) {
+      hsa_signal_store_relaxed(so, de ? (hsa_signal_value_t)nch : 0);
+      hsa_signal_store_relaxed(si, he > 0 ? (hsa_signal_value_t)nch : 0);
+      const double t0 = now();
+      for (size_t j = 0; j < nch; ++j) {
+        const size_t off = j * chunk, len = n - off < chunk ? n - off : chunk;
+        if (de)
+          HSACK(hsa_amd_memory_async_copy_on_engine((char*)hd_out + off, ag.cpu,
+                                                    (char*)dev_out + off, ag.gpu, len, 0,
+                                                    nullptr, so, (hsa_amd_sdma_engine_id_t)de,
+                                                    true));
+        if (he > 0)
+          HSACK(hsa_amd_memory_async_copy_on_engine((char*)dev_in + off, ag.gpu,
+                                                    (char*)hd_in + off, ag.cpu, len, 0, nullptr,
+                                                    si, (hsa_amd_sdma_engine_id_t)he, true));
+        else if (he == 0)
+          HIPCK(hipMemcpyAsync((char*)dev_in + off, (char*)host_in + off, len,
+                               hipMemcpyHostToDevice, s));
+      }
+      if (he == 0) HIPCK(hipEventRecord(ev, s));
+      double t_out = de ? 0 : t0, t_in = he < 0 ? t0 : 0;
+      while (!t_out || !t_in) {
+        if (!t_out && hsa_signal_load_scacquire(so) < 1) t_out = now();
+        if (!t_in) {
+          if (he > 0 ? hsa_signal_load_scacquire(si) < 1 : hipEventQuery(ev) == hipSuccess)
+            t_in = now();
+        }
+      }
+      if (r >= 0) {
+        to_sum += t_out - t0;
+        ti_sum += t_in - t0;
+      }
+    }
+    printf("%-44s out %6.1f GB/s  in %6.1f GB/s\n", label,
+           de ? reps * n / to_sum / 1e9 : 0.0, he >= 0 ? reps * n / ti_sum / 1e9 : 0.0);
+  };
+  run(0x4, -1, "D2H engine 2 alone");
+  run(0, 0, "H2D hipMemcpyAsync alone");
+  run(0, 0x2, "H2D engine 1 alone");
+  run(0x4, 0, "D2H engine 2 + H2D hipMemcpyAsync");
+  run(0x4, 0x2, "D2H engine 2 + H2D engine 1");
+  run(0x8, 0x2, "D2H engine 3 + H2D engine 1");
+  run(0x4, 0x1, "D2H engine 2 + H2D engine 0");
+  run(0x2, 0x8, "D2H engine 1 + H2D engine 3");
+  return 0;
+}
