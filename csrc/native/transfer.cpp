@@ -99,6 +99,7 @@ struct FileJob {
 struct Piece {
   FileJob* job;
   uint64_t off, len;
+  uint64_t index;  // piece number within its file
 };
 
 bool copy_range(int in, int out, uint64_t off, uint64_t len, std::string& err) {
@@ -218,14 +219,18 @@ TransferStats copy_dir(const std::string& src, const std::string& dst, const Fil
     if (cloned) stats.cloned++;
     j->pieces_left = (int)n;
     for (uint64_t k = 0; k < n; ++k)
-      pieces.push_back({j.get(), k * piece_bytes, std::min(piece_bytes, e.size - k * piece_bytes)});
+      pieces.push_back(
+          {j.get(), k * piece_bytes, std::min(piece_bytes, e.size - k * piece_bytes), k});
     stats.files++;
     stats.bytes += e.size;
     jobs.push_back(std::move(j));
   }
-  // Largest pieces first keeps the pool busy until the end.
-  std::stable_sort(pieces.begin(), pieces.end(),
-                   [](const Piece& a, const Piece& b) { return a.len > b.len; });
+  // Round-robin over files (every file's first piece, then every second piece, ...): writers
+  // of one file serialise on its inode lock, so threads working side by side should be on
+  // different files.  Within a round, largest pieces first keeps the pool busy to the end.
+  std::stable_sort(pieces.begin(), pieces.end(), [](const Piece& a, const Piece& b) {
+    return a.index != b.index ? a.index < b.index : a.len > b.len;
+  });
   std::atomic<size_t> next{0};
   auto worker = [&] {
     for (;;) {

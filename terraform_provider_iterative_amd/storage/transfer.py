@@ -73,6 +73,18 @@ def _local_path(remote: str) -> str:
     return conn.local_path()
 
 
+def _copy_threads() -> int:
+    """``TPI_PUSH_THREADS``, else one per CPU this process may run on, 8-16."""
+    env = os.environ.get("TPI_PUSH_THREADS")
+    if env:
+        return max(1, int(env))
+    try:
+        cpus = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        cpus = os.cpu_count() or 8
+    return max(8, min(16, cpus))
+
+
 def transfer(source: str, destination: str, exclude: Optional[Iterable[str]] = None,
              rules: Optional[List[str]] = None, threads: int = 0) -> Dict:
     """Copy ``source`` -> ``destination`` with filter rules (``storage.go:123-159``).
@@ -86,9 +98,10 @@ def transfer(source: str, destination: str, exclude: Optional[Iterable[str]] = N
     entries = native().walk(src, flt)
     files = [e for e in entries if not e[4]]
     log.info("Transferring %s (%d files)...", human_size(sum(e[1] for e in files)), len(files))
-    # 8 threads x 256 MiB copy_file_range pieces measured best on the MI355X box (23 GB/s for
-    # a 10 GB workdir; 16 x 64 MiB: 15.6 GB/s, inode-lock contention within files)
-    stats = native().copy_dir(src, dst, flt, threads or 8, 256 << 20)
+    # 256 MiB copy_file_range pieces, handed out round-robin over files (writers of one file
+    # serialise on its inode lock).  A copy into tmpfs / the page cache is bound per thread by
+    # page allocation + memcpy (~2-3 GB/s), so it scales with the threads the task may use.
+    stats = native().copy_dir(src, dst, flt, threads or _copy_threads(), 256 << 20)
     log.debug("transfer %s -> %s: %s", src, dst, stats)
     return stats
 
