@@ -61,6 +61,8 @@
 
 #include <algorithm>
 #include <fstream>
+#include <map>
+#include <set>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -414,44 +416,70 @@ class Supervisor {
   double next_memory_check_ = 0, next_disk_check_ = 0;
 
   // ---- machine-type limits -------------------------------------------------------------------
-  // Host memory of a process group: the resident set of each member (/proc/<pid>/statm, O(1)
-  // per process from the kernel's counters -- smaps_rollup's proportional set size would walk
-  // the page tables of a 100 GB pinned spill on every sample and stall this event loop).
-  // Pages shared inside the group (forked workers) count once per member.
-  static uint64_t group_memory_kb(pid_t pgid) {
+  // Host memory of the ranks' process groups, from one pass over /proc.  The resident set
+  // (/proc/<pid>/statm) is O(1) per process but counts pages shared inside a group (forked
+  // data-loader workers, a spill region mapped twice) once per member, so it is an upper bound.
+  // Only a group whose bound is over its limit pays for the proportional set size
+  // (smaps_rollup walks the page tables: tens of ms for a 100 GB pinned spill), which splits
+  // shared pages between their users and decides the OOM kill.
+  static bool read_small(const char* path, char* buf, size_t cap) {
+    int fd = open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return false;
+    ssize_t n = read(fd, buf, cap - 1);
+    close(fd);
+    if (n <= 0) return false;
+    buf[n] = 0;
+    return true;
+  }
+
+  struct GroupMemory {
+    uint64_t rss_kb = 0;
+    std::vector<long> pids;
+  };
+
+  static std::map<long, GroupMemory> groups_memory(const std::set<long>& pgids) {
     static const uint64_t page_kb = (uint64_t)sysconf(_SC_PAGESIZE) / 1024;
-    uint64_t total = 0;
+    std::map<long, GroupMemory> out;
     DIR* d = opendir("/proc");
-    if (!d) return 0;
+    if (!d) return out;
     while (struct dirent* e = readdir(d)) {
       char* end = nullptr;
       long pid = strtol(e->d_name, &end, 10);
       if (!end || *end || pid <= 0) continue;
       char path[64], buf[512];
       snprintf(path, sizeof(path), "/proc/%ld/stat", pid);
-      int fd = open(path, O_RDONLY | O_CLOEXEC);
-      if (fd < 0) continue;
-      ssize_t n = read(fd, buf, sizeof(buf) - 1);
-      close(fd);
-      if (n <= 0) continue;
-      buf[n] = 0;
+      if (!read_small(path, buf, sizeof(buf))) continue;
       const char* rp = strrchr(buf, ')');
-      long pgrp = 0;
+      long pgrp = 0, ppid = 0;
       char state = 0;
-      long ppid = 0;
-      if (!rp || sscanf(rp + 1, " %c %ld %ld", &state, &ppid, &pgrp) != 3 || pgrp != (long)pgid)
+      if (!rp || sscanf(rp + 1, " %c %ld %ld", &state, &ppid, &pgrp) != 3 || !pgids.count(pgrp))
         continue;
       snprintf(path, sizeof(path), "/proc/%ld/statm", pid);
-      fd = open(path, O_RDONLY | O_CLOEXEC);
-      if (fd < 0) continue;
-      n = read(fd, buf, sizeof(buf) - 1);
-      close(fd);
-      if (n <= 0) continue;
-      buf[n] = 0;
+      if (!read_small(path, buf, sizeof(buf))) continue;
       unsigned long long size = 0, resident = 0;
-      if (sscanf(buf, "%llu %llu", &size, &resident) == 2) total += resident * page_kb;
+      if (sscanf(buf, "%llu %llu", &size, &resident) != 2) continue;
+      GroupMemory& g = out[pgrp];
+      g.rss_kb += resident * page_kb;
+      g.pids.push_back(pid);
     }
     closedir(d);
+    return out;
+  }
+
+  static uint64_t pss_kb(const std::vector<long>& pids) {
+    uint64_t total = 0;
+    for (long pid : pids) {
+      std::ifstream in("/proc/" + std::to_string(pid) + "/smaps_rollup");
+      std::string key;
+      uint64_t value;
+      while (in >> key) {
+        if (key == "Pss:" && in >> value) {
+          total += value;
+          break;
+        }
+        in.ignore(1 << 20, '\n');
+      }
+    }
     return total;
   }
 
@@ -469,9 +497,15 @@ class Supervisor {
   void check_limits(double t) {
     if (s_.rank_memory_kb && t >= next_memory_check_) {
       next_memory_check_ = t + s_.memory_interval;
+      std::set<long> pgids;
+      for (auto& r : ranks_)
+        if (r.state == Rank::RUNNING && r.pid > 0 && !r.killed) pgids.insert(r.pid);
+      const auto groups = pgids.empty() ? std::map<long, GroupMemory>() : groups_memory(pgids);
       for (auto& r : ranks_) {
         if (r.state != Rank::RUNNING || r.pid <= 0 || r.killed) continue;
-        const uint64_t kb = group_memory_kb(r.pid);
+        auto g = groups.find(r.pid);
+        if (g == groups.end() || g->second.rss_kb <= s_.rank_memory_kb) continue;
+        const uint64_t kb = pss_kb(g->second.pids);
         if (kb <= s_.rank_memory_kb) continue;
         // like a container OOM kill: no grace, the rank fails (no respawn)
         r.reason = TermReason::OOM;

@@ -241,3 +241,24 @@ def test_limit_mode_caps_affinity_to_the_machine_cores(tmp_path, monkeypatch):
     for s in sets:
         assert len(s) == min(2, len(available)) or s == available, sets
     task.delete()
+
+
+def test_memory_shared_with_forked_workers_counts_once(tmp_path):
+    """machine 1-400 (400 MB): a rank touches 250 MB and forks three workers that share those
+    pages copy-on-write.  Their resident sets add up to ~1 GB, over the limit, but the
+    proportional set size that decides the kill counts the shared pages once: no OOM."""
+    cloud = _cloud(tmp_path, "local")
+    script = ("#!%s\nimport os, time\nx = bytearray(250 << 20)\nfor i in range(0, len(x), 4096):\n"
+              "    x[i] = 1\nkids = []\nfor _ in range(3):\n    pid = os.fork()\n"
+              "    if pid == 0:\n        time.sleep(2.5)\n        os._exit(0)\n"
+              "    kids.append(pid)\n"
+              "print('up', flush=True)\ntime.sleep(2.5)\n"
+              "for k in kids:\n    os.waitpid(k, 0)\nprint('survived', flush=True)\n"
+              % sys.executable)
+    task = _task(cloud, "shared", script, machine="1-400")
+    task.create()
+    status = task.wait(30)
+    assert status["succeeded"] == 1, (status, task.logs())
+    assert "survived" in "".join(task.logs())
+    assert "rank-oom-killed" not in [e.code for e in task.events()]
+    task.delete()
