@@ -54,8 +54,11 @@ def version() -> str:
 
 
 def _digest(cmd: Sequence[str], deps: Sequence[str]) -> str:
+    # Paths inside the tree are hashed relative to it: a copy of the tree elsewhere (a GPU
+    # box runs a snapshot from a scratch directory) keeps its stamps valid instead of
+    # recompiling everything on first use.
     h = hashlib.sha256()
-    h.update("\0".join(c for c in cmd if ".tmp." not in c).encode())
+    h.update("\0".join(c.replace(ROOT, "@ROOT@") for c in cmd if ".tmp." not in c).encode())
     for dep in sorted(set(deps)):
         h.update(b"\0" + os.path.relpath(dep, ROOT).encode() + b"\0")
         with open(dep, "rb") as handle:

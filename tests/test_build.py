@@ -48,3 +48,29 @@ def test_version_everywhere():
     from terraform_provider_iterative_amd.utils import analytics
 
     assert analytics.VERSION == __version__
+
+
+def test_stamps_survive_moving_the_tree(tmp_path):
+    """A GPU box runs a snapshot of the tree from a scratch directory: the stamps built here
+    must still match there, or the first use on every box recompiles (libtpi_hip: minutes)."""
+    import shutil
+
+    _build.build_native()
+    _build.build_supervisor()
+    copy = tmp_path / "elsewhere"
+    shutil.copytree(os.path.join(ROOT, "csrc"), copy / "csrc")
+    shutil.copytree(os.path.join(ROOT, "terraform_provider_iterative_amd"),
+                    copy / "terraform_provider_iterative_amd",
+                    ignore=shutil.ignore_patterns("__pycache__"))
+    code = ("from terraform_provider_iterative_amd import _build as b\n"
+            "import pybind11, sysconfig\n"
+            "assert b.ROOT == %r, b.ROOT\n"
+            "srcs = b._sources('supervisor/*.cpp')\n"
+            "cmd = [__import__('os').environ.get('CXX', 'g++'), '-O2', '-std=c++17', '-Wall', "
+            "'-pthread', b._define_version(), *srcs, '-o', '@OUT@']\n"
+            "assert not b._stale(b.SUPERVISOR, cmd, srcs + b._sources('supervisor/*.h'))\n"
+            "import time; t = time.time(); b.build_native(); b.build_supervisor()\n"
+            "assert time.time() - t < 2, 'rebuilt'\n" % str(copy))
+    res = subprocess.run([sys.executable, "-c", code], cwd=str(copy), capture_output=True,
+                         text=True, timeout=120)
+    assert res.returncode == 0, res.stderr
