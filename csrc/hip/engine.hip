@@ -203,6 +203,7 @@ struct tpi_engine {
   void* d_meta = nullptr;
   uint32_t* d_csize = nullptr;
   uint64_t* d_coff = nullptr;
+  uint64_t* h_coff = nullptr;  // pinned: per-chunk slices go up asynchronously (restore_stream)
   size_t z_cap = 0;
   // host region registered window by window (tpi_host_pin_start): host copies are split at
   // window boundaries and wait until their window is pinned (tpi_engine_set_host_region)
@@ -512,6 +513,7 @@ void tpi_engine_destroy(tpi_engine* e) {
   if (e->d_count) (void)hipFree(e->d_count);
   for (void* p : {e->zraw, e->d_meta, (void*)e->d_csize, (void*)e->d_coff})
     if (p) (void)hipFree(p);
+  if (e->h_coff) (void)hipHostFree(e->h_coff);
   if (e->compute) (void)hipStreamDestroy(e->compute);
   if (e->copy) (void)hipStreamDestroy(e->copy);
   delete e;
@@ -791,9 +793,15 @@ int prepare_codec(tpi_engine* e, uint64_t ntiles) {
   if (ntiles + 1 > e->z_cap) {
     if (e->d_csize) HIP_OK(hipFree(e->d_csize));
     if (e->d_coff) HIP_OK(hipFree(e->d_coff));
-    e->z_cap = std::max<size_t>(ntiles + 1, 1024);
-    HIP_OK(hipMalloc(&e->d_csize, e->z_cap * sizeof(uint32_t)));
-    HIP_OK(hipMalloc(&e->d_coff, e->z_cap * sizeof(uint64_t)));
+    if (e->h_coff) HIP_OK(hipHostFree(e->h_coff));
+    e->d_csize = nullptr;
+    e->d_coff = e->h_coff = nullptr;
+    e->z_cap = 0;
+    const size_t cap = std::max<size_t>(ntiles + 1, 1024);
+    HIP_OK(hipMalloc(&e->d_csize, cap * sizeof(uint32_t)));
+    HIP_OK(hipMalloc(&e->d_coff, cap * sizeof(uint64_t)));
+    HIP_OK(hipHostMalloc(&e->h_coff, cap * sizeof(uint64_t), hipHostMallocDefault));
+    e->z_cap = cap;
   }
   return 0;
 }
@@ -972,8 +980,9 @@ int tpi_restore_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total,
   const uint64_t ntiles = (total + tile - 1) / tile;
   if (prepare_codec(e, ntiles)) return -1;
   e->hash_valid = false;
-  // Blob offsets; a size that cannot come from the encoder means a corrupt index.
-  std::vector<uint64_t> coff(ntiles + 1, 0);
+  // Blob offsets (pinned); a size that cannot come from the encoder means a corrupt index.
+  uint64_t* coff = e->h_coff;
+  coff[0] = 0;
   for (uint64_t i = 0; i < ntiles; ++i) {
     const uint64_t tl = std::min(tile, total - i * tile);
     if (csizes[i] < TPZ_HDR || csizes[i] > tpz_bound(tl) || csizes[i] % 16)
@@ -989,8 +998,8 @@ int tpi_restore_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total,
   }
   HIP_OK(region_copy(e, e->d_crcs, crcs, ntiles * sizeof(uint32_t), hipMemcpyHostToDevice,
                         e->compute));
-  HIP_OK(region_copy(e, e->d_coff, coff.data(), (ntiles + 1) * sizeof(uint64_t),
-                        hipMemcpyHostToDevice, e->compute));
+  HIP_OK(hipMemcpyAsync(e->d_coff, coff, (ntiles + 1) * sizeof(uint64_t), hipMemcpyHostToDevice,
+                        e->compute));
   HIP_OK(region_copy(e, e->d_bad, bad_init, sizeof(bad_init), hipMemcpyHostToDevice,
                         e->compute));
   HIP_OK(hipEventRecord(e->ev_wait, e->compute));
@@ -1297,7 +1306,15 @@ int tpi_restore_stream(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total
   }
   HIP_OK(region_copy(e, e->d_bad, bad_init, sizeof(bad_init), hipMemcpyHostToDevice,
                      e->compute));
-  std::vector<uint64_t> coff(ntiles + 1, 0);
+  // blob offsets: pinned, so each chunk's slice goes up asynchronously (a pageable source
+  // made every per-chunk copy wait for the copy stream to drain: ~1 ms of idle link a chunk)
+  uint64_t* coff = zipped ? e->h_coff : nullptr;
+  std::vector<uint64_t> raw_coff;
+  if (!zipped) {
+    raw_coff.assign(ntiles + 1, 0);
+    coff = raw_coff.data();
+  }
+  coff[0] = 0;
   const uint8_t* src = (const uint8_t*)host_src;
   uint64_t nchunks = 0;
   for (uint64_t base = 0, k = 0; base < total; base += e->chunk, ++k) {
@@ -1326,7 +1343,7 @@ int tpi_restore_stream(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total
     // are disjoint (the shared boundary offset is rewritten with the same value)
     if (k >= (uint64_t)e->nbuf) HIP_OK(hipStreamWaitEvent(e->copy, e->ev_b[b], 0));
     if (zipped)
-      HIP_OK(hipMemcpyAsync(e->d_coff + t0i, coff.data() + t0i, (nt + 1) * sizeof(uint64_t),
+      HIP_OK(hipMemcpyAsync(e->d_coff + t0i, coff + t0i, (nt + 1) * sizeof(uint64_t),
                             hipMemcpyHostToDevice, e->copy));
     HIP_OK(region_copy(e, e->d_crcs + t0i, crcs + t0i, nt * sizeof(uint32_t),
                        hipMemcpyHostToDevice, e->copy));

@@ -4,11 +4,15 @@
 // and ~45-50 in (raw, TPZ1 0.80 on the wire); this isolates the link from the pipeline.
 //
 //   hipcc -O2 -std=c++17 scripts/exp/duplex.cpp -lhsa-runtime64 -o scripts/exp/duplex
-//   ./duplex [GiB]
+//   ./duplex [GiB] [thp|shm]
 #include <hip/hip_runtime.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
+#include <fcntl.h>
 #include <sys/mman.h>
+#include <unistd.h>
+#include <string>
+#include <thread>
 
 #include <chrono>
 #include <cstdio>
@@ -57,8 +61,24 @@ static double now() {
       .count();
 }
 
+// kind "thp": private anonymous memory with transparent huge pages; "shm": a /dev/shm file
+// mapping (what a spill region shared with a successor process is: 4 KiB pages unless the
+// kernel enables shmem THP)
+static std::string g_kind = "thp";
+
 static void* pinned(size_t n, int fill) {
-  void* p = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  void* p;
+  if (g_kind == "shm") {
+    char name[64];
+    snprintf(name, sizeof(name), "/dev/shm/duplex-%d-%d", (int)getpid(), fill);
+    int fd = open(name, O_RDWR | O_CREAT | O_TRUNC, 0600);
+    if (fd < 0 || ftruncate(fd, (off_t)n)) exit(1);
+    unlink(name);
+    p = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+  } else {
+    p = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  }
   if (p == MAP_FAILED) exit(1);
   madvise(p, n, MADV_HUGEPAGE);
   memset(p, fill, n);
@@ -68,6 +88,8 @@ static void* pinned(size_t n, int fill) {
 
 int main(int argc, char** argv) {
   const double gib = argc > 1 ? atof(argv[1]) : 2.0;
+  if (argc > 2) g_kind = argv[2];
+  printf("host memory: %s\n", g_kind.c_str());
   const size_t n = (size_t)(gib * (1ull << 30));
   const size_t chunk = 256ull << 20;
   HIPCK(hipSetDevice(0));
@@ -137,6 +159,58 @@ int main(int argc, char** argv) {
     printf("%-44s out %6.1f GB/s  in %6.1f GB/s\n", label,
            de ? reps * n / to_sum / 1e9 : 0.0, he >= 0 ? reps * n / ti_sum / 1e9 : 0.0);
   };
+  // "chase": what the overlapped bench does -- the H2D of chunk j reads the bytes the D2H of
+  // chunk j just wrote into the same host buffer, as soon as that copy has completed.
+  auto chase = [&](uint32_t de, int he, const char* label) {
+    double to_sum = 0, ti_sum = 0;
+    const int reps = 4;
+    for (int r = -1; r < reps; ++r) {
+      hsa_signal_store_relaxed(so, (hsa_signal_value_t)nch);
+      hsa_signal_store_relaxed(si, he > 0 ? (hsa_signal_value_t)nch : 0);
+      const double t0 = now();
+      double t_in = 0;
+      std::thread reader([&] {
+        for (size_t j = 0; j < nch; ++j) {
+          const size_t off = j * chunk, len = n - off < chunk ? n - off : chunk;
+          while (hsa_signal_load_scacquire(so) > (hsa_signal_value_t)(nch - j - 1)) {
+          }
+          if (he > 0)
+            HSACK(hsa_amd_memory_async_copy_on_engine((char*)dev_in + off, ag.gpu,
+                                                      (char*)hd_out + off, ag.cpu, len, 0,
+                                                      nullptr, si, (hsa_amd_sdma_engine_id_t)he,
+                                                      true));
+          else
+            HIPCK(hipMemcpyAsync((char*)dev_in + off, (char*)host_out + off, len,
+                                 hipMemcpyHostToDevice, s));
+        }
+        if (he > 0) {
+          while (hsa_signal_load_scacquire(si) >= 1) {
+          }
+        } else {
+          HIPCK(hipStreamSynchronize(s));
+        }
+        t_in = now();
+      });
+      for (size_t j = 0; j < nch; ++j) {
+        const size_t off = j * chunk, len = n - off < chunk ? n - off : chunk;
+        HSACK(hsa_amd_memory_async_copy_on_engine((char*)hd_out + off, ag.cpu,
+                                                  (char*)dev_out + off, ag.gpu, len, 0, nullptr,
+                                                  so, (hsa_amd_sdma_engine_id_t)de, true));
+      }
+      while (hsa_signal_load_scacquire(so) >= 1) {
+      }
+      const double t_out = now();
+      reader.join();
+      if (r >= 0) {
+        to_sum += t_out - t0;
+        ti_sum += t_in - t0;
+      }
+    }
+    printf("%-44s out %6.1f GB/s  in %6.1f GB/s (in: from its own start)\n", label,
+           reps * n / to_sum / 1e9, reps * n / ti_sum / 1e9);
+  };
+  chase(0x4, 0, "chase: D2H engine 2 -> H2D hipMemcpyAsync");
+  chase(0x4, 0x2, "chase: D2H engine 2 -> H2D engine 1");
   run(0x4, -1, "D2H engine 2 alone");
   run(0, 0, "H2D hipMemcpyAsync alone");
   run(0, 0x2, "H2D engine 1 alone");
