@@ -1338,15 +1338,17 @@ int tpi_restore_stream(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total
       cbeg = coff[t0i];
       cend = coff[t0i + nt];
     }
-    // the chunk's CRCs (and blob offsets) go up on the copy stream ahead of its bytes, so the
-    // kernels that wait for the bytes (copied[b]) see them too; slices of different chunks
-    // are disjoint (the shared boundary offset is rewritten with the same value)
-    if (k >= (uint64_t)e->nbuf) HIP_OK(hipStreamWaitEvent(e->copy, e->ev_b[b], 0));
+    // The chunk's CRCs (and blob offsets) go up on the compute stream, ahead of the kernels
+    // that read them.  Copies this small run as blit kernels: queued between two SDMA copies
+    // on the copy stream, each engine hand-off left the link idle ~1 ms per chunk (rocprofv3
+    // memory-copy trace of bench.py).  Slices of different chunks are disjoint (the shared
+    // boundary offset is rewritten with the same value).
     if (zipped)
       HIP_OK(hipMemcpyAsync(e->d_coff + t0i, coff + t0i, (nt + 1) * sizeof(uint64_t),
-                            hipMemcpyHostToDevice, e->copy));
+                            hipMemcpyHostToDevice, e->compute));
     HIP_OK(region_copy(e, e->d_crcs + t0i, crcs + t0i, nt * sizeof(uint32_t),
-                       hipMemcpyHostToDevice, e->copy));
+                       hipMemcpyHostToDevice, e->compute));
+    if (k >= (uint64_t)e->nbuf) HIP_OK(hipStreamWaitEvent(e->copy, e->ev_b[b], 0));
     HIP_OK(region_copy(e, e->staging[b], src + cbeg, cend - cbeg, hipMemcpyHostToDevice,
                        e->copy));
     HIP_OK(hipEventRecord(e->ev_a[b], e->copy));
