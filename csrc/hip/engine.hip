@@ -179,6 +179,11 @@ struct tpi_engine {
   uint64_t chunk = 0, tile = 0;
   int nbuf = 0;
   hipStream_t compute = nullptr, copy = nullptr;
+  // streamed restore: the per-chunk CRC / blob-offset uploads.  A small host -> device copy
+  // does not return before its stream has reached it, so on the copy or compute stream it
+  // held the issuing thread -- and the next chunk's H2D -- behind the previous chunk's work.
+  hipStream_t aux = nullptr;
+  std::vector<hipEvent_t> ev_c;  // aux uploads of staging slot b done
   std::vector<void*> staging;
   std::vector<hipEvent_t> ev_a, ev_b;  // save: packed/copied; restore: copied/unpacked
   hipEvent_t ev_wait = nullptr, ev_done = nullptr;
@@ -462,12 +467,17 @@ tpi_engine* tpi_engine_create(int device, uint64_t chunk_bytes, int nbuf, uint64
     return bail("hipStreamCreate(compute)", err);
   if ((err = hipStreamCreateWithFlags(&e->copy, hipStreamNonBlocking)) != hipSuccess)
     return bail("hipStreamCreate(copy)", err);
+  if ((err = hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking)) != hipSuccess)
+    return bail("hipStreamCreate(aux)", err);
   // staging chunks also hold TPZ1 blobs: worst case tpz_bound() per tile
   const uint64_t staging_bytes = chunk_bytes + (chunk_bytes / tile_bytes) * (TPZ_HDR + 128);
   e->staging.assign(nbuf, nullptr);
   e->ev_a.assign(nbuf, nullptr);
   e->ev_b.assign(nbuf, nullptr);
+  e->ev_c.assign(nbuf, nullptr);
   for (int i = 0; i < nbuf; ++i) {
+    if ((err = hipEventCreateWithFlags(&e->ev_c[i], hipEventDisableTiming)) != hipSuccess)
+      return bail("hipEventCreate", err);
     if ((err = hipMalloc(&e->staging[i], staging_bytes)) != hipSuccess)
       return bail("hipMalloc(staging)", err);
     if ((err = hipEventCreateWithFlags(&e->ev_a[i], hipEventDisableTiming)) != hipSuccess)
@@ -495,12 +505,15 @@ void tpi_engine_destroy(tpi_engine* e) {
   (void)hipSetDevice(e->device);
   if (e->compute) (void)hipStreamSynchronize(e->compute);
   if (e->copy) (void)hipStreamSynchronize(e->copy);
+  if (e->aux) (void)hipStreamSynchronize(e->aux);
   tpi_sdma_close(e->sdma);  // waits for copies still in flight
   for (void* p : e->staging)
     if (p) (void)hipFree(p);
   for (hipEvent_t ev : e->ev_a)
     if (ev) (void)hipEventDestroy(ev);
   for (hipEvent_t ev : e->ev_b)
+    if (ev) (void)hipEventDestroy(ev);
+  for (hipEvent_t ev : e->ev_c)
     if (ev) (void)hipEventDestroy(ev);
   if (e->ev_wait) (void)hipEventDestroy(e->ev_wait);
   if (e->ev_done) (void)hipEventDestroy(e->ev_done);
@@ -516,6 +529,7 @@ void tpi_engine_destroy(tpi_engine* e) {
   if (e->h_coff) (void)hipHostFree(e->h_coff);
   if (e->compute) (void)hipStreamDestroy(e->compute);
   if (e->copy) (void)hipStreamDestroy(e->copy);
+  if (e->aux) (void)hipStreamDestroy(e->aux);
   delete e;
 }
 
@@ -1324,6 +1338,7 @@ int tpi_restore_stream(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total
     if (wait_published(words, t0i + nt, timeout_s)) {
       // leave no copy or kernel of the chunks already issued running past this call
       (void)hipStreamSynchronize(e->copy);
+      (void)hipStreamSynchronize(e->aux);
       (void)hipStreamSynchronize(e->compute);
       return -1;
     }
@@ -1338,20 +1353,23 @@ int tpi_restore_stream(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total
       cbeg = coff[t0i];
       cend = coff[t0i + nt];
     }
-    // The chunk's CRCs (and blob offsets) go up on the compute stream, ahead of the kernels
-    // that read them.  Copies this small run as blit kernels: queued between two SDMA copies
-    // on the copy stream, each engine hand-off left the link idle ~1 ms per chunk (rocprofv3
-    // memory-copy trace of bench.py).  Slices of different chunks are disjoint (the shared
-    // boundary offset is rewritten with the same value).
+    // The chunk's CRCs (and blob offsets) go up on their own stream (see tpi_engine::aux),
+    // which the kernels that read them wait for.  On the copy or compute stream these small
+    // copies held this thread until the previous chunk's H2D / kernels were done, leaving the
+    // link idle ~1 ms per chunk (rocprofv3 memory-copy trace of bench.py).  Slices of
+    // different chunks are disjoint (the shared boundary offset is rewritten with the same
+    // value).
     if (zipped)
       HIP_OK(hipMemcpyAsync(e->d_coff + t0i, coff + t0i, (nt + 1) * sizeof(uint64_t),
-                            hipMemcpyHostToDevice, e->compute));
+                            hipMemcpyHostToDevice, e->aux));
     HIP_OK(region_copy(e, e->d_crcs + t0i, crcs + t0i, nt * sizeof(uint32_t),
-                       hipMemcpyHostToDevice, e->compute));
+                       hipMemcpyHostToDevice, e->aux));
+    HIP_OK(hipEventRecord(e->ev_c[b], e->aux));
     if (k >= (uint64_t)e->nbuf) HIP_OK(hipStreamWaitEvent(e->copy, e->ev_b[b], 0));
     HIP_OK(region_copy(e, e->staging[b], src + cbeg, cend - cbeg, hipMemcpyHostToDevice,
                        e->copy));
     HIP_OK(hipEventRecord(e->ev_a[b], e->copy));
+    HIP_OK(hipStreamWaitEvent(e->compute, e->ev_c[b], 0));
     HIP_OK(hipStreamWaitEvent(e->compute, e->ev_a[b], 0));
     if (zipped) {
       HIP_OK(tpi_launch_tpz_decode(e->staging[b], e->d_coff + t0i, cbeg, len, tile, e->zraw,
