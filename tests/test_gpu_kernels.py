@@ -486,6 +486,50 @@ def test_streamed_restore_follows_the_writers_progress(codec, tmp_path):
     writer.close()
 
 
+@pytest.mark.parametrize("codec", ["none", "tpz1"])
+def test_restore_streams_behind_a_concurrent_save(codec, tmp_path):
+    """What bench.py's headline step does: a save streams into the host region while a
+    restore in another thread copies each published chunk back into other tensors (the
+    per-chunk CRC / blob-offset uploads on their own stream, staging slots reused)."""
+    import threading
+
+    from terraform_provider_iterative_amd.checkpoint import Checkpointer
+
+    g = torch.Generator().manual_seed(11)
+    src = {"a": torch.randn(3 << 20, generator=g).to(torch.bfloat16).cuda(),
+           "b": torch.randn(5 << 20, generator=g).mul(1e-3).cuda(),
+           "t": torch.randn(640, 1000, generator=g).cuda().t()}
+    dst = {k: torch.zeros_like(v) for k, v in src.items()}
+    dst["t"] = torch.zeros(640, 1000, device="cuda").t()
+    path = str(tmp_path / "spill")
+    kw = dict(tile_bytes=1 << 16, chunk_bytes=1 << 20, nbuf=2, codec=codec)
+    writer = Checkpointer(src, path=path, **kw)
+    reader = Checkpointer(dst, path=path, **kw)
+    for step in (1, 2):  # the second pass reuses every buffer of the first
+        box = {}
+
+        def restore():
+            try:
+                box["res"] = reader.restore(stream_timeout=20)
+            except BaseException as error:  # surfaced below
+                box["err"] = error
+
+        th = threading.Thread(target=restore)
+        writer.save({"step": step}, on_stream=th.start)
+        th.join(60)
+        assert "err" not in box, box.get("err")
+        assert box["res"].bad_tiles == 0
+        torch.cuda.synchronize()
+        for k in src:
+            assert torch.equal(dst[k], src[k]), (step, k)
+        for v in src.values():
+            v.mul_(-1)
+        for v in dst.values():
+            v.zero_()
+    reader.close()
+    writer.close()
+
+
 def test_streamed_restore_gives_up_on_a_stalled_writer(tmp_path):
     from terraform_provider_iterative_amd.checkpoint import CheckpointError, Checkpointer
     from terraform_provider_iterative_amd.checkpoint import checkpointer as ckmod
