@@ -364,6 +364,11 @@ def main(argv=None):
         if on_gpu:
             torch.cuda.empty_cache()
 
+    host_numa = None
+    if rank == 0 and ck.region is not None:  # which socket(s) the spill pages landed on
+        from terraform_provider_iterative_amd.checkpoint.host import numa_placement
+
+        host_numa = numa_placement(ck.region.addr, ck.region.size)
     elapsed = allmax(elapsed)
     save_max, restore_max = allmax(save_s), allmax(restore_s)
     total = ck.plan.total * world  # packed bytes per direction per step (all ranks)
@@ -407,6 +412,7 @@ def main(argv=None):
             "raw_GBps": None,
             "sequential": None,
             "rank0_cpu_affinity": len(pinned_cpus) if pinned_cpus else None,
+            "host_region_numa": host_numa,
             "restore_verified": verified,
             "save_async": None,
             "setup_s": round(setup_s, 2),

@@ -76,6 +76,13 @@ run_job() {
           --gpus $n --total-gb 8 --steps 2 --warmup 1 --broadcast-gb 0 $extra \
           > "$OUT/rehearse_n$n.json" 2> "$OUT/rehearse_n$n.log" || return 1
       done ;;
+    hostinfo) { for n in /sys/devices/system/node/node*; do
+                  echo "$(basename $n) cpus=$(cat $n/cpulist) $(grep -E 'MemTotal|MemFree|FilePages|Shmem:' $n/meminfo | awk '{printf "%s=%s%s ", $3, $4, $5}')"
+                done
+                grep -E 'MemTotal|MemAvailable|Shmem:|HugePages_Total|Hugepagesize' /proc/meminfo
+                echo "shmem THP: $(cat /sys/kernel/mm/transparent_hugepage/shmem_enabled 2>/dev/null)"
+                echo "anon THP: $(cat /sys/kernel/mm/transparent_hugepage/enabled 2>/dev/null)"
+                df -h /dev/shm /tmp; } > "$OUT/hostinfo.txt" 2>&1 ;;
     *) echo "unknown job: $job" >&2; return 2 ;;
   esac
 }

@@ -116,6 +116,44 @@ class HostRegion:
             pass
 
 
+def numa_placement(addr: int, size: int) -> Optional[Dict[str, object]]:
+    """Where the kernel put the pages of the mapping ``[addr, addr + size)``: bytes per NUMA
+    node and the page size, from ``/proc/self/numa_maps`` (None when unreadable).  The regions
+    are bound MPOL_PREFERRED to the GPU's socket, so a node short of free memory spills the
+    rest to the other socket, whose pages then cross the inter-socket link on every copy."""
+    try:
+        with open("/proc/self/numa_maps") as f:
+            lines = f.readlines()
+    except OSError:
+        return None
+    out: Dict[str, object] = {}
+    nodes: Dict[str, int] = {}
+    page_kb = 4
+    for line in lines:
+        fields = line.split()
+        try:
+            start = int(fields[0], 16)
+        except (IndexError, ValueError):
+            continue
+        if not (addr <= start < addr + size) or len(fields) < 2:
+            continue
+        out.setdefault("policy", fields[1])  # e.g. "prefer:0", "default"
+        counts = {}
+        for f in fields[2:]:
+            key, _, value = f.partition("=")
+            if key == "kernelpagesize_kB":
+                page_kb = int(value)
+            elif key.startswith("N") and key[1:].isdigit():
+                counts[key] = int(value)
+        for key, pages in counts.items():  # the page size comes last on the line
+            nodes[key] = nodes.get(key, 0) + pages * page_kb * 1024
+    if not nodes:
+        return None
+    out["bytes_per_node"] = nodes
+    out["page_kB"] = page_kb
+    return out
+
+
 # path -> (thread, result box) of regions being mapped + registered in the background
 _prefetched: Dict[str, Tuple[threading.Thread, dict]] = {}
 _prefetch_lock = threading.Lock()
