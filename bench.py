@@ -322,7 +322,7 @@ def main(argv=None):
     barrier()
 
     save_s = restore_s = 0.0
-    wire = 0
+    wire = split_chunks = 0
     t0 = time.perf_counter()
     for step in range(args.steps):
         if overlap and successor is not None:
@@ -330,6 +330,8 @@ def main(argv=None):
             for t in list(successor.values())[:2]:
                 t.zero_()
         wire, s_s, r_s, res = save_restore({"step": step})
+        if ck_in is not None and ck_in.engine is not None:  # duplex balancing of this step
+            split_chunks += ck_in.engine.split_chunks
         if res.bad_tiles:
             raise SystemExit("bench: %d corrupt tiles after restore" % res.bad_tiles)
         save_s += s_s
@@ -401,6 +403,9 @@ def main(argv=None):
             "save_GBps": round(total * args.steps / save_max / 1e9, 3),
             "restore_GBps": round(total * args.steps / restore_max / 1e9, 3),
             "restore_streams_behind_save": overlap,
+            # chunks of the timed restores whose H2D went over two copy streams (the restore
+            # trailed the save by TPI_H2D_SPLIT_LEAD chunks): the link's share moves to it
+            "restore_split_chunks": split_chunks if overlap else None,
             "per_gpu_save_GBps": round(ck.plan.total * args.steps / save_max / 1e9, 3),
             "per_gpu_restore_GBps": round(ck.plan.total * args.steps / restore_max / 1e9, 3),
             "wire_bytes_per_step": wire_total,

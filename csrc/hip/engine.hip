@@ -184,6 +184,13 @@ struct tpi_engine {
   // held the issuing thread -- and the next chunk's H2D -- behind the previous chunk's work.
   hipStream_t aux = nullptr;
   std::vector<hipEvent_t> ev_c;  // aux uploads of staging slot b done
+  // streamed restore, behind a save that shares the PCIe link: a chunk's H2D split over the
+  // copy stream and this one (HIP gives each stream its own SDMA engine) takes the larger share
+  // of a duplex link -- in/out 56/34 GB/s instead of 46/51 (profiles/duplex_split_round3.md)
+  hipStream_t copy2 = nullptr;
+  std::vector<hipEvent_t> ev_d;  // second half of staging slot b copied
+  uint64_t split_lead = 2;       // split once the restore trails the writer by this many chunks
+  uint64_t split_chunks = 0;     // chunks split by the last streamed restore
   std::vector<void*> staging;
   std::vector<hipEvent_t> ev_a, ev_b;  // save: packed/copied; restore: copied/unpacked
   hipEvent_t ev_wait = nullptr, ev_done = nullptr;
@@ -469,14 +476,21 @@ tpi_engine* tpi_engine_create(int device, uint64_t chunk_bytes, int nbuf, uint64
     return bail("hipStreamCreate(copy)", err);
   if ((err = hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking)) != hipSuccess)
     return bail("hipStreamCreate(aux)", err);
+  if ((err = hipStreamCreateWithFlags(&e->copy2, hipStreamNonBlocking)) != hipSuccess)
+    return bail("hipStreamCreate(copy2)", err);
+  if (const char* lead = getenv("TPI_H2D_SPLIT_LEAD"))  // "off": never split
+    e->split_lead = strcmp(lead, "off") == 0 ? ~0ull : strtoull(lead, nullptr, 10);
   // staging chunks also hold TPZ1 blobs: worst case tpz_bound() per tile
   const uint64_t staging_bytes = chunk_bytes + (chunk_bytes / tile_bytes) * (TPZ_HDR + 128);
   e->staging.assign(nbuf, nullptr);
   e->ev_a.assign(nbuf, nullptr);
   e->ev_b.assign(nbuf, nullptr);
   e->ev_c.assign(nbuf, nullptr);
+  e->ev_d.assign(nbuf, nullptr);
   for (int i = 0; i < nbuf; ++i) {
     if ((err = hipEventCreateWithFlags(&e->ev_c[i], hipEventDisableTiming)) != hipSuccess)
+      return bail("hipEventCreate", err);
+    if ((err = hipEventCreateWithFlags(&e->ev_d[i], hipEventDisableTiming)) != hipSuccess)
       return bail("hipEventCreate", err);
     if ((err = hipMalloc(&e->staging[i], staging_bytes)) != hipSuccess)
       return bail("hipMalloc(staging)", err);
@@ -506,6 +520,7 @@ void tpi_engine_destroy(tpi_engine* e) {
   if (e->compute) (void)hipStreamSynchronize(e->compute);
   if (e->copy) (void)hipStreamSynchronize(e->copy);
   if (e->aux) (void)hipStreamSynchronize(e->aux);
+  if (e->copy2) (void)hipStreamSynchronize(e->copy2);
   tpi_sdma_close(e->sdma);  // waits for copies still in flight
   for (void* p : e->staging)
     if (p) (void)hipFree(p);
@@ -514,6 +529,8 @@ void tpi_engine_destroy(tpi_engine* e) {
   for (hipEvent_t ev : e->ev_b)
     if (ev) (void)hipEventDestroy(ev);
   for (hipEvent_t ev : e->ev_c)
+    if (ev) (void)hipEventDestroy(ev);
+  for (hipEvent_t ev : e->ev_d)
     if (ev) (void)hipEventDestroy(ev);
   if (e->ev_wait) (void)hipEventDestroy(e->ev_wait);
   if (e->ev_done) (void)hipEventDestroy(e->ev_done);
@@ -530,12 +547,14 @@ void tpi_engine_destroy(tpi_engine* e) {
   if (e->compute) (void)hipStreamDestroy(e->compute);
   if (e->copy) (void)hipStreamDestroy(e->copy);
   if (e->aux) (void)hipStreamDestroy(e->aux);
+  if (e->copy2) (void)hipStreamDestroy(e->copy2);
   delete e;
 }
 
 uint64_t tpi_engine_tile_bytes(const tpi_engine* e) { return e->tile; }
 uint64_t tpi_engine_chunk_bytes(const tpi_engine* e) { return e->chunk; }
 uint32_t tpi_engine_d2h_engine(const tpi_engine* e) { return tpi_sdma_engine(e->sdma); }
+uint64_t tpi_engine_split_chunks(const tpi_engine* e) { return e->split_chunks; }
 
 }  // extern "C"
 
@@ -686,6 +705,7 @@ int tpi_restore(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, const
   if (signal_stream != TPI_NO_STREAM) HIP_OK(hipStreamWaitEvent((hipStream_t)signal_stream, e->ev_done, 0));
   HIP_OK(hipStreamSynchronize(e->compute));
   HIP_OK(hipStreamSynchronize(e->copy));
+  HIP_OK(hipStreamSynchronize(e->copy2));
   *bad_tiles = bad[0];
   *first_bad = bad[0] ? (int64_t)bad[1] : -1;
   if (stats) {
@@ -1044,6 +1064,7 @@ int tpi_restore_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total,
   if (signal_stream != TPI_NO_STREAM) HIP_OK(hipStreamWaitEvent((hipStream_t)signal_stream, e->ev_done, 0));
   HIP_OK(hipStreamSynchronize(e->compute));
   HIP_OK(hipStreamSynchronize(e->copy));
+  HIP_OK(hipStreamSynchronize(e->copy2));
   *bad_tiles = bad[0];
   *first_bad = bad[0] ? (int64_t)bad[1] : -1;
   if (stats) {
@@ -1331,6 +1352,9 @@ int tpi_restore_stream(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total
   coff[0] = 0;
   const uint8_t* src = (const uint8_t*)host_src;
   uint64_t nchunks = 0;
+  const uint64_t chunk_tiles = e->chunk / tile;
+  std::vector<bool> was_split(e->nbuf, false);
+  e->split_chunks = 0;
   for (uint64_t base = 0, k = 0; base < total; base += e->chunk, ++k) {
     const int b = (int)(k % e->nbuf);
     const uint64_t len = std::min(e->chunk, total - base);
@@ -1338,10 +1362,22 @@ int tpi_restore_stream(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total
     if (wait_published(words, t0i + nt, timeout_s)) {
       // leave no copy or kernel of the chunks already issued running past this call
       (void)hipStreamSynchronize(e->copy);
+      (void)hipStreamSynchronize(e->copy2);
       (void)hipStreamSynchronize(e->aux);
       (void)hipStreamSynchronize(e->compute);
       return -1;
     }
+    // How far the restore trails the writer.  The host may run at most nbuf chunks ahead of
+    // the copies (wait for chunk k - nbuf's H2D), so the chunks published past this one are
+    // the copies' real backlog.  A backlog of split_lead chunks means the save is taking the
+    // larger share of the link: split this chunk's H2D over two streams (two SDMA engines).
+    if (k >= (uint64_t)e->nbuf) {
+      HIP_OK(hipEventSynchronize(e->ev_a[b]));
+      if (was_split[b]) HIP_OK(hipEventSynchronize(e->ev_d[b]));
+    }
+    const uint64_t published = __atomic_load_n(&words[0], __ATOMIC_ACQUIRE);
+    const bool split = chunk_tiles > 0 && published >= t0i + nt && len >= (4ull << 20) &&
+                       (published - (t0i + nt)) / chunk_tiles >= e->split_lead;
     uint64_t cbeg = base, cend = base + len;
     if (zipped) {
       for (uint64_t i = t0i; i < t0i + nt; ++i) {
@@ -1366,9 +1402,20 @@ int tpi_restore_stream(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total
                        hipMemcpyHostToDevice, e->aux));
     HIP_OK(hipEventRecord(e->ev_c[b], e->aux));
     if (k >= (uint64_t)e->nbuf) HIP_OK(hipStreamWaitEvent(e->copy, e->ev_b[b], 0));
-    HIP_OK(region_copy(e, e->staging[b], src + cbeg, cend - cbeg, hipMemcpyHostToDevice,
+    // halves split on a 64 KiB boundary of the wire stream
+    const uint64_t mid = split ? cbeg + ((cend - cbeg) / 2 & ~0xFFFFull) : cend;
+    HIP_OK(region_copy(e, e->staging[b], src + cbeg, mid - cbeg, hipMemcpyHostToDevice,
                        e->copy));
     HIP_OK(hipEventRecord(e->ev_a[b], e->copy));
+    was_split[b] = mid < cend;
+    if (was_split[b]) {
+      if (k >= (uint64_t)e->nbuf) HIP_OK(hipStreamWaitEvent(e->copy2, e->ev_b[b], 0));
+      HIP_OK(region_copy(e, (uint8_t*)e->staging[b] + (mid - cbeg), src + mid, cend - mid,
+                         hipMemcpyHostToDevice, e->copy2));
+      HIP_OK(hipEventRecord(e->ev_d[b], e->copy2));
+      HIP_OK(hipStreamWaitEvent(e->compute, e->ev_d[b], 0));
+      ++e->split_chunks;
+    }
     HIP_OK(hipStreamWaitEvent(e->compute, e->ev_c[b], 0));
     HIP_OK(hipStreamWaitEvent(e->compute, e->ev_a[b], 0));
     if (zipped) {
@@ -1393,6 +1440,7 @@ int tpi_restore_stream(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total
     HIP_OK(hipStreamWaitEvent((hipStream_t)signal_stream, e->ev_done, 0));
   HIP_OK(hipStreamSynchronize(e->compute));
   HIP_OK(hipStreamSynchronize(e->copy));
+  HIP_OK(hipStreamSynchronize(e->copy2));
   *bad_tiles = bad[0];
   *first_bad = bad[0] ? (int64_t)bad[1] : -1;
   if (stats) {

@@ -75,6 +75,9 @@ uint64_t tpi_engine_chunk_bytes(const tpi_engine* e);
 // SDMA engine bit (hsa_amd_sdma_engine_id_t) that carries the engine's device -> host copies,
 // 0 when they run as HIP blit kernels (TPI_D2H_ENGINE=blit or no engine available).
 uint32_t tpi_engine_d2h_engine(const tpi_engine* e);
+// Chunks whose H2D the last tpi_restore_stream split over two copy streams (it trailed the
+// writer by TPI_H2D_SPLIT_LEAD chunks, default 2; "off" never splits).
+uint64_t tpi_engine_split_chunks(const tpi_engine* e);
 
 // Pack `segs` (n entries, sorted by off) into a stream of `total` bytes written to `host_dst`
 // (pinned or host-mapped).  `crcs_out` (host, ceil(total/tile) entries) receives the CRC32C of

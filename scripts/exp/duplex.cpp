@@ -56,6 +56,25 @@ static hsa_status_t find_gpu(hsa_agent_t a, void* data) {
   return HSA_STATUS_SUCCESS;
 }
 
+// Copy kernel for the "kernel" directions: every workgroup moves a contiguous 1 MiB slab with
+// dwordx4 loads/stores; reading host-mapped memory turns each load into a PCIe read request
+// issued by the CUs (many more outstanding reads than one SDMA engine keeps in flight).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_copy(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                              size_t n16) {
+  const size_t per = (1u << 20) / 16, b = (size_t)blockIdx.x * per;
+  const size_t e = b + per < n16 ? b + per : n16;
+  for (size_t i = b + threadIdx.x; i < e; i += 256 * 4) {
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i + u * 256 < e) v[u] = __builtin_nontemporal_load(src + i + u * 256);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i + u * 256 < e) __builtin_nontemporal_store(v[u], dst + i + u * 256);
+  }
+}
+
 static double now() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
       .count();
@@ -111,25 +130,36 @@ int main(int argc, char** argv) {
   HIPCK(hipHostGetDevicePointer(&hd_in, host_in, 0));
   hipStream_t s;
   HIPCK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  hipEvent_t ev;
+  hipStream_t s2, s3;
+  HIPCK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+  HIPCK(hipStreamCreateWithFlags(&s3, hipStreamNonBlocking));
+  hipEvent_t ev, ev2, ev3;
+  HIPCK(hipEventCreateWithFlags(&ev3, hipEventDisableTiming));
   HIPCK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  HIPCK(hipEventCreateWithFlags(&ev2, hipEventDisableTiming));
   hsa_signal_t so, si;
   HSACK(hsa_signal_create(1, 0, nullptr, &so));
   HSACK(hsa_signal_create(1, 0, nullptr, &si));
   const size_t nch = (n + chunk - 1) / chunk;
 
-  // out: D2H on SDMA engine `de` (0 = none); in: H2D on SDMA engine `he`, or via
-  // hipMemcpyAsync when he == 0 (what the restore uses), or none when he < 0.
+  // out: D2H on SDMA engine `de` (0 = none, KOUT = copy kernel); in: H2D on SDMA engine
+  // `he`, or via hipMemcpyAsync when he == 0 (what the restore uses), KIN = copy kernel,
+  // TWO = SDMA engines 0 and 1 taking alternate halves of each chunk, none when he == -1.
+  const uint32_t KOUT = 0x100;
+  const int KIN = -2, TWO = -3, HIP2 = -4;  // HIP2: hipMemcpyAsync halves on two streams
   auto run = [&](uint32_t de, int he, const char* label) {
     double to_sum = 0, ti_sum = 0;
     const int reps = 4;
     for (int r = -1; r < reps; ++r) {
-      hsa_signal_store_relaxed(so, de ? (hsa_signal_value_t)nch : 0);
-      hsa_signal_store_relaxed(si, he > 0 ? (hsa_signal_value_t)nch : 0);
+      hsa_signal_store_relaxed(so, de && de != KOUT ? (hsa_signal_value_t)nch : 0);
+      hsa_signal_store_relaxed(si, he > 0 ? (hsa_signal_value_t)nch : he == TWO ? (hsa_signal_value_t)(2 * nch) : 0);
       const double t0 = now();
       for (size_t j = 0; j < nch; ++j) {
         const size_t off = j * chunk, len = n - off < chunk ? n - off : chunk;
-        if (de)
+        if (de == KOUT)
+          hipLaunchKernelGGL(k_copy, dim3((unsigned)((len + (1u << 20) - 1) >> 20)), dim3(256), 0, s2,
+                             (const u32x4*)((char*)dev_out + off), (u32x4*)((char*)hd_out + off), len / 16);
+        else if (de)
           HSACK(hsa_amd_memory_async_copy_on_engine((char*)hd_out + off, ag.cpu,
                                                     (char*)dev_out + off, ag.gpu, len, 0,
                                                     nullptr, so, (hsa_amd_sdma_engine_id_t)de,
@@ -141,13 +171,40 @@ int main(int argc, char** argv) {
         else if (he == 0)
           HIPCK(hipMemcpyAsync((char*)dev_in + off, (char*)host_in + off, len,
                                hipMemcpyHostToDevice, s));
+        else if (he == KIN)
+          hipLaunchKernelGGL(k_copy, dim3((unsigned)((len + (1u << 20) - 1) >> 20)), dim3(256), 0, s,
+                             (const u32x4*)((char*)hd_in + off), (u32x4*)((char*)dev_in + off), len / 16);
+        else if (he == HIP2) {
+          const size_t h = len / 2;
+          HIPCK(hipMemcpyAsync((char*)dev_in + off, (char*)host_in + off, h,
+                               hipMemcpyHostToDevice, s));
+          HIPCK(hipMemcpyAsync((char*)dev_in + off + h, (char*)host_in + off + h, len - h,
+                               hipMemcpyHostToDevice, s3));
+        } else if (he == TWO) {
+          const size_t h = len / 2;
+          HSACK(hsa_amd_memory_async_copy_on_engine((char*)dev_in + off, ag.gpu, (char*)hd_in + off,
+                                                    ag.cpu, h, 0, nullptr, si,
+                                                    (hsa_amd_sdma_engine_id_t)0x1, true));
+          HSACK(hsa_amd_memory_async_copy_on_engine((char*)dev_in + off + h, ag.gpu,
+                                                    (char*)hd_in + off + h, ag.cpu, len - h, 0,
+                                                    nullptr, si, (hsa_amd_sdma_engine_id_t)0x2, true));
+        }
       }
-      if (he == 0) HIPCK(hipEventRecord(ev, s));
-      double t_out = de ? 0 : t0, t_in = he < 0 ? t0 : 0;
+      if (he == 0 || he == KIN || he == HIP2) HIPCK(hipEventRecord(ev, s));
+      if (he == HIP2) {  // ev: both halves
+        HIPCK(hipEventRecord(ev3, s3));
+        HIPCK(hipStreamWaitEvent(s, ev3, 0));
+        HIPCK(hipEventRecord(ev, s));
+      }
+      if (de == KOUT) HIPCK(hipEventRecord(ev2, s2));
+      double t_out = de ? 0 : t0, t_in = he == -1 ? t0 : 0;
       while (!t_out || !t_in) {
-        if (!t_out && hsa_signal_load_scacquire(so) < 1) t_out = now();
+        if (!t_out && (de == KOUT ? hipEventQuery(ev2) == hipSuccess
+                                  : hsa_signal_load_scacquire(so) < 1))
+          t_out = now();
         if (!t_in) {
-          if (he > 0 ? hsa_signal_load_scacquire(si) < 1 : hipEventQuery(ev) == hipSuccess)
+          if (he > 0 || he == TWO ? hsa_signal_load_scacquire(si) < 1
+                                  : hipEventQuery(ev) == hipSuccess)
             t_in = now();
         }
       }
@@ -157,7 +214,7 @@ int main(int argc, char** argv) {
       }
     }
     printf("%-44s out %6.1f GB/s  in %6.1f GB/s\n", label,
-           de ? reps * n / to_sum / 1e9 : 0.0, he >= 0 ? reps * n / ti_sum / 1e9 : 0.0);
+           de ? reps * n / to_sum / 1e9 : 0.0, he != -1 ? reps * n / ti_sum / 1e9 : 0.0);
   };
   // "chase": what the overlapped bench does -- the H2D of chunk j reads the bytes the D2H of
   // chunk j just wrote into the same host buffer, as soon as that copy has completed.
@@ -209,6 +266,23 @@ int main(int argc, char** argv) {
     printf("%-44s out %6.1f GB/s  in %6.1f GB/s (in: from its own start)\n", label,
            reps * n / to_sum / 1e9, reps * n / ti_sum / 1e9);
   };
+  if (argc > 3 && std::string(argv[3]) == "kernels") {  // the kernel-copy variants only
+    run(0, HIP2, "H2D hipMemcpyAsync x2 streams alone");
+    run(0x4, HIP2, "D2H engine 2 + H2D hipMemcpyAsync x2 streams");
+    run(0x4, 0, "D2H engine 2 + H2D hipMemcpyAsync");
+    run(0x4, TWO, "D2H engine 2 + H2D engines 0+1");
+    run(0x8, TWO, "D2H engine 3 + H2D engines 0+1");
+    if (argc > 4) return 0;
+    run(0, KIN, "H2D kernel alone");
+    run(KOUT, -1, "D2H kernel alone");
+    run(0, TWO, "H2D engines 0+1 alone");
+    run(0x4, 0, "D2H engine 2 + H2D hipMemcpyAsync");
+    run(0x4, KIN, "D2H engine 2 + H2D kernel");
+    run(0x4, TWO, "D2H engine 2 + H2D engines 0+1");
+    run(KOUT, 0x2, "D2H kernel + H2D engine 1");
+    run(KOUT, KIN, "D2H kernel + H2D kernel");
+    return 0;
+  }
   chase(0x4, 0, "chase: D2H engine 2 -> H2D hipMemcpyAsync");
   chase(0x4, 0x2, "chase: D2H engine 2 -> H2D engine 1");
   run(0x4, -1, "D2H engine 2 alone");

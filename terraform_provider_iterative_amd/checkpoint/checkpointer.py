@@ -103,6 +103,7 @@ class DeviceEngine:
         # TPI_D2H_ENGINE=blit / no engine, HIP's blit kernels on the CUs ("blit")
         bit = int(self.lib.tpi_engine_d2h_engine(handle))
         self.d2h_engine = "sdma%d" % (bit.bit_length() - 1) if bit else "blit"
+        self.split_chunks = 0
 
     def save(self, plan: PackPlan, host_addr: int, crcs: np.ndarray, mode: int,
              wait_stream: int) -> TransferResult:
@@ -185,6 +186,8 @@ class DeviceEngine:
             ctypes.c_void_p(words_addr), ctypes.c_double(timeout), signal_stream,
             ctypes.byref(bad), ctypes.byref(first), ctypes.byref(st))
         self.lib.check(rc, "tpi_restore_stream")
+        # chunks copied over two streams because the restore trailed its writer (duplex link)
+        self.split_chunks = int(self.lib.tpi_engine_split_chunks(self.handle))
         return TransferResult(plan.total, time.perf_counter() - t0, int(st.chunks),
                               int(bad.value), int(first.value), wire_bytes=int(st.bytes))
 

@@ -69,6 +69,7 @@ class HipLib:
             "tpi_engine_tile_bytes": (u64, [vp]),
             "tpi_engine_chunk_bytes": (u64, [vp]),
             "tpi_engine_d2h_engine": (c.c_uint32, [vp]),
+            "tpi_engine_split_chunks": (u64, [vp]),
             "tpi_engine_set_progress": (i32, [vp, vp]),
             "tpi_ipc_export": (i32, [vp, vp, c.POINTER(u64), c.POINTER(u64)]),
             "tpi_mem_range": (i32, [vp, c.POINTER(u64), c.POINTER(u64)]),
