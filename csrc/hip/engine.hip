@@ -1376,7 +1376,7 @@ int tpi_restore_stream(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total
       if (was_split[b]) HIP_OK(hipEventSynchronize(e->ev_d[b]));
     }
     const uint64_t published = __atomic_load_n(&words[0], __ATOMIC_ACQUIRE);
-    const bool split = chunk_tiles > 0 && published >= t0i + nt && len >= (4ull << 20) &&
+    const bool split = chunk_tiles > 0 && published >= t0i + nt &&
                        (published - (t0i + nt)) / chunk_tiles >= e->split_lead;
     uint64_t cbeg = base, cend = base + len;
     if (zipped) {
@@ -1402,8 +1402,9 @@ int tpi_restore_stream(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total
                        hipMemcpyHostToDevice, e->aux));
     HIP_OK(hipEventRecord(e->ev_c[b], e->aux));
     if (k >= (uint64_t)e->nbuf) HIP_OK(hipStreamWaitEvent(e->copy, e->ev_b[b], 0));
-    // halves split on a 64 KiB boundary of the wire stream
-    const uint64_t mid = split ? cbeg + ((cend - cbeg) / 2 & ~0xFFFFull) : cend;
+    // halves split on a 64 KiB boundary of the wire stream (chunks under 128 KiB stay whole)
+    const uint64_t mid = split && cend - cbeg >= (128ull << 10)
+                             ? cbeg + ((cend - cbeg) / 2 & ~0xFFFFull) : cend;
     HIP_OK(region_copy(e, e->staging[b], src + cbeg, mid - cbeg, hipMemcpyHostToDevice,
                        e->copy));
     HIP_OK(hipEventRecord(e->ev_a[b], e->copy));

@@ -486,15 +486,19 @@ def test_streamed_restore_follows_the_writers_progress(codec, tmp_path):
     writer.close()
 
 
-@pytest.mark.parametrize("codec", ["none", "tpz1"])
-def test_restore_streams_behind_a_concurrent_save(codec, tmp_path):
+@pytest.mark.parametrize("codec,split", [("none", "2"), ("tpz1", "2"), ("none", "0"),
+                                         ("tpz1", "0")])
+def test_restore_streams_behind_a_concurrent_save(codec, split, tmp_path, monkeypatch):
     """What bench.py's headline step does: a save streams into the host region while a
     restore in another thread copies each published chunk back into other tensors (the
-    per-chunk CRC / blob-offset uploads on their own stream, staging slots reused)."""
+    per-chunk CRC / blob-offset uploads on their own stream, staging slots reused).
+    ``split`` = TPI_H2D_SPLIT_LEAD: 0 sends every chunk's H2D as two halves on two copy
+    streams (the duplex-link balancing a trailing restore gets)."""
     import threading
 
     from terraform_provider_iterative_amd.checkpoint import Checkpointer
 
+    monkeypatch.setenv("TPI_H2D_SPLIT_LEAD", split)
     g = torch.Generator().manual_seed(11)
     src = {"a": torch.randn(3 << 20, generator=g).to(torch.bfloat16).cuda(),
            "b": torch.randn(5 << 20, generator=g).mul(1e-3).cuda(),
@@ -519,6 +523,8 @@ def test_restore_streams_behind_a_concurrent_save(codec, tmp_path):
         th.join(60)
         assert "err" not in box, box.get("err")
         assert box["res"].bad_tiles == 0
+        if split == "0":  # every chunk of at least 128 KiB on the wire went as two halves
+            assert reader.engine.split_chunks > 0
         torch.cuda.synchronize()
         for k in src:
             assert torch.equal(dst[k], src[k]), (step, k)
