@@ -64,6 +64,11 @@ extern "C" hipError_t tpi_launch_stream_hash(const tpi_seg* segs, int nseg, uint
 extern "C" hipError_t tpi_launch_dirty_tiles(const uint64_t* hash, uint64_t* prev, uint64_t n,
                                              int all, uint32_t* idx, unsigned int* count,
                                              hipStream_t stream);
+extern "C" hipError_t tpi_launch_stream_copy_hash(const tpi_seg* src, const tpi_seg* dst,
+                                                  int nseg, uint64_t stream_base, uint64_t len,
+                                                  uint64_t total, uint64_t tile_bytes,
+                                                  uint64_t seed, uint64_t* digests,
+                                                  unsigned long long* bad, hipStream_t stream);
 
 extern "C" hipError_t tpi_launch_tpz_encode(const void* raw, uint64_t len, uint64_t tile,
                                             void* meta, uint32_t* csize, void* out,
@@ -207,6 +212,9 @@ struct tpi_engine {
   uint32_t* d_idx = nullptr;
   unsigned int* d_count = nullptr;
   size_t hash_cap = 0;
+  // HBM hand-off: tile digests of the fused copy, checked by its read-back pass
+  uint64_t* d_digest = nullptr;
+  size_t digest_cap = 0;
   uint64_t hash_ntiles = 0;
   bool hash_valid = false;
   // TPZ1 codec: raw pack scratch (one chunk), per-tile headers of the chunk in flight,
@@ -538,6 +546,7 @@ void tpi_engine_destroy(tpi_engine* e) {
   if (e->d_crcs) (void)hipFree(e->d_crcs);
   if (e->d_bad) (void)hipFree(e->d_bad);
   if (e->d_hash) (void)hipFree(e->d_hash);
+  if (e->d_digest) (void)hipFree(e->d_digest);
   if (e->d_prev) (void)hipFree(e->d_prev);
   if (e->d_idx) (void)hipFree(e->d_idx);
   if (e->d_count) (void)hipFree(e->d_count);
@@ -1520,17 +1529,40 @@ int tpi_copy_segments(tpi_engine* e, const tpi_seg* src, const tpi_seg* dst, int
   for (int i = 0; i < n && fused; ++i)
     fused = src[i].off == dst[i].off && src[i].nbytes == dst[i].nbytes;
   if (const char* m = getenv("TPI_HANDOFF_COPY")) fused = fused && strcmp(m, "staged") != 0;
+  // The fused route's tile digest: the XXH64-class stream hash (no table lookups, reads at
+  // ~6 TB/s) by default; TPI_HANDOFF_HASH=crc32c keeps the CRC32C tile kernels (~4.3 TB/s
+  // read-back, LDS-lookup bound).
+  const char* hash_env = getenv("TPI_HANDOFF_HASH");
+  const bool xxh = !(hash_env && strcmp(hash_env, "crc32c") == 0);
+  const uint64_t ntiles = (total + tile - 1) / tile;
+  if (good && fused && xxh && ntiles > e->digest_cap) {
+    if (e->d_digest) good = ok(hipFree(e->d_digest), "hipFree(digests)");
+    e->d_digest = nullptr;
+    e->digest_cap = 0;
+    good = good && ok(hipMalloc(&e->d_digest, std::max<uint64_t>(ntiles, 1024) * sizeof(uint64_t)),
+                      "hipMalloc(digests)");
+    if (good) e->digest_cap = std::max<uint64_t>(ntiles, 1024);
+  }
   uint64_t nchunks = 0;
   // No staging buffer bounds the fused route's spans: 4 GiB (4096 one-MiB tiles, 16
   // workgroups per CU) keeps the chip full, where a 256 MB chunk is one workgroup per CU.
   const uint64_t span = std::max<uint64_t>(e->chunk, ((4ull << 30) / tile) * tile);
   for (uint64_t base = 0, k = 0; good && fused && base < total; base += span, ++k) {
     const uint64_t len = std::min(span, total - base);
-    good = ok(tpi_launch_stream_copy(d_src, e->d_segs, n, base, len, tile, e->tables, e->d_crcs,
-                                     init_full, init_last, nullptr, e->compute), "copy") &&
-           ok(tpi_launch_stream_copy(e->d_segs, nullptr, n, base, len, tile, e->tables,
-                                     e->d_crcs, init_full, init_last, e->d_bad, e->compute),
-              "verify");
+    if (xxh)
+      good = ok(tpi_launch_stream_copy_hash(d_src, e->d_segs, n, base, len, total, tile,
+                                            TPI_SYNC_SEED, e->d_digest, nullptr, e->compute),
+                "copy") &&
+             ok(tpi_launch_stream_copy_hash(e->d_segs, nullptr, n, base, len, total, tile,
+                                            TPI_SYNC_SEED, e->d_digest, e->d_bad, e->compute),
+                "verify");
+    else
+      good = ok(tpi_launch_stream_copy(d_src, e->d_segs, n, base, len, tile, e->tables,
+                                       e->d_crcs, init_full, init_last, nullptr, e->compute),
+                "copy") &&
+             ok(tpi_launch_stream_copy(e->d_segs, nullptr, n, base, len, tile, e->tables,
+                                       e->d_crcs, init_full, init_last, e->d_bad, e->compute),
+                "verify");
     nchunks = k + 1;
   }
   for (uint64_t base = 0, k = 0; good && !fused && base < total; base += e->chunk, ++k) {

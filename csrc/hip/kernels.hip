@@ -273,7 +273,7 @@ __device__ static inline void scatter16(const tpi_seg* __restrict__ segs, const 
   if (rel >= c.nbytes) return;
   const uint64_t addr = c.ptr + rel;
   if (c.kind == TPI_SEG_CONTIG && rel + 16 <= c.nbytes && (addr & 15) == 0) {
-    *(u32x4*)addr = w;
+    __builtin_nontemporal_store(w, (u32x4*)addr);  // streamed once: no L2 allocation
     return;
   }
   if (c.kind == TPI_SEG_TRANSPOSE && staged) return;  // k_transpose scatters it afterwards
@@ -757,16 +757,30 @@ __global__ __launch_bounds__(WG) void k_shard_hash(const uint8_t* __restrict__ d
 // digest is the XOR of the avalanched lane states, mixed with the tile length.  It is a
 // private format (only compared with itself), so it needs no host reference beyond tests.
 
-__global__ __launch_bounds__(WG) void k_stream_hash(const tpi_seg* __restrict__ segs, int nseg,
-                                                    uint64_t total, uint64_t tile_bytes,
-                                                    uint64_t seed, uint64_t* __restrict__ out) {
+//
+// The same digest drives the HBM hand-off's fused copy (HASH_COPY: every word gathered from the
+// predecessor's tensors is also scattered into the successor's, and the tile digest of what
+// was read is recorded) and its read-back check (HASH_VERIFY: the successor's tensors are
+// hashed again and compared).  No table lookups: where the CRC32C verify is bound by its LDS
+// lookups at ~4.3 TB/s, this reads at the ~6 TB/s class of k_shard_hash
+// (profiles/handoff_hash_round3.md).  Workgroup i handles tile tile0 + i.
+enum { HASH_ONLY = 0, HASH_COPY = 1, HASH_VERIFY = 2 };
+
+template <int KIND>
+__global__ __launch_bounds__(WG) void k_stream_hash(const tpi_seg* __restrict__ segs,
+                                                    const tpi_seg* __restrict__ dsegs, int nseg,
+                                                    uint64_t tile0, uint64_t total,
+                                                    uint64_t tile_bytes, uint64_t seed,
+                                                    uint64_t* __restrict__ out,
+                                                    unsigned long long* __restrict__ bad) {
   __shared__ uint64_t red[WG / 64];
   const int lane = threadIdx.x;
-  const uint64_t gtile = blockIdx.x;
+  const uint64_t gtile = tile0 + blockIdx.x;
   const uint64_t gbase = gtile * tile_bytes;
   const uint64_t len = umin64(tile_bytes, total - gbase);
-  SegCursor cur;
+  SegCursor cur, dcur;
   seg_load(segs, nseg, seg_find(segs, nseg, gbase + lane * 16), cur);
+  if (KIND == HASH_COPY) seg_load(dsegs, nseg, seg_find(dsegs, nseg, gbase + lane * 16), dcur);
   // two independent round chains per lane (low and high 8 bytes of each word): a single
   // chain of dependent 64-bit multiplies left the kernel latency-bound (4.8 TB/s)
   uint64_t va = seed + (uint64_t)(lane + 1) * TPI_XXH_P1, vb = va ^ TPI_XXH_P2;
@@ -781,6 +795,14 @@ __global__ __launch_bounds__(WG) void k_stream_hash(const tpi_seg* __restrict__ 
       advance(segs, nseg, pos, cur);
       w[u] = gather16(segs, cur, pos, nullptr, false);
     }
+    if (KIND == HASH_COPY) {
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        const uint64_t pos = gbase + (row + u) * TPI_ROW_BYTES + lane * 16;
+        advance(dsegs, nseg, pos, dcur);
+        scatter16(dsegs, dcur, pos, w[u], false);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       va = tpi_xxh_round(va, ((uint64_t)w[u].y << 32) | w[u].x);
@@ -791,6 +813,10 @@ __global__ __launch_bounds__(WG) void k_stream_hash(const tpi_seg* __restrict__ 
   for (uint64_t rel = row * TPI_ROW_BYTES + lane * 16; rel < len; rel += TPI_ROW_BYTES) {
     advance(segs, nseg, gbase + rel, cur);
     const u32x4 w = gather16(segs, cur, gbase + rel, nullptr, false);
+    if (KIND == HASH_COPY) {
+      advance(dsegs, nseg, gbase + rel, dcur);
+      scatter16(dsegs, dcur, gbase + rel, w, false);
+    }
     va = tpi_xxh_round(va, ((uint64_t)w.y << 32) | w.x);
     vb = tpi_xxh_round(vb, ((uint64_t)w.w << 32) | w.z);
     ++nwords;
@@ -800,7 +826,17 @@ __global__ __launch_bounds__(WG) void k_stream_hash(const tpi_seg* __restrict__ 
   for (int o = 32; o >= 1; o >>= 1) h ^= __shfl_xor(h, o, 64);
   if ((lane & 63) == 0) red[lane >> 6] = h;
   __syncthreads();
-  if (lane == 0) out[gtile] = tpi_xxh_avalanche(red[0] ^ red[1] ^ red[2] ^ red[3] ^ len);
+  if (lane == 0) {
+    const uint64_t digest = tpi_xxh_avalanche(red[0] ^ red[1] ^ red[2] ^ red[3] ^ len);
+    if (KIND == HASH_VERIFY) {
+      if (digest != out[gtile]) {
+        atomicAdd(&bad[0], 1ull);
+        atomicMin(&bad[1], (unsigned long long)gtile);
+      }
+    } else {
+      out[gtile] = digest;
+    }
+  }
 }
 
 // Compare digests with the previous sync, append dirty tile indices, remember the new ones.
@@ -948,8 +984,30 @@ extern "C" hipError_t tpi_launch_stream_hash(const tpi_seg* segs, int nseg, uint
                                              hipStream_t stream) {
   if (total == 0) return hipSuccess;
   const uint64_t ntiles = (total + tile_bytes - 1) / tile_bytes;
-  hipLaunchKernelGGL(k_stream_hash, dim3((unsigned)ntiles), dim3(WG), 0, stream, segs, nseg,
-                     total, tile_bytes, seed, out);
+  hipLaunchKernelGGL(k_stream_hash<HASH_ONLY>, dim3((unsigned)ntiles), dim3(WG), 0, stream,
+                     segs, nullptr, nseg, (uint64_t)0, total, tile_bytes, seed, out, nullptr);
+  return hipGetLastError();
+}
+
+// Hand-off over the stream bytes [stream_base, stream_base + len) (tile aligned) of a plan
+// whose stream is `total` bytes: dst != nullptr copies src -> dst and records the tile
+// digests of what was read into `digests` (indexed by global tile); dst == nullptr re-hashes
+// src and counts tiles whose digest differs (bad[0]; bad[1] = first such tile).
+extern "C" hipError_t tpi_launch_stream_copy_hash(const tpi_seg* src, const tpi_seg* dst,
+                                                  int nseg, uint64_t stream_base, uint64_t len,
+                                                  uint64_t total, uint64_t tile_bytes,
+                                                  uint64_t seed, uint64_t* digests,
+                                                  unsigned long long* bad, hipStream_t stream) {
+  if (len == 0) return hipSuccess;
+  if (stream_base % tile_bytes || stream_base + len > total) return hipErrorInvalidValue;
+  const uint64_t tile0 = stream_base / tile_bytes;
+  const dim3 grid((unsigned)((len + tile_bytes - 1) / tile_bytes)), block(WG);
+  if (dst)
+    hipLaunchKernelGGL(k_stream_hash<HASH_COPY>, grid, block, 0, stream, src, dst, nseg, tile0,
+                       total, tile_bytes, seed, digests, bad);
+  else
+    hipLaunchKernelGGL(k_stream_hash<HASH_VERIFY>, grid, block, 0, stream, src, nullptr, nseg,
+                       tile0, total, tile_bytes, seed, digests, bad);
   return hipGetLastError();
 }
 

@@ -1,6 +1,6 @@
 """Experiment: the HBM hand-off's copy + read-back verify in one process (no IPC), so a
-kernel trace splits its time between the fused copy (k_stream_crc<3>) and the verify
-(k_stream_crc<4>).
+kernel trace splits its time between the fused copy and the verify: k_stream_hash<1> / <2>
+(default tile digest) or, with TPI_HANDOFF_HASH=crc32c, k_stream_crc<3> / <4>.
 
     python scripts/exp/handoff_kernels.py [GB]
 """

@@ -974,7 +974,7 @@ class Checkpointer:
 
     def restore_hbm(self, strict: bool = True) -> TransferResult:
         """Copy the state of a preempted predecessor on the same GPU straight from its HBM
-        (HIP IPC; one fused copy pass + a read-back verify, every tile CRC-checked) into the
+        (HIP IPC; one fused copy pass + a read-back verify, every tile's digest checked) into the
         bound tensors."""
         doc = self._hbm_doc()
         if doc is None:

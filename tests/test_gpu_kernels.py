@@ -577,6 +577,41 @@ def test_streamed_restore_gives_up_on_a_stalled_writer(tmp_path):
     writer.close()
 
 
+@pytest.mark.parametrize("digest", ["xxh", "crc32c"])
+def test_handoff_copy_verify_catches_a_bad_destination(digest, monkeypatch):
+    """The hand-off's fused copy records a digest per tile of what it read; the read-back pass
+    must flag tiles whose destination differs.  Two destination segments aliasing the same
+    memory make the copy overwrite one tensor with another, as a wrong mapping would."""
+    from terraform_provider_iterative_amd.checkpoint import Checkpointer
+    from terraform_provider_iterative_amd.ops.packing import PackPlan
+
+    monkeypatch.setenv("TPI_HANDOFF_HASH", digest)  # read by every tpi_copy_segments call
+    g = torch.Generator(device="cuda").manual_seed(5)
+    src = {"a": torch.randn(1 << 20, device="cuda", generator=g),
+           "b": torch.randn(1 << 20, device="cuda", generator=g).to(torch.bfloat16),
+           "c": torch.randn(300, 1000, device="cuda", generator=g).t()}  # strided view
+    dst = {"a": torch.zeros(1 << 20, device="cuda"),
+           "b": torch.zeros(1 << 20, device="cuda", dtype=torch.bfloat16),
+           "c": torch.zeros(300, 1000, device="cuda").t()}
+    ck = Checkpointer(dst, tile_bytes=1 << 16, chunk_bytes=1 << 20, populate=False)
+    src_segs = PackPlan.from_tensors(src, ck.plan.tile_bytes).segs.copy()
+    stream = torch.cuda.current_stream().cuda_stream
+    res = ck.engine.copy_segments(src_segs, ck.plan, stream)
+    torch.cuda.synchronize()
+    assert res.bad_tiles == 0
+    for k in src:
+        assert torch.equal(dst[k], src[k]), k
+    ptr = ck.plan.segs["ptr"].copy()
+    try:
+        ck.plan.segs["ptr"][1] = ptr[0]  # "b" lands on top of "a"
+        res = ck.engine.copy_segments(src_segs, ck.plan, stream)
+        torch.cuda.synchronize()
+    finally:
+        ck.plan.segs["ptr"][:] = ptr
+    assert res.bad_tiles > 0
+    ck.close()
+
+
 HBM_EXPORTER = r'''
 import sys, torch
 sys.path.insert(0, %(root)r)
