@@ -22,8 +22,8 @@ trained AdamW state (an untrained one would be all-zero moments, which compress 
     python bench.py --gpus N --steps K --warmup W
 
 Rank 0 prints one JSON line.  ``value`` = checkpoint bytes moved (save + restore) by all
-ranks per second of wall time (max over ranks of the timed region).  Before the timed
-region rank 0 also measures task apply -> first-log latency of an ``iterative_task`` on the
+ranks per second of wall time (max over ranks of the timed region).  After the timed region
+rank 0 also measures task apply -> first-log latency of an ``iterative_task`` on the
 node-local runtime (reported as ``first_log_latency_s``; not part of ``value``).
 """
 from __future__ import annotations
@@ -192,6 +192,12 @@ def host_memory_check(per_rank: int, local_world: int) -> None:
 
 def main(argv=None):
     args = parse_args(argv)
+    # HIP spreads a process's streams over GPU_MAX_HW_QUEUES hardware queues (4 by default).
+    # The saving and the restoring engine hold 8 streams between them; on 4 queues the save's
+    # kernels can sit behind the restore's cross-stream waits, idling the save's PCIe leg
+    # (117-119 -> 121 GB/s with 8 queues, profiles/hw_queues_round3.md).  Set before the
+    # first HIP call, inherited by ranks this process launches.
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         raise SystemExit(launch_ranks(args, argv))
     import torch
@@ -250,13 +256,6 @@ def main(argv=None):
                          device=device if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
-
-    latency = None
-    if rank == 0 and not args.no_latency:
-        # an iterative_task with parallelism = N (one GPU per rank), like the job measured
-        # (one GPU per rank: a rehearsal with more ranks than GPUs probes with what exists)
-        gpus = torch.cuda.device_count() if on_gpu else world
-        latency = first_log_latency(parallelism=max(1, min(world, gpus)))
 
     from terraform_provider_iterative_amd.checkpoint import Checkpointer
 
@@ -373,6 +372,12 @@ def main(argv=None):
         host_numa = numa_placement(ck.region.addr, ck.region.size)
     elapsed = allmax(elapsed)
     save_max, restore_max = allmax(save_s), allmax(restore_s)
+    latency = None
+    if rank == 0 and not args.no_latency:  # after the timed region: nothing of it overlaps
+        # an iterative_task with parallelism = N (one GPU per rank), like the job measured
+        # (one GPU per rank: a rehearsal with more ranks than GPUs probes with what exists)
+        gpus = torch.cuda.device_count() if on_gpu else world
+        latency = first_log_latency(parallelism=max(1, min(world, gpus)))
     total = ck.plan.total * world  # packed bytes per direction per step (all ranks)
     wire_total = int(allmax(float(wire))) * world  # (upper bound: max rank x N)
     value = 2 * total * args.steps / elapsed / 1e9
