@@ -22,8 +22,8 @@ trained AdamW state (an untrained one would be all-zero moments, which compress 
     python bench.py --gpus N --steps K --warmup W
 
 Rank 0 prints one JSON line.  ``value`` = checkpoint bytes moved (save + restore) by all
-ranks per second of wall time (max over ranks of the timed region).  After the timed region
-rank 0 also measures task apply -> first-log latency of an ``iterative_task`` on the
+ranks per second of wall time (max over ranks of the timed region).  Before the timed
+region rank 0 also measures task apply -> first-log latency of an ``iterative_task`` on the
 node-local runtime (reported as ``first_log_latency_s``; not part of ``value``).
 """
 from __future__ import annotations
@@ -257,6 +257,15 @@ def main(argv=None):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    latency = None
+    if rank == 0 and not args.no_latency:
+        # an iterative_task with parallelism = N (one GPU per rank), like the job measured
+        # (one GPU per rank: a rehearsal with more ranks than GPUs probes with what exists).
+        # Measured first: a process that already maps the 100 GB host region and the HBM
+        # state spawns the probe's `tpi apply` ~17 ms slower (profiles/hw_queues_round3.md).
+        gpus = torch.cuda.device_count() if on_gpu else world
+        latency = first_log_latency(parallelism=max(1, min(world, gpus)))
+
     from terraform_provider_iterative_amd.checkpoint import Checkpointer
 
     per_rank = int(args.total_gb * 1e9 / world)
@@ -372,12 +381,7 @@ def main(argv=None):
         host_numa = numa_placement(ck.region.addr, ck.region.size)
     elapsed = allmax(elapsed)
     save_max, restore_max = allmax(save_s), allmax(restore_s)
-    latency = None
-    if rank == 0 and not args.no_latency:  # after the timed region: nothing of it overlaps
-        # an iterative_task with parallelism = N (one GPU per rank), like the job measured
-        # (one GPU per rank: a rehearsal with more ranks than GPUs probes with what exists)
-        gpus = torch.cuda.device_count() if on_gpu else world
-        latency = first_log_latency(parallelism=max(1, min(world, gpus)))
+
     total = ck.plan.total * world  # packed bytes per direction per step (all ranks)
     wire_total = int(allmax(float(wire))) * world  # (upper bound: max rank x N)
     value = 2 * total * args.steps / elapsed / 1e9
