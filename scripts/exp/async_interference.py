@@ -5,7 +5,7 @@ A bf16 GEMM loop stands in for training.  The script measures its TFLOP/s alone,
 a save_async spill of the synthetic AdamW state runs (TPZ1 codec on the engine's streams),
 and reports the spill time with and without the GEMMs.
 
-    python scripts/exp/async_interference.py [GB] [gemm_n] [chunk_MiB]
+    python scripts/exp/async_interference.py [GB] [gemm_n] [chunk_MiB] [codec]
 """
 import os
 import sys
@@ -38,12 +38,13 @@ def main():
     gb = float(sys.argv[1]) if len(sys.argv) > 1 else 32.0
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
     chunk = int(sys.argv[3]) if len(sys.argv) > 3 else 256
+    codec = sys.argv[4] if len(sys.argv) > 4 else "tpz1"
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     state = synthetic_checkpoint(int(gb * 1e9), 8192, dev)
     a = torch.randn(n, n, dtype=torch.bfloat16, device=dev)
     b = torch.randn(n, n, dtype=torch.bfloat16, device=dev)
-    ck = Checkpointer(state, codec="tpz1", chunk_bytes=chunk << 20)
+    ck = Checkpointer(state, codec=codec, chunk_bytes=chunk << 20)
     ck.save_async({"warm": True}).result()  # snapshot buffer, engine and codec buffers
     gemm_rate(a, b, 1.0)  # warm the GEMM
     alone, _ = gemm_rate(a, b, 3.0)
@@ -56,6 +57,9 @@ def main():
     pending.result()
     spill_shared = time.perf_counter() - t
     out = {"state_GB": round(ck.plan.total / 1e9, 1), "gemm_n": n, "chunk_MiB": chunk,
+           "codec": codec,
+           # GEMM work the spill cost: the window's shortfall against the loop alone
+           "gemm_seconds_lost": round(dt * (1 - shared / alone), 3),
            "gemm_TFLOPs_alone": round(alone, 1), "gemm_TFLOPs_during_spill": round(shared, 1),
            "gemm_slowdown": round(1 - shared / alone, 3), "gemm_window_s": round(dt, 3),
            "spill_s_alone": round(spill_alone, 3), "spill_s_with_gemm": round(spill_shared, 3),

@@ -685,25 +685,36 @@ class Checkpointer:
         slot.crcs[:] = crcs
         return TransferResult(self.plan.total, time.perf_counter() - t0, wire_bytes=wire)
 
-    def save_async(self, metadata: Optional[Dict] = None) -> PendingSave:
+    def save_async(self, metadata: Optional[Dict] = None,
+                   codec: Optional[str] = None) -> PendingSave:
         """Checkpoint without stalling the training stream on PCIe.
 
         The tensors are packed (with tile CRCs) into a snapshot buffer in HBM -- a device-side
         copy at TB/s, ordered on the current stream, which then waits for it, so tensors may
         be updated right after this returns.  A background thread spills the snapshot to the
-        host region (TPZ1-encoded when the checkpointer's codec is on) and writes the header;
-        ``result()`` returns its :class:`TransferResult`.  The snapshot costs ``plan.total``
-        bytes of HBM (allocated on first use).  Host tensors fall back to a synchronous save.
-        With ``slots=2`` the previous checkpoint stays valid for the whole spill.
+        host region (TPZ1-encoded when the codec is on) and writes the header; ``result()``
+        returns its :class:`TransferResult`.  The snapshot costs ``plan.total`` bytes of HBM
+        (allocated on first use).  Host tensors fall back to a synchronous save.  With
+        ``slots=2`` the previous checkpoint stays valid for the whole spill.
+
+        ``codec`` overrides the checkpointer's codec for this spill.  A spill next to a
+        training loop is a trade: TPZ1 shortens it by ~20 %, but its encode kernels take CU
+        time from the loop (a bf16 GEMM loop loses 0.10 s per 32 GB spilled with TPZ1 against
+        0.017 s without, ``profiles/async_codec_round3.md``).
         """
+        if codec is not None and codec not in ("none", "tpz1"):
+            raise ValueError("codec must be 'none' or 'tpz1', not %r" % (codec,))
         self.wait_pending()
         if self.engine is None:
             t0 = time.perf_counter()
             pending = PendingSave(0.0)
+            own, self.codec = self.codec, codec or self.codec
             try:
                 pending._result = self.save(metadata)
             except BaseException as error:  # surfaced by result()
                 pending._error = error
+            finally:
+                self.codec = own
             pending.stall_s = time.perf_counter() - t0
             pending._done.set()
             return pending
@@ -721,7 +732,7 @@ class Checkpointer:
                              torch.cuda.current_stream(dev).cuda_stream)
         pending = PendingSave(time.perf_counter() - t0)
         self.saves += 1
-        zipped = self.codec == "tpz1"
+        zipped = (codec or self.codec) == "tpz1"
 
         def spill():
             try:

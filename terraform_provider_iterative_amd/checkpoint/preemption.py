@@ -165,6 +165,18 @@ def sync_interval() -> float:
         return 10.0
 
 
+def sync_codec() -> Optional[str]:
+    """Codec of the periodic background spills (``TPI_SYNC_CODEC``): ``none`` by default --
+    a spill next to the training loop costs the loop ~6x less GPU time without the TPZ1
+    encode kernels, and nothing waits for it (``profiles/async_codec_round3.md``); ``tpz1``
+    shortens the spill instead; ``auto`` uses each checkpointer's own codec.  Preemption
+    saves keep the checkpointer's codec: their spill is on the recovery path."""
+    value = os.environ.get("TPI_SYNC_CODEC", "none").strip().lower()
+    if value in ("none", "tpz1"):
+        return value
+    return None
+
+
 def _collect_finished() -> bool:
     """Journal the async spills of earlier ticks that have completed; True if none is still
     running."""
@@ -190,6 +202,7 @@ def _periodic_save(step_no: Optional[int], metadata: Optional[Dict]) -> None:
         meta["step"] = step_no
     meta.update(metadata or {})
     mode = os.environ.get("TPI_SYNC_MODE", "async")
+    codec = sync_codec()
     for ck in _registered:
         if len(ck.slots) == 1 and not _slots_warned:
             _slots_warned = True  # the spill overwrites the one copy: a crash mid-spill loses it
@@ -201,7 +214,7 @@ def _periodic_save(step_no: Optional[int], metadata: Optional[Dict]) -> None:
             journal("checkpoint-synced", "incremental", "%d dirty tiles" % res.dirty_tiles,
                     *_describe(res), "%.1f ms" % ((time.perf_counter() - t0) * 1e3))
         else:
-            _tick_pending[id(ck)] = ck.save_async(meta)
+            _tick_pending[id(ck)] = ck.save_async(meta, codec=codec)
     _collect_finished()  # host tensors save synchronously: journal them now
 
 

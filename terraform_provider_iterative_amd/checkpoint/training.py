@@ -119,11 +119,11 @@ class TrainingState:
     def save(self, metadata: Optional[Dict] = None):
         return self.checkpointer.save(self._metadata(metadata))
 
-    def save_async(self, metadata: Optional[Dict] = None):
+    def save_async(self, metadata: Optional[Dict] = None, codec: Optional[str] = None):
         """Periodic checkpoint that stalls the training stream only for the HBM snapshot;
         host-side tensors are captured now, with the snapshot (see
-        :meth:`Checkpointer.save_async`)."""
-        return self.checkpointer.save_async(self._metadata(metadata))
+        :meth:`Checkpointer.save_async`, also for ``codec``)."""
+        return self.checkpointer.save_async(self._metadata(metadata), codec=codec)
 
     def restore_host(self, metadata: Dict) -> None:
         blobs = metadata.get("host_tensors", {})

@@ -388,3 +388,31 @@ def test_durable_reports_a_complete_copy_of_a_generation(tmp_path):
     ck.save({"step": 2})
     assert ck.durable(gen) and ck.durable(gen + 1)
     ck.close()
+
+
+def test_save_async_codec_override_and_periodic_policy(tmp_path, monkeypatch):
+    """A periodic background spill goes out without the codec by default (TPI_SYNC_CODEC);
+    the header records what the spill used, and the restore follows it."""
+    from terraform_provider_iterative_amd.checkpoint import preemption
+
+    g = torch.Generator().manual_seed(3)
+    t = {"w": torch.randn(1 << 16, generator=g), "b": torch.randn(999, generator=g)}
+    ref = {k: v.clone() for k, v in t.items()}
+    ck = Checkpointer(t, path=str(tmp_path / "spill"), tile_bytes=1 << 14, codec="tpz1")
+    ck.save_async({"step": 1}, codec="none").result()
+    assert ck.latest()["codec"] == "none" and ck.codec == "tpz1"
+    for v in t.values():
+        v.zero_()
+    ck.restore()
+    assert all(torch.equal(t[k], ref[k]) for k in t)
+    ck.save_async({"step": 2}).result()
+    assert ck.latest()["codec"] == "tpz1"
+    with pytest.raises(ValueError):
+        ck.save_async({"step": 3}, codec="zstd")
+    ck.close()
+    monkeypatch.delenv("TPI_SYNC_CODEC", raising=False)
+    assert preemption.sync_codec() == "none"
+    monkeypatch.setenv("TPI_SYNC_CODEC", "tpz1")
+    assert preemption.sync_codec() == "tpz1"
+    monkeypatch.setenv("TPI_SYNC_CODEC", "auto")
+    assert preemption.sync_codec() is None
