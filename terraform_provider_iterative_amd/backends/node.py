@@ -726,37 +726,7 @@ class NodeTask(Task):
         directory = self.spec.environment.directory
         if not directory:
             return
-        # The copies' new page-cache pages land on the NUMA node of the threads that write
-        # them.  When the task's GPUs all sit on one socket, write from that socket's cores:
-        # the stager then reads the workdir into its NUMA-local pinned ring without crossing
-        # the inter-socket link (TPI_PUSH_NUMA=0: the caller's affinity).
-        cpus = self._push_cpus()
-        saved = None
-        if cpus and hasattr(os, "sched_setaffinity"):
-            try:
-                saved = os.sched_getaffinity(0)
-                os.sched_setaffinity(0, cpus)  # this thread; the copy threads inherit it
-            except OSError:
-                saved = None
-        try:
-            storage.transfer(directory, self.data_dir, self.spec.environment.exclude_list)
-        finally:
-            if saved is not None:
-                try:
-                    os.sched_setaffinity(0, saved)
-                except OSError:
-                    pass
-
-    def _push_cpus(self) -> List[int]:
-        """Cores of the one NUMA node holding all of the task's GPUs (empty: no preference)."""
-        if self._knob("TPI_PUSH_NUMA", "1") == "0" or not hasattr(os, "sched_getaffinity"):
-            return []
-        from ..parallel.placement import numa_cpus
-
-        nodes = {g.get("numa_node", -1) for g in self._definition().get("gpu_info") or []}
-        if len(nodes) != 1 or min(nodes) < 0:
-            return []
-        return sorted(set(numa_cpus(min(nodes))) & os.sched_getaffinity(0))
+        storage.transfer(directory, self.data_dir, self.spec.environment.exclude_list)
 
     def pull(self) -> None:
         saved = self._saved or {}

@@ -206,34 +206,3 @@ def test_bench_concurrent_config5(monkeypatch, tmp_path):
     assert out["fifth_queued"] and out["fifth_succeeded"] and out["queued_start_s"] < 5
     assert out["reused_all_gpus"]
     assert len(out["first_log_s"]) == 4
-
-
-def test_push_writes_from_the_gpus_numa_node(cloud, tmp_path, monkeypatch):
-    """The workdir copy runs on the cores of the socket holding the task's GPUs (its page
-    cache then sits next to the stager's pinned ring), and the caller's affinity comes back."""
-    from terraform_provider_iterative_amd.backends import node as nodemod
-    from terraform_provider_iterative_amd.parallel.placement import numa_cpus
-
-    if not hasattr(os, "sched_getaffinity") or not numa_cpus(0):
-        pytest.skip("no NUMA topology")
-    work = tmp_path / "work"
-    work.mkdir()
-    (work / "a.bin").write_bytes(b"x" * 4096)
-    spec = Task(size=Size(machine="m+mi355x"),
-                environment=Environment(script="#!/bin/sh\n", directory=str(work),
-                                        variables=Variables({})))
-    task = backends.new(cloud, new_deterministic_identifier("pushnuma"), spec)
-    seen = []
-    monkeypatch.setattr(nodemod.storage, "transfer",
-                        lambda *a, **k: seen.append(set(os.sched_getaffinity(0))))
-    before = set(os.sched_getaffinity(0))
-    for gpu_info, pinned in (([{"numa_node": 0}, {"numa_node": 0}], True),
-                             ([{"numa_node": 0}, {"numa_node": 1}], False), ([], False)):
-        monkeypatch.setattr(task, "_definition", lambda g=gpu_info: {"gpu_info": g})
-        task.push()
-        want = set(numa_cpus(0)) & before if pinned else before
-        assert seen[-1] == want and set(os.sched_getaffinity(0)) == before
-    monkeypatch.setenv("TPI_PUSH_NUMA", "0")
-    monkeypatch.setattr(task, "_definition", lambda: {"gpu_info": [{"numa_node": 0}]})
-    task.push()
-    assert seen[-1] == before
