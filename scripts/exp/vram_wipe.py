@@ -8,6 +8,8 @@ HBM frees its memory after the boundary save, profiles/preempt_e2e_170g_round3.m
 
     python scripts/exp/vram_wipe.py [GB] [delay ...]
     python scripts/exp/vram_wipe.py [GB] alive      # the first process frees but stays alive
+    python scripts/exp/vram_wipe.py [GB] many       # the state as ~400 tensors, cold vs one
+                                                    # block reserved first
 """
 import json
 import subprocess
@@ -67,8 +69,49 @@ def alive(gb):
     return out
 
 
+MANY = r'''
+import sys, time, torch
+sys.path.insert(0, ".")
+from bench import synthetic_checkpoint
+gb, warm = float(sys.argv[1]), sys.argv[2] == "warm"
+torch.empty(1, device="cuda")
+torch.cuda.synchronize()
+t = time.perf_counter()
+if warm:  # one block of the state's size into the caching allocator, given back at once
+    block = torch.empty(int(gb * 1e9) + (1 << 30), dtype=torch.uint8, device="cuda")
+    del block
+t1 = time.perf_counter()
+state = synthetic_checkpoint(int(gb * 1e9), 8192, torch.device("cuda"), fill=False)
+torch.cuda.synchronize()
+print(t1 - t, time.perf_counter() - t1, len(state), flush=True)
+'''
+
+
+def many(gb):
+    """The successor's state as the training script allocates it (hundreds of tensors) right
+    after a releaser freed the memory: cold caching allocator vs one block reserved first."""
+    out = {}
+    for mode in ("cold", "warm"):
+        holder = subprocess.Popen([sys.executable, "-c", HOLDER, str(gb)], stdin=subprocess.PIPE,
+                                  stdout=subprocess.PIPE, text=True)
+        assert holder.stdout.readline().strip() == "freed"
+        r = subprocess.run([sys.executable, "-c", MANY, str(gb), mode], capture_output=True,
+                           text=True, timeout=300)
+        holder.stdin.write("\n")
+        holder.stdin.flush()
+        holder.wait(120)
+        if r.returncode != 0:
+            raise RuntimeError(r.stderr[-2000:])
+        reserve, alloc, n = r.stdout.split()
+        out[mode] = {"reserve_s": float(reserve), "tensors_s": float(alloc), "tensors": int(n)}
+    return out
+
+
 def main():
     gb = float(sys.argv[1]) if len(sys.argv) > 1 else 100.0
+    if sys.argv[2:3] == ["many"]:
+        print(json.dumps(dict(many(gb), GB=gb)), flush=True)
+        return
     if sys.argv[2:3] == ["alive"]:
         print(json.dumps(dict(alive(gb), GB=gb)), flush=True)
         return
