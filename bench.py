@@ -58,7 +58,9 @@ def parse_args(argv=None):
     p.add_argument("--codec", choices=("none", "tpz1"), default="tpz1")
     p.add_argument("--tile-mb", type=float, default=1.0)
     p.add_argument("--chunk-mb", type=float, default=256.0)
-    p.add_argument("--nbuf", type=int, default=3)
+    p.add_argument("--nbuf", type=int, default=4,
+                   help="staging buffers per engine (4: +0.8 %% over 3 in alternating runs, "
+                        "profiles/pipeline_depth_round3.md)")
     p.add_argument("--hidden", type=int, default=8192)
     p.add_argument("--no-latency", action="store_true", help="skip apply->first-log")
     p.add_argument("--broadcast-gb", type=float, default=10.0,
