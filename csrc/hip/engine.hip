@@ -486,8 +486,12 @@ tpi_engine* tpi_engine_create(int device, uint64_t chunk_bytes, int nbuf, uint64
     return bail("hipStreamCreate(aux)", err);
   if ((err = hipStreamCreateWithFlags(&e->copy2, hipStreamNonBlocking)) != hipSuccess)
     return bail("hipStreamCreate(copy2)", err);
-  if (const char* lead = getenv("TPI_H2D_SPLIT_LEAD"))  // "off": never split
-    e->split_lead = strcmp(lead, "off") == 0 ? ~0ull : strtoull(lead, nullptr, 10);
+  if (const char* lead = getenv("TPI_H2D_SPLIT_LEAD")) {  // "off": never split
+    char* end = nullptr;
+    const unsigned long long v = strtoull(lead, &end, 10);
+    if (strcmp(lead, "off") == 0) e->split_lead = ~0ull;
+    else if (end != lead && *end == '\0') e->split_lead = v;  // else: keep the default
+  }
   // staging chunks also hold TPZ1 blobs: worst case tpz_bound() per tile
   const uint64_t staging_bytes = chunk_bytes + (chunk_bytes / tile_bytes) * (TPZ_HDR + 128);
   e->staging.assign(nbuf, nullptr);
