@@ -179,6 +179,7 @@ struct Rank {
   int nfd = -1;  // read end of the rank's notify pipe (TPI_NOTIFY_FD in the rank)
   std::string uuid;
   std::string partial;
+  std::string note;  // partial line read from the notify pipe
   enum State { PENDING, RUNNING, DONE, PREEMPTED } state = PENDING;
   int restarts = 0;
   TermReason reason = TermReason::NONE;
@@ -192,6 +193,14 @@ struct Rank {
   int hot_spawns = 0;            // hot standbys started for this incarnation
   int gofd = -1;                 // standby only: write end of its activation pipe
   double hold_until = 0;  // a resuming incarnation: no new hot standby until it restored
+  // restored from its predecessor's HBM ("restored hbm"): the predecessor must stay alive
+  // until this incarnation has unmapped the IPC imports ("closed") or died
+  bool awaiting_close = false;
+  // detached (released / discarded): when it was told to go, and the exit trace so far
+  double exit_requested_at = 0;
+  std::string trace_last;
+  double trace_last_at = 0;
+  int trace_events = 0;
 };
 
 struct Spec {
@@ -210,6 +219,10 @@ struct Spec {
   int max_restarts = -1;
   double grace = 30, respawn_delay = 0;
   std::string reports_dir, state_path, events_path, control_path;
+  // written before a spot reclaim's SIGTERM: the ranks save without hand-off, free their HBM
+  // and leave at once (TPI_REQUEUE_FILE; nobody restores from this GPU)
+  std::string requeue_path;
+  bool exit_trace = true;  // journal state/wchan of released processes until they are reaped
   std::vector<std::string> leases;
   // workdir stager (spec "stager", runtime/stage.py): started before the ranks, holds the
   // HBM copies of the workdir for the task's lifetime
@@ -265,6 +278,12 @@ Spec load_spec(const std::string& path) {
   s.state_path = v["state_path"].str(s.task_dir + "/supervisor/state.json");
   s.events_path = v["events_path"].str(s.task_dir + "/supervisor/events.jsonl");
   s.control_path = v["control_path"].str(s.task_dir + "/supervisor/control.sock");
+  {
+    const size_t slash = s.state_path.rfind('/');
+    const std::string dir = slash == std::string::npos ? "." : s.state_path.substr(0, slash);
+    s.requeue_path = v["requeue_path"].str(dir + "/requeue");
+  }
+  s.exit_trace = v["exit_trace"].boolean(true);
   for (auto& l : v["leases"].a) s.leases.push_back(l.str());
   const Value& st = v["stager"];
   for (auto& a : st["argv"].a) s.stager_argv.push_back(a.str());
@@ -307,6 +326,7 @@ class Supervisor {
     sfd_ = signalfd(-1, &mask, SFD_CLOEXEC | SFD_NONBLOCK);
     signal(SIGPIPE, SIG_IGN);
     open_control();
+    unlink(s_.requeue_path.c_str());  // a reclaimed incarnation's marker
     started_ = now();
     event("supervisor-start", {"pid " + std::to_string(getpid()),
                                "parallelism " + std::to_string(s_.parallelism)});
@@ -343,6 +363,13 @@ class Supervisor {
       check_grace(t);
       check_respawn(t);
       check_limits(t);
+      trace_exits(t);
+      // Every rank is down (exited, or released after its save): the GPUs, cores and memory
+      // go back to the node now, not when the last released process has been reaped -- its
+      // kernel teardown (unpinning a 100 GB host region, freeing HBM) can take seconds, and a
+      // queued task or an on-demand reclaim would wait for it (tpl:10-15: the group scales to
+      // 0 right after the task's exit).
+      if (!resources_released_ && ranks_settled()) release_resources();
       if (all_finished()) break;
       double timeout = 2.0;
       if (s_.deadline > 0 && !timed_out_) timeout = std::min(timeout, s_.deadline - t);
@@ -350,6 +377,10 @@ class Supervisor {
         for (auto& r : *list)
           if (r.pid > 0 && r.term_at > 0 && !r.killed)
             timeout = std::min(timeout, r.term_at + s_.grace - t);
+      if (s_.exit_trace)
+        for (auto& d : detached_)
+          if (d.pid > 0 && (d.exit_requested_at > 0 || d.killed))
+            timeout = std::min(timeout, kTraceInterval);
       if (respawn_at_ > 0) timeout = std::min(timeout, respawn_at_ - t);
       if (s_.rank_memory_kb) timeout = std::min(timeout, next_memory_check_ - t);
       if (s_.disk_limit_bytes) timeout = std::min(timeout, next_disk_check_ - t);
@@ -409,6 +440,8 @@ class Supervisor {
   int ctl_fd_ = -1;
   double started_ = 0, respawn_at_ = 0;
   bool stop_ = false, timed_out_ = false, dirty_ = true;
+  bool resources_released_ = false;  // leases gone; released processes may still be exiting
+  bool requeued_ = false;            // the queue waiter was started (it owns state.json)
   int total_restarts_ = 0;
   pid_t stager_pid_ = -1;
   bool staged_ = false;
@@ -714,14 +747,18 @@ class Supervisor {
     return n;
   }
 
-  void write_state(const char* phase = nullptr) { atomic_write(s_.state_path, state_json(phase)); }
+  void write_state(const char* phase = nullptr) {
+    if (requeued_) return;  // the queue waiter owns state.json now
+    atomic_write(s_.state_path, state_json(phase));
+  }
 
   std::string state_json(const char* phase = nullptr) {
     std::string p = phase ? phase
                     : stop_ ? "stopping"
                     : timed_out_ ? "timing-out"
                     : respawn_at_ > 0 ? "respawning"
-                                      : "running";
+                    : resources_released_ ? "draining"
+                                          : "running";
     std::string out = "{\"pid\": " + std::to_string(getpid()) +
                       ", \"task_id\": " + quote(s_.task_id) + ", \"phase\": " + quote(p) +
                       ", \"started_at\": " + std::to_string(started_) +
@@ -773,6 +810,7 @@ class Supervisor {
     add("TPI_RESTART_COUNT", std::to_string(r.restarts));
     add("TPI_EVENTS_FILE", s_.events_path);  // ranks journal checkpoint phases here
     add("TPI_NOTIFY_FD", "3");                 // "released": spill done, respawn may start
+    add("TPI_REQUEUE_FILE", s_.requeue_path);  // exists: reclaimed, no successor here
     // SIGTERM -> SIGKILL window: a preempted rank saves at its next step boundary and falls
     // back to an immediate save after half of it (checkpoint/preemption.py)
     add("TPI_GRACE_SECONDS", std::to_string(s_.grace));
@@ -958,6 +996,7 @@ class Supervisor {
     kill(sb.pid, SIGKILL);
     sb.killed = true;
     sb.term_at = now();
+    sb.exit_requested_at = sb.term_at;
     sb.state = Rank::DONE;
     event("standby-discarded", {"rank " + std::to_string(index), "machine " + sb.uuid, why});
     detached_.push_back(sb);
@@ -1048,20 +1087,42 @@ class Supervisor {
   }
 
   // Notify pipe readable: returns true when the rank announced "released" and may be handed
-  // off (its spill is complete; the supervisor is terminating it as a preemption).
+  // off (its spill is complete -- or streaming -- and the supervisor is terminating it as a
+  // preemption or a reclaim).  One message per line:
+  //   released      the save no longer needs this process's place: respawn / requeue now
+  //   standby       the script calls preemption.standby() (warm successors possible)
+  //   restored      this incarnation restored its state: its predecessor may go
+  //   restored hbm  ... from the predecessor's HBM: the predecessor goes only after "closed"
+  //   closed        the IPC mappings of the predecessor's HBM are gone
   bool notified(Rank& r) {
     char buf[256];
     bool got = false;
     for (;;) {
       ssize_t n = read(r.nfd, buf, sizeof(buf));
       if (n > 0) {
-        const std::string msg(buf, (size_t)n);
-        if (msg.find("released") != std::string::npos) got = true;
-        if (msg.find("standby") != std::string::npos) r.standby_capable = true;
-        if (msg.find("restored") != std::string::npos) {
-          release_predecessors(r.index);
-          r.hold_until = 0;  // its hot standby may start now
+        r.note.append(buf, (size_t)n);
+        size_t start = 0, nl;
+        while ((nl = r.note.find('\n', start)) != std::string::npos) {
+          const std::string msg = r.note.substr(start, nl - start);
+          start = nl + 1;
+          if (msg == "released") {
+            got = true;
+          } else if (msg == "standby") {
+            r.standby_capable = true;
+          } else if (msg.compare(0, 8, "restored") == 0) {
+            r.hold_until = 0;  // its hot standby may start now
+            if (msg == "restored hbm") {
+              r.awaiting_close = true;  // the predecessor's memory is still mapped here
+            } else {
+              release_predecessors(r.index, "successor restored");
+            }
+          } else if (msg == "closed") {
+            r.awaiting_close = false;
+            release_predecessors(r.index, "successor closed the HBM hand-off");
+          }
         }
+        r.note.erase(0, start);
+        if (r.note.size() > 4096) r.note.clear();
         continue;
       }
       if (n == 0) {
@@ -1072,27 +1133,25 @@ class Supervisor {
       }
       break;
     }
-    if (got && r.pid > 0 && r.reason == TermReason::REQUEUE) {
-      kill(r.pid, SIGUSR2);  // nobody restores from this GPU: end its linger now
-      return false;
-    }
     if (!got || r.pid <= 0 || r.state != Rank::RUNNING || stop_ || timed_out_) return false;
-    if (!(r.reason == TermReason::PREEMPT ||
+    if (!(r.reason == TermReason::PREEMPT || r.reason == TermReason::REQUEUE ||
           (r.reason == TermReason::NONE && s_.respawn_on_sigterm)))
       return false;
     r.released = true;
     return true;
   }
 
-  // The successor of rank `index` has restored its state: a predecessor that lingers after its
-  // spill (keeping its host region pinned so its teardown cannot slow the restore's DMA) may
-  // exit now.
-  void release_predecessors(int index) {
+  // The successor of rank `index` no longer needs its predecessor (restored from the host
+  // region, closed its HBM imports, or died): a predecessor that lingers after its spill
+  // (keeping its host region pinned so its teardown cannot slow the restore's DMA, and its
+  // exported HBM mapped) may exit now.
+  void release_predecessors(int index, const char* why) {
     for (auto& d : detached_)
-      if (d.index == index && d.pid > 0) {
+      if (d.index == index && d.pid > 0 && d.exit_requested_at <= 0 && !d.killed) {
         kill(d.pid, SIGUSR2);
+        d.exit_requested_at = now();
         event("predecessor-exit-requested", {"rank " + std::to_string(index),
-                                             "machine " + d.uuid});
+                                             "machine " + d.uuid, why});
       }
   }
 
@@ -1113,7 +1172,25 @@ class Supervisor {
       r.pid = -1;
       r.fd = -1;
       r.logfd = -1;
+      r.nfd = -1;
       r.partial.clear();
+      r.note.clear();
+      r.awaiting_close = false;
+      if (r.reason == TermReason::REQUEUE) {
+        // reclaimed: its checkpoint is in host memory and its HBM is free; nobody restores
+        // from this GPU, so it may exit now and its resources go to the reclaiming task
+        // without waiting for its teardown (release_resources once the gang is down)
+        Rank& d = detached_.back();
+        kill(d.pid, SIGUSR2);
+        d.exit_requested_at = now();
+        r.exit_code = -1;
+        r.state = Rank::DONE;
+        desc.push_back("requeue");
+        event("rank-released", desc);
+        desc.pop_back();
+        event("rank-requeued", desc);
+        continue;
+      }
       r.exit_code = 143;
       r.state = Rank::PREEMPTED;
       event("rank-released", desc);
@@ -1140,6 +1217,53 @@ class Supervisor {
       r.term_at = now();
       kill(-r.pid, SIGTERM);
       kill(r.pid, SIGTERM);
+    }
+  }
+
+  // Exit trace: a released or discarded process should be gone within ~1-2 s (its kernel
+  // teardown: unpinning the host region, freeing HBM and the GPU context).  Where one spends
+  // longer shows in /proc: its scheduler state (D = uninterruptible, inside the driver or the
+  // mm teardown; Z = exited, not yet reaped) and the kernel function it sleeps in (wchan),
+  // journalled whenever they change, with its resident set, every kTraceInterval seconds.
+  static constexpr double kTraceInterval = 0.1;
+  static constexpr int kTraceMax = 64;  // events per process
+
+  void trace_exits(double t) {
+    if (!s_.exit_trace) return;
+    for (auto& d : detached_) {
+      if (d.pid <= 0 || (d.exit_requested_at <= 0 && !d.killed)) continue;
+      if (d.exit_requested_at <= 0) d.exit_requested_at = d.term_at > 0 ? d.term_at : t;
+      if (d.trace_events >= kTraceMax || t - d.trace_last_at < kTraceInterval * 0.9) continue;
+      char path[64], buf[512];
+      snprintf(path, sizeof(path), "/proc/%d/stat", (int)d.pid);
+      if (!read_small(path, buf, sizeof(buf))) continue;
+      const char* rp = strrchr(buf, ')');
+      char state = rp && rp[1] == ' ' ? rp[2] : '?';
+      snprintf(path, sizeof(path), "/proc/%d/wchan", (int)d.pid);
+      char wchan[128] = "-";
+      if (read_small(path, wchan, sizeof(wchan)) && !wchan[0]) snprintf(wchan, sizeof(wchan), "-");
+      long rss_mb = -1, threads = -1;
+      snprintf(path, sizeof(path), "/proc/%d/status", (int)d.pid);
+      std::ifstream in(path);
+      std::string key;
+      while (in >> key) {
+        long value = 0;
+        if (key == "VmRSS:" && in >> value) rss_mb = value / 1024;
+        else if (key == "Threads:" && in >> value) threads = value;
+        in.ignore(1 << 16, '\n');
+      }
+      const std::string sample = std::string(1, state) + " " + wchan;
+      // a change of state / wait point, or once a second while nothing changes (RSS drains)
+      if (sample == d.trace_last && t - d.trace_last_at < 1.0) continue;
+      d.trace_last = sample;
+      d.trace_last_at = t;
+      ++d.trace_events;
+      char el[48];
+      snprintf(el, sizeof(el), "+%.3f s", t - d.exit_requested_at);
+      event("exit-trace", {"rank " + std::to_string(d.index), "machine " + d.uuid,
+                           "pid " + std::to_string(d.pid), el, std::string("state ") + state,
+                           std::string("wchan ") + wchan, "rss " + std::to_string(rss_mb) + " MB",
+                           "threads " + std::to_string(threads)});
     }
   }
 
@@ -1273,6 +1397,8 @@ class Supervisor {
     if (requeue_) return true;
     requeue_ = true;
     respawn_at_ = 0;
+    // before any SIGTERM: a rank that sees the marker saves without hand-off and leaves
+    atomic_write(s_.requeue_path, source + "\n");
     event("requeue-requested", {source});
     for (int i = 0; i < s_.parallelism; ++i) discard_standby(i, "requeue");
     for (auto& r : ranks_) {
@@ -1393,8 +1519,15 @@ class Supervisor {
           close_log(d);
           const std::string code = WIFSIGNALED(st) ? std::string("signal ") + signame(WTERMSIG(st))
                                                    : "code " + std::to_string(WEXITSTATUS(st));
-          event("rank-released-exit", {"rank " + std::to_string(d.index), "machine " + d.uuid,
-                                       code});
+          std::vector<std::string> desc = {"rank " + std::to_string(d.index),
+                                           "machine " + d.uuid, code};
+          if (d.exit_requested_at > 0) {
+            char took[64];
+            snprintf(took, sizeof(took), "%.3f s after the exit request",
+                     now() - d.exit_requested_at);
+            desc.push_back(took);
+          }
+          event("rank-released-exit", desc);
           detached_.erase(detached_.begin() + i);
           break;
         }
@@ -1415,6 +1548,11 @@ class Supervisor {
   }
 
   void on_exit(Rank& r, int st) {
+    if (r.nfd >= 0) notified(r);  // "closed" / "restored" written just before the exit
+    if (r.awaiting_close) {  // died with the predecessor's HBM mapped: the kernel unmapped it
+      r.awaiting_close = false;
+      release_predecessors(r.index, "successor exited");
+    }
     if (r.fd >= 0) pump(r);  // drain what is already buffered
     if (r.nfd >= 0) {
       close(r.nfd);
@@ -1483,12 +1621,48 @@ class Supervisor {
         if (o.state == Rank::RUNNING) terminate(o, TermReason::FAILFAST);
   }
 
-  bool all_finished() {
+  // No rank will run again and none is running: only released / discarded processes may
+  // still be exiting.
+  bool ranks_settled() {
     for (auto& r : ranks_)
       if (r.state != Rank::DONE || r.pid > 0) return false;
     for (auto& sb : standby_)
       if (sb.pid > 0) return false;
-    return detached_.empty();
+    return true;
+  }
+
+  bool all_finished() { return ranks_settled() && detached_.empty(); }
+
+  // Give the task's node resources back: the stager (its HBM workdir images), the GPU lease
+  // files and the reservation; a reclaimed task goes back to the queue.  Released processes
+  // that are still tearing down are left to exit (traced, reaped, SIGKILLed after the grace
+  // period) -- they hold no state anybody needs: their checkpoint is in host memory.
+  void release_resources() {
+    if (resources_released_) return;
+    resources_released_ = true;
+    // predecessors still lingering for a successor that will never come (or is done)
+    for (auto& d : detached_)
+      if (d.pid > 0 && d.exit_requested_at <= 0 && !d.killed) {
+        kill(d.pid, SIGUSR2);
+        d.exit_requested_at = now();
+      }
+    stop_stager();
+    int unlinked = 0, exiting = 0;
+    for (auto& l : s_.leases) unlinked += unlink(l.c_str()) == 0;
+    for (auto& d : detached_) exiting += d.pid > 0;
+    event("resources-released", {std::to_string(unlinked) + " lease file(s)",
+                                 std::to_string(exiting) + " released process(es) still exiting"});
+    if (requeue_ && !stop_ && !timed_out_) {
+      bool pending = false;  // a rank that has not finished on its own
+      for (auto& r : ranks_)
+        if (r.reason == TermReason::REQUEUE && !(r.exit_signal == 0 && r.exit_code == 0))
+          pending = true;
+      if (pending) {
+        close_control();  // the next incarnation binds the same socket path
+        requeued_ = spawn_requeue();
+      }
+    }
+    dirty_ = true;
   }
 
   int finish() {
@@ -1517,19 +1691,10 @@ class Supervisor {
       }
       close_log(r);
     }
-    stop_stager();
-    for (auto& l : s_.leases) unlink(l.c_str());
-    close_control();
-    bool requeued = false;
-    if (requeue_ && !stop_ && !timed_out_) {
-      bool pending = false;  // a rank that has not finished on its own
-      for (auto& r : ranks_)
-        if (r.reason == TermReason::REQUEUE && !(r.exit_signal == 0 && r.exit_code == 0))
-          pending = true;
-      if (pending) requeued = spawn_requeue();
-    }
-    event("supervisor-exit", {requeued ? "requeued" : stop_ ? "stopped" : "all ranks finished"});
-    if (!requeued) write_state("stopped");
+    release_resources();
+    if (!requeued_) close_control();
+    event("supervisor-exit", {requeued_ ? "requeued" : stop_ ? "stopped" : "all ranks finished"});
+    if (!requeued_) write_state("stopped");
     signal_ready();
     return 0;
   }

@@ -19,6 +19,8 @@
 #   preempt      bench/bench_preempt.py --gb 100 (config 4 end to end)
 #   preempt-standby  the same with a warm standby successor (TPI_WARM_STANDBY=1)
 #   preempt-hot  hot standby (started with the rank) restoring behind the streamed spill
+#   preempt-170  the hot-standby run with a 170 GB rank (more than half of HBM)
+#   reclaim      bench/bench_reclaim.py --gb 100 (an on-demand task takes a spot task's GPU)
 #   handoff      bench/bench_handoff.py --gb 16 (same-GPU HBM hand-off alone, per copy route)
 #   async        bench/bench_async.py --gb 100
 #   concurrent   bench/bench_concurrent.py (config 5)
@@ -63,6 +65,10 @@ run_job() {
                        > "$OUT/preempt-standby.json" 2> "$OUT/preempt-standby.log" ;;
     preempt-hot) timeout -k 10 900 python bench/bench_preempt.py --gb 100 --hot $extra \
                    > "$OUT/preempt-hot.json" 2> "$OUT/preempt-hot.log" ;;
+    preempt-170) timeout -k 10 900 python bench/bench_preempt.py --gb 170 --hot $extra \
+                   > "$OUT/preempt-170.json" 2> "$OUT/preempt-170.log" ;;
+    reclaim) timeout -k 10 900 python bench/bench_reclaim.py --gb 100 $extra \
+               > "$OUT/reclaim.json" 2> "$OUT/reclaim.log" ;;
     handoff) timeout -k 10 600 python bench/bench_handoff.py $extra \
                > "$OUT/handoff.json" 2> "$OUT/handoff.log" ;;
     async) timeout -k 10 900 python bench/bench_async.py --gb 100 $extra \

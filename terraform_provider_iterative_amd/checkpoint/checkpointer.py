@@ -537,6 +537,19 @@ class Checkpointer:
                 return False
             time.sleep(0.002)
 
+    def _wait_writers(self) -> None:
+        """:meth:`wait_stream` before writing the region: a foreign writer that is still alive
+        after the timeout keeps its slot -- two processes must never write one slot."""
+        if self.wait_stream() is not False:
+            return
+        for slot in self.slots:
+            prog = slot.progress
+            owner = int(prog[5])
+            if (int(prog[0]) == PROGRESS_MAGIC and int(prog[4]) == STREAM_RUNNING
+                    and owner not in (0, os.getpid()) and _writer_alive(owner)):
+                raise CheckpointError("process %d is still streaming a checkpoint into this "
+                                      "region (TPI_STREAM_TIMEOUT passed)" % owner)
+
     def _target(self) -> Tuple[_Slot, int]:
         """(slot the next save writes, generation it gets): never the active one if there
         are two slots."""
@@ -621,7 +634,7 @@ class Checkpointer:
         runs behind the spill over the other direction of the link instead of after it.
         """
         self.wait_pending()
-        self.wait_stream()
+        self._wait_writers()
         slot, generation = self._target()
         self._invalidate(slot)
         zipped = self.codec == "tpz1"
@@ -725,7 +738,7 @@ class Checkpointer:
             self._snap = torch.empty(self.plan.total, dtype=torch.uint8, device=dev)
             self._snap_crcs = torch.empty(self.plan.ntiles, dtype=torch.int32, device=dev)
         t0 = time.perf_counter()
-        self.wait_stream()
+        self._wait_writers()
         slot, generation = self._target()
         self._invalidate(slot)
         self.engine.snapshot(self.plan, self._snap.data_ptr(), self._snap_crcs.data_ptr(),
@@ -798,7 +811,7 @@ class Checkpointer:
         import torch
 
         self.wait_pending()
-        self.wait_stream()
+        self._wait_writers()
         slot, generation = self._target()
         full = not slot.digests_valid
         self._invalidate(slot)
@@ -911,12 +924,14 @@ class Checkpointer:
     def _hbm_manifest_path(self) -> Optional[str]:
         return self.path + ".hbm" if self.path and self.engine is not None else None
 
-    def export_hbm(self) -> Optional[str]:
+    def export_hbm(self, metadata: Optional[Dict] = None) -> Optional[str]:
         """Preempted rank: publish HIP IPC handles of the bound tensors next to the spill file
         (``<path>.hbm``), so a successor on the same GPU can copy the state device to device
         (:meth:`restore_hbm`) while this process is still spilling it to host memory.  The
         caller must keep the tensors unchanged (and this process alive) until the successor
-        has restored -- the preemption handler does (it lingers until ``restored``)."""
+        has restored -- the preemption handler does (it lingers until ``restored``).
+        ``metadata``: that of the save this export accompanies; a successor resuming from the
+        HBM gets it even when the host copy failed."""
         manifest = self._hbm_manifest_path()
         if manifest is None:
             return None
@@ -949,7 +964,10 @@ class Checkpointer:
         doc = {"format": "tpi-hbm-1", "pid": os.getpid(), "device": bus.value.decode(),
                "entries_sha256": self._entries_digest, "total": self.plan.total,
                "tile_bytes": self.plan.tile_bytes, "allocations": handles, "where": where,
-               "segs": self.plan.segs.tobytes().hex(), "created": time.time()}
+               "segs": self.plan.segs.tobytes().hex(), "created": time.time(),
+               "metadata": metadata or {},
+               # the generation the save that follows this export will write
+               "generation": self._target()[1]}
         tmp = manifest + ".tmp"
         with open(tmp, "w") as handle_file:
             json.dump(doc, handle_file)
@@ -983,12 +1001,79 @@ class Checkpointer:
         """A live predecessor on this GPU exported its tensors for :meth:`restore_hbm`."""
         return self._hbm_doc() is not None
 
+    def hbm_metadata(self) -> Optional[Dict]:
+        """``{"generation", "metadata"}`` of the live predecessor's exported state (None: no
+        hand-off)."""
+        doc = self._hbm_doc()
+        if doc is None:
+            return None
+        return {"generation": doc.get("generation"), "metadata": dict(doc.get("metadata") or {})}
+
+    # The hand-off claim (``<path>.hbm.claim``, one pid): whoever creates it first owns the
+    # exported memory's fate.  A successor claims before it reads the manifest and removes its
+    # claim only after every IPC mapping is closed; a predecessor that wants to exit claims it
+    # itself, after which no successor can import (it falls back to the host copy).  So the
+    # exporter never exits while its memory is imported, whatever the supervisor does.
+    def _hbm_claim_path(self) -> Optional[str]:
+        manifest = self._hbm_manifest_path()
+        return manifest + ".claim" if manifest else None
+
+    def hbm_claim_owner(self) -> Optional[int]:
+        """pid holding the hand-off claim (None: unclaimed)."""
+        path = self._hbm_claim_path()
+        if path is None:
+            return None
+        try:
+            with open(path) as f:
+                return int(f.read().strip() or 0)
+        except (OSError, ValueError):
+            return None
+
+    def claim_hbm(self) -> bool:
+        """Take the hand-off claim for this process (a stale claim of a dead process is taken
+        over); False when another live process holds it."""
+        path = self._hbm_claim_path()
+        if path is None:
+            return False
+        for _ in range(3):
+            try:
+                fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_EXCL, 0o600)
+            except FileExistsError:
+                owner = self.hbm_claim_owner()
+                if owner == os.getpid():
+                    return True
+                if owner is not None and _writer_alive(owner):
+                    return False
+                try:  # its holder died: the claim is void
+                    os.remove(path)
+                except OSError:
+                    pass
+                continue
+            try:
+                os.write(fd, str(os.getpid()).encode())
+            finally:
+                os.close(fd)
+            return True
+        return False
+
+    def release_hbm_claim(self) -> None:
+        """Drop this process's claim (after its IPC mappings are closed)."""
+        if self.hbm_claim_owner() == os.getpid():
+            try:
+                os.remove(self._hbm_claim_path())
+            except OSError:
+                pass
+
     def restore_hbm(self, strict: bool = True) -> TransferResult:
         """Copy the state of a preempted predecessor on the same GPU straight from its HBM
         (HIP IPC; one fused copy pass + a read-back verify, every tile's digest checked) into the
         bound tensors."""
+        if not self.claim_hbm():
+            raise CheckpointError("the HBM hand-off is claimed by another process (withdrawn "
+                                  "by its exporter, or taken by another successor)")
         doc = self._hbm_doc()
         if doc is None:
+            self.release_hbm_claim()
             raise CheckpointError("no HBM hand-off from a live predecessor on this GPU")
         import torch
 
@@ -1023,6 +1108,7 @@ class Checkpointer:
             t1 = time.perf_counter()
             each(close_one)
             self.hbm_close_s = time.perf_counter() - t1
+            self.release_hbm_claim()  # nothing of the predecessor is mapped any more
 
         try:
             each(open_one)
@@ -1083,7 +1169,7 @@ class Checkpointer:
         like a streamed save's (progress block), so the device restore runs behind the file
         read instead of after it."""
         self.wait_pending()
-        self.wait_stream()
+        self._wait_writers()
         slot, generation = self._target()
         with open(path, "rb") as f:
             head = np.frombuffer(f.read(PREAMBLE + self.header_cap), np.uint8)

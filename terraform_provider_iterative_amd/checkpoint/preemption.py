@@ -117,10 +117,13 @@ def _collect_metadata(base: Dict) -> Dict:
     return meta
 
 
-def checkpoint_all(metadata: Optional[Dict] = None, on_stream=None) -> List[float]:
+def checkpoint_all(metadata: Optional[Dict] = None, on_stream=None,
+                   exported: Optional[List[Checkpointer]] = None) -> List[float]:
     """Save every registered checkpointer; returns per-checkpointer GB/s.  ``on_stream``
     (single checkpointer only): stream the save to the successor (see
-    :meth:`Checkpointer.save`); called once the successor may start."""
+    :meth:`Checkpointer.save`); called once the successor may start.  Checkpointers whose
+    tensors were exported for an HBM hand-off are appended to ``exported``: their memory must
+    stay allocated, and this process alive, until the successor is done with it."""
     t0 = time.perf_counter()
     meta = _collect_metadata({})
     meta.update(metadata or {})
@@ -130,7 +133,9 @@ def checkpoint_all(metadata: Optional[Dict] = None, on_stream=None) -> List[floa
         if on_stream is not None and len(_registered) == 1 and _hbm_handoff():
             try:  # the successor on this GPU copies our HBM while we spill to the host
                 t1 = time.perf_counter()
-                if ck.export_hbm():
+                if ck.export_hbm(meta):
+                    if exported is not None:
+                        exported.append(ck)
                     journal("checkpoint-hbm-export", "successor may copy device to device",
                             "hand-off check %.3f s" % _phase.get("handoff-check", 0.0),
                             "callbacks %.3f s" % t_cb,
@@ -309,21 +314,39 @@ def _hbm_handoff() -> bool:
     return os.environ.get("TPI_HBM_HANDOFF", "1") not in ("0", "false", "no")
 
 
-def _stream_handoff() -> bool:
+def _stream_handoff(safe: Optional[bool] = None) -> bool:
     """Release the successor when the spill *starts* (TPI_STREAM_HANDOFF, default on): it
     restores each chunk as it lands.  Needs one registered checkpointer, a supervisor to tell,
-    and room for the successor's copy of the state next to ours (:func:`_handoff_safe`)."""
+    and room for the successor's copy of the state next to ours (:func:`_handoff_safe`, or
+    the caller's ``safe`` when it already asked)."""
     if os.environ.get("TPI_STREAM_HANDOFF", "1") in ("0", "false", "no"):
         return False
-    return len(_registered) == 1 and bool(os.environ.get("TPI_NOTIFY_FD")) and _handoff_safe()
+    if len(_registered) != 1 or not os.environ.get("TPI_NOTIFY_FD"):
+        return False
+    return _handoff_safe() if safe is None else safe
+
+
+# The preemption save decides once whether a successor may run next to this process (one
+# device-memory query); notify_released() then follows that decision instead of asking again
+# (the answer can flip while the footprint sits near half of HBM).
+_handoff_decision: Optional[bool] = None
 
 
 def notify_released() -> bool:
     """Tell the supervisor the spill is complete (``TPI_NOTIFY_FD``), so it can respawn this
     rank now instead of after the exit; returns whether a notification was sent."""
-    if not os.environ.get("TPI_NOTIFY_FD") or not _handoff_safe():
+    safe = _handoff_decision if _handoff_decision is not None else _handoff_safe()
+    if not os.environ.get("TPI_NOTIFY_FD") or not safe:
         return False
     return _notify(b"released\n")
+
+
+def requeue_requested() -> bool:
+    """The supervisor is reclaiming this task for an on-demand one (``TPI_REQUEUE_FILE``
+    exists): no successor will run on this GPU, so the save hands nothing off, frees the HBM
+    and the process leaves right after it."""
+    path = os.environ.get("TPI_REQUEUE_FILE")
+    return bool(path) and os.path.exists(path)
 
 
 def _notify(message: bytes) -> bool:
@@ -402,9 +425,63 @@ def _linger() -> None:
     journal("predecessor-exit", "successor restored" if got else "linger timeout")
 
 
-def notify_restored() -> bool:
-    """Tell the supervisor this incarnation restored its state (its predecessor may go)."""
-    return _notify(b"restored\n")
+def _await_successor(ck: Checkpointer) -> str:
+    """After exporting ``ck``'s tensors for an HBM hand-off: return only once no successor
+    can still be reading them (:meth:`Checkpointer.claim_hbm` protocol) -- a successor that
+    claimed them closed its mappings (claim and manifest gone) or died, or nobody claimed them
+    and this process withdrew the offer by claiming them itself, which it does on SIGUSR2
+    (the supervisor: the successor restored elsewhere / closed / died) or after
+    ``TPI_LINGER_SECONDS``.  A live claimer is waited for up to ``TPI_HANDOFF_CLOSE_TIMEOUT``
+    (default 600 s).  Returns how it ended (journalled)."""
+    try:
+        soft = float(os.environ.get("TPI_LINGER_SECONDS", "20"))
+    except ValueError:
+        soft = 20.0
+    try:
+        hard = float(os.environ.get("TPI_HANDOFF_CLOSE_TIMEOUT", "600"))
+    except ValueError:
+        hard = 600.0
+    from .checkpointer import _writer_alive
+
+    sys.stdout.flush()
+    t0 = time.monotonic()
+    me = os.getpid()
+    manifest = ck._hbm_manifest_path()
+    while True:
+        owner = ck.hbm_claim_owner()
+        waited = time.monotonic() - t0
+        if owner == me:
+            how = "withdrawn"
+        elif owner is None:
+            if manifest and not os.path.exists(manifest):
+                how = "successor closed"  # claimed, copied, unmapped, claim dropped
+            elif (_usr2.is_set() or waited >= max(soft, 0.0)) and ck.claim_hbm():
+                how = "withdrawn"
+            else:
+                how = None
+        elif not _writer_alive(owner):
+            how = "successor died"
+        elif waited >= hard:
+            how = "timeout with the hand-off still mapped by pid %d" % owner
+        else:
+            how = None
+        if how is not None:
+            journal("predecessor-exit", how, "waited %.3f s" % waited)
+            return how
+        _usr2.wait(0.005)
+        if _usr2.is_set() and owner not in (None, me):
+            time.sleep(0.005)  # a live claimer: SIGUSR2 alone is no reason to go
+
+
+def notify_restored(hbm: bool = False) -> bool:
+    """Tell the supervisor this incarnation restored its state.  From the host region its
+    predecessor may go now; from the predecessor's HBM (``hbm``) only after :func:`notify_closed`."""
+    return _notify(b"restored hbm\n" if hbm else b"restored\n")
+
+
+def notify_closed() -> bool:
+    """The predecessor's exported HBM is no longer mapped here: it may exit."""
+    return _notify(b"closed\n")
 
 
 def fallback_seconds() -> float:
@@ -447,60 +524,131 @@ def _note_signal(signum: int) -> bool:
 
 
 def _save_and_exit(consistency: str, ordinal: Optional[int] = None) -> None:
-    """Run the preemption save once and exit; returns only if another thread is saving."""
+    """Run the preemption save once and exit; returns only if another thread is saving.
+
+    * preemption (a successor follows on this GPU): stream the spill to it, export the HBM
+      for a device-to-device copy when both copies fit, and stay until the successor no
+      longer needs this process (:func:`_await_successor` / :func:`_linger`);
+    * reclaim (:func:`requeue_requested`: an on-demand task takes the GPU): plain save, free
+      the HBM, ``released`` -- the supervisor hands the GPU over at once -- and leave;
+    * a failed spill after an HBM export still waits for the successor: its device copy is
+      then the only good one.
+    """
+    global _handoff_decision
     if not _save_lock.acquire(blocking=False):
         return
     _fired.set()
     signum = int(_signal_info.get("signum", signal.SIGTERM))
     t0 = time.perf_counter()
-    released = []
-    stream_ok = False
+    released: List[bool] = []
+    exported: List[Checkpointer] = []
+    requeue = requeue_requested()
+    t_safe = time.perf_counter()
+    _handoff_decision = safe = _handoff_safe()  # evaluated once: one device-memory query
+    stream_ok = not requeue and _stream_handoff(safe)
+    _phase["handoff-check"] = time.perf_counter() - t_safe
 
     def stream_started():
         # the successor starts now and restores behind the spill (other PCIe direction);
         # journalled first, so the phase journal orders it before the supervisor's release
-        if stream_ok:
-            journal("checkpoint-streaming", "successor may start")
+        journal("checkpoint-streaming", "successor may start")
         if notify_released():
             released.append(True)
 
-    meta = {"reason": "preempted", "signal": signum, "consistency": consistency}
+    meta = {"reason": "requeued" if requeue else "preempted", "signal": signum,
+            "consistency": consistency}
     if _last_step is not None:
         meta["step"] = _last_step
     if ordinal is not None:
         meta["boundary"] = ordinal
+    code = 1
+    at_boundary = consistency == "boundary" or (
+        consistency == "signal" and threading.current_thread() is threading.main_thread())
     try:
-        t_safe = time.perf_counter()
-        stream_ok = _stream_handoff()  # evaluated once: one device-memory query
-        _phase["handoff-check"] = time.perf_counter() - t_safe
-        rates = checkpoint_all(meta, on_stream=stream_started if stream_ok else None)
+        rates = checkpoint_all(meta, on_stream=stream_started if stream_ok else None,
+                               exported=exported)
         print("tpi: preemption checkpoint saved in %.3fs (%s GB/s)" % (
             time.perf_counter() - t0, ", ".join("%.1f" % r for r in rates)), flush=True)
         code = PREEMPTED_EXIT_CODE
-        if not released and consistency == "boundary" and _release_hbm_enabled() and \
-                not _handoff_safe():
-            # a state too big for two copies in HBM: the successor could only start after
-            # this process exits (and unpins its region, ~1.4 s per 100 GB).  Free our HBM
-            # now instead -- we are at a step boundary on the main thread, nothing will touch
-            # the tensors again -- and hand off while the host region stays pinned.
+        freed = 0
+        if (not released and not exported and consistency == "boundary"
+                and _release_hbm_enabled() and (requeue or not safe)):
+            # a reclaim, or a state too big for two copies in HBM: the next process on this
+            # GPU could only allocate after our exit (and the kernel's unpinning of our region,
+            # ~1.4 s per 100 GB).  Free our HBM now instead -- we are at a step boundary on
+            # the main thread, nothing will touch the tensors again, nobody imported them --
+            # and hand off while the host region stays pinned.
             t1 = time.perf_counter()
             freed = _release_device_memory()
             journal("device-memory-released", "%.1f GB" % (freed / 1e9),
                     "%.3f s" % (time.perf_counter() - t1))
-        if released or notify_released():
-            if not released:
-                journal("checkpoint-released", "successor may start")
-            _linger()
-        for ck in _registered:  # an HBM hand-off nobody took is stale once we exit
-            manifest = ck._hbm_manifest_path()
-            if manifest and os.path.exists(manifest):
-                try:
-                    os.remove(manifest)
-                except OSError:
-                    pass
+        if not released and (safe or freed) and os.environ.get("TPI_NOTIFY_FD"):
+            if _notify(b"released\n"):
+                released.append(True)
+                journal("checkpoint-released", "reclaim: the GPU may go" if requeue
+                        else "successor may start")
+        if released and not requeue:
+            if exported:
+                _await_successor(exported[0])
+            else:
+                _linger()
     except Exception as error:
         print("tpi: preemption checkpoint FAILED: %s" % error, file=sys.stderr, flush=True)
-        code = 1
+        journal("checkpoint-failed", str(error))
+        if exported:  # a successor may be copying our HBM: now the only good copy
+            _await_successor(exported[0])
+    _withdraw_handoffs()
+    sys.stdout.flush()
+    _teardown(code, at_boundary)
+
+
+def _withdraw_handoffs() -> None:
+    """An HBM hand-off nobody took is stale once we exit: claim it (no successor can start
+    importing now), then remove the manifest and the claim."""
+    for ck in _registered:
+        manifest = ck._hbm_manifest_path()
+        if not manifest:
+            continue
+        owner = ck.hbm_claim_owner()
+        if owner not in (None, os.getpid()):
+            continue  # a successor's (alive: timeout) -- it removes it after closing
+        if os.path.exists(manifest) and not ck.claim_hbm():
+            continue
+        for path in (manifest, ck._hbm_claim_path()):
+            try:
+                os.remove(path)
+            except OSError:
+                pass
+
+
+def _teardown(code: int, release_device: bool = True) -> None:
+    """Give back this process's HBM and host-region pinning explicitly, each phase timed in
+    the journal (``predecessor-teardown``), then ``os._exit``.  What remains -- the kernel's
+    own teardown of the address space and GPU context -- shows in the supervisor's
+    ``exit-trace`` events.  ``release_device`` only when no other thread may still run device
+    work on the tensors (a boundary save on the main thread).  ``TPI_EXPLICIT_TEARDOWN=0``:
+    straight to ``os._exit`` (the kernel does all of it)."""
+    if os.environ.get("TPI_EXPLICIT_TEARDOWN", "1") in ("0", "false", "no"):
+        os._exit(code)
+    phases = []
+    try:
+        t0 = time.perf_counter()
+        if release_device:
+            freed = _release_device_memory()
+            if freed:
+                phases.append("hbm %.1f GB %.3f s" % (freed / 1e9, time.perf_counter() - t0))
+        for ck in _registered:
+            region = getattr(ck, "region", None)
+            if region is None or not getattr(region, "registered", False):
+                continue
+            t1 = time.perf_counter()
+            region.close()  # unregister (unpin) + unmap; a /dev/shm file keeps its pages
+            phases.append("host region %.1f GB %.3f s" % (region.size / 1e9,
+                                                          time.perf_counter() - t1))
+        if phases:
+            journal("predecessor-teardown", *phases)
+    except Exception as error:  # never keep a preempted process alive over its teardown
+        journal("predecessor-teardown-failed", str(error))
     sys.stdout.flush()
     os._exit(code)
 
@@ -632,7 +780,6 @@ def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None,
     """
     failure: Optional[CheckpointError] = None
     header = checkpointer.latest()  # complete, or still streaming in from the predecessor
-    newest = header
     if generation is not None:
         header = next(({"generation": c["generation"], "metadata": c["metadata"]}
                        for c in checkpointer.candidates() if c["generation"] == generation),
@@ -643,22 +790,31 @@ def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None,
     if meta.get("consistency") in ("torn-risk", "signal"):
         journal("checkpoint-torn-risk", "restoring a save taken at %s" % meta["consistency"],
                 "step %s" % meta.get("step"))
-    if header is not None and header is newest and checkpointer.hbm_ready():
+    # The HBM copy is the state of the predecessor's last save (its boundary): the newest
+    # state there is -- newer than a host copy whose spill failed, present even when none
+    # completed.  A caller that asks for a specific generation (resume_consistent: the copy the
+    # gang agreed on) gets the HBM only when it is that generation.
+    hbm = checkpointer.hbm_metadata()
+    if hbm is not None and generation is not None and hbm["generation"] != generation:
+        hbm = None
+    if hbm is not None:
         try:  # the predecessor on this GPU is alive and exported its tensors: copy from HBM
             res = checkpointer.restore_hbm()
             journal("checkpoint-restored", "HBM hand-off", *_describe(res),
                     "ipc open %.3f s" % getattr(checkpointer, "hbm_open_s", 0.0))
-            notify_restored()
+            notify_restored(hbm=True)
 
             def behind():  # after "restored": the unmapping, then the host copy's durability
                 checkpointer.wait_hbm_close()
                 journal("hbm-handoff-closed",
                         "ipc close %.3f s" % getattr(checkpointer, "hbm_close_s", 0.0))
+                notify_closed()  # the predecessor may exit now
                 t0 = time.perf_counter()
                 done = checkpointer.wait_stream(timeout=float(os.environ.get(
                     "TPI_DURABLE_TIMEOUT", "600")))
                 if done is None:  # no spill running (any more): is the restored copy there?
-                    if checkpointer.durable(header.get("generation", 0)):
+                    if checkpointer.durable(hbm["generation"] or
+                                            (header or {}).get("generation") or 0):
                         done = True
                     elif not checkpointer.closing:
                         done = False
@@ -676,7 +832,9 @@ def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None,
                             % (time.perf_counter() - t0))
 
             checkpointer.watch(behind, "tpi-handoff-durability")
-            return header.get("metadata", {})
+            # the exported state is the predecessor's last boundary: newer than a host copy
+            # whose spill failed, and there even when no host copy completed at all
+            return hbm["metadata"] or (header or {}).get("metadata", {})
         except Exception as error:  # fall back to the host region
             journal("checkpoint-hbm-failed", str(error))
     if header is not None:

@@ -298,3 +298,125 @@ def test_on_demand_task_reclaims_a_spot_task_on_the_gpu(cloud):
     assert od_codes.index("queued") < od_codes.index("reclaim") < od_codes.index("placed")
     od.delete()
     spot.delete()
+
+
+FAILING_SPILL = r'''#!%(python)s
+import os, sys, time
+sys.path.insert(0, %(root)r)
+import torch
+from terraform_provider_iterative_amd.checkpoint import Checkpointer, CheckpointError, preemption
+dev = torch.device("cuda", 0)
+g = torch.Generator(device=dev).manual_seed(11)
+state = {"w": torch.zeros(32 << 20, device=dev), "noise": torch.randn(1 << 20, device=dev, generator=g)}
+ck = Checkpointer(state, path=os.path.join(os.environ["TPI_DATA_DIRECTORY"], ".spill"))
+meta = preemption.resume(ck)
+start = (meta or {}).get("step", 0)
+print("start", start, "restart", os.environ["TPI_RESTART_COUNT"], flush=True)
+if start == 0:
+    _save = ck.save
+    def failing_save(metadata=None, on_stream=None):
+        on_stream()      # "released": the successor starts and finds the exported HBM
+        time.sleep(0.5)
+        raise CheckpointError("host spill failed (injected)")
+    ck.save = failing_save
+preemption.register(ck)
+preemption.install()
+for step in range(start, 40):
+    state["w"].add_(1)
+    torch.cuda.synchronize()
+    time.sleep(0.03)
+    preemption.step(step + 1)
+print("final", int(state["w"][0].item()), int(state["w"][-1].item()), flush=True)
+'''
+
+
+def test_failed_spill_hands_off_from_hbm_and_waits_for_close(cloud):
+    """The host spill of a preempted rank fails after it exported its HBM: the successor
+    restores from the predecessor's HBM (the only good copy), and the predecessor exits
+    (code 1) only after the successor closed its IPC mappings."""
+    spec = Task(size=Size(machine="m+mi355x"),
+                environment=Environment(script=FAILING_SPILL % {"python": sys.executable,
+                                                                 "root": ROOT},
+                                        timeout=600, variables=Variables({"TPI_TASK": "true"})))
+    task = backends.new(cloud, new_deterministic_identifier("gpu-failed-spill"), spec)
+    task.create()
+    deadline = time.time() + 300
+    while time.time() < deadline and "start 0" not in "".join(task.logs()):
+        time.sleep(0.1)
+    time.sleep(0.5)
+    task.preempt()
+    status = task.wait(300)
+    logs = task.logs()
+    assert status["succeeded"] == 1, logs
+    resumed = int(logs[1].split("start ")[1].split()[0])
+    assert resumed > 0 and "final 40 40" in logs[1], logs
+    events = task.events()
+    codes = [e.code for e in events]
+    restored = [e for e in events if e.code == "checkpoint-restored"]
+    assert restored and restored[0].description[1] == "HBM hand-off", restored
+    t = {c: next(e.time for e in events if e.code == c)
+         for c in ("checkpoint-failed", "hbm-handoff-closed", "predecessor-exit",
+                   "rank-released-exit")}
+    assert t["checkpoint-failed"] <= t["predecessor-exit"]
+    assert t["hbm-handoff-closed"] <= t["predecessor-exit"] <= t["rank-released-exit"], codes
+    exit_ev = next(e for e in events if e.code == "rank-released-exit")
+    assert "code 1" in exit_ev.description, exit_ev
+    assert "checkpoint-not-durable" in codes
+    task.delete()
+
+
+HOLDING_EXPORTER = r'''
+import os, sys
+sys.path.insert(0, %(root)r)
+import torch
+from terraform_provider_iterative_amd.checkpoint import TrainingState
+torch.manual_seed(7)
+model = torch.nn.Sequential(torch.nn.Linear(256, 512), torch.nn.Linear(512, 64)).cuda()
+state = TrainingState(model, path=%(spill)r)
+meta = {"step": 12, "reason": "preempted", "consistency": "boundary"}
+assert state.checkpointer.export_hbm(meta)
+state.checkpointer.save(meta, on_stream=lambda: None)
+print("exported", flush=True)
+sys.stdin.readline()  # hold the memory until the successor is done
+'''
+
+
+def test_resume_consistent_takes_the_hbm_hand_off(tmp_path):
+    """ADVICE r3: resume_consistent passes the agreed generation; when that is the exported
+    state's generation the device-to-device copy must be used (0 bytes over PCIe)."""
+    import subprocess
+
+    import torch.distributed as dist
+
+    from terraform_provider_iterative_amd.checkpoint import TrainingState
+
+    spill = str(tmp_path / "spill")
+    proc = subprocess.Popen([sys.executable, "-c", HOLDING_EXPORTER % {"root": ROOT,
+                                                                       "spill": spill}],
+                            stdin=subprocess.PIPE, stdout=subprocess.PIPE)
+    try:
+        assert proc.stdout.readline().strip() == b"exported"
+        torch.manual_seed(7)
+        want = torch.nn.Sequential(torch.nn.Linear(256, 512), torch.nn.Linear(512, 64)).cuda()
+        model = torch.nn.Sequential(torch.nn.Linear(256, 512), torch.nn.Linear(512, 64)).cuda()
+        for p in model.parameters():
+            p.data.zero_()
+        dist.init_process_group("gloo", store=dist.FileStore(str(tmp_path / "store"), 1),
+                                rank=0, world_size=1)
+        try:
+            state = TrainingState(model, path=spill)
+            meta = state.resume_consistent()
+            torch.cuda.synchronize()
+            assert meta["step"] == 12
+            assert state.checkpointer.last_restore.wire_bytes == 0  # device to device
+            state.checkpointer.wait_hbm_close()
+            assert state.checkpointer.hbm_claim_owner() is None
+            for a, b in zip(model.parameters(), want.parameters()):
+                assert torch.equal(a, b)
+            state.close()
+        finally:
+            dist.destroy_process_group()
+    finally:
+        proc.stdin.write(b"\n")
+        proc.stdin.flush()
+        proc.wait(60)

@@ -1,0 +1,358 @@
+"""The hand-off protocol between a preempted rank, its successor and the supervisor.
+
+Reference: a reclaimed spot VM is replaced and restores the bucket's ``data/`` (machine-script
+.sh.tpl:89); the scaling group goes to 0 right after the task exits (tpl:10-15, 51;
+resource_auto_scaling_group.go:188-199).  Here the successor copies the predecessor's HBM over
+IPC, so the predecessor must outlive every mapping of its memory ("closed"), and the node's
+resources go back as soon as the ranks are down -- not when the last released process has
+finished its kernel teardown.
+
+* supervisor: SIGUSR2 to the predecessor only after the successor's ``closed`` (or its
+  death), never on ``restored hbm``; leases released before a slow released process is reaped;
+  its exit traced (``exit-trace``);
+* rank: :func:`preemption._await_successor` holds the exporter until the claim protocol says
+  nobody maps its memory -- on the success path and after a failed spill;
+* reclaim: a queued on-demand task starts while the victim's process is still exiting.
+"""
+import json
+import os
+import signal
+import subprocess
+import sys
+import time
+
+import pytest
+
+from terraform_provider_iterative_amd import _build
+from terraform_provider_iterative_amd.checkpoint import preemption
+from terraform_provider_iterative_amd.checkpoint.checkpointer import Checkpointer
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def binary():
+    return _build.build_supervisor()
+
+
+def _spec(tmp_path, script, **extra):
+    task = tmp_path / "task"
+    for d in ("data", "reports", "supervisor"):
+        (task / d).mkdir(parents=True, exist_ok=True)
+    path = task / "supervisor" / "script"
+    path.write_text(script)
+    path.chmod(0o755)
+    spec = {"task_id": "tpi-handoff-test", "task_dir": str(task), "workdir": str(task / "data"),
+            "script": str(path), "env": {"PATH": os.environ["PATH"]}, "parallelism": 1,
+            "ranks": [{"gpus": "", "rank_gpus": ""}], "grace_seconds": 20,
+            "master_port": 29998}
+    spec.update(extra)
+    spec_path = task / "supervisor" / "spec.json"
+    spec_path.write_text(json.dumps(spec))
+    return task, str(spec_path)
+
+
+def _events(task):
+    with open(task / "supervisor" / "events.jsonl") as handle:
+        return [json.loads(line) for line in handle if line.strip()]
+
+
+def _wait_file(path, timeout=30):
+    deadline = time.time() + timeout
+    while time.time() < deadline:
+        if os.path.exists(path) and os.path.getsize(path):
+            return
+        time.sleep(0.01)
+    raise AssertionError("%s never appeared" % path)
+
+
+# A rank that speaks the notify protocol by hand (no torch): incarnation 0 is preempted,
+# releases, waits for SIGUSR2 and records when it came; incarnation 1 "restores from its HBM"
+# and, unless told to die first, closes the hand-off one second later.
+PROTOCOL_RANK = r'''#!%(python)s
+import os, signal, sys, time
+out = %(out)r
+def note(name):
+    with open(os.path.join(out, name), "w") as f:
+        f.write(repr(time.time()))
+restart = int(os.environ["TPI_RESTART_COUNT"])
+fd = int(os.environ["TPI_NOTIFY_FD"])
+if restart == 0:
+    signal.pthread_sigmask(signal.SIG_BLOCK, {signal.SIGTERM, signal.SIGUSR2})
+    print("ready", flush=True)
+    signal.sigwait({signal.SIGTERM})
+    os.write(fd, b"released\n")
+    signal.sigwait({signal.SIGUSR2})
+    note("usr2")
+    time.sleep(%(slow_exit)r)  # a slow teardown after the exit request
+    os._exit(143)
+os.write(fd, b"restored hbm\n")
+time.sleep(1.0)
+if %(die)r:
+    note("successor-exit")
+    os._exit(0)
+note("closed")
+os.write(fd, b"closed\n")
+time.sleep(0.2)
+print("successor done", flush=True)
+'''
+
+
+@pytest.mark.parametrize("die", [False, True], ids=["closed", "successor-dies"])
+def test_predecessor_released_only_after_closed(binary, tmp_path, die):
+    out = tmp_path / "out"
+    out.mkdir()
+    lease = tmp_path / "gpu-0.lease"
+    lease.write_text("{}")
+    script = PROTOCOL_RANK % {"python": sys.executable, "out": str(out), "die": die,
+                              "slow_exit": 2.0}
+    task, spec = _spec(tmp_path, script, leases=[str(lease)])
+    sup = subprocess.Popen([binary, spec], stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    try:
+        deadline = time.time() + 30
+        while time.time() < deadline and not any(
+                "ready" in (task / "reports" / n).read_text()
+                for n in os.listdir(task / "reports") if n.startswith("task-")):
+            time.sleep(0.02)
+        sup.send_signal(signal.SIGUSR1)  # preempt
+        sup.wait(60)
+    finally:
+        if sup.poll() is None:
+            sup.kill()
+    usr2 = float((out / "usr2").read_text())
+    after = float((out / ("successor-exit" if die else "closed")).read_text())
+    # "restored hbm" alone never lets the predecessor go: its memory is still mapped
+    assert usr2 >= after, (usr2, after)
+    events = _events(task)
+    codes = [e["code"] for e in events]
+    req = [e for e in events if e["code"] == "predecessor-exit-requested"]
+    assert len(req) == 1, codes
+    assert req[0]["description"][-1] == ("successor exited" if die else
+                                         "successor closed the HBM hand-off")
+    # the successor finished; the predecessor takes 2 s more to exit: the lease is released
+    # before it is reaped, and its exit is traced meanwhile
+    t = {c: next(e["time"] for e in events if e["code"] == c)
+         for c in ("resources-released", "rank-released-exit", "supervisor-exit")}
+    assert t["resources-released"] < t["rank-released-exit"] <= t["supervisor-exit"]
+    assert t["rank-released-exit"] - t["resources-released"] > 0.5
+    assert not lease.exists()
+    traces = [e for e in events if e["code"] == "exit-trace"]
+    assert traces and all(e["description"][3].startswith("+") for e in traces), traces[:3]
+    released_exit = next(e for e in events if e["code"] == "rank-released-exit")
+    assert released_exit["description"][-1].endswith("after the exit request")
+
+
+# -- the exporter side: _await_successor / _save_and_exit with a stand-in checkpointer ----------
+
+class _FakeHandoff:
+    """The parts of a Checkpointer the hand-off protocol touches (the manifest is what
+    export_hbm() would write; no GPU)."""
+
+    def __init__(self, path):
+        self.path = path
+        self.region = None
+
+    def _hbm_manifest_path(self):
+        return self.path + ".hbm"
+
+    _hbm_claim_path = Checkpointer._hbm_claim_path
+    hbm_claim_owner = Checkpointer.hbm_claim_owner
+    claim_hbm = Checkpointer.claim_hbm
+    release_hbm_claim = Checkpointer.release_hbm_claim
+
+
+def _claimer(path, hold, remove_manifest=True, die=False):
+    """A "successor" process: claims the hand-off, holds it ``hold`` s, then closes (drops
+    manifest + claim) -- or dies holding it."""
+    code = ("import os, sys, time\nsys.path.insert(0, %r)\n"
+            "from tests.test_handoff_protocol import _FakeHandoff\n"
+            "ck = _FakeHandoff(%r)\nassert ck.claim_hbm()\nprint('claimed', flush=True)\n"
+            "time.sleep(%r)\n"
+            "if %r:\n    os._exit(0)\n"
+            "if %r:\n    os.remove(ck._hbm_manifest_path())\n"
+            "ck.release_hbm_claim()\n" % (ROOT, path, hold, die, remove_manifest))
+    proc = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE)
+    assert proc.stdout.readline().strip() == b"claimed"
+    return proc
+
+
+@pytest.fixture()
+def exporter(tmp_path, monkeypatch):
+    ck = _FakeHandoff(str(tmp_path / "spill"))
+    with open(ck._hbm_manifest_path(), "w") as f:
+        f.write("{}")
+    monkeypatch.setattr(preemption, "_usr2", type(preemption._usr2)())
+    monkeypatch.setenv("TPI_LINGER_SECONDS", "30")
+    monkeypatch.delenv("TPI_EVENTS_FILE", raising=False)
+    return ck
+
+
+def test_exporter_waits_for_the_claimer_to_close_even_after_sigusr2(exporter):
+    proc = _claimer(exporter.path, hold=1.0)
+    preemption._usr2.set()  # a supervisor that says "go" too early
+    t0 = time.monotonic()
+    how = preemption._await_successor(exporter)
+    took = time.monotonic() - t0
+    proc.wait(10)
+    assert how == "successor closed" and took >= 0.8, (how, took)
+
+
+def test_exporter_goes_when_the_claimer_dies(exporter):
+    proc = _claimer(exporter.path, hold=0.5, die=True)
+    how = preemption._await_successor(exporter)
+    proc.wait(10)
+    assert how == "successor died"
+
+
+def test_exporter_withdraws_an_unclaimed_offer(exporter):
+    preemption._usr2.set()
+    assert preemption._await_successor(exporter) == "withdrawn"
+    assert exporter.hbm_claim_owner() == os.getpid()
+    # a successor arriving now cannot import any more: it restores from the host copy
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from tests.test_handoff_protocol import _FakeHandoff\n"
+            "print(_FakeHandoff(%r).claim_hbm())" % (ROOT, exporter.path))
+    assert subprocess.check_output([sys.executable, "-c", code]).strip() == b"False"
+
+
+def test_exporter_withdraws_after_the_linger_timeout(exporter, monkeypatch):
+    monkeypatch.setenv("TPI_LINGER_SECONDS", "0.3")
+    t0 = time.monotonic()
+    assert preemption._await_successor(exporter) == "withdrawn"
+    assert time.monotonic() - t0 >= 0.3
+
+
+EXPORTER = r'''
+import os, sys, time
+sys.path.insert(0, %(root)r)
+from terraform_provider_iterative_amd.checkpoint import preemption
+from terraform_provider_iterative_amd.checkpoint.checkpointer import CheckpointError
+from tests.test_handoff_protocol import _FakeHandoff
+
+class Res:
+    bytes = wire_bytes = 1000
+    seconds = 0.1
+    gbps = 1e-5
+
+class Exporting(_FakeHandoff):
+    def export_hbm(self, metadata=None):
+        with open(self._hbm_manifest_path(), "w") as f:
+            f.write("{}")
+        return self._hbm_manifest_path()
+    def save(self, metadata, on_stream=None):
+        on_stream()  # "released": the successor starts and may import our HBM
+        time.sleep(0.3)
+        if %(fail)r:
+            raise CheckpointError("host spill failed (injected)")
+        return Res()
+
+preemption.register(Exporting(%(path)r))
+preemption.install()  # SIGUSR2 handler, as in every rank
+preemption._save_and_exit("boundary")
+'''
+
+
+@pytest.mark.parametrize("fail", [False, True], ids=["spill-ok", "spill-failed"])
+def test_preempted_rank_never_exits_while_its_hbm_is_claimed(tmp_path, fail):
+    """_save_and_exit end to end with a fake notify pipe: after "released" a successor claims
+    the export; the rank must stay alive until the claim is dropped (spill ok: code 143;
+    spill failed: code 1 -- the HBM copy is the only good one, so it waits just the same)."""
+    path = str(tmp_path / "spill")
+    r, w = os.pipe()
+    env = dict(os.environ, TPI_NOTIFY_FD=str(w), TPI_LINGER_SECONDS="30",
+               TPI_EVENTS_FILE=str(tmp_path / "events.jsonl"))
+    env.pop("TPI_REQUEUE_FILE", None)
+    proc = subprocess.Popen([sys.executable, "-c", EXPORTER % {"root": ROOT, "path": path,
+                                                                 "fail": fail}],
+                            env=env, pass_fds=(w,))
+    os.close(w)
+    try:
+        assert os.read(r, 64) == b"released\n"
+        ck = _FakeHandoff(path)
+        assert ck.claim_hbm()  # this test process is the successor
+        os.kill(proc.pid, signal.SIGUSR2)  # an early "go" must not matter while claimed
+        time.sleep(1.5)
+        assert proc.poll() is None, "the exporter exited while its HBM was claimed"
+        os.remove(ck._hbm_manifest_path())  # copy done ...
+        ck.release_hbm_claim()              # ... and every mapping closed
+        assert proc.wait(10) == (1 if fail else preemption.PREEMPTED_EXIT_CODE)
+    finally:
+        if proc.poll() is None:
+            proc.kill()
+        os.close(r)
+    with open(tmp_path / "events.jsonl") as f:
+        events = [json.loads(line) for line in f]
+    exit_ev = [e for e in events if e["code"] == "predecessor-exit"]
+    assert exit_ev and exit_ev[0]["description"][1] == "successor closed", events
+    assert not os.path.exists(path + ".hbm") and not os.path.exists(path + ".hbm.claim")
+
+
+# -- reclaim: the on-demand task starts while the victim is still exiting ----------------------
+
+SPOT = r'''#!%(python)s
+import os, sys, time
+sys.path.insert(0, %(root)r)
+import torch
+from terraform_provider_iterative_amd.checkpoint import Checkpointer, preemption
+state = {"w": torch.zeros(1000, dtype=torch.float64)}
+ck = Checkpointer(state, path=os.path.join(os.environ["TPI_DATA_DIRECTORY"], ".spill"),
+                  tile_bytes=4096)
+meta = preemption.resume(ck)
+start = (meta or {}).get("step", 0)
+print("start", start, flush=True)
+preemption.register(ck)
+preemption.install()
+_exit = preemption._teardown
+def slow_teardown(code, release_device=True):  # a victim whose kernel teardown is slow
+    time.sleep(3.0)
+    _exit(code, release_device)
+preemption._teardown = slow_teardown
+for step in range(start, %(steps)d):
+    state["w"] += 1
+    time.sleep(0.05)
+    preemption.step(step + 1)
+print("final", int(state["w"][0]), flush=True)
+'''
+
+
+def test_reclaimed_gpu_goes_to_the_on_demand_task_before_the_victim_is_reaped(tmp_path,
+                                                                                monkeypatch):
+    from tests.test_scheduler import _cloud, _task
+
+    monkeypatch.setenv("TPI_MI355X_GPUS", "0")
+    monkeypatch.setenv("TPI_NODE_CPUS", "0-31")
+    monkeypatch.setenv("TPI_NODE_MEMORY_MB", "512000")
+    cloud = _cloud(tmp_path)
+    spot = _task(cloud, "spot-slow", SPOT % {"python": sys.executable, "root": ROOT,
+                                             "steps": 30}, spot=0)
+    spot.create()
+    deadline = time.time() + 60
+    while time.time() < deadline and "start 0" not in "".join(spot.logs()):
+        time.sleep(0.05)
+    time.sleep(0.3)
+    od = _task(cloud, "ondemand-fast", "#!/bin/sh\necho on-demand running\n")
+    t_apply = time.time()
+    od.create()
+    deadline = time.time() + 60
+    while time.time() < deadline and "on-demand running" not in "".join(od.logs()):
+        time.sleep(0.01)
+    t_first_log = time.time()
+    deadline = time.time() + 120
+    while time.time() < deadline and (spot.supervisor_running() or od.supervisor_running()
+                                      or spot.status()["succeeded"] < 1):
+        time.sleep(0.05)
+    spot_ev = {e.code: e.time.timestamp() for e in reversed(spot.events())}  # first of each
+    od_start = next(e.time.timestamp() for e in od.events() if e.code == "rank-start")
+    assert spot.status()["succeeded"] == 1 and od.status()["succeeded"] == 1, spot.logs()
+    # saved -> released (no linger, no hand-off) -> resources back -> on-demand starts,
+    # all while the victim still sleeps in its teardown
+    assert spot_ev["checkpoint-released"] <= spot_ev["resources-released"] < od_start
+    assert od_start < spot_ev["rank-released-exit"], (od_start, spot_ev)
+    assert t_first_log - t_apply < 3.0, t_first_log - t_apply
+    codes = [e.code for e in spot.events()]
+    assert "checkpoint-streaming" not in codes and "checkpoint-hbm-export" not in codes
+    assert "exit-trace" in codes
+    logs = spot.logs()
+    assert "final 30" in logs[-1], logs
+    od.delete()
+    spot.delete()

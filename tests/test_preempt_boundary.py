@@ -414,5 +414,5 @@ def test_big_state_rank_releases_hbm_before_the_hand_off(cloud):
     idx = [codes.index(c) for c in order]
     assert idx == sorted(idx), list(zip(order, idx))
     exits = [e for e in events if e.code == "rank-released-exit"]
-    assert exits[0].description[-1] == "code 143"
+    assert "code 143" in exits[0].description
     task.delete()
