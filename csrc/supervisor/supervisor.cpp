@@ -236,6 +236,14 @@ struct Spec {
   // host memory per rank (its process group; 0 = none) and the task's workdir size
   uint64_t rank_memory_kb = 0;
   uint64_t disk_limit_bytes = 0;
+  // hard cap: each rank's processes in a memory cgroup (v2 memory.max / v1
+  // memory.limit_in_bytes) of rank_memory + headroom -- "auto" (the hierarchy this process is
+  // in, when writable), "off", or a cgroup directory; the poll below keeps enforcing the limit
+  // itself (without checkpoint regions), the cgroup stops a runaway allocation between polls
+  std::string cgroup = "auto";
+  int cgroup_version = 0;
+  uint64_t cgroup_headroom_kb = 0;  // checkpoint regions (shm pages charge the first toucher)
+  std::string regions_path;         // checkpoint regions announced by the ranks (host.py)
   double memory_interval = 1.0, disk_interval = 10.0;
   // spot reclaim: after `requeue` the task goes back to the node queue through this command
   std::vector<std::string> requeue_argv;
@@ -296,6 +304,14 @@ Spec load_spec(const std::string& path) {
   s.rank_memory_kb = (uint64_t)lim["rank_memory_mb"].num(0) * 1024;
   s.disk_limit_bytes = (uint64_t)(lim["disk_gb"].num(0) * 1e9);
   s.memory_interval = lim["memory_interval"].num(1.0);
+  s.cgroup = lim["cgroup"].str("auto");
+  s.cgroup_version = (int)lim["cgroup_version"].num(0);
+  s.cgroup_headroom_kb = (uint64_t)lim["cgroup_headroom_mb"].num(0) * 1024;
+  {
+    const size_t slash = s.state_path.rfind('/');
+    const std::string dir = slash == std::string::npos ? "." : s.state_path.substr(0, slash);
+    s.regions_path = v["regions_path"].str(dir + "/regions");
+  }
   s.disk_interval = lim["disk_interval"].num(10.0);
   for (auto& a : v["requeue_argv"].a) s.requeue_argv.push_back(a.str());
   s.restart_base = (int)v["restart_base"].num(0);
@@ -328,6 +344,7 @@ class Supervisor {
     open_control();
     unlink(s_.requeue_path.c_str());  // a reclaimed incarnation's marker
     started_ = now();
+    setup_cgroups();
     event("supervisor-start", {"pid " + std::to_string(getpid()),
                                "parallelism " + std::to_string(s_.parallelism)});
     if (s_.deadline > 0 && now() >= s_.deadline) {
@@ -516,6 +533,208 @@ class Supervisor {
     return total;
   }
 
+  // Checkpoint spill regions announced by the ranks (checkpoint/host.py: one line
+  // "<pid> <start> <end> <path|->" per mapping).  They mirror device state -- a rank's
+  // checkpoint of 100+ GB of HBM -- and are not its working set, so the limit leaves them out
+  // (a file-backed region matches by path in every process that maps it, an anonymous one by
+  // the announcing pid and address range).
+  struct Region {
+    long pid = 0;
+    uint64_t start = 0, end = 0;
+    std::string path;
+  };
+
+  std::vector<Region> load_regions() const {
+    std::vector<Region> out;
+    std::ifstream in(s_.regions_path);
+    std::string line;
+    while (std::getline(in, line)) {
+      Region r;
+      char path[4096] = "";
+      unsigned long long a = 0, b = 0;
+      if (sscanf(line.c_str(), "%ld %llx %llx %4095[^\n]", &r.pid, &a, &b, path) < 3) continue;
+      r.start = a;
+      r.end = b;
+      if (strcmp(path, "-") != 0) r.path = path;
+      out.push_back(r);
+    }
+    return out;
+  }
+
+  // Proportional set size of a group, and the part of it in checkpoint regions (kB).
+  static std::pair<uint64_t, uint64_t> pss_split_kb(const std::vector<long>& pids,
+                                                    const std::vector<Region>& regions) {
+    if (regions.empty()) return {pss_kb(pids), 0};
+    uint64_t total = 0, excluded = 0;
+    for (long pid : pids) {
+      std::ifstream in("/proc/" + std::to_string(pid) + "/smaps");
+      std::string line;
+      bool skip = false;
+      while (std::getline(in, line)) {
+        if (line.empty()) continue;
+        const char c = line[0];
+        if ((c >= '0' && c <= '9') || (c >= 'a' && c <= 'f')) {  // "start-end perms ... path"
+          unsigned long long a = 0, b = 0;
+          int consumed = 0;
+          skip = false;
+          if (sscanf(line.c_str(), "%llx-%llx %*s %*s %*s %*s%n", &a, &b, &consumed) < 2) continue;
+          std::string path = consumed > 0 && (size_t)consumed < line.size()
+                                 ? line.substr((size_t)consumed) : std::string();
+          path.erase(0, path.find_first_not_of(' '));
+          const std::string deleted = " (deleted)";
+          if (path.size() > deleted.size() &&
+              path.compare(path.size() - deleted.size(), deleted.size(), deleted) == 0)
+            path.resize(path.size() - deleted.size());
+          for (const Region& r : regions)
+            if ((!r.path.empty() && r.path == path) ||
+                (r.path.empty() && r.pid == pid && a < r.end && r.start < b)) {
+              skip = true;
+              break;
+            }
+        } else if (line.compare(0, 4, "Pss:") == 0) {
+          const uint64_t v = strtoull(line.c_str() + 4, nullptr, 10);
+          total += v;
+          if (skip) excluded += v;
+        }
+      }
+    }
+    return {total, excluded};
+  }
+
+  std::map<int, uint64_t> region_kb_;  // rank index -> its regions' share at the last check
+
+  // ---- memory cgroups (the hard cap) ----------------------------------------------------------
+  // k8s turns the machine type into a pod memory limit (resource_job.go:112-118): the kernel
+  // stops a container at it, however fast it allocates.  The /proc poll above sees a rank only
+  // every memory_interval; a rank that allocates faster than that could take the node down
+  // first.  So each rank also gets a memory cgroup -- v2 memory.max or v1
+  // memory.limit_in_bytes -- when the hierarchy is writable (root, or a delegated subtree),
+  // capped at limit + headroom: shm pages of a checkpoint region are charged to the cgroup of
+  // the process that first touched them, so a GPU rank gets room for its GPUs' HBM.
+  std::vector<std::string> cg_dirs_;  // per rank index; empty: no cgroup
+  std::vector<uint64_t> cg_oom_;      // kernel OOM kills seen per rank
+  int cg_version_ = 0;
+  std::string cg_root_;
+
+  static bool write_text(const std::string& path, const std::string& text, bool append = false) {
+    int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_CLOEXEC | (append ? O_APPEND : O_TRUNC),
+                  0644);
+    if (fd < 0) return false;
+    const ssize_t n = write(fd, text.data(), text.size());
+    const int saved = errno;
+    close(fd);
+    errno = saved;
+    return n == (ssize_t)text.size();
+  }
+
+  // Our own cgroup path ("" controller: the v2 entry "0::/path").
+  static std::string own_cgroup(const std::string& controller) {
+    std::ifstream in("/proc/self/cgroup");
+    std::string line;
+    while (std::getline(in, line)) {
+      const size_t a = line.find(':'), b = line.find(':', a + 1);
+      if (a == std::string::npos || b == std::string::npos) continue;
+      const std::string ctl = line.substr(a + 1, b - a - 1), path = line.substr(b + 1);
+      if (controller.empty() ? (line.compare(0, a, "0") == 0 && ctl.empty())
+                             : ("," + ctl + ",").find("," + controller + ",") != std::string::npos)
+        return path == "/" ? "" : path;
+    }
+    return "";
+  }
+
+  // cgroups of supervisors that died without cleaning up (tpi-<task>-<pid>-r<i>)
+  static void sweep_stale_cgroups(const std::string& root) {
+    DIR* d = opendir(root.c_str());
+    if (!d) return;
+    while (struct dirent* e = readdir(d)) {
+      const std::string name = e->d_name;
+      if (name.compare(0, 4, "tpi-") != 0) continue;
+      const size_t r = name.rfind("-r"), dash = r == std::string::npos ? r : name.rfind('-', r - 1);
+      if (dash == std::string::npos) continue;
+      const long pid = strtol(name.c_str() + dash + 1, nullptr, 10);
+      if (pid > 0 && kill((pid_t)pid, 0) != 0 && errno == ESRCH)
+        rmdir((root + "/" + name).c_str());
+    }
+    closedir(d);
+  }
+
+  void setup_cgroups() {
+    cg_dirs_.assign(s_.parallelism, "");
+    cg_oom_.assign(s_.parallelism, 0);
+    if (!s_.rank_memory_kb || s_.cgroup.empty() || s_.cgroup == "off") return;
+    std::string root, why;
+    int ver = s_.cgroup_version;
+    struct stat st;
+    if (s_.cgroup == "auto") {
+      if (stat("/sys/fs/cgroup/cgroup.controllers", &st) == 0) {
+        ver = 2;
+        root = "/sys/fs/cgroup" + own_cgroup("");
+        // children need the memory controller in our subtree (granted only where the
+        // hierarchy is delegated to us)
+        write_text(root + "/cgroup.subtree_control", "+memory");
+      } else if (stat("/sys/fs/cgroup/memory/memory.limit_in_bytes", &st) == 0) {
+        ver = 1;
+        const std::string own = "/sys/fs/cgroup/memory" + own_cgroup("memory");
+        root = stat(own.c_str(), &st) == 0 ? own : "/sys/fs/cgroup/memory";
+      } else {
+        why = "no cgroup memory controller";
+      }
+    } else {
+      root = s_.cgroup;
+      if (!ver) ver = stat((root + "/cgroup.controllers").c_str(), &st) == 0 ? 2 : 1;
+    }
+    const uint64_t bytes = (s_.rank_memory_kb + s_.cgroup_headroom_kb) * 1024;
+    if (why.empty()) {
+      sweep_stale_cgroups(root);
+      for (int i = 0; i < s_.parallelism; ++i) {
+        const std::string dir = root + "/tpi-" + s_.task_id + "-" + std::to_string(getpid()) +
+                                "-r" + std::to_string(i);
+        if (mkdir(dir.c_str(), 0755) && errno != EEXIST) {
+          why = "mkdir " + dir + ": " + strerror(errno);
+          break;
+        }
+        cg_dirs_[i] = dir;
+        const std::string limit = dir + (ver == 2 ? "/memory.max" : "/memory.limit_in_bytes");
+        if (!write_text(limit, std::to_string(bytes))) {
+          why = "write " + limit + ": " + strerror(errno);
+          break;
+        }
+        if (ver == 2) write_text(dir + "/memory.swap.max", "0");
+      }
+    }
+    if (!why.empty()) {
+      for (auto& d : cg_dirs_)
+        if (!d.empty()) {
+          rmdir(d.c_str());
+          d.clear();
+        }
+      event("memory-cgroup-unavailable", {why, "the /proc poll enforces the limit"});
+      return;
+    }
+    cg_version_ = ver;
+    cg_root_ = root;
+    event("memory-cgroup", {"v" + std::to_string(ver), root,
+                            "cap " + std::to_string(bytes >> 20) + " MB per rank",
+                            "limit " + std::to_string(s_.rank_memory_kb / 1024) + " MB (poll)"});
+  }
+
+  uint64_t cgroup_oom_kills(int index) {
+    if (index < 0 || index >= (int)cg_dirs_.size() || cg_dirs_[index].empty()) return 0;
+    std::ifstream in(cg_dirs_[index] + (cg_version_ == 2 ? "/memory.events" : "/memory.oom_control"));
+    std::string key;
+    uint64_t value = 0;
+    while (in >> key) {
+      if (key == "oom_kill" && in >> value) return value;
+      in.ignore(1 << 16, '\n');
+    }
+    return 0;
+  }
+
+  void remove_cgroups() {
+    for (auto& d : cg_dirs_)
+      if (!d.empty()) rmdir(d.c_str());
+  }
+
   static thread_local uint64_t du_total_;
   static int du_visit(const char*, const struct stat* st, int type, struct FTW*) {
     if (type == FTW_F) du_total_ += (uint64_t)st->st_blocks * 512;
@@ -537,8 +756,13 @@ class Supervisor {
       for (auto& r : ranks_) {
         if (r.state != Rank::RUNNING || r.pid <= 0 || r.killed) continue;
         auto g = groups.find(r.pid);
-        if (g == groups.end() || g->second.rss_kb <= s_.rank_memory_kb) continue;
-        const uint64_t kb = pss_kb(g->second.pids);
+        if (g == groups.end()) continue;
+        // quick bound: resident set minus the regions' share measured last time
+        const uint64_t known = region_kb_[r.index];
+        if (g->second.rss_kb <= s_.rank_memory_kb + known) continue;
+        const auto split = pss_split_kb(g->second.pids, load_regions());
+        region_kb_[r.index] = split.second;
+        const uint64_t kb = split.first - std::min(split.first, split.second);
         if (kb <= s_.rank_memory_kb) continue;
         // like a container OOM kill: no grace, the rank fails (no respawn)
         r.reason = TermReason::OOM;
@@ -546,9 +770,14 @@ class Supervisor {
         kill(-r.pid, SIGKILL);
         kill(r.pid, SIGKILL);
         r.killed = true;
-        event("rank-oom-killed", {"rank " + std::to_string(r.index),
-                                  "memory " + std::to_string(kb / 1024) + " MB",
-                                  "limit " + std::to_string(s_.rank_memory_kb / 1024) + " MB"});
+        std::vector<std::string> desc = {"rank " + std::to_string(r.index),
+                                         "memory " + std::to_string(kb / 1024) + " MB",
+                                         "limit " + std::to_string(s_.rank_memory_kb / 1024) +
+                                             " MB"};
+        if (split.second)
+          desc.push_back("checkpoint regions " + std::to_string(split.second / 1024) +
+                         " MB not counted");
+        event("rank-oom-killed", desc);
       }
     }
     if (s_.disk_limit_bytes && t >= next_disk_check_ && !stop_) {
@@ -811,6 +1040,7 @@ class Supervisor {
     add("TPI_EVENTS_FILE", s_.events_path);  // ranks journal checkpoint phases here
     add("TPI_NOTIFY_FD", "3");                 // "released": spill done, respawn may start
     add("TPI_REQUEUE_FILE", s_.requeue_path);  // exists: reclaimed, no successor here
+    add("TPI_REGIONS_FILE", s_.regions_path);  // checkpoint regions: not the working set
     // SIGTERM -> SIGKILL window: a preempted rank saves at its next step boundary and falls
     // back to an immediate save after half of it (checkpoint/preemption.py)
     add("TPI_GRACE_SECONDS", std::to_string(s_.grace));
@@ -876,10 +1106,22 @@ class Supervisor {
       }
     }
     std::string exec_cmd = "exec \"$0\"";
+    const std::string cg_procs = r.index < (int)cg_dirs_.size() && !cg_dirs_[r.index].empty()
+                                     ? cg_dirs_[r.index] + "/cgroup.procs" : std::string();
     pid_t parent = getpid();
     pid_t pid = fork();
     if (pid == 0) {
       setpgid(0, 0);
+      if (!cg_procs.empty()) {  // before exec: everything the rank allocates is capped
+        char num[32];
+        const int n = snprintf(num, sizeof(num), "%d\n", (int)getpid());
+        const int cfd = open(cg_procs.c_str(), O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
+        if (cfd >= 0) {
+          if (write(cfd, num, (size_t)n) != n) {
+          }
+          close(cfd);
+        }
+      }
       prctl(PR_SET_PDEATHSIG, SIGTERM);
       if (getppid() != parent) _exit(127);
       sigset_t none;
@@ -1563,6 +1805,15 @@ class Supervisor {
     bool signaled = WIFSIGNALED(st);
     int sig = signaled ? WTERMSIG(st) : 0;
     int code = WIFEXITED(st) ? WEXITSTATUS(st) : -1;
+    if (signaled && sig == SIGKILL && !r.killed && r.reason == TermReason::NONE) {
+      const uint64_t kills = cgroup_oom_kills(r.index);
+      if (kills > cg_oom_[r.index]) {  // the kernel stopped it at the cgroup cap
+        cg_oom_[r.index] = kills;
+        r.reason = TermReason::OOM;
+        event("rank-oom-killed", {"rank " + std::to_string(r.index), "memory cgroup cap",
+                                  "limit " + std::to_string(s_.rank_memory_kb / 1024) + " MB"});
+      }
+    }
     r.exit_code = code;
     r.exit_signal = sig;
     std::string code_s = signaled ? signame(sig) : std::to_string(code);
@@ -1692,6 +1943,7 @@ class Supervisor {
       close_log(r);
     }
     release_resources();
+    remove_cgroups();
     if (!requeued_) close_control();
     event("supervisor-exit", {requeued_ ? "requeued" : stop_ ? "stopped" : "all ranks finished"});
     if (!requeued_) write_state("stopped");

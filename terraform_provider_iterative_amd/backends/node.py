@@ -47,6 +47,7 @@ PASSTHROUGH_PREFIXES = ("LC_", "HSA_", "HIP_", "ROCR_", "ROCM_", "NCCL_", "RCCL_
                         "AMD_", "MIOPEN_", "TORCH_", "PYTORCH_")
 
 DEFAULT_MASTER_PORT_BASE = 29500
+HBM_MB_PER_GPU = 288 * 1024  # MI355X: 288 GiB of HBM3E per GPU
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
@@ -429,8 +430,25 @@ class NodeTask(Task):
         (``TPI_ENFORCE_LIMITS=0`` disables)."""
         if self._knob("TPI_ENFORCE_LIMITS", "1") == "0":
             return {}
-        memory = int(alloc.get("memory_mb_per_rank") or 0) or self._machine().memory_mb
-        out = {"rank_memory_mb": memory}
+        machine = self._machine()
+        memory = int(alloc.get("memory_mb_per_rank") or 0) or machine.memory_mb
+        out = {"rank_memory_mb": memory,
+               # the kernel's hard cap (supervisor setup_cgroups): "auto", "off" or a cgroup
+               # directory; checkpoint regions (shm, charged to the rank) get one GPU's HBM of
+               # headroom per GPU -- a spill mirrors device state, it is not the working set
+               "cgroup": self._knob("TPI_MEMORY_CGROUP", "auto")}
+        headroom = self._knob("TPI_CGROUP_HEADROOM_MB", "")
+        try:
+            out["cgroup_headroom_mb"] = int(headroom) if headroom else \
+                machine.gpus * HBM_MB_PER_GPU
+        except ValueError:
+            out["cgroup_headroom_mb"] = machine.gpus * HBM_MB_PER_GPU
+        interval = self._knob("TPI_MEMORY_CHECK_INTERVAL", "")
+        if interval:
+            try:
+                out["memory_interval"] = float(interval)
+            except ValueError:
+                pass
         try:
             disk = float(self._definition().get("disk_size", -1) or -1)
         except (TypeError, ValueError):

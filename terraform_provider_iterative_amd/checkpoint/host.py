@@ -75,6 +75,7 @@ class HostRegion:
             buf = (ctypes.c_char * size).from_buffer(self._mmap)
             self.addr = ctypes.addressof(buf)
             del buf
+        _announce(self.addr, size, path)
 
     def array(self, offset: int = 0, length: Optional[int] = None, dtype=np.uint8) -> np.ndarray:
         """numpy view of ``[offset, offset + length)``."""
@@ -114,6 +115,27 @@ class HostRegion:
             self.close()
         except Exception:
             pass
+
+
+def _announce(addr: int, size: int, path: Optional[str]) -> None:
+    """Record a checkpoint region in the task's region list (``TPI_REGIONS_FILE``, set by
+    the supervisor): its memory-limit check leaves these mappings out of a rank's host memory
+    -- a spill region mirrors device state, it is not the rank's working set (a legacy alias
+    like ``m+t4`` allows 16 GB per rank, less than one GPU's checkpoint).  One ``O_APPEND``
+    line ``<pid> <start hex> <end hex> <path or ->``."""
+    registry = os.environ.get("TPI_REGIONS_FILE")
+    if not registry or not addr:
+        return
+    line = "%d %x %x %s\n" % (os.getpid(), addr, addr + size, os.path.abspath(path) if path
+                              else "-")
+    try:
+        fd = os.open(registry, os.O_WRONLY | os.O_CREAT | os.O_APPEND, 0o644)
+        try:
+            os.write(fd, line.encode())
+        finally:
+            os.close(fd)
+    except OSError:
+        pass
 
 
 def numa_placement(addr: int, size: int) -> Optional[Dict[str, object]]:

@@ -7,18 +7,21 @@
 // remove_tree on a scratch tree, CRC32C tiles + combine, shard hash, pack/unpack of
 // contiguous and strided segments, and the TPZ1 codec: round trips on float-like data plus
 // a decoder fuzz over randomly corrupted and truncated blobs (checkpoint files are untrusted
-// input).
+// input), the parallel checkpoint file I/O and the step-boundary agreement block.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/stat.h>
 
+#include <algorithm>
 #include <random>
 #include <stdexcept>
 #include <string>
 #include <vector>
 
 #include "../../csrc/common/tpz.h"
+#include "../../csrc/native/ctl.h"
+#include "../../csrc/native/fileio.h"
 #include "../../csrc/native/filter.h"
 #include "../../csrc/native/hostops.h"
 #include "../../csrc/native/transfer.h"
@@ -191,6 +194,71 @@ static void test_codec() {
   (void)used;
 }
 
+// Checkpoint file I/O: parallel write + streamed read with progress words, odd sizes,
+// more threads than pieces, a truncated file and a missing one.
+static void test_fileio(const std::string& scratch) {
+  for (uint64_t n : {0ull, 1ull, 4095ull, (3ull << 20) + 17}) {
+    std::vector<uint8_t> src = float_like(n + 16, (unsigned)n);
+    src.resize(n);
+    const std::string path = scratch + "/ckpt-" + std::to_string(n);
+    CHECK(tpi::write_file(path, src.data(), n, 5, true).empty());
+    std::vector<uint8_t> back(n + 1, 0xAB);
+    std::vector<uint64_t> tile_ends;
+    for (uint64_t e = 65536; e < n; e += 65536) tile_ends.push_back(e);
+    tile_ends.push_back(n);
+    uint64_t words[2] = {0, 0};
+    CHECK(tpi::read_stream(path, back.data(), 0, n, 3, 1 << 20, words, tile_ends.data(),
+                           tile_ends.size()).empty());
+    CHECK(std::equal(src.begin(), src.end(), back.begin()));
+    CHECK(back[n] == 0xAB);  // nothing past the end
+    if (n) CHECK(words[1] == n && words[0] == tile_ends.size());
+    // offset read of the tail, zero threads (clamped to one)
+    if (n > 100) {
+      std::vector<uint8_t> tail(n - 100);
+      CHECK(tpi::read_stream(path, tail.data(), 100, n - 100, 0, 4096, nullptr, nullptr, 0)
+                .empty());
+      CHECK(std::equal(tail.begin(), tail.end(), src.begin() + 100));
+    }
+    // asking for more than the file holds is an error, not an overrun
+    std::vector<uint8_t> over(n + 8192);
+    CHECK(!tpi::read_stream(path, over.data(), 0, n + 8192, 4, 4096, nullptr, nullptr, 0)
+               .empty());
+  }
+  std::vector<uint8_t> buf(64);
+  CHECK(!tpi::read_stream(scratch + "/missing", buf.data(), 0, 64, 2, 4096, nullptr, nullptr, 0)
+             .empty());
+  CHECK(!tpi::write_file(scratch + "/no/such/dir/f", buf.data(), 64, 2, false).empty());
+}
+
+// Step-boundary agreement, single thread: the targets a proposer chooses (see ctl.h).
+static void test_ctl() {
+  const int world = 3;
+  std::vector<uint64_t> mem(tpi::ctl::bytes(world) / 8);
+  void* b = mem.data();
+  CHECK(!tpi::ctl::valid(b, world));
+  tpi::ctl::init(b, world);
+  CHECK(tpi::ctl::valid(b, world) && !tpi::ctl::valid(b, world + 1));
+  uint64_t pre = 1, per = 1;
+  tpi::ctl::arrive(b, 0, 5, &pre, &per);
+  CHECK(pre == 0 && per == 0);
+  tpi::ctl::arrive(b, 1, 7, &pre, &per);
+  tpi::ctl::arrive(b, 2, 6, &pre, &per);
+  // rank 0 (at 5) proposes: past everyone else's published boundary
+  CHECK(tpi::ctl::propose_preempt(b, world, 0) == 8);
+  CHECK(tpi::ctl::propose_preempt(b, world, 2) == 8);  // chosen once
+  tpi::ctl::arrive(b, 1, 8, &pre, &per);
+  CHECK(pre == 8);
+  // periodic: rank 0 proposes only when everybody passed the previous target
+  CHECK(tpi::ctl::propose_periodic(b, world, 0) == 9);
+  CHECK(tpi::ctl::propose_periodic(b, world, 0) == 0);  // rank 0 itself is at 5
+  tpi::ctl::arrive(b, 0, 10, &pre, &per);
+  tpi::ctl::arrive(b, 1, 10, &pre, &per);
+  tpi::ctl::arrive(b, 2, 10, &pre, &per);
+  CHECK(per == 9);
+  CHECK(tpi::ctl::propose_periodic(b, world, 0) == 11);
+  CHECK(tpi::ctl::ordinal_of(b, 2) == 10);
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) {
     fprintf(stderr, "usage: %s <scratch-dir>\n", argv[0]);
@@ -200,6 +268,8 @@ int main(int argc, char** argv) {
   test_transfer(argv[1]);
   test_hostops();
   test_codec();
+  test_fileio(argv[1]);
+  test_ctl();
   if (g_fail) return 1;
   printf("sanitize harness ok\n");
   return 0;

@@ -262,3 +262,113 @@ def test_memory_shared_with_forked_workers_counts_once(tmp_path):
     assert "survived" in "".join(task.logs())
     assert "rank-oom-killed" not in [e.code for e in task.events()]
     task.delete()
+
+
+REGION_RANK = r'''#!%(python)s
+import os, sys, time
+sys.path.insert(0, %(root)r)
+if not %(announce)r:
+    os.environ.pop("TPI_REGIONS_FILE", None)  # an unannounced mapping is working set
+from terraform_provider_iterative_amd.checkpoint.host import HostRegion
+region = HostRegion(%(mb)d << 20, os.path.join(os.environ["TPI_DATA_DIRECTORY"], ".spill"))
+region.array()[:] = 7  # resident: every page touched
+print("up", flush=True)
+time.sleep(2.5)  # > 2 polls of the limit
+print("survived", flush=True)
+'''
+
+
+@pytest.mark.parametrize("announce", [True, False], ids=["region", "working-set"])
+def test_checkpoint_region_larger_than_the_memory_limit_survives(tmp_path, monkeypatch,
+                                                                 announce):
+    """ADVICE r3: a GPU machine type's memory (e.g. m+t4 -> 16 GB) is smaller than one GPU's
+    checkpoint.  A spill region the rank announced (checkpoint/host.py does for every region)
+    is not counted against the limit; the same mapping unannounced is, and is killed."""
+    monkeypatch.setenv("TPI_MI355X_GPUS", "0")
+    monkeypatch.setenv("TPI_NODE_CPUS", "0-31")
+    monkeypatch.setenv("TPI_NODE_MEMORY_MB", "512000")
+    cloud = _cloud(tmp_path)
+    script = REGION_RANK % {"python": sys.executable, "root": ROOT, "mb": 700,
+                            "announce": announce}
+    task = _task(cloud, "region-" + str(announce), script, machine="1-400+mi355x*1",
+                 env={"TPI_MEMORY_CHECK_INTERVAL": "0.2"})
+    task.create()
+    status = task.wait(60)
+    logs = "".join(task.logs())
+    codes = [e.code for e in task.events()]
+    if announce:
+        assert status["succeeded"] == 1 and "survived" in logs, (status, logs, codes)
+        assert "rank-oom-killed" not in codes
+    else:
+        assert status["failed"] == 1 and "survived" not in logs, (status, logs)
+        assert "rank-oom-killed" in codes
+    task.delete()
+
+
+def test_supervisor_puts_each_rank_in_a_memory_cgroup(tmp_path):
+    """The hard cap: a cgroup per rank with memory.max = limit + headroom, the rank inside it
+    before exec (a directory standing in for the cgroup hierarchy)."""
+    from tests.test_supervisor import _events, _run, _spec
+
+    from terraform_provider_iterative_amd import _build
+
+    root = tmp_path / "cgroot"
+    root.mkdir()
+    (root / "cgroup.controllers").write_text("memory\n")  # looks like cgroup v2
+    task, spec = _spec(tmp_path, "#!/bin/sh\necho pid $$\n", parallelism=2,
+                       limits={"rank_memory_mb": 1000, "cgroup": str(root),
+                               "cgroup_headroom_mb": 24})
+    _run(_build.build_supervisor(), spec)
+    events = _events(task)
+    cg = [e for e in events if e["code"] == "memory-cgroup"]
+    assert cg and cg[0]["description"][:2] == ["v2", str(root)], events
+    dirs = sorted(d for d in os.listdir(root) if d.startswith("tpi-"))
+    assert len(dirs) == 2 and dirs[0].endswith("-r0") and dirs[1].endswith("-r1")
+    for d in dirs:
+        assert (root / d / "memory.max").read_text() == str((1000 + 24) << 20)
+    pids = {int(l.split()[-1]) for f in os.listdir(task / "reports") if f.startswith("task-")
+            for l in (task / "reports" / f).read_text().splitlines()}
+    joined = {int((root / d / "cgroup.procs").read_text().split()[0]) for d in dirs}
+    assert joined == pids, (joined, pids)
+
+
+def _cgroup_writable() -> bool:
+    if os.geteuid() != 0:
+        return False
+    probe = None
+    if os.path.exists("/sys/fs/cgroup/memory/memory.limit_in_bytes"):
+        probe = "/sys/fs/cgroup/memory/tpi-probe-%d" % os.getpid()
+    if probe is None:
+        return False
+    try:
+        os.mkdir(probe)
+        os.rmdir(probe)
+        return True
+    except OSError:
+        return False
+
+
+@pytest.mark.skipif(not _cgroup_writable(), reason="no writable memory cgroup hierarchy")
+def test_fast_allocation_over_the_limit_is_stopped_by_the_kernel(tmp_path):
+    """machine 1-1000 (1 GB): a rank that writes 2 GB in well under a poll interval is stopped
+    by its memory cgroup (the poll is set to 30 s here, so only the kernel can act)."""
+    cloud = _cloud(tmp_path, "local")
+    script = ("#!%s\nimport time\nprint('up', flush=True)\nt = time.time()\n"
+              "x = b'\\x01' * (2 << 30)\nprint('survived %%.3f s' %% (time.time() - t), flush=True)\n"
+              "time.sleep(5)\n" % sys.executable)
+    task = _task(cloud, "cg-oom", script, machine="1-1000",
+                 env={"TPI_MEMORY_CHECK_INTERVAL": "30"})
+    task.create()
+    status = task.wait(30)
+    logs = "".join(task.logs())
+    assert status["failed"] == 1 and "survived" not in logs, (status, logs)
+    events = task.events()
+    assert "memory-cgroup" in [e.code for e in events]
+    kills = [e for e in events if e.code == "rank-oom-killed"]
+    assert kills and "memory cgroup cap" in kills[0].description, kills
+    import json
+
+    reports = [f for f in os.listdir(task.reports_dir) if f.startswith("status-")]
+    assert json.load(open(os.path.join(task.reports_dir, reports[0])))["result"] == "oom"
+    task.delete()
+    assert not [d for d in os.listdir("/sys/fs/cgroup/memory") if d.startswith("tpi-" + task.id)]
