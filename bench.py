@@ -331,15 +331,43 @@ def main(argv=None):
         progress("warmup %d/%d" % (i + 1, args.warmup))
     barrier()
 
+    fault = os.environ.get("TPI_BENCH_FAULT", "")
+    if fault and fault != "skip-restore-after-first":
+        raise SystemExit("bench: unknown TPI_BENCH_FAULT %r" % fault)
+
+    def poison(tensors_):
+        """Overwrite every successor tensor with a pattern no checkpoint holds (outside the
+        timed window): only a restore that rewrites all of them passes the final digest check."""
+        for t in tensors_.values():
+            t.view(-1).view(torch.uint8).fill_(0xA5)
+
+    if fault:  # fault injection for the contract test: a restore that stops rewriting
+        real_restore = ck_in.restore if ck_in is not None else ck.restore
+        calls = [0]
+
+        def broken_restore(*a, **kw):
+            res = real_restore(*a, **kw)
+            calls[0] += 1
+            if calls[0] > 1 + args.warmup:  # "skips" tensors 3.. after the first timed step
+                poison(dict(list((successor or tensors).items())[2:]))
+            return res
+
+        if ck_in is not None:
+            ck_in.restore = broken_restore
+        else:
+            ck.restore = broken_restore
+
     save_s = restore_s = 0.0
     wire = split_chunks = 0
-    t0 = time.perf_counter()
+    elapsed = 0.0
     for step in range(args.steps):
         if overlap and successor is not None:
-            # the successor's tensors must really be rewritten by every step's restore
-            for t in list(successor.values())[:2]:
-                t.zero_()
+            poison(successor)  # untimed: the restore must rewrite every successor tensor
+        barrier()
+        t0 = time.perf_counter()
         wire, s_s, r_s, res = save_restore({"step": step})
+        barrier()
+        elapsed += time.perf_counter() - t0
         if ck_in is not None and ck_in.engine is not None:  # duplex balancing of this step
             split_chunks += ck_in.engine.split_chunks
         if res.bad_tiles:
@@ -347,8 +375,6 @@ def main(argv=None):
         save_s += s_s
         restore_s += r_s
         progress("step %d/%d save %.3f s restore %.3f s" % (step + 1, args.steps, s_s, r_s))
-    barrier()
-    elapsed = time.perf_counter() - t0
 
     verified = None
     if args.verify:  # outside the timed region: prove the restore really rewrote HBM
@@ -358,8 +384,8 @@ def main(argv=None):
             out = ops.shard_hash(d[n].view(-1).view(torch.uint8))
             return out.cpu().tolist() if hasattr(out, "cpu") else out.tolist()
 
-        if overlap:  # every tensor of the successor equals the saved state
-            sync()
+        if overlap:  # every tensor of the successor (poisoned before the last step) equals
+            sync()   # the saved state
             verified = all(digest(successor, n) == digest(tensors, n) for n in tensors)
         else:
             names = list(tensors)[:3]
@@ -369,6 +395,8 @@ def main(argv=None):
             ck.restore()
             sync()
             verified = before == [digest(tensors, n) for n in names]
+        if world > 1:  # the job is verified only if every rank's restore is
+            verified = verified and allmax(0.0 if verified else 1.0) == 0.0
     if ck_in is not None:  # the side measurements need the HBM back
         ck_in.close()
         ck_in = None
@@ -411,11 +439,19 @@ def main(argv=None):
                        "mode": args.mode, "codec": args.codec,
                        "d2h_engine": ck.engine.d2h_engine if ck.engine else None,
                        "tensors_per_rank": len(tensors)},
+            # what `value` counts: checkpoint bytes saved + restored per second, the restore
+            # streaming behind the save over the other direction of the PCIe link (the
+            # preemption hand-off's streamed route); rounds 1-2 measured save-then-restore,
+            # which is `value_sequential` below
+            "value_kind": "overlapped_duplex" if overlap else "sequential",
+            "value_sequential": None,
             "save_GBps": round(total * args.steps / save_max / 1e9, 3),
             "restore_GBps": round(total * args.steps / restore_max / 1e9, 3),
             "restore_streams_behind_save": overlap,
-            # chunks of the timed restores whose H2D went over two copy streams (the restore
-            # trailed the save by TPI_H2D_SPLIT_LEAD chunks): the link's share moves to it
+            # chunks of the timed restores whose H2D went over two copy streams: the safety
+            # valve for a restore trailing the save by TPI_H2D_SPLIT_LEAD chunks.  0 is the
+            # healthy value -- the bounded run-ahead keeps the restore within a chunk of the
+            # save (profiles/duplex_split_round3.md section 4)
             "restore_split_chunks": split_chunks if overlap else None,
             "per_gpu_save_GBps": round(ck.plan.total * args.steps / save_max / 1e9, 3),
             "per_gpu_restore_GBps": round(ck.plan.total * args.steps / restore_max / 1e9, 3),
@@ -551,10 +587,16 @@ def main(argv=None):
         out["raw_GBps"] = raw
         out["workdir_broadcast"] = fanout
         out["sequential"] = sequential
+        if isinstance(sequential, dict) and "GBps" in sequential:
+            out["value_sequential"] = sequential["GBps"]
     emit()
     ck.close()
     if world > 1:
         dist.destroy_process_group()
+    if verified is False:  # a restore that did not rewrite the state is no measurement
+        print("bench: restore NOT verified: the restored tensors differ from the saved ones",
+              file=sys.stderr, flush=True)
+        raise SystemExit(3)
 
 
 if __name__ == "__main__":

@@ -51,6 +51,10 @@ resuming = os.path.exists(spill)
 if resuming and %(prefetch)r:
     prefetch(spill)  # map + pin the spill while the model state is being allocated
 t_prefetch = time.time()
+free_before = torch.cuda.mem_get_info(0)[0]
+probe = torch.empty(1 << 20, dtype=torch.uint8, device=dev)  # context + allocator warm
+torch.cuda.synchronize()
+t_probe = time.time()
 tensors = synthetic_checkpoint(nbytes, 8192, dev, fill=not resuming)
 torch.cuda.synchronize()
 t_alloc = time.time()
@@ -70,10 +74,11 @@ if resuming:
     t1 = time.time()
     ok = meta is not None and meta.get("digests") == digests()
     print("restored %%d bytes in %%.3f s, verified %%s, warm standby %%s, activation -> restored "
-          "%%.3f s (prefetch %%.3f, HBM state %%.3f, host region map+register %%.3f after it); "
+          "%%.3f s (prefetch %%.3f, HBM state %%.3f [first 1 MiB %%.3f, %%.1f GB free before], "
+          "host region map+register %%.3f after it); "
           "process start -> import done %%.3f s; Checkpointer %%s" %% (
               ck.plan.total, t1 - t0, ok, activated, t1 - t_active, t_prefetch - t_active,
-              t_alloc - t_prefetch, t_map - t_alloc,
+              t_alloc - t_prefetch, t_probe - t_prefetch, free_before / 1e9, t_map - t_alloc,
                                   t_import - t_start, ck.init_times),
           flush=True)
     # the predecessor is still spilling behind the HBM hand-off: wait for the host copy, so

@@ -107,9 +107,13 @@ def main():
     model(x).float().pow(2).mean().backward()
     opt.step()
     opt.zero_grad(set_to_none=False)
-    # model + optimizer device state by reference; CPU-side Adam step counters ride in the
-    # checkpoint header (bias correction needs them after a resume)
-    state = TrainingState(model, opt, extra={"step": step_t}, path=spill)
+    # the batch generator: part of the checkpoint, so a resumed run draws the batches the
+    # uninterrupted one would have (not the first batches again)
+    gen = torch.Generator(device=device).manual_seed(rank + 7)
+    # model + optimizer device state by reference; CPU-side Adam step counters, the optimizer
+    # hyper-parameters, every RNG and `gen` ride in the checkpoint header
+    state = TrainingState(model, opt, extra={"step": step_t}, path=spill,
+                          generators={"data": gen})
     ck = state.checkpointer
     # ranks agree on the step to resume from (or all start fresh)
     meta = state.resume_consistent() if world > 1 else state.resume()
@@ -117,7 +121,6 @@ def main():
     log("resumed from step %d" % start if meta else "fresh start")
     state.install()
 
-    gen = torch.Generator(device=device).manual_seed(rank + 7)
     t_steps, stalls = [], []
     for step in range(start, args.steps):
         t0 = time.perf_counter()

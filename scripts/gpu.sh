@@ -65,6 +65,8 @@ run_job() {
                        > "$OUT/preempt-standby.json" 2> "$OUT/preempt-standby.log" ;;
     preempt-hot) timeout -k 10 900 python bench/bench_preempt.py --gb 100 --hot $extra \
                    > "$OUT/preempt-hot.json" 2> "$OUT/preempt-hot.log" ;;
+    preempt-hot2) timeout -k 10 900 python bench/bench_preempt.py --gb 100 --hot $extra \
+                   > "$OUT/preempt-hot2.json" 2> "$OUT/preempt-hot2.log" ;;
     preempt-170) timeout -k 10 900 python bench/bench_preempt.py --gb 170 --hot $extra \
                    > "$OUT/preempt-170.json" 2> "$OUT/preempt-170.log" ;;
     reclaim) timeout -k 10 900 python bench/bench_reclaim.py --gb 100 $extra \

@@ -3,8 +3,8 @@ from .checkpointer import (CheckpointError, Checkpointer, DeviceEngine, Transfer
                            describe_checkpoint, prewarm_engine, verify_checkpoint)
 from .host import HostRegion, early_prefetch, prefetch
 from . import preemption
-from .training import TrainingState, collect
+from .training import DataCursor, TrainingState, collect
 
 __all__ = ["CheckpointError", "Checkpointer", "DeviceEngine", "TransferResult",
-           "describe_checkpoint", "verify_checkpoint", "HostRegion", "TrainingState", "collect",
-           "preemption", "prefetch", "early_prefetch", "prewarm_engine"]
+           "describe_checkpoint", "verify_checkpoint", "HostRegion", "TrainingState",
+           "DataCursor", "collect", "preemption", "prefetch", "early_prefetch", "prewarm_engine"]

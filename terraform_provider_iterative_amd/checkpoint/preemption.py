@@ -677,12 +677,16 @@ def _release_device_memory() -> int:
             ck.release_device()
         except Exception as error:  # keep going: the rest still frees memory
             journal("device-memory-release-failed", str(error))
-    for obj in gc.get_objects():
-        try:
-            if isinstance(obj, torch.Tensor) and obj.is_cuda:
-                obj.untyped_storage().resize_(0)
-        except Exception:
-            continue
+    import warnings
+
+    with warnings.catch_warnings():  # isinstance() on lazy module objects can warn
+        warnings.simplefilter("ignore")
+        for obj in gc.get_objects():
+            try:
+                if isinstance(obj, torch.Tensor) and obj.is_cuda:
+                    obj.untyped_storage().resize_(0)
+            except Exception:
+                continue
     torch.cuda.empty_cache()
     return max(0, before - sum(torch.cuda.memory_reserved(d) for d in devices))
 

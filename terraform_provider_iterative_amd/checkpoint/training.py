@@ -7,13 +7,23 @@ per-parameter ``step`` counters of non-capturable Adam/AdamW, which bias correct
 on) in the checkpoint header.  ``resume()`` restores both; ``install()`` arms the SIGTERM
 handler of :mod:`.preemption`.
 
+The header also carries everything else an ordinary loop needs to continue *bit-identically*
+after a respawn (``training_state``): the random number generators (torch CPU and every
+initialised GPU, Python ``random``, NumPy's global generator, plus any ``generators`` handed
+in), the optimizer's hyper-parameters per param group (an LR schedule changes them), the LR
+scheduler, the AMP ``GradScaler``, and any object with ``state_dict``/``load_state_dict``
+registered as ``stateful`` (a sampler, a data cursor: :class:`DataCursor`).  All of it is
+captured at the same step boundary as the tensors.
+
 This is the tensor-level counterpart of the reference's workdir sync: there the user script
 had to re-read its own files after a spot respawn (README.md:93-101).
 """
 from __future__ import annotations
 
+import base64
 import json
-from typing import Any, Dict, Optional, Tuple
+import random
+from typing import Any, Dict, List, Optional, Tuple
 
 from . import preemption
 from .checkpointer import Checkpointer
@@ -78,6 +88,162 @@ def _decode_into(t, blob: Dict[str, Any]) -> None:
 TORN = ("torn-risk", "signal")  # saves not taken at a step boundary
 
 
+# -- small host state as JSON (the checkpoint header) ---------------------------------------------
+
+def to_jsonable(obj: Any) -> Any:
+    """``obj`` (a ``state_dict()``-like tree) as JSON, keeping what JSON would lose: tuples,
+    non-string dict keys, tensors (dtype, shape, device), NumPy arrays and bytes.  Anything
+    else raises ``TypeError`` -- at construction time, not in the middle of a preemption."""
+    import numpy as np
+
+    if obj is None or isinstance(obj, (bool, int, float, str)):
+        return obj
+    if isinstance(obj, tuple):
+        return {"__tuple__": [to_jsonable(v) for v in obj]}
+    if isinstance(obj, list):
+        return [to_jsonable(v) for v in obj]
+    if isinstance(obj, dict):
+        if all(isinstance(k, str) and not k.startswith("__") for k in obj):
+            return {k: to_jsonable(v) for k, v in obj.items()}
+        return {"__items__": [[to_jsonable(k), to_jsonable(v)] for k, v in obj.items()]}
+    if isinstance(obj, (bytes, bytearray)):
+        return {"__bytes__": base64.b64encode(bytes(obj)).decode()}
+    if isinstance(obj, np.ndarray):
+        return {"__ndarray__": obj.tolist(), "dtype": str(obj.dtype)}
+    if isinstance(obj, np.generic):
+        return obj.item()
+    import torch
+
+    if torch.is_tensor(obj):
+        out = _encode(obj)
+        out["__tensor__"] = True
+        out["device"] = str(obj.device)
+        return out
+    raise TypeError("cannot carry a %s in a checkpoint header" % type(obj).__name__)
+
+
+def from_jsonable(obj: Any) -> Any:
+    """Inverse of :func:`to_jsonable` (tensors come back on their original device)."""
+    if isinstance(obj, list):
+        return [from_jsonable(v) for v in obj]
+    if not isinstance(obj, dict):
+        return obj
+    if "__tuple__" in obj:
+        return tuple(from_jsonable(v) for v in obj["__tuple__"])
+    if "__items__" in obj:
+        return {from_jsonable(k): from_jsonable(v) for k, v in obj["__items__"]}
+    if "__bytes__" in obj:
+        return base64.b64decode(obj["__bytes__"])
+    if "__ndarray__" in obj:
+        import numpy as np
+
+        return np.array(obj["__ndarray__"], dtype=obj["dtype"])
+    if obj.get("__tensor__"):
+        import torch
+
+        t = torch.tensor(obj["data"], dtype=getattr(torch, obj["dtype"])).reshape(obj["shape"])
+        return t.to(obj.get("device", "cpu"))
+    return {k: from_jsonable(v) for k, v in obj.items()}
+
+
+def _b64_tensor(t) -> str:
+    return base64.b64encode(t.detach().cpu().contiguous().numpy().tobytes()).decode()
+
+
+def _tensor_b64(text: str):
+    import numpy as np
+    import torch
+
+    return torch.from_numpy(np.frombuffer(base64.b64decode(text), dtype=np.uint8).copy())
+
+
+def capture_rng() -> Dict[str, Any]:
+    """Every global generator a training step may draw from: torch's CPU generator, the
+    default generator of each initialised GPU, Python's ``random`` and NumPy's global one."""
+    import torch
+
+    out: Dict[str, Any] = {"torch": _b64_tensor(torch.get_rng_state()),
+                           "python": to_jsonable(random.getstate())}
+    try:
+        import numpy as np
+
+        out["numpy"] = to_jsonable(np.random.get_state())
+    except ImportError:  # pragma: no cover
+        pass
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        out["cuda"] = [_b64_tensor(torch.cuda.get_rng_state(i))
+                       for i in range(torch.cuda.device_count())]
+    return out
+
+
+def restore_rng(state: Dict[str, Any]) -> None:
+    import torch
+
+    if "torch" in state:
+        torch.set_rng_state(_tensor_b64(state["torch"]))
+    if "python" in state:
+        random.setstate(from_jsonable(state["python"]))
+    if "numpy" in state:
+        import numpy as np
+
+        np.random.set_state(from_jsonable(state["numpy"]))
+    for i, text in enumerate(state.get("cuda") or []):
+        if i < torch.cuda.device_count():
+            torch.cuda.set_rng_state(_tensor_b64(text), i)
+
+
+class DataCursor:
+    """A resumable, reproducible sample order: epoch ``e`` visits ``0..n-1`` in the
+    permutation seeded by ``seed + e`` (or in order, ``shuffle=False``), and the position
+    within it is part of :meth:`state_dict` -- register it as ``stateful`` and a resumed run
+    draws exactly the batches the uninterrupted one would have."""
+
+    def __init__(self, n: int, seed: int = 0, shuffle: bool = True):
+        if n <= 0:
+            raise ValueError("DataCursor needs at least one sample")
+        self.n, self.seed, self.shuffle = int(n), int(seed), bool(shuffle)
+        self.epoch = 0
+        self.index = 0
+        self._order: Optional[List[int]] = None
+
+    def _permutation(self) -> List[int]:
+        if self._order is None:
+            if self.shuffle:
+                import torch
+
+                g = torch.Generator().manual_seed(self.seed + self.epoch)
+                self._order = torch.randperm(self.n, generator=g).tolist()
+            else:
+                self._order = list(range(self.n))
+        return self._order
+
+    def next(self, count: int) -> List[int]:
+        """The next ``count`` sample indices (crossing into the next epoch as needed)."""
+        out: List[int] = []
+        while len(out) < count:
+            order = self._permutation()
+            take = min(count - len(out), self.n - self.index)
+            out.extend(order[self.index:self.index + take])
+            self.index += take
+            if self.index == self.n:
+                self.epoch += 1
+                self.index = 0
+                self._order = None
+        return out
+
+    def state_dict(self) -> Dict[str, int]:
+        return {"n": self.n, "seed": self.seed, "shuffle": int(self.shuffle),
+                "epoch": self.epoch, "index": self.index}
+
+    def load_state_dict(self, state: Dict[str, int]) -> None:
+        if int(state["n"]) != self.n:
+            raise ValueError("DataCursor over %d samples cannot resume one over %d"
+                             % (self.n, int(state["n"])))
+        self.seed, self.shuffle = int(state["seed"]), bool(state["shuffle"])
+        self.epoch, self.index = int(state["epoch"]), int(state["index"])
+        self._order = None
+
+
 class TrainingState:
     """Checkpointer over a model + optimizer (see module docstring).
 
@@ -88,16 +254,49 @@ class TrainingState:
     """
 
     def __init__(self, model, optimizer=None, extra: Optional[Dict[str, Any]] = None,
-                 path: Optional[str] = None, device=None, **checkpointer_kwargs):
+                 path: Optional[str] = None, device=None, *, lr_scheduler=None, scaler=None,
+                 rng: bool = True, generators: Optional[Dict[str, Any]] = None,
+                 stateful: Optional[Dict[str, Any]] = None, **checkpointer_kwargs):
         tensors, self.host = collect(model, optimizer, extra, device)
         if not tensors:
             raise ValueError("nothing to checkpoint on the model's device")
+        self.optimizer = optimizer
+        self.lr_scheduler = lr_scheduler
+        self.scaler = scaler
+        self.rng = rng
+        self.generators: Dict[str, Any] = dict(generators or {})
+        self.stateful: Dict[str, Any] = dict(stateful or {})
+        self.host_metadata()  # anything the header cannot carry fails here, not at SIGTERM
         self.checkpointer = Checkpointer(tensors, path=path, **checkpointer_kwargs)
         self.path = path
         self.step_value: Optional[int] = None  # last step reported (or restored)
 
+    def register(self, name: str, obj: Any) -> None:
+        """Carry ``obj.state_dict()`` in every checkpoint and ``load_state_dict`` it on resume
+        (a sampler, a data cursor, a curriculum...)."""
+        if not (hasattr(obj, "state_dict") and hasattr(obj, "load_state_dict")):
+            raise TypeError("%s has no state_dict()/load_state_dict()" % type(obj).__name__)
+        to_jsonable(obj.state_dict())
+        self.stateful[name] = obj
+
     def host_metadata(self) -> Dict[str, Any]:
-        return {"host_tensors": {k: _encode(t) for k, t in self.host.items()}}
+        state: Dict[str, Any] = {}
+        if self.optimizer is not None:  # lr, betas, ... (an LR schedule rewrites them)
+            state["optimizer_groups"] = [to_jsonable({k: v for k, v in g.items() if k != "params"})
+                                         for g in self.optimizer.param_groups]
+        if self.lr_scheduler is not None:
+            state["lr_scheduler"] = to_jsonable(self.lr_scheduler.state_dict())
+        if self.scaler is not None:
+            state["grad_scaler"] = to_jsonable(self.scaler.state_dict())
+        if self.rng:
+            state["rng"] = capture_rng()
+        if self.generators:
+            state["generators"] = {k: _b64_tensor(g.get_state())
+                                   for k, g in self.generators.items()}
+        if self.stateful:
+            state["stateful"] = {k: to_jsonable(o.state_dict()) for k, o in self.stateful.items()}
+        return {"host_tensors": {k: _encode(t) for k, t in self.host.items()},
+                "training_state": state}
 
     def _metadata(self, metadata: Optional[Dict] = None) -> Dict[str, Any]:
         meta: Dict[str, Any] = {}
@@ -132,6 +331,26 @@ class TrainingState:
             raise ValueError("checkpoint lacks host tensors %s" % missing[:5])
         for name, t in self.host.items():
             _decode_into(t, blobs[name])
+        state = metadata.get("training_state") or {}
+        groups = state.get("optimizer_groups")
+        if groups is not None and self.optimizer is not None:
+            if len(groups) != len(self.optimizer.param_groups):
+                raise ValueError("checkpoint has %d optimizer param groups, the optimizer %d"
+                                 % (len(groups), len(self.optimizer.param_groups)))
+            for group, saved in zip(self.optimizer.param_groups, groups):
+                group.update(from_jsonable(saved))
+        if "lr_scheduler" in state and self.lr_scheduler is not None:
+            self.lr_scheduler.load_state_dict(from_jsonable(state["lr_scheduler"]))
+        if "grad_scaler" in state and self.scaler is not None:
+            self.scaler.load_state_dict(from_jsonable(state["grad_scaler"]))
+        if "rng" in state and self.rng:
+            restore_rng(state["rng"])
+        for name, text in (state.get("generators") or {}).items():
+            if name in self.generators:
+                self.generators[name].set_state(_tensor_b64(text))
+        for name, saved in (state.get("stateful") or {}).items():
+            if name in self.stateful:
+                self.stateful[name].load_state_dict(from_jsonable(saved))
 
     def resume(self, persist_path: Optional[str] = None) -> Optional[Dict]:
         """Restore device tensors (host region, else ``persist_path``) and host tensors;

@@ -135,3 +135,31 @@ def test_eight_rank_rehearsal_finishes_inside_the_watchdog(tmp_path):
     assert d["restore_verified"] is True
     assert "stall_ms" in d["save_async"] and "GBps" in d["raw_GBps"], d
     assert time.time() - t0 < 120 + 60
+
+
+def test_a_restore_that_stops_rewriting_fails_the_bench(tmp_path):
+    """every step poisons every successor tensor outside the timed window, so a
+    restore that skips tensors after the first step (fault injected) cannot print
+    ``restore_verified: true`` -- the bench says so and exits non-zero.  The same run without
+    the fault verifies."""
+    def run(fault):
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu",
+               "--total-gb", "0.01", "--steps", "3", "--warmup", "1", "--no-latency",
+               "--hidden", "256", "--broadcast-gb", "0"]
+        env = dict(os.environ, OMP_NUM_THREADS="2")
+        env.pop("TPI_BENCH_FAULT", None)
+        if fault:
+            env["TPI_BENCH_FAULT"] = fault
+        return subprocess.run(cmd, cwd=str(tmp_path), capture_output=True, text=True,
+                              timeout=300, env=env)
+
+    good = run(None)
+    assert good.returncode == 0, good.stderr[-2000:]
+    d = json.loads([l for l in good.stdout.splitlines() if l.startswith("{")][0])
+    assert d["restore_verified"] is True and d["value_kind"] == "overlapped_duplex"
+    assert d["value_sequential"] and d["value_sequential"] > 0
+    bad = run("skip-restore-after-first")
+    assert bad.returncode != 0, bad.stdout[-2000:]
+    d = json.loads([l for l in bad.stdout.splitlines() if l.startswith("{")][0])
+    assert d["restore_verified"] is False
+    assert "restore NOT verified" in bad.stderr
