@@ -77,6 +77,9 @@ def parse_args(argv=None):
                    help="restore after the save instead of streaming behind it")
     p.add_argument("--spill-dir", default="/dev/shm",
                    help="where the host region lives (shared by saver and restorer)")
+    p.add_argument("--allow-remote-numa", action="store_true",
+                   help="measure even when a rank's host region is not on its GPU's socket "
+                        "(default: fail before the timed steps)")
     p.add_argument("--device", choices=("cuda", "cpu"), default="cuda",
                    help="cpu: rehearse the multi-rank control flow on CPU tensors over gloo "
                         "(tests; not a measurement of the MI355X path)")
@@ -293,6 +296,7 @@ def main(argv=None):
     except OSError:
         pass
     setup_s = time.perf_counter() - t_setup
+
     barrier()
 
     def save_restore(meta):
@@ -329,6 +333,45 @@ def main(argv=None):
     for i in range(args.warmup):
         save_restore({"warmup": True})
         progress("warmup %d/%d" % (i + 1, args.warmup))
+    # Where each rank's host region landed vs its GPU's socket, gathered from every rank: at
+    # N = 8 the overlapped step moves ~0.74 TB/s through host DRAM over two sockets, and a
+    # region on the wrong socket also crosses the inter-socket link.  Checked after the warmup
+    # (its saves touched every page of the regions), before timing.
+    from terraform_provider_iterative_amd.checkpoint.host import numa_placement
+    from terraform_provider_iterative_amd.parallel.placement import region_placement_report
+
+    gpu_numa = -1
+    if on_gpu:
+        import ctypes
+
+        from terraform_provider_iterative_amd.ops import hip
+
+        node = ctypes.c_int(-1)
+        if hip().tpi_device_numa_node(device.index, ctypes.byref(node)) == 0:
+            gpu_numa = node.value
+    elif os.environ.get("TPI_FAKE_GPU_NUMA"):  # CPU rehearsal of a multi-socket node
+        fake = [int(v) for v in os.environ["TPI_FAKE_GPU_NUMA"].split(",")]
+        gpu_numa = fake[local_rank % len(fake)]
+    placed = numa_placement(ck.region.addr, ck.region.size) if ck.region is not None else None
+    mine = {"rank": rank, "gpu_numa": gpu_numa,
+            "bytes_per_node": (placed or {}).get("bytes_per_node", {}),
+            "policy": (placed or {}).get("policy"),
+            "cpus": len(pinned_cpus) if pinned_cpus else None}
+
+    def gather(obj):
+        if world == 1:
+            return [obj]
+        objs = [None] * world
+        dist.all_gather_object(objs, obj)
+        return objs
+
+    placements = gather(mine)
+    _, numa_problems = region_placement_report(placements)
+    if numa_problems and not args.allow_remote_numa:
+        if rank == 0:
+            print("bench: host regions off their GPU's socket (--allow-remote-numa to measure "
+                  "anyway): " + "; ".join(numa_problems), file=sys.stderr, flush=True)
+        raise SystemExit(4)
     barrier()
 
     fault = os.environ.get("TPI_BENCH_FAULT", "")
@@ -348,7 +391,7 @@ def main(argv=None):
         def broken_restore(*a, **kw):
             res = real_restore(*a, **kw)
             calls[0] += 1
-            if calls[0] > 1 + args.warmup:  # "skips" tensors 3.. after the first timed step
+            if calls[0] > 1:  # "skips" tensors 3.. after the first timed step
                 poison(dict(list((successor or tensors).items())[2:]))
             return res
 
@@ -404,11 +447,13 @@ def main(argv=None):
         if on_gpu:
             torch.cuda.empty_cache()
 
-    host_numa = None
-    if rank == 0 and ck.region is not None:  # which socket(s) the spill pages landed on
-        from terraform_provider_iterative_amd.checkpoint.host import numa_placement
-
-        host_numa = numa_placement(ck.region.addr, ck.region.size)
+    host_numa = placed if rank == 0 else None  # rank 0's spill pages (kept for history)
+    # every rank's region moves its wire bytes into host DRAM (save) and out again (restore)
+    wires = gather(int(wire))
+    for entry, w in zip(placements, wires):
+        entry["wire_bytes_per_step"] = 2 * w
+    placement_report, _ = region_placement_report(placements)
+    placement_report["remote_numa_ranks"] = numa_problems
     elapsed = allmax(elapsed)
     save_max, restore_max = allmax(save_s), allmax(restore_s)
 
@@ -465,6 +510,9 @@ def main(argv=None):
             "sequential": None,
             "rank0_cpu_affinity": len(pinned_cpus) if pinned_cpus else None,
             "host_region_numa": host_numa,
+            # per rank: GPU socket, where its host region's pages are, the bytes it moves
+            # through host DRAM per step; and the per-socket totals
+            "rank_placement": placement_report,
             "restore_verified": verified,
             "save_async": None,
             "setup_s": round(setup_s, 2),

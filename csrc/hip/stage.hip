@@ -441,6 +441,38 @@ int comm_stream(tpi_comm* c) {
   return 0;
 }
 
+// Collectives of several ranks are enqueued in one NCCL group.  Whatever fails -- an enqueue
+// or the group end -- the group is ended before returning: a thread left inside
+// ncclGroupStart() would silently fold every later NCCL call into that unfinished group.
+// TPI_NCCL_FAIL_AT=<i> (fault injection, tests) fails the i-th enqueue without calling NCCL.
+thread_local int g_groups_open = 0;  // NCCL group depth is per thread
+
+template <class Enqueue>
+int grouped(const char* what, int n, Enqueue&& enqueue) {
+  ncclResult_t r = ncclGroupStart();
+  if (r != ncclSuccess) return tpi_fail(std::string("ncclGroupStart: ") + ncclGetErrorString(r));
+  ++g_groups_open;
+  int fail_at = -1;
+  if (const char* f = getenv("TPI_NCCL_FAIL_AT")) fail_at = atoi(f);
+  ncclResult_t first = ncclSuccess;
+  int at = -1;
+  for (int i = 0; i < n && first == ncclSuccess; ++i) {
+    const ncclResult_t e = i == fail_at ? ncclInvalidArgument : enqueue(i);
+    if (e != ncclSuccess) {
+      first = e;
+      at = i;
+    }
+  }
+  const ncclResult_t end = ncclGroupEnd();
+  --g_groups_open;
+  if (first != ncclSuccess)
+    return tpi_fail(std::string(what) + " (rank " + std::to_string(at) + "): " +
+                    ncclGetErrorString(first) + (end != ncclSuccess ? std::string("; ncclGroupEnd: ") +
+                                                     ncclGetErrorString(end) : std::string()));
+  if (end != ncclSuccess) return tpi_fail(std::string("ncclGroupEnd: ") + ncclGetErrorString(end));
+  return 0;
+}
+
 int finish(tpi_comm** comms, int n, int sync) {
   if (!sync) return 0;
   for (int i = 0; i < n; ++i) {
@@ -519,29 +551,28 @@ int tpi_comm_size(const tpi_comm* c) { return c->nranks; }
 int tpi_comm_allgather_inplace(tpi_comm** comms, int n, void** bufs, uint64_t shard_bytes,
                                int sync) {
   roctxRangePushA("tpi_comm_allgather");
-  TPI_NCCL(ncclGroupStart());
-  for (int i = 0; i < n; ++i) {
+  int rc = grouped("ncclAllGather", n, [&](int i) {
     uint8_t* b = (uint8_t*)bufs[i];
-    TPI_NCCL(ncclAllGather(b + (uint64_t)comms[i]->rank * shard_bytes, b, shard_bytes, ncclUint8,
-                           comms[i]->comm, comms[i]->stream));
-  }
-  TPI_NCCL(ncclGroupEnd());
-  int rc = finish(comms, n, sync);
+    return ncclAllGather(b + (uint64_t)comms[i]->rank * shard_bytes, b, shard_bytes, ncclUint8,
+                         comms[i]->comm, comms[i]->stream);
+  });
+  if (rc == 0) rc = finish(comms, n, sync);
   roctxRangePop();
   return rc;
 }
 
 int tpi_comm_broadcast(tpi_comm** comms, int n, void** bufs, uint64_t bytes, int root, int sync) {
   roctxRangePushA("tpi_comm_broadcast");
-  TPI_NCCL(ncclGroupStart());
-  for (int i = 0; i < n; ++i)
-    TPI_NCCL(ncclBroadcast(bufs[i], bufs[i], bytes, ncclUint8, root, comms[i]->comm,
-                           comms[i]->stream));
-  TPI_NCCL(ncclGroupEnd());
-  int rc = finish(comms, n, sync);
+  int rc = grouped("ncclBroadcast", n, [&](int i) {
+    return ncclBroadcast(bufs[i], bufs[i], bytes, ncclUint8, root, comms[i]->comm,
+                         comms[i]->stream);
+  });
+  if (rc == 0) rc = finish(comms, n, sync);
   roctxRangePop();
   return rc;
 }
+
+int tpi_nccl_groups_open() { return g_groups_open; }
 
 int tpi_comm_sync(tpi_comm** comms, int n) { return finish(comms, n, 1); }
 

@@ -251,6 +251,9 @@ int tpi_comm_allgather_inplace(tpi_comm** comms, int n, void** bufs, uint64_t sh
                                int sync);
 int tpi_comm_broadcast(tpi_comm** comms, int n, void** bufs, uint64_t bytes, int root, int sync);
 int tpi_comm_sync(tpi_comm** comms, int n);
+// NCCL groups this library has started and not ended (0 outside a collective call, also after
+// a failed one); TPI_NCCL_FAIL_AT=<i> makes the i-th enqueue of a grouped collective fail.
+int tpi_nccl_groups_open(void);
 
 #ifdef __cplusplus
 }

@@ -122,6 +122,7 @@ class HipLib:
             "tpi_comm_allgather_inplace": (i32, [c.POINTER(vp), i32, c.POINTER(vp), u64, i32]),
             "tpi_comm_broadcast": (i32, [c.POINTER(vp), i32, c.POINTER(vp), u64, i32, i32]),
             "tpi_comm_sync": (i32, [c.POINTER(vp), i32]),
+            "tpi_nccl_groups_open": (i32, []),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)

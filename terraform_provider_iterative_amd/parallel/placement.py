@@ -583,6 +583,40 @@ def _alloc_from(data: dict) -> "Allocation":
                       spot=bool(data.get("spot")), notes=list(data.get("notes") or []))
 
 
+def region_placement_report(entries: List[dict], tolerance: float = 0.10):
+    """Host-region NUMA placement of a job's ranks against their GPUs' sockets.
+
+    ``entries``: one per rank, ``{"rank", "gpu_numa", "bytes_per_node": {"N0": bytes, ...},
+    "wire_bytes_per_step"}`` (``gpu_numa`` -1: unknown, not checked).  Every rank's spill and
+    restore cross the host memory its region lives in; a region on the other socket puts that
+    traffic on the inter-socket link as well (at 8 ranks, ~0.74 TB/s of host-DRAM traffic over
+    two sockets).  Returns ``(report, problems)``: the report adds the host-DRAM bytes each
+    NUMA node moves per step (save into + restore out of the regions on it), ``problems``
+    names every rank with more than ``tolerance`` of its region off its GPU's node."""
+    traffic: Dict[str, float] = {}
+    problems: List[str] = []
+    for e in entries:
+        per_node = {k: int(v) for k, v in (e.get("bytes_per_node") or {}).items()}
+        total = sum(per_node.values())
+        wire = float(e.get("wire_bytes_per_step") or 0)
+        for node, nbytes in per_node.items():
+            if total:
+                traffic[node] = traffic.get(node, 0.0) + wire * nbytes / total
+        gpu = e.get("gpu_numa")
+        if gpu is None or int(gpu) < 0 or not total:
+            continue
+        remote = total - per_node.get("N%d" % int(gpu), 0)
+        if remote > tolerance * total:
+            problems.append("rank %s: %.1f of its %.1f GB host region on %s, but its GPU is on "
+                            "NUMA node %d" % (e.get("rank"), remote / 1e9, total / 1e9,
+                                              ",".join(sorted(n for n in per_node
+                                                              if n != "N%d" % int(gpu))),
+                                              int(gpu)))
+    report = {"ranks": entries,
+              "host_dram_bytes_per_step": {k: int(v) for k, v in sorted(traffic.items())}}
+    return report, problems
+
+
 def numa_cpus(node: int) -> List[int]:
     """CPU cores of NUMA node ``node`` (empty when unknown)."""
     if node is None or node < 0:

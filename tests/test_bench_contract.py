@@ -163,3 +163,55 @@ def test_a_restore_that_stops_rewriting_fails_the_bench(tmp_path):
     d = json.loads([l for l in bad.stdout.splitlines() if l.startswith("{")][0])
     assert d["restore_verified"] is False
     assert "restore NOT verified" in bad.stderr
+
+
+def test_region_placement_report_on_a_two_socket_node():
+    """8 ranks, GPUs 0-3 on socket 0 and 4-7 on socket 1 (the MI355X node layout): regions on
+    their own socket pass; one spilled to the other socket is named; the per-socket host-DRAM
+    traffic adds up the ranks' wire bytes in proportion to where their pages are."""
+    from terraform_provider_iterative_amd.parallel.placement import region_placement_report
+
+    gb = 10 ** 9
+    entries = [{"rank": r, "gpu_numa": 0 if r < 4 else 1,
+                "bytes_per_node": {"N%d" % (0 if r < 4 else 1): 12 * gb},
+                "wire_bytes_per_step": 20 * gb} for r in range(8)]
+    report, problems = region_placement_report(entries)
+    assert problems == []
+    assert report["host_dram_bytes_per_step"] == {"N0": 80 * gb, "N1": 80 * gb}
+    entries[5]["bytes_per_node"] = {"N0": 9 * gb, "N1": 3 * gb}  # node 1 ran short
+    report, problems = region_placement_report(entries)
+    assert len(problems) == 1 and problems[0].startswith("rank 5:") and "node 1" in problems[0]
+    assert report["host_dram_bytes_per_step"] == {"N0": 95 * gb, "N1": 65 * gb}
+    entries[5]["gpu_numa"] = -1  # unknown GPU socket: reported, not judged
+    assert region_placement_report(entries)[1] == []
+
+
+def _eight_rank_cpu_bench(tmp_path, fake_numa, *extra):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "8", "--device", "cpu", "--total-gb",
+           "0.016", "--steps", "1", "--warmup", "1", "--no-latency", "--hidden", "128",
+           "--broadcast-gb", "0", "--no-async", *extra]
+    env = dict(os.environ, OMP_NUM_THREADS="1", TPI_FAKE_GPU_NUMA=fake_numa)
+    return subprocess.run(cmd, cwd=str(tmp_path), capture_output=True, text=True, timeout=400,
+                          env=env)
+
+
+def test_eight_ranks_report_their_placement_and_fail_fast_off_socket(tmp_path):
+    """8 gloo ranks: every rank's GPU socket and region placement reaches rank 0's JSON.  This
+    container has one NUMA node, so on a fake 2-socket topology ranks 4-7 ("GPUs on socket 1")
+    hold regions on the wrong socket: the bench stops before timing, naming them."""
+    ok = _eight_rank_cpu_bench(tmp_path, "0")
+    assert ok.returncode == 0, ok.stderr[-3000:]
+    d = json.loads([l for l in ok.stdout.splitlines() if l.startswith("{")][0])
+    ranks = d["rank_placement"]["ranks"]
+    assert [e["rank"] for e in ranks] == list(range(8))
+    assert all(e["gpu_numa"] == 0 and e["bytes_per_node"].get("N0") for e in ranks), ranks
+    per_node = d["rank_placement"]["host_dram_bytes_per_step"]
+    assert per_node["N0"] == sum(e["wire_bytes_per_step"] for e in ranks) > 0
+    bad = _eight_rank_cpu_bench(tmp_path, "0,0,0,0,1,1,1,1")
+    assert bad.returncode != 0
+    assert "off their GPU's socket" in bad.stderr
+    for r in (4, 5, 6, 7):
+        assert "rank %d:" % r in bad.stderr
+    assert "rank 3:" not in bad.stderr

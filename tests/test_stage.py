@@ -249,3 +249,26 @@ def test_eight_rank_write_back_takes_every_ranks_changes(cloud, tmp_path, method
     assert "dirty_shards 8" in final.description, final.description
     assert any(e.code == "workdir-sync-conflict" for e in events)
     task.delete()
+
+
+def test_nccl_error_inside_a_group_still_ends_the_group(monkeypatch):
+    """an NCCL error while enqueueing a grouped collective used to return from
+    inside ncclGroupStart(), leaving the thread in an open group (every later NCCL call would
+    join it).  Injected failure (TPI_NCCL_FAIL_AT): the call fails with the collective and rank
+    named, and no group is left open -- for the all-gather and the broadcast."""
+    import ctypes
+
+    from terraform_provider_iterative_amd.ops import hip
+
+    lib = hip(required=False)
+    if lib is None:
+        pytest.skip("libtpi_hip.so not built")
+    monkeypatch.setenv("TPI_NCCL_FAIL_AT", "0")  # before any communicator is touched
+    comms = (ctypes.c_void_p * 2)(None, None)
+    bufs = (ctypes.c_void_p * 2)(None, None)
+    assert lib.tpi_comm_broadcast(comms, 2, bufs, 64, 0, 1) == -1
+    assert "ncclBroadcast (rank 0)" in lib.error()
+    assert lib.tpi_nccl_groups_open() == 0
+    assert lib.tpi_comm_allgather_inplace(comms, 2, bufs, 32, 1) == -1
+    assert "ncclAllGather (rank 0)" in lib.error()
+    assert lib.tpi_nccl_groups_open() == 0
