@@ -32,6 +32,7 @@ from ..models.values import (STATUS_RUNNING, Event, NotFoundError, NotImplemente
                              RemoteStorage, Task as TaskSpec, new_status)
 from ..parallel.placement import (Allocation, Placement, PlacementBusy, PlacementError,
                                   Request, node_cpus, pid_alive)
+from ..storage import remote as remote_storage
 from ..storage import transfer as storage
 from ..utils.identifier import Identifier, parse_identifier
 from ..utils.steps import Step, StepTiming, run_steps
@@ -42,7 +43,8 @@ log = logging.getLogger("tpi")
 # Host environment a rank inherits besides the task's own variables (the systemd unit of
 # the reference starts from a clean environment + EnvironmentFile, tpl:45-59).
 PASSTHROUGH_EXACT = ("PATH", "HOME", "USER", "LOGNAME", "LANG", "TZ", "TMPDIR",
-                     "LD_LIBRARY_PATH", "PYTHONPATH", "OMP_NUM_THREADS", "MAX_JOBS")
+                     "LD_LIBRARY_PATH", "PYTHONPATH", "OMP_NUM_THREADS", "MAX_JOBS",
+                     "TPI_SSH_COMMAND")  # the transport to an off-node storage.container
 PASSTHROUGH_PREFIXES = ("LC_", "HSA_", "HIP_", "ROCR_", "ROCM_", "NCCL_", "RCCL_", "GPU_",
                         "AMD_", "MIOPEN_", "TORCH_", "PYTORCH_")
 
@@ -144,7 +146,11 @@ class NodeTask(Task):
             rs = self._saved["remote_storage"]
             remote = RemoteStorage(rs["container"], rs.get("path", ""), rs.get("config", {}))
         self.remote = remote
-        if remote is not None:
+        # an off-node container (storage/remote.py): the node works on a local copy that is
+        # restored from it at create and mirrored back while the task runs
+        self.remote_conn = remote_storage.parse(remote.container, remote.path,
+                                                remote.config) if remote is not None else None
+        if remote is not None and self.remote_conn is None:
             conn = storage.Connection.parse(remote.container)
             base = conn.local_path()
             self.data_dir = os.path.join(base, remote.path.lstrip("/")) if remote.path else base
@@ -366,7 +372,7 @@ class NodeTask(Task):
         env.update({
             "TPI_TASK_CLOUD_PROVIDER": self.provider,
             "TPI_TASK_CLOUD_REGION": str(d.get("region", "")),
-            "RCLONE_REMOTE": str(storage.Connection("local", self.root)),
+            "RCLONE_REMOTE": str(self.remote_conn or storage.Connection("local", self.root)),
         })
         visible = ",".join(str(g) for g in gpus)
         numa = [g.get("numa_node", -1) for g in d.get("gpu_info") or []]
@@ -406,7 +412,24 @@ class NodeTask(Task):
                       ([self.placement.alloc_path(self.id)] if alloc else []),
             "limits": self._limits(alloc),
             "requeue_argv": self._waiter_argv(),
+            "sync": self._remote_sync(knob),
         }
+
+    def _remote_sync(self, knob) -> Optional[Dict]:
+        """The supervisor's mirror of an off-node container: every ``TPI_SYNC_INTERVAL`` s
+        (default 10, as the reference's data loop, tpl:118-124) and once when the ranks are
+        done, before the task counts as finished."""
+        if self.remote_conn is None:
+            return None
+        try:
+            interval = float(knob("TPI_SYNC_INTERVAL", "10"))
+        except ValueError:
+            interval = 10.0
+        code = ("import sys; sys.path.insert(0, %r); "
+                "from terraform_provider_iterative_amd.storage.remote import main; "
+                "sys.exit(main(['sync', %r]))" % (ROOT, self.root))
+        return {"argv": [sys.executable, "-c", code], "interval": interval if interval > 0 else 0,
+                "timeout": float(knob("TPI_REMOTE_SYNC_TIMEOUT", "600"))}
 
     def _rank_cpus(self, rank: int, alloc: Dict) -> List[int]:
         """Affinity of rank ``rank``: its reserved cores (``reserve`` mode), else -- a limit
@@ -523,6 +546,8 @@ class NodeTask(Task):
                  Step("Writing machine script...", self._write_script)]
         if self.spec.environment.directory:
             steps.append(Step("Uploading Directory...", self.push))
+        if self.remote_conn is not None:  # tpl:89: the workdir comes from the container
+            steps.append(Step("Restoring Directory from the container...", self._restore_remote))
         steps.append(Step("Starting task...", start))
         run_steps(steps, self.timings)
         log.info("Creation completed" + (" (queued: %s)" % queued[0] if queued else ""))
@@ -744,7 +769,18 @@ class NodeTask(Task):
         directory = self.spec.environment.directory
         if not directory:
             return
+        if self.remote_conn is not None:  # into the container; the node restores from it
+            stats = remote_storage.SSHRemote(self.remote_conn).put_tree(
+                directory, "data", storage.transfer_rules(self.spec.environment.exclude_list))
+            log.info("Uploaded %d files to %s", stats["files"], self.remote_conn)
+            return
         storage.transfer(directory, self.data_dir, self.spec.environment.exclude_list)
+
+    def _restore_remote(self) -> None:
+        stats = remote_storage.SSHRemote(self.remote_conn).get_tree("data", self.data_dir,
+                                                                    ["+ **"])
+        self._event("container-restored", str(self.remote_conn),
+                    "%d files" % stats["files"], "%d bytes" % stats["bytes"])
 
     def pull(self) -> None:
         saved = self._saved or {}
@@ -752,6 +788,9 @@ class NodeTask(Task):
         out = self.spec.environment.directory_out or saved.get("directory_out") or ""
         excludes = self.spec.environment.exclude_list or saved.get("exclude") or []
         rules = storage.limit_transfer(out, storage.transfer_rules(excludes))
+        if self.remote_conn is not None:  # the container holds the task's final data
+            remote_storage.SSHRemote(self.remote_conn).get_tree("data", directory, rules)
+            return
         storage.transfer(self.data_dir, directory, rules=rules)
 
     def status(self) -> Dict[str, int]:

@@ -35,6 +35,7 @@ import hashlib
 import json
 import os
 import struct
+import tempfile
 import threading
 import time
 from dataclasses import dataclass
@@ -305,6 +306,15 @@ def _writer_alive(pid: int) -> bool:
         return state not in ("Z", "X")
     except (OSError, IndexError):
         return True
+
+
+def _local_scratch(remote_path: str) -> str:
+    """Where a checkpoint bound for (or fetched from) another node is staged on this one:
+    ``TPI_PERSIST_TMPDIR``, else the task directory, else the temp directory."""
+    base = (os.environ.get("TPI_PERSIST_TMPDIR") or os.environ.get("TPI_TASK_DIRECTORY")
+            or tempfile.gettempdir())
+    return os.path.join(base, ".tpi-persist-%d-%s" % (os.getpid(),
+                                                     os.path.basename(remote_path) or "ckpt"))
 
 
 class PendingSave:
@@ -1147,7 +1157,20 @@ class Checkpointer:
 
     def persist(self, path: str) -> str:
         """Write the current checkpoint (header, CRCs, stream: one slot) to ``path``
-        atomically."""
+        atomically.  ``path`` may name a file on another node (``ssh://host/dir/file``,
+        ``host:/dir/file``: an off-node ``storage.container``, :mod:`..storage.remote`); the
+        file is written locally first, then moved there."""
+        from ..storage import remote
+
+        if remote.is_remote(path):
+            tmp = _local_scratch(path)
+            try:
+                self.persist(tmp)
+                remote.store(tmp, path)
+            finally:
+                if os.path.exists(tmp):
+                    os.remove(tmp)
+            return path
         self.wait_pending()
         active = self._active()
         if active is None:
@@ -1167,7 +1190,16 @@ class Checkpointer:
 
         The stream section is read by parallel native readers in chunks that are published
         like a streamed save's (progress block), so the device restore runs behind the file
-        read instead of after it."""
+        read instead of after it.  ``path`` may name a file on another node (see
+        :meth:`persist`): it is fetched first."""
+        from ..storage import remote
+
+        if remote.is_remote(path):
+            tmp = remote.fetch(path, os.path.dirname(_local_scratch(path)))
+            try:
+                return self.load(tmp)
+            finally:
+                os.remove(tmp)
         self.wait_pending()
         self._wait_writers()
         slot, generation = self._target()

@@ -771,6 +771,19 @@ def install(signals=(signal.SIGTERM,)) -> None:
     _handoff_safe()
 
 
+def _persisted(path: str) -> bool:
+    """A persisted checkpoint exists at ``path`` (a local file, or one in an off-node
+    ``storage.container``)."""
+    from ..storage import remote
+
+    if remote.is_remote(path):
+        try:
+            return remote.file_exists(path)
+        except (OSError, ValueError):
+            return False
+    return os.path.exists(path)
+
+
 def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None,
            generation: Optional[int] = None) -> Optional[Dict]:
     """Restore from the host region (or ``persist_path``) if a complete checkpoint exists.
@@ -850,7 +863,7 @@ def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None,
         except CheckpointError as error:
             failure = error
             journal("checkpoint-corrupt", "host region", str(error))
-    if persist_path and os.path.exists(persist_path):
+    if persist_path and _persisted(persist_path):
         try:
             res = checkpointer.load(persist_path)
         except CheckpointError as error:

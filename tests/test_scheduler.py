@@ -143,8 +143,10 @@ def test_on_demand_task_reclaims_a_spot_task_which_resumes_later(tmp_path, monke
     time.sleep(0.3)
     od = _task(cloud, "ondemand", "#!/bin/sh\necho on-demand on GPU $HIP_VISIBLE_DEVICES\n"
                                   "sleep 1\necho done\n")
+    # the spot task is handed back within ~0.1 s of the reclaim (save, release, requeue):
+    # observe its "running" before the on-demand task is applied
+    seen = {"spot": [reduce_status(spot.status(), 1)], "od": []}
     od.create()
-    seen = {"spot": [], "od": []}
     deadline = time.time() + 120
     while time.time() < deadline:
         for name, task in (("spot", spot), ("od", od)):
