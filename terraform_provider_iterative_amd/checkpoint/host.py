@@ -85,12 +85,18 @@ class HostRegion:
         arr = np.frombuffer(buf, dtype=np.uint8, count=length)
         return arr.view(dtype) if itemsize > 1 else arr
 
-    def close(self) -> None:
+    def close(self, timings: Optional[Dict[str, float]] = None) -> None:
+        """Unregister (unpin) and unmap; ``timings`` receives the seconds of each phase
+        (``unregister``, ``unmap``)."""
         if self.addr is None:
             return
+        import time
+
+        t0 = time.perf_counter()
         if self.device and self._mmap is not None:  # early-prefetched mapping
             if self.registered:
                 hip().tpi_host_unregister(ctypes.c_void_p(self.addr))
+            t1 = time.perf_counter()
             try:
                 self._mmap.close()
             except BufferError:
@@ -102,12 +108,18 @@ class HostRegion:
                 self.pinner = None
             elif self.registered:
                 lib.tpi_host_unregister(ctypes.c_void_p(self.addr))
+            t1 = time.perf_counter()
             lib.tpi_host_unmap(ctypes.c_void_p(self.addr), self.size)
-        elif self._mmap is not None:
-            try:
-                self._mmap.close()
-            except BufferError:  # outstanding numpy views; the mapping dies with them
-                pass
+        else:
+            t1 = t0
+            if self._mmap is not None:
+                try:
+                    self._mmap.close()
+                except BufferError:  # outstanding numpy views; the mapping dies with them
+                    pass
+        if timings is not None:
+            timings["unregister"] = t1 - t0
+            timings["unmap"] = time.perf_counter() - t1
         self.addr = None
 
     def __del__(self):  # pragma: no cover - best effort

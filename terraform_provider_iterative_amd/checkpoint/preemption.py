@@ -641,10 +641,10 @@ def _teardown(code: int, release_device: bool = True) -> None:
             region = getattr(ck, "region", None)
             if region is None or not getattr(region, "registered", False):
                 continue
-            t1 = time.perf_counter()
-            region.close()  # unregister (unpin) + unmap; a /dev/shm file keeps its pages
-            phases.append("host region %.1f GB %.3f s" % (region.size / 1e9,
-                                                          time.perf_counter() - t1))
+            split: Dict[str, float] = {}
+            region.close(split)  # unregister (unpin) + unmap; a /dev/shm file keeps its pages
+            phases.append("host region %.1f GB: unregister %.3f s, unmap %.3f s" % (
+                region.size / 1e9, split.get("unregister", 0.0), split.get("unmap", 0.0)))
         if phases:
             journal("predecessor-teardown", *phases)
     except Exception as error:  # never keep a preempted process alive over its teardown
