@@ -622,13 +622,20 @@ def _withdraw_handoffs() -> None:
 
 
 def _teardown(code: int, release_device: bool = True) -> None:
-    """Give back this process's HBM and host-region pinning explicitly, each phase timed in
-    the journal (``predecessor-teardown``), then ``os._exit``.  What remains -- the kernel's
-    own teardown of the address space and GPU context -- shows in the supervisor's
-    ``exit-trace`` events.  ``release_device`` only when no other thread may still run device
-    work on the tensors (a boundary save on the main thread).  ``TPI_EXPLICIT_TEARDOWN=0``:
-    straight to ``os._exit`` (the kernel does all of it)."""
-    if os.environ.get("TPI_EXPLICIT_TEARDOWN", "1") in ("0", "false", "no"):
+    """Give back this process's HBM explicitly (timed in the journal: ``predecessor-teardown``)
+    and ``os._exit``; the kernel's own teardown of the address space and GPU context that
+    follows shows in the supervisor's ``exit-trace`` events.  ``release_device`` only when no
+    other thread may still run device work on the tensors (a boundary save on the main thread).
+
+    ``TPI_EXPLICIT_TEARDOWN``: ``hbm`` (default) frees the device memory and leaves the pinned
+    host region to the kernel; ``full`` also unregisters and unmaps the region first; ``0``
+    goes straight to ``os._exit``.  Measured on MI355X with a 100 GB region
+    (profiles/round4/teardown.md): unmapping it explicitly after a hot hand-off takes ~11 s
+    (the munmap keeps invalidating the live GPU context's user-pointer mappings), the kernel's
+    exit-time teardown ~1.3 s; freeing 100 GB of HBM first costs 0.07 s and hands it to the
+    next process on the GPU at once."""
+    mode = os.environ.get("TPI_EXPLICIT_TEARDOWN", "hbm").strip().lower()
+    if mode in ("0", "false", "no", "off"):
         os._exit(code)
     phases = []
     try:
@@ -637,7 +644,7 @@ def _teardown(code: int, release_device: bool = True) -> None:
             freed = _release_device_memory()
             if freed:
                 phases.append("hbm %.1f GB %.3f s" % (freed / 1e9, time.perf_counter() - t0))
-        for ck in _registered:
+        for ck in _registered if mode in ("full", "1", "true", "yes") else ():
             region = getattr(ck, "region", None)
             if region is None or not getattr(region, "registered", False):
                 continue
