@@ -79,6 +79,7 @@ class TransferResult:
     crc: int = 0
     dirty_tiles: int = -1  # incremental sync: tiles that changed since the previous sync
     wire_bytes: int = -1   # bytes that crossed the link / landed in the region (codec)
+    released_bytes: int = 0  # device memory freed behind the spill (save(release_behind=True))
 
     def __post_init__(self):
         if self.wire_bytes < 0:
@@ -306,6 +307,32 @@ def _writer_alive(pid: int) -> bool:
         return state not in ("Z", "X")
     except (OSError, IndexError):
         return True
+
+
+def streaming_writer(path: str) -> Optional[Dict[str, int]]:
+    """``{"pid", "total"}`` of a live process streaming a save into the region file ``path``
+    right now (a preempted predecessor), else None.  Reads the file only (no mapping)."""
+    try:
+        with open(path, "rb") as f:
+            head = f.read(PREAMBLE + Checkpointer.HEADER_RESERVE)
+            header = Checkpointer.read_header(np.frombuffer(head, np.uint8))
+            bases = [0]
+            if header.get("entries_len") is not None:
+                slot_end = _layout(Checkpointer.HEADER_RESERVE, int(header["entries_len"]),
+                                   int(header["ntiles"]), int(header["total"]),
+                                   int(header["tile_bytes"]))[4]
+                if os.fstat(f.fileno()).st_size >= 2 * align_up(slot_end, 4096):
+                    bases.append(align_up(slot_end, 4096))
+            for base in bases:
+                f.seek(base + int(header["entries_offset"]) - 64)
+                prog = np.frombuffer(f.read(64), np.uint64)
+                if (len(prog) == 8 and int(prog[0]) == PROGRESS_MAGIC
+                        and int(prog[4]) == STREAM_RUNNING and _writer_alive(int(prog[5]))
+                        and int(prog[5]) != os.getpid()):
+                    return {"pid": int(prog[5]), "total": int(header["total"])}
+    except (OSError, ValueError, KeyError, CheckpointError):
+        return None
+    return None
 
 
 def _local_scratch(remote_path: str) -> str:
@@ -634,14 +661,66 @@ class Checkpointer:
         return self.read_header(self.region.array(0, self.crc_offset))
 
     # -- operations --------------------------------------------------------------------------
+    def _release_behind(self, progress: np.ndarray, stop: threading.Event,
+                        out: Dict[str, float]) -> None:
+        """Free each bound tensor's device storage as soon as the streamed save has
+        published (spilled to host memory) every tile of it, and hand the freed segments back
+        to the driver (``empty_cache``) every ~8 GB -- a preempted rank's HBM returns while
+        its spill runs, so the driver's clearing of it overlaps the PCIe leg instead of
+        delaying the successor's allocations.  Storages shared by several bound tensors go
+        when the last of them is covered."""
+        import torch
+
+        schedule = self.release_schedule(device_only=True)
+        tile = self.plan.tile_bytes
+        freed = pending = 0
+        i = 0
+        while i < len(schedule):
+            done = int(progress[0]) * tile
+            finished = stop.is_set() and out.get("finish", 0.0) == 1.0
+            if stop.is_set() and not finished:  # the save failed: keep the rest
+                break
+            while i < len(schedule) and (schedule[i][0] <= done or finished):
+                st = schedule[i][1]
+                nbytes = st.nbytes()
+                st.resize_(0)
+                freed += nbytes
+                pending += nbytes
+                i += 1
+            if pending >= (8 << 30) or (pending and (i == len(schedule) or stop.is_set())):
+                torch.cuda.empty_cache()
+                pending = 0
+            if i < len(schedule):
+                stop.wait(0.002)
+        out["released_bytes"] = freed
+
+    def release_schedule(self, device_only: bool = False) -> List[Tuple[int, Any]]:
+        """``[(end, storage)]`` in release order: each storage behind the bound tensors with
+        the byte offset in the packed stream where its last bound tensor ends -- it may be
+        freed once the save has published every tile below that offset."""
+        ends: Dict[int, int] = {}
+        storages: Dict[int, Any] = {}
+        for t, e in zip(self.plan._bound, self.plan.entries):
+            if device_only and not getattr(t, "is_cuda", False):
+                continue
+            st = t.untyped_storage()
+            key = st.data_ptr()
+            ends[key] = max(ends.get(key, 0), e.offset + e.nbytes)
+            storages[key] = st
+        return [(ends[k], storages[k]) for k in sorted(ends, key=ends.get)]
+
     def save(self, metadata: Optional[Dict] = None,
-             on_stream: Optional[Any] = None) -> TransferResult:
+             on_stream: Optional[Any] = None, release_behind: bool = False) -> TransferResult:
         """Pack every tensor into the region; returns bytes/seconds (GB/s via ``.gbps``).
 
         ``on_stream`` (preemption hand-off): the save first writes a ``streaming`` header and
         a progress block, calls ``on_stream()`` -- which lets the successor start -- and then
         publishes every chunk as it reaches host memory, so :meth:`restore` in the successor
         runs behind the spill over the other direction of the link instead of after it.
+
+        ``release_behind`` (a preempted rank whose state is too big for a successor's copy next
+        to it): every bound tensor's device memory is freed as soon as its tiles are in host
+        memory (:meth:`_release_behind`); the tensors are unusable afterwards.
         """
         self.wait_pending()
         self._wait_writers()
@@ -649,7 +728,14 @@ class Checkpointer:
         self._invalidate(slot)
         zipped = self.codec == "tpz1"
         dst = self.region.addr + slot.base + self.stream_offset
-        streaming = on_stream is not None
+        release_behind = release_behind and self.engine is not None
+        streaming = on_stream is not None or release_behind
+        if on_stream is None:
+            on_stream = lambda: None  # noqa: E731 (the progress block alone)
+        releaser = None
+        released: Dict[str, float] = {}
+        stop_release = threading.Event()
+        saved_ok = False
         if streaming:
             prog = slot.progress
             prog[1], prog[2], prog[3], prog[5] = generation, 0, 0, os.getpid()
@@ -667,11 +753,18 @@ class Checkpointer:
                 wait = torch.cuda.current_stream(self.device_index).cuda_stream
                 if streaming:
                     self.engine.set_progress(slot.progress.ctypes.data + 16)
+                if release_behind:
+                    torch.cuda.current_stream(self.device_index).synchronize()
+                    releaser = threading.Thread(
+                        target=self._release_behind, name="tpi-release-behind",
+                        args=(slot.progress[2:3], stop_release, released), daemon=True)
+                    releaser.start()
                 try:
                     if zipped:
                         res = self.engine.save_z(self.plan, dst, slot.crcs, slot.csizes, wait)
                     else:
                         res = self.engine.save(self.plan, dst, slot.crcs, self.mode, wait)
+                    saved_ok = True
                 finally:
                     if streaming:
                         self.engine.set_progress(0)
@@ -681,6 +774,12 @@ class Checkpointer:
             if streaming:
                 slot.progress[4] = STREAM_FAILED
             raise
+        finally:
+            if releaser is not None:
+                # spilled: the rest goes now; failed: what is not in host memory must stay
+                released["finish"] = 1.0 if saved_ok else 0.0
+                stop_release.set()
+                releaser.join()
         res.crc = native().crc32c_combine_tiles_ptr(slot.crcs.ctypes.data, self.plan.ntiles,
                                                      self.plan.tile_bytes, self.plan.total)
         self.saves += 1
@@ -690,6 +789,8 @@ class Checkpointer:
             slot.progress[3] = res.wire_bytes
             slot.progress[2] = self.plan.ntiles
             slot.progress[4] = STREAM_COMPLETE
+        if releaser is not None:
+            res.released_bytes = int(released.get("released_bytes", 0))
         self.last_save = res
         return res
 

@@ -61,6 +61,7 @@ _boundary_seen = False           # the loop calls step()/tick(): saves wait for 
 _last_step: Optional[int] = None  # user step of the last boundary
 _agreement = None
 _wakeup_r: Optional[int] = None
+_standby_script = False          # the script calls standby(spill): its successor waits for HBM
 
 
 def register(checkpointer: Checkpointer, persist_path: Optional[str] = None) -> None:
@@ -118,7 +119,8 @@ def _collect_metadata(base: Dict) -> Dict:
 
 
 def checkpoint_all(metadata: Optional[Dict] = None, on_stream=None,
-                   exported: Optional[List[Checkpointer]] = None) -> List[float]:
+                   exported: Optional[List[Checkpointer]] = None,
+                   release_behind: bool = False) -> List[float]:
     """Save every registered checkpointer; returns per-checkpointer GB/s.  ``on_stream``
     (single checkpointer only): stream the save to the successor (see
     :meth:`Checkpointer.save`); called once the successor may start.  Checkpointers whose
@@ -130,7 +132,8 @@ def checkpoint_all(metadata: Optional[Dict] = None, on_stream=None,
     t_cb = time.perf_counter() - t0
     rates = []
     for ck in _registered:
-        if on_stream is not None and len(_registered) == 1 and _hbm_handoff():
+        if (on_stream is not None and len(_registered) == 1 and _hbm_handoff()
+                and not release_behind):  # memory freed behind the spill is no hand-off
             try:  # the successor on this GPU copies our HBM while we spill to the host
                 t1 = time.perf_counter()
                 if ck.export_hbm(meta):
@@ -142,9 +145,13 @@ def checkpoint_all(metadata: Optional[Dict] = None, on_stream=None,
                             "export %.3f s" % (time.perf_counter() - t1))
             except Exception as error:  # the host path still works
                 journal("checkpoint-hbm-export-failed", str(error))
-        res = ck.save(meta, on_stream=on_stream if len(_registered) == 1 else None)
+        res = ck.save(meta, on_stream=on_stream if len(_registered) == 1 else None,
+                      release_behind=release_behind)
         rates.append(res.gbps)
         journal("checkpoint-saved", *_describe(res))
+        if getattr(res, "released_bytes", 0):
+            journal("device-memory-released", "%.1f GB behind the spill" % (
+                res.released_bytes / 1e9))
         path = _persist_paths.get(id(ck))
         if path:
             t0 = time.perf_counter()
@@ -371,8 +378,12 @@ def standby(prefetch_path: Optional[str] = None) -> bool:
     right after the old rank has released -- then returns True and resumes from the spill.
     A standby that is not needed is killed (or sees EOF and exits quietly).
     """
+    global _standby_script
+    _standby_script = bool(prefetch_path)
     if os.environ.get("TPI_STANDBY") != "1":
         _notify(b"standby\n")
+        if prefetch_path:  # a cold successor of a big-state predecessor
+            wait_for_device_memory(prefetch_path)
         return False
     cancel = threading.Event()
     torch = sys.modules.get("torch")
@@ -404,8 +415,40 @@ def standby(prefetch_path: Optional[str] = None) -> bool:
             os.environ["MASTER_PORT"] = word[5:].decode()
     os.environ.pop("TPI_STANDBY", None)
     journal("standby-activated")
+    if prefetch_path:
+        wait_for_device_memory(prefetch_path)
     _notify(b"standby\n")  # the activated process can itself be succeeded by a standby
     return True
+
+
+def wait_for_device_memory(spill: str, margin: float = 0.05,
+                           timeout: Optional[float] = None) -> Optional[float]:
+    """A successor started while its predecessor on the same GPU still streams a state too big
+    for two copies (``spill`` is being written by a live process): block until the device has
+    room for the state (+ ``margin``, + 2 GiB for the engine and context) -- the predecessor
+    frees its tensors behind its spill (``Checkpointer.save(release_behind=True)``) -- or the
+    predecessor is gone / done.  Returns the seconds waited (None: nothing to wait for).
+    Called by :func:`standby` before the script allocates its state, so the restore can stream
+    behind the spill instead of starting after the predecessor's exit."""
+    from .checkpointer import streaming_writer
+
+    peer = streaming_writer(spill)
+    torch = sys.modules.get("torch")
+    if peer is None or torch is None or not torch.cuda.is_available():
+        return None
+    need = int(peer["total"] * (1 + margin)) + (2 << 30)
+    if timeout is None:
+        timeout = float(os.environ.get("TPI_STREAM_TIMEOUT", "30"))
+    dev = torch.cuda.current_device()
+    t0 = time.monotonic()
+    while time.monotonic() - t0 < timeout:
+        free, _ = torch.cuda.mem_get_info(dev)
+        if free >= need or streaming_writer(spill) is None:
+            break
+        time.sleep(0.005)
+    waited = time.monotonic() - t0
+    journal("successor-hbm-wait", "%.1f GB needed" % (need / 1e9), "waited %.3f s" % waited)
+    return waited
 
 
 def _linger() -> None:
@@ -546,13 +589,20 @@ def _save_and_exit(consistency: str, ordinal: Optional[int] = None) -> None:
     t_safe = time.perf_counter()
     _handoff_decision = safe = _handoff_safe()  # evaluated once: one device-memory query
     stream_ok = not requeue and _stream_handoff(safe)
+    # too big for two copies, but the successor waits for room (standby(spill)): stream to
+    # it anyway and free each tensor's HBM behind the spill -- its allocation and restore
+    # then run under our spill instead of after it
+    big_stream = (not requeue and not safe and consistency == "boundary" and _standby_script
+                  and _release_hbm_enabled() and _stream_handoff(True)
+                  and os.environ.get("TPI_BIG_STREAM", "1") not in ("0", "false", "no"))
     _phase["handoff-check"] = time.perf_counter() - t_safe
 
     def stream_started():
         # the successor starts now and restores behind the spill (other PCIe direction);
         # journalled first, so the phase journal orders it before the supervisor's release
-        journal("checkpoint-streaming", "successor may start")
-        if notify_released():
+        journal("checkpoint-streaming", "successor may start" if not big_stream else
+                "successor may start; it waits for the HBM freed behind the spill")
+        if (_notify(b"released\n") if big_stream else notify_released()):
             released.append(True)
 
     meta = {"reason": "requeued" if requeue else "preempted", "signal": signum,
@@ -564,9 +614,13 @@ def _save_and_exit(consistency: str, ordinal: Optional[int] = None) -> None:
     code = 1
     at_boundary = consistency == "boundary" or (
         consistency == "signal" and threading.current_thread() is threading.main_thread())
+    # a reclaim, or a state too big for a successor's copy next to ours: every tensor's HBM
+    # goes back as soon as it is in host memory, so the driver clears it under the spill
+    release_behind = (consistency == "boundary" and _release_hbm_enabled() and not stream_ok
+                      and (requeue or not safe))
     try:
-        rates = checkpoint_all(meta, on_stream=stream_started if stream_ok else None,
-                               exported=exported)
+        rates = checkpoint_all(meta, on_stream=stream_started if (stream_ok or big_stream)
+                               else None, exported=exported, release_behind=release_behind)
         print("tpi: preemption checkpoint saved in %.3fs (%s GB/s)" % (
             time.perf_counter() - t0, ", ".join("%.1f" % r for r in rates)), flush=True)
         code = PREEMPTED_EXIT_CODE

@@ -314,7 +314,7 @@ start = (meta or {}).get("step", 0)
 print("start", start, "restart", os.environ["TPI_RESTART_COUNT"], flush=True)
 if start == 0:
     _save = ck.save
-    def failing_save(metadata=None, on_stream=None):
+    def failing_save(metadata=None, on_stream=None, **kw):
         on_stream()      # "released": the successor starts and finds the exported HBM
         time.sleep(0.5)
         raise CheckpointError("host spill failed (injected)")
@@ -420,3 +420,32 @@ def test_resume_consistent_takes_the_hbm_hand_off(tmp_path):
         proc.stdin.write(b"\n")
         proc.stdin.flush()
         proc.wait(60)
+
+
+def test_save_releases_device_memory_behind_the_spill(tmp_path):
+    """Big-state preemption: with release_behind the device storages are freed while the
+    spill runs (each once its tiles are in host memory) and handed back to the driver; the
+    host copy is complete and restores into fresh tensors."""
+    from terraform_provider_iterative_amd.checkpoint import Checkpointer
+
+    g = torch.Generator(device="cuda").manual_seed(21)
+    src = {"w%d" % i: torch.randn(64 << 20, device="cuda", generator=g) for i in range(6)}
+    src["view_a"] = src["w5"][: 1 << 20]
+    ref = {k: v.clone() for k, v in src.items()}
+    spill = str(tmp_path / "spill")
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    ck = Checkpointer(src, path=spill, chunk_bytes=64 << 20, codec="tpz1")
+    before = torch.cuda.memory_reserved()
+    res = ck.save({"step": 1}, release_behind=True)
+    assert res.released_bytes == 6 * (64 << 20) * 4
+    assert all(t.untyped_storage().nbytes() == 0 for t in src.values())
+    assert torch.cuda.memory_reserved() <= before - res.released_bytes
+    ck.close()
+    dst = {k: torch.zeros_like(v) for k, v in ref.items() if k != "view_a"}
+    dst["view_a"] = dst["w5"][: 1 << 20]
+    with Checkpointer(dst, path=spill, chunk_bytes=64 << 20, codec="tpz1") as ck2:
+        assert ck2.restore().bad_tiles == 0 and ck2.header()["metadata"] == {"step": 1}
+        torch.cuda.synchronize()
+    for k in ref:
+        assert torch.equal(dst[k], ref[k]), k

@@ -239,7 +239,7 @@ class Exporting(_FakeHandoff):
         with open(self._hbm_manifest_path(), "w") as f:
             f.write("{}")
         return self._hbm_manifest_path()
-    def save(self, metadata, on_stream=None):
+    def save(self, metadata, on_stream=None, **kw):
         on_stream()  # "released": the successor starts and may import our HBM
         time.sleep(0.3)
         if %(fail)r:

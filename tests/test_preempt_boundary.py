@@ -392,7 +392,8 @@ def test_big_state_rank_releases_hbm_before_the_hand_off(cloud):
     the successor wait for its full exit."""
     spec = Task(environment=Environment(
         script=BIG_STATE % {"python": sys.executable, "root": ROOT}, timeout=300,
-        variables=Variables({"TPI_TASK": "true"})))
+        # a loaded CI box can take longer than the default 20 s linger to start the successor
+        variables=Variables({"TPI_TASK": "true", "TPI_LINGER_SECONDS": "120"})))
     task = backends.new(cloud, new_deterministic_identifier("big-state"), spec)
     task.create()
     deadline = time.time() + 60
