@@ -440,3 +440,35 @@ def test_release_schedule_frees_a_storage_after_its_last_tensor(tmp_path):
         assert got == want
         assert [end for end, _ in schedule] == sorted(end for end, _ in schedule)
         assert ck.release_schedule(device_only=True) == []
+
+
+def test_save_refuses_a_slot_a_live_foreign_writer_still_streams(tmp_path, monkeypatch):
+    """when wait_stream() gives up on a foreign writer that is still alive, a save
+    must not go on to write the slot that writer is streaming into."""
+    import subprocess
+    import sys
+
+    import torch
+
+    from terraform_provider_iterative_amd.checkpoint import CheckpointError, Checkpointer
+    from terraform_provider_iterative_amd.checkpoint.checkpointer import (PROGRESS_MAGIC,
+                                                                          STREAM_RUNNING)
+
+    monkeypatch.setenv("TPI_STREAM_TIMEOUT", "0.2")
+    state = {"w": torch.ones(4096)}
+    writer = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(30)"])
+    try:
+        with Checkpointer(state, path=str(tmp_path / "spill"), tile_bytes=4096) as ck:
+            ck.save({"step": 1})
+            prog = ck.slots[0].progress  # another live process "is streaming" into it
+            prog[1], prog[4], prog[5] = 2, STREAM_RUNNING, writer.pid
+            prog[0] = PROGRESS_MAGIC
+            with pytest.raises(CheckpointError, match="still streaming"):
+                ck.save({"step": 2})
+            writer.kill()
+            writer.wait()
+            ck.save({"step": 3})  # its writer is gone: the slot is free again
+            assert ck.header()["metadata"] == {"step": 3}
+    finally:
+        if writer.poll() is None:
+            writer.kill()
