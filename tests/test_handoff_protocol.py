@@ -115,10 +115,13 @@ def test_predecessor_released_only_after_closed(binary, tmp_path, die):
                 for n in os.listdir(task / "reports") if n.startswith("task-")):
             time.sleep(0.02)
         sup.send_signal(signal.SIGUSR1)  # preempt
-        sup.wait(60)
+        _, err = sup.communicate(timeout=60)
     finally:
         if sup.poll() is None:
             sup.kill()
+    for marker in (b"AddressSanitizer", b"LeakSanitizer", b"runtime error"):  # (ASan build)
+        assert marker not in err, err[-3000:]
+    assert sup.returncode == 0, err[-2000:]
     usr2 = float((out / "usr2").read_text())
     after = float((out / ("successor-exit" if die else "closed")).read_text())
     # "restored hbm" alone never lets the predecessor go: its memory is still mapped

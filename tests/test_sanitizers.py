@@ -195,3 +195,22 @@ def test_stager_under_asan_ubsan(tmp_path, monkeypatch):
         assert data[:3] == b"XYZ" and len(data) == sizes["a.bin"]
     finally:
         task.delete()
+
+
+def test_supervisor_hand_off_protocol_under_asan_ubsan(tmp_path, monkeypatch):
+    """The round-4 supervisor paths under ASan/UBSan: the notify line protocol (`released`,
+    `restored hbm`, `closed`), SIGUSR2 on close, exit tracing from /proc, resources released
+    before a slow released process is reaped, and the memory cgroup set-up."""
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_handoff_protocol import test_predecessor_released_only_after_closed
+
+    exe = str(tmp_path / "tpi-supervisor-asan")
+    _compile(exe, [os.path.join(ROOT, "csrc", "supervisor", "supervisor.cpp")])
+    monkeypatch.setenv("ASAN_OPTIONS", ENV["ASAN_OPTIONS"])
+    monkeypatch.setenv("UBSAN_OPTIONS", ENV["UBSAN_OPTIONS"])
+    for die in (False, True):
+        run = tmp_path / ("die" if die else "closed")
+        run.mkdir()
+        test_predecessor_released_only_after_closed(exe, run, die)
