@@ -45,7 +45,9 @@ torch.cuda.set_device(dev)
 spill = %(spill)r
 nbytes = int(%(gb)r * 1e9)
 # warm standby: the successor waits here (imports done, spill being mapped) for its activation
-activated = preemption.standby(spill if %(prefetch)r else None) if %(standby)r else False
+materialize = %(materialize)r
+activated = (preemption.standby(spill if %(prefetch)r else None, materialize=materialize)
+             if %(standby)r else False)
 t_active = time.time()
 resuming = os.path.exists(spill)
 if resuming and %(prefetch)r:
@@ -55,15 +57,35 @@ free_before = torch.cuda.mem_get_info(0)[0]
 probe = torch.empty(1 << 20, dtype=torch.uint8, device=dev)  # context + allocator warm
 torch.cuda.synchronize()
 t_probe = time.time()
+
+def digests():
+    return [ops.shard_hash(tensors[n].view(-1).view(torch.uint8)).cpu().tolist() for n in names]
+
+if resuming and materialize:
+    # the state is allocated group by group as the predecessor frees its HBM, each group
+    # restored behind the predecessor's spill: no up-front allocation of the whole state
+    t0 = time.time()
+    ck, tensors, meta = preemption.materialize(spill, dev)
+    torch.cuda.synchronize()
+    t1 = time.time()
+    names = list(tensors)[:4]
+    ok = meta is not None and meta.get("digests") == digests()
+    print("restored %%d bytes in %%.3f s, verified %%s, warm standby %%s, materialized %%s, "
+          "activation -> restored %%.3f s (prefetch %%.3f, %%.1f GB free before); "
+          "process start -> import done %%.3f s; Checkpointer %%s" %% (
+              ck.plan.total, t1 - t0, ok, activated, ck.materialize_stats, t1 - t_active,
+              t_prefetch - t_active, free_before / 1e9, t_import - t_start, ck.init_times),
+          flush=True)
+    ck.wait_stream(timeout=600)
+    ck.close()
+    os.remove(spill)
+    sys.exit(0 if ok else 3)
 tensors = synthetic_checkpoint(nbytes, 8192, dev, fill=not resuming)
 torch.cuda.synchronize()
 t_alloc = time.time()
 ck = Checkpointer(tensors, path=spill, codec=%(codec)r)
 t_map = time.time()
 names = list(tensors)[:4]
-
-def digests():
-    return [ops.shard_hash(tensors[n].view(-1).view(torch.uint8)).cpu().tolist() for n in names]
 
 if resuming:
     # no zero-fill needed to prove the restore: a fresh process's allocations never hold the
@@ -120,6 +142,9 @@ def main():
     p.add_argument("--early-prefetch", action="store_true",
                    help="successor maps + pins the spill before importing torch (measured "
                         "slower on MI355X: the pinning stalls the import)")
+    p.add_argument("--materialize", action="store_true",
+                   help="the successor restores with preemption.materialize(): its state is "
+                        "allocated group by group while the predecessor frees its HBM")
     p.add_argument("--step-seconds", type=float, default=0.002,
                    help="duration of the rank's (idle) training step")
     p.add_argument("--signal-mode", action="store_true",
@@ -147,7 +172,8 @@ def main():
     script = RANK % {"python": sys.executable, "root": ROOT, "spill": spill, "gb": args.gb,
                      "codec": args.codec, "prefetch": not args.no_prefetch,
                      "early": args.early_prefetch, "standby": args.standby,
-                     "step_s": args.step_seconds, "boundary": not args.signal_mode}
+                     "step_s": args.step_seconds, "boundary": not args.signal_mode,
+                     "materialize": args.materialize}
     # the ranks' runtime knobs travel as task variables (the rank environment is the task's)
     rank_env = {"TPI_TASK": "true", "TPI_STREAM_HANDOFF": "0" if args.no_stream else "1"}
     for knob in ("TPI_D2H_ENGINE", "TPI_STREAM_TIMEOUT", "TPI_LINGER_SECONDS",
@@ -165,7 +191,7 @@ def main():
               "hot_standby": args.hot, "stream_handoff": not args.no_stream,
               "save_at": "signal" if args.signal_mode else "step boundary",
               "release_hbm": os.environ.get("TPI_RELEASE_HBM", "1") != "0",
-              "step_seconds": args.step_seconds}
+              "step_seconds": args.step_seconds, "materialize": args.materialize}
     os.environ["TPI_WARM_STANDBY"] = "hot" if args.hot else ("1" if args.standby else "0")
     try:
         task.create()

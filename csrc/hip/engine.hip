@@ -1336,6 +1336,18 @@ int tpi_restore_stream(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total
                        const void* host_src, const uint32_t* crcs, const uint32_t* csizes,
                        const uint64_t* words, double timeout_s, uint64_t signal_stream,
                        uint64_t* bad_tiles, int64_t* first_bad, tpi_stats* stats) {
+  return tpi_restore_stream_at(e, segs, n, total, host_src, crcs, csizes, words, 0, timeout_s,
+                               signal_stream, bad_tiles, first_bad, stats);
+}
+
+// The same for a stretch of the writer's stream starting at its tile `tile_base` (a
+// progressive restore allocates and restores the state group by group: the plan, `host_src`,
+// `crcs` and `csizes` describe the stretch, the progress words count the whole stream's tiles).
+int tpi_restore_stream_at(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total,
+                          const void* host_src, const uint32_t* crcs, const uint32_t* csizes,
+                          const uint64_t* words, uint64_t tile_base, double timeout_s,
+                          uint64_t signal_stream, uint64_t* bad_tiles, int64_t* first_bad,
+                          tpi_stats* stats) {
   Range range("tpi_restore_stream");
   std::lock_guard<std::mutex> lk(e->mu);
   auto t0 = std::chrono::steady_clock::now();
@@ -1372,7 +1384,7 @@ int tpi_restore_stream(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total
     const int b = (int)(k % e->nbuf);
     const uint64_t len = std::min(e->chunk, total - base);
     const uint64_t t0i = base / tile, nt = (len + tile - 1) / tile;
-    if (wait_published(words, t0i + nt, timeout_s)) {
+    if (wait_published(words, tile_base + t0i + nt, timeout_s)) {
       // leave no copy or kernel of the chunks already issued running past this call
       (void)hipStreamSynchronize(e->copy);
       (void)hipStreamSynchronize(e->copy2);
@@ -1388,7 +1400,7 @@ int tpi_restore_stream(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total
       HIP_OK(hipEventSynchronize(e->ev_a[b]));
       if (was_split[b]) HIP_OK(hipEventSynchronize(e->ev_d[b]));
     }
-    const uint64_t published = __atomic_load_n(&words[0], __ATOMIC_ACQUIRE);
+    const uint64_t published = __atomic_load_n(&words[0], __ATOMIC_ACQUIRE) - tile_base;
     const bool split = chunk_tiles > 0 && published >= t0i + nt &&
                        (published - (t0i + nt)) / chunk_tiles >= e->split_lead;
     uint64_t cbeg = base, cend = base + len;

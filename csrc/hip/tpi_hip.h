@@ -57,7 +57,7 @@ typedef struct tpi_stats {
 } tpi_stats;
 
 // Bumped whenever a signature below changes (ops/_loader.py checks it).
-#define TPI_ABI_VERSION 4
+#define TPI_ABI_VERSION 5
 
 // Library / device
 const char* tpi_last_error(void);
@@ -181,6 +181,13 @@ int tpi_restore_stream(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total
                        const void* host_src, const uint32_t* crcs, const uint32_t* csizes,
                        const uint64_t* words, double timeout_s, uint64_t signal_stream,
                        uint64_t* bad_tiles, int64_t* first_bad, tpi_stats* stats);
+// tpi_restore_stream of a stretch of the writer's stream that starts at its tile `tile_base`
+// (segs/total/host_src/crcs/csizes describe the stretch; words count the whole stream).
+int tpi_restore_stream_at(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total,
+                          const void* host_src, const uint32_t* crcs, const uint32_t* csizes,
+                          const uint64_t* words, uint64_t tile_base, double timeout_s,
+                          uint64_t signal_stream, uint64_t* bad_tiles, int64_t* first_bad,
+                          tpi_stats* stats);
 // HBM-to-HBM hand-off between processes on one GPU.  tpi_ipc_export: IPC handle
 // (TPI_IPC_HANDLE_BYTES) of the allocation holding `ptr` -- e.g. inside a torch caching-
 // allocator segment -- and ptr's offset in it; the successor maps it with tpi_ipc_open.

@@ -20,6 +20,7 @@
 #   preempt-standby  the same with a warm standby successor (TPI_WARM_STANDBY=1)
 #   preempt-hot  hot standby (started with the rank) restoring behind the streamed spill
 #   preempt-170  the hot-standby run with a 170 GB rank (more than half of HBM)
+#   preempt-170m the same with the successor materializing its state group by group
 #   reclaim      bench/bench_reclaim.py --gb 100 (an on-demand task takes a spot task's GPU)
 #   handoff      bench/bench_handoff.py --gb 16 (same-GPU HBM hand-off alone, per copy route)
 #   async        bench/bench_async.py --gb 100
@@ -69,6 +70,8 @@ run_job() {
                    > "$OUT/preempt-hot2.json" 2> "$OUT/preempt-hot2.log" ;;
     preempt-170) timeout -k 10 900 python bench/bench_preempt.py --gb 170 --hot $extra \
                    > "$OUT/preempt-170.json" 2> "$OUT/preempt-170.log" ;;
+    preempt-170m) timeout -k 10 900 python bench/bench_preempt.py --gb 170 --hot --materialize \
+                    $extra > "$OUT/preempt-170m.json" 2> "$OUT/preempt-170m.log" ;;
     reclaim) timeout -k 10 900 python bench/bench_reclaim.py --gb 100 $extra \
                > "$OUT/reclaim.json" 2> "$OUT/reclaim.log" ;;
     handoff) timeout -k 10 600 python bench/bench_handoff.py $extra \

@@ -38,6 +38,7 @@ NATIVE_SO = os.path.join(LIB, "_tpi_native" + (sysconfig.get_config_var("EXT_SUF
 HIP_SO = os.path.join(LIB, "libtpi_hip.so")
 SUPERVISOR = os.path.join(LIB, "tpi-supervisor")
 STAGER = os.path.join(LIB, "tpi-stager")
+TORCH_EXT = os.path.join(LIB, "_tpi_torch" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
 
 
 def _sources(*patterns: str) -> List[str]:
@@ -176,8 +177,31 @@ def build_stager(force: bool = False, verbose: bool = False) -> str:
     return _build(STAGER, cmd, deps, force, verbose)
 
 
+def build_torch_ext(force: bool = False, verbose: bool = False) -> str:
+    """``_tpi_torch``: torch helpers that release the GIL (``csrc/torchext``; host code against
+    torch's own headers and libraries, same C++ ABI)."""
+    srcs = _sources("torchext/*.cpp")
+    if not srcs:
+        return ""
+    import torch
+
+    inc = os.path.join(os.path.dirname(torch.__file__), "include")
+    tl = torch_lib_dir()
+    cxx = os.environ.get("CXX", "g++")
+    cmd = [cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           "-D_GLIBCXX_USE_CXX11_ABI=%d" % int(torch._C._GLIBCXX_USE_CXX11_ABI),
+           "-DTORCH_EXTENSION_NAME=_tpi_torch", "-DTORCH_API_INCLUDE_EXTENSION_H",
+           "-isystem", inc, "-isystem", os.path.join(inc, "torch", "csrc", "api", "include"),
+           "-isystem", sysconfig.get_paths()["include"], *srcs, "-L" + tl, "-Wl,-rpath," + tl,
+           "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-o", "@OUT@"]
+    # torch's version file is a dependency: a different torch needs a rebuild
+    deps = srcs + [os.path.join(os.path.dirname(torch.__file__), "version.py")]
+    return _build(TORCH_EXT, cmd, deps, force, verbose)
+
+
 def build_all(force: bool = False, verbose: bool = False, hip: bool = True) -> List[str]:
-    outs = [build_native(force, verbose), build_supervisor(force, verbose)]
+    outs = [build_native(force, verbose), build_supervisor(force, verbose),
+            build_torch_ext(force, verbose)]
     if hip:
         outs.append(build_hip(force, verbose))
         outs.append(build_stager(force, verbose))

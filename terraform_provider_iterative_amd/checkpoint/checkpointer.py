@@ -34,6 +34,7 @@ import ctypes
 import hashlib
 import json
 import os
+import queue
 import struct
 import tempfile
 import threading
@@ -45,7 +46,7 @@ import numpy as np
 
 from ..ops import codec as tpz
 from ..ops import hip, native
-from ..ops.packing import PackPlan, align_up
+from ..ops.packing import PackPlan, TensorEntry, align_up
 from ..ops.packing import pack as host_pack, unpack as host_unpack
 from . import host
 from .host import HostRegion
@@ -176,16 +177,19 @@ class DeviceEngine:
 
     def restore_stream(self, plan: PackPlan, host_addr: int, crcs: np.ndarray,
                        csizes: Optional[np.ndarray], words_addr: int, timeout: float,
-                       signal_stream: int) -> TransferResult:
+                       signal_stream: int, tile_base: int = 0) -> TransferResult:
+        """``tile_base``: ``plan`` (and ``host_addr``, ``crcs``, ``csizes``) describe the
+        stretch of the writer's stream that starts at that tile; the progress words count the
+        whole stream."""
         st = _Stats()
         bad = ctypes.c_uint64(0)
         first = ctypes.c_int64(-1)
         t0 = time.perf_counter()
-        rc = self.lib.tpi_restore_stream(
+        rc = self.lib.tpi_restore_stream_at(
             self.handle, plan.segs.ctypes.data, len(plan.entries), plan.total,
             ctypes.c_void_p(host_addr), crcs.ctypes.data,
             ctypes.c_void_p(csizes.ctypes.data if csizes is not None else None),
-            ctypes.c_void_p(words_addr), ctypes.c_double(timeout), signal_stream,
+            ctypes.c_void_p(words_addr), tile_base, ctypes.c_double(timeout), signal_stream,
             ctypes.byref(bad), ctypes.byref(first), ctypes.byref(st))
         self.lib.check(rc, "tpi_restore_stream")
         # chunks copied over two streams because the restore trailed its writer (duplex link)
@@ -409,9 +413,10 @@ class Checkpointer:
                  path: Optional[str] = None, *, tile_bytes: int = 1 << 20,
                  chunk_bytes: int = 256 << 20, nbuf: int = 3, mode: str = "sdma",
                  numa: bool = True, populate: bool = True, codec: str = "none",
-                 slots: int = 1):
+                 slots: int = 1, _plan: Optional[PackPlan] = None):
         t0 = time.perf_counter()
-        self.plan = PackPlan.from_tensors(tensors, tile_bytes)
+        # _plan: a layout without tensors yet (materialize(): they are allocated group by group)
+        self.plan = _plan if _plan is not None else PackPlan.from_tensors(tensors, tile_bytes)
         self.path = path
         self.mode = MODES[mode]
         if codec not in CODECS:
@@ -1031,6 +1036,258 @@ class Checkpointer:
                                                                       res.first_bad))
         return res
 
+    # -- progressive materialisation: allocate the state while it streams in -----------------
+    @classmethod
+    def materialize(cls, path: str, device: Any = None, *, group_bytes: int = 4 << 30,
+                    stream_timeout: Optional[float] = None,
+                    memory_timeout: Optional[float] = None,
+                    **kwargs) -> Tuple["Checkpointer", Dict[str, Any], TransferResult]:
+        """Create the tensors a checkpoint region holds and restore them, group by group.
+
+        For a successor whose state does not fit next to its predecessor's on one GPU (a
+        170 GB rank on 288 GB of HBM): instead of allocating the whole state up front -- which
+        waits until the predecessor has spilled *and* freed all of it -- each group of about
+        ``group_bytes`` is allocated as soon as the device has room for it (a background
+        thread retries the allocation while the predecessor frees its tensors behind its
+        spill, ``save(release_behind=True)``) and restored at once, behind the predecessor's
+        streamed save when one is still running.  Allocation, the driver's clearing of the
+        freed HBM, the spill and the restore then overlap instead of running one after the
+        other.  Tensors come back contiguous, with the saved names, shapes and dtypes; the
+        returned checkpointer is bound to them (later saves go to the same region).
+        ``device`` may be ``"cpu"`` (host tensors, complete checkpoints only).
+        ``memory_timeout`` (default ``TPI_STREAM_TIMEOUT`` or 30 s): give up when no
+        allocation has succeeded for that long.  Returns ``(checkpointer, tensors, result)``.
+        """
+        import torch
+
+        layout = _region_layout(path)
+        dev = torch.device(device if device is not None else "cuda")
+        if dev.type == "cuda" and dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        entries = [TensorEntry.from_json(e) for e in layout["entries"]]
+        plan = PackPlan.from_entries(entries, layout["total"], layout["tile_bytes"])
+        plan.device = str(dev)
+        plan._bound = []
+        kwargs.setdefault("codec", layout["codec"])
+        ck = cls(None, path, tile_bytes=layout["tile_bytes"], slots=layout["slots"], _plan=plan,
+                 **kwargs)
+        try:
+            if ck._entries_digest != layout["entries_sha256"] or ck.size != layout["size"]:
+                raise CheckpointError("%s: region layout not reproducible from its entries"
+                                      % path)
+            tensors, res = ck._materialize(dev, group_bytes, stream_timeout, memory_timeout)
+        except BaseException:
+            ck.close()
+            raise
+        return ck, tensors, res
+
+    def _groups(self, group_bytes: int) -> List[Tuple[int, int]]:
+        """Entry index ranges ``[lo, hi)`` of about ``group_bytes`` each, in stream order."""
+        out, lo, acc = [], 0, 0
+        for i, e in enumerate(self.plan.entries):
+            acc += e.nbytes
+            if acc >= group_bytes or i == len(self.plan.entries) - 1:
+                out.append((lo, i + 1))
+                lo, acc = i + 1, 0
+        return out
+
+    def _sub_plan(self, lo: int, hi: int, tensors: Sequence[Any],
+                  lead: Any) -> Tuple[PackPlan, int, int]:
+        """(plan, first tile, end tile) of entries ``[lo, hi)``: the tiles that hold them, the
+        plan's offsets relative to the first tile.  Neighbouring groups may share a boundary
+        tile; each restore scatters only its own tensors from it.  The bytes of the first tile
+        before the group's first tensor (the previous group's tail) land in ``lead``, a
+        scratch buffer of one tile: the device kernels need a segment at offset 0."""
+        tile = self.plan.tile_bytes
+        group = self.plan.entries[lo:hi]
+        ta = group[0].offset // tile
+        tb = min(self.plan.ntiles, -(-(group[-1].offset + group[-1].nbytes) // tile))
+        base = ta * tile
+        entries = [TensorEntry(e.name, e.dtype, e.shape, e.nbytes, e.offset - base)
+                   for e in group]
+        named = {e.name: t for e, t in zip(group, tensors)}
+        gap = group[0].offset - base
+        if gap:
+            entries.insert(0, TensorEntry("\0lead", "uint8", (gap,), gap, 0))
+            named = dict([("\0lead", lead[:gap])] + list(named.items()))
+        sub = PackPlan.from_entries(entries, min(self.plan.total, tb * tile) - base, tile)
+        sub.bind(named)
+        return sub, ta, tb
+
+    def _materialize(self, dev, group_bytes: int, stream_timeout: Optional[float],
+                     memory_timeout: Optional[float]) -> Tuple[Dict[str, Any], TransferResult]:
+        import torch
+
+        t_start = time.perf_counter()
+        self.wait_pending()
+        found = self._streaming()
+        streaming = found is not None
+        if found is None:
+            found = self._active()
+        if found is None:
+            raise CheckpointError("no checkpoint to materialize in %s" % self.path)
+        slot, header = found
+        self._check_compatible(header)
+        if streaming and self.engine is None:
+            streaming = False  # host tensors: wait for the whole spill first
+            self._restore_streaming_wait(slot, stream_timeout)
+            header = self._slot_header(slot) or header
+        zipped = header.get("codec", "none") == "tpz1"
+        if stream_timeout is None:
+            stream_timeout = float(os.environ.get("TPI_STREAM_TIMEOUT", "30"))
+        if memory_timeout is None:
+            memory_timeout = float(os.environ.get("TPI_STREAM_TIMEOUT", "30"))
+        entries = self.plan.entries
+        groups = self._groups(max(1, int(group_bytes)))
+        ready: "queue.Queue[Any]" = queue.Queue()
+        stop = threading.Event()
+        waited = [0.0]
+        # per group, seconds from the start: [allocation start, allocated, restore start, end]
+        trace: List[List[float]] = []
+
+        # torch.empty() holds the GIL while the driver clears just-freed HBM (seconds behind a
+        # big spill), which would stall the restoring thread at its next Python step: allocate
+        # through _tpi_torch.empty (the same caching-allocator call, GIL released) when built
+        try:
+            from ..ops._loader import torch_ext
+
+            empty_nogil = torch_ext().empty
+        except Exception:  # not built: torch.empty (correct, restores may stall behind it)
+            empty_nogil = None
+        likes: Dict[str, Any] = {}
+
+        def empty(e: TensorEntry):
+            dtype = getattr(torch, e.dtype)
+            if empty_nogil is None:
+                return torch.empty(e.shape, dtype=dtype, device=dev)
+            like = likes.get(e.dtype)
+            if like is None:
+                like = likes[e.dtype] = torch.empty(0, dtype=dtype, device=dev)
+            return empty_nogil(list(e.shape), like)
+
+        def allocate():  # runs ahead of the restores, as far as the device has room
+            try:
+                if dev.type == "cuda":
+                    torch.cuda.set_device(dev)
+                for lo, hi in groups:
+                    out = []
+                    t_group = time.perf_counter()
+                    for e in entries[lo:hi]:
+                        last = time.monotonic()
+                        while True:
+                            if stop.is_set():
+                                return
+                            try:
+                                out.append(empty(e))
+                                break
+                            except RuntimeError as error:  # torch's OOM error included
+                                if "out of memory" not in str(error).lower():
+                                    raise
+                                # the predecessor is still freeing (behind its spill)
+                                if time.monotonic() - last > memory_timeout:
+                                    raise CheckpointError(
+                                        "no room for %s (%.1f GB) within %.0f s" % (
+                                            e.name, e.nbytes / 1e9, memory_timeout))
+                                t = time.monotonic()
+                                stop.wait(0.002)
+                                waited[0] += time.monotonic() - t
+                    trace.append([round(t_group - t_start, 4),
+                                  round(time.perf_counter() - t_start, 4)])
+                    ready.put(out)
+            except BaseException as error:  # surfaced by the restoring thread
+                ready.put(error)
+
+        lead = torch.empty(self.plan.tile_bytes, dtype=torch.uint8, device=dev)
+        worker = threading.Thread(target=allocate, name="tpi-materialize-alloc", daemon=True)
+        worker.start()
+        tensors: Dict[str, Any] = {}
+        stream_base = self.region.addr + slot.base + self.stream_offset
+        total = TransferResult(self.plan.total, 0.0, wire_bytes=0)
+        try:
+            for gi, (lo, hi) in enumerate(groups):
+                item = ready.get()
+                if isinstance(item, BaseException):
+                    raise item
+                t_group = time.perf_counter()
+                sub, ta, tb = self._sub_plan(lo, hi, item, lead)
+                crcs = slot.crcs[ta:tb]
+                csizes = slot.csizes[ta:tb] if zipped else None
+                # earlier tiles are in host memory: the previous group waited for them
+                start = int(slot.csizes[:ta].sum(dtype=np.uint64)) if zipped \
+                    else ta * self.plan.tile_bytes
+                if self.engine is not None:
+                    sig = torch.cuda.current_stream(dev).cuda_stream
+                    if streaming:
+                        from ..ops._loader import HipError
+
+                        try:
+                            res = self.engine.restore_stream(
+                                sub, stream_base + start, crcs, csizes,
+                                slot.progress.ctypes.data + 16, stream_timeout, sig,
+                                tile_base=ta)
+                        except HipError as error:
+                            raise CheckpointError(str(error)) from error
+                    elif zipped:
+                        res = self.engine.restore_z(sub, stream_base + start, crcs, csizes, sig)
+                    else:
+                        res = self.engine.restore(sub, stream_base + start, crcs, self.mode, sig)
+                else:
+                    t0 = time.perf_counter()
+                    if zipped:
+                        nbytes = int(csizes.sum(dtype=np.uint64))
+                        stream, _ = tpz.decode(self.region.array(
+                            slot.base + self.stream_offset + start, nbytes),
+                            csizes, sub.total, self.plan.tile_bytes)
+                    else:
+                        nbytes = sub.total
+                        stream = self.region.array(slot.base + self.stream_offset + start,
+                                                   sub.total)
+                    bad, first = host_unpack(sub, stream, crcs)
+                    res = TransferResult(sub.total, time.perf_counter() - t0, 0, bad, first,
+                                         wire_bytes=nbytes)
+                total.chunks += res.chunks
+                total.wire_bytes += res.wire_bytes
+                if res.bad_tiles:
+                    total.bad_tiles += res.bad_tiles
+                    if total.first_bad < 0:
+                        total.first_bad = ta + res.first_bad
+                for e, t in zip(entries[lo:hi], item):
+                    tensors[e.name] = t
+                trace[gi] += [
+                    round(t_group - t_start, 4), round(time.perf_counter() - t_start, 4)]
+        finally:
+            stop.set()
+            worker.join()
+        self.plan.bind(tensors)
+        total.seconds = time.perf_counter() - t_start
+        total.crc = int(header.get("crc32c", 0)) if not streaming else \
+            native().crc32c_combine_tiles_ptr(slot.crcs.ctypes.data, self.plan.ntiles,
+                                              self.plan.tile_bytes, self.plan.total)
+        self.materialize_stats = {"groups": len(groups), "alloc_wait_s": round(waited[0], 4),
+                                  "streamed": streaming, "trace": trace,
+                                  "alloc": "nogil" if empty_nogil is not None else "torch"}
+        self.materialized_metadata = header.get("metadata", {})
+        self.last_restore = total
+        if total.bad_tiles:
+            raise CheckpointError("%d corrupt tile(s), first at %d" % (total.bad_tiles,
+                                                                      total.first_bad))
+        return tensors, total
+
+    def _restore_streaming_wait(self, slot: _Slot, timeout: Optional[float]) -> None:
+        """Host path of a streamed checkpoint: wait until its writer completed it."""
+        if timeout is None:
+            timeout = float(os.environ.get("TPI_STREAM_TIMEOUT", "30"))
+        prog = slot.progress
+        last, seen = time.monotonic(), -1
+        while int(prog[4]) != STREAM_COMPLETE:
+            if int(prog[4]) == STREAM_FAILED:
+                raise CheckpointError("the streamed checkpoint failed in its writer")
+            if int(prog[2]) != seen:
+                seen, last = int(prog[2]), time.monotonic()
+            elif time.monotonic() - last > timeout:
+                raise CheckpointError("streamed checkpoint stalled (writer gone?)")
+            time.sleep(0.001)
+
     # -- HBM-to-HBM hand-off (preemption on the same GPU) --------------------------------------
     def _hbm_manifest_path(self) -> Optional[str]:
         return self.path + ".hbm" if self.path and self.engine is not None else None
@@ -1421,6 +1678,36 @@ class Checkpointer:
 
     def __exit__(self, *exc):
         self.close()
+
+
+def _region_layout(path: str) -> Dict[str, Any]:
+    """What :meth:`Checkpointer.materialize` needs from a region file without its tensors:
+    the entries (and their blob's digest), total, tile size, codec, slot count and size.
+    Reads the first slot's preamble, or the second slot's (at half the file) when a save in
+    progress has cleared the first."""
+    size = os.path.getsize(path)
+    with open(path, "rb") as f:
+        for base in (0, size // 2):
+            f.seek(base)
+            pre = f.read(PREAMBLE)
+            if pre[:8] != MAGIC:
+                continue
+            n, entries_offset, entries_len = struct.unpack("<QQQ", pre[8:32])
+            header = json.loads(f.read(n))
+            f.seek(base + entries_offset)
+            blob = f.read(entries_len)
+            slot_end = _layout(Checkpointer.HEADER_RESERVE, entries_len, header["ntiles"],
+                               header["total"], header["tile_bytes"])[4]
+            slot_bytes = align_up(slot_end, 4096)
+            slots = 2 if size >= 2 * slot_bytes else 1
+            if base and slots != 2:
+                continue
+            return {"entries": json.loads(blob),
+                    "entries_sha256": hashlib.sha256(blob).hexdigest(),
+                    "total": header["total"], "tile_bytes": header["tile_bytes"],
+                    "codec": header.get("codec", "none"), "slots": slots,
+                    "size": slot_bytes * slots if slots > 1 else slot_end}
+    raise CheckpointError("%s holds no checkpoint header" % path)
 
 
 def describe_checkpoint(path: str, entries: bool = True) -> Dict:

@@ -37,7 +37,7 @@ import signal
 import sys
 import threading
 import time
-from typing import Callable, Dict, List, Optional
+from typing import Any, Callable, Dict, List, Optional, Tuple
 
 from .checkpointer import Checkpointer, CheckpointError
 
@@ -367,7 +367,7 @@ def _notify(message: bytes) -> bool:
         return False
 
 
-def standby(prefetch_path: Optional[str] = None) -> bool:
+def standby(prefetch_path: Optional[str] = None, materialize: bool = False) -> bool:
     """Warm-standby point of a rank script: call it once the imports are done.
 
     In a normal incarnation it announces to the supervisor that this script can run as a warm
@@ -377,12 +377,17 @@ def standby(prefetch_path: Optional[str] = None) -> bool:
     spill region, :func:`..host.prefetch`) and blocks until the supervisor activates it --
     right after the old rank has released -- then returns True and resumes from the spill.
     A standby that is not needed is killed (or sees EOF and exits quietly).
+
+    ``materialize``: the script restores with :func:`materialize` (the state is allocated
+    group by group as the predecessor frees it), so nothing waits here for room for the whole
+    state (:func:`wait_for_device_memory`).
     """
     global _standby_script
     _standby_script = bool(prefetch_path)
+    wait_memory = bool(prefetch_path) and not materialize
     if os.environ.get("TPI_STANDBY") != "1":
         _notify(b"standby\n")
-        if prefetch_path:  # a cold successor of a big-state predecessor
+        if wait_memory:  # a cold successor of a big-state predecessor
             wait_for_device_memory(prefetch_path)
         return False
     cancel = threading.Event()
@@ -415,7 +420,7 @@ def standby(prefetch_path: Optional[str] = None) -> bool:
             os.environ["MASTER_PORT"] = word[5:].decode()
     os.environ.pop("TPI_STANDBY", None)
     journal("standby-activated")
-    if prefetch_path:
+    if wait_memory:
         wait_for_device_memory(prefetch_path)
     _notify(b"standby\n")  # the activated process can itself be succeeded by a standby
     return True
@@ -843,6 +848,33 @@ def _persisted(path: str) -> bool:
         except (OSError, ValueError):
             return False
     return os.path.exists(path)
+
+
+def materialize(spill: str, device: Any = None, **kwargs) -> Optional[Tuple[Checkpointer,
+                                                                          Dict[str, Any], Dict]]:
+    """Successor side of a big-state hand-off: create and restore the tensors of the spill
+    region ``spill`` group by group (:meth:`Checkpointer.materialize`), behind the
+    predecessor's streamed save while it runs, each group allocated as soon as the
+    predecessor's freed HBM has room for it.  Returns ``(checkpointer, tensors, metadata)``,
+    or None when ``spill`` holds no checkpoint (a fresh start: allocate as usual).  The
+    script builds its model around the tensors (e.g. on the ``meta`` device, then
+    :func:`..training.assign_materialized`) instead of allocating it first; call
+    :func:`standby` with ``materialize=True``."""
+    if not spill or not os.path.exists(spill) or os.path.getsize(spill) == 0:
+        return None
+    try:
+        ck, tensors, res = Checkpointer.materialize(spill, device, **kwargs)
+    except CheckpointError as error:
+        if "no checkpoint" in str(error):
+            return None
+        journal("checkpoint-corrupt", "host region (materialize)", str(error))
+        raise
+    stats = getattr(ck, "materialize_stats", {})
+    journal("checkpoint-restored", "host region, materialized in %d groups" % stats.get("groups", 0),
+            *_describe(res), "allocation waits %.3f s" % stats.get("alloc_wait_s", 0.0),
+            "streamed" if stats.get("streamed") else "complete copy")
+    notify_restored()
+    return ck, tensors, dict(getattr(ck, "materialized_metadata", {}) or {})
 
 
 def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None,

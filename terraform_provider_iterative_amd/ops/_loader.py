@@ -15,7 +15,7 @@ from typing import Optional
 
 from .. import _build
 
-ABI_VERSION = 4  # TPI_ABI_VERSION of csrc/hip/tpi_hip.h
+ABI_VERSION = 5  # TPI_ABI_VERSION of csrc/hip/tpi_hip.h
 
 _lock = threading.Lock()
 _native = None
@@ -43,6 +43,31 @@ def native():
             spec.loader.exec_module(module)
             _native = module
     return _native
+
+
+_torch_ext = None
+
+
+def torch_ext():
+    """``_tpi_torch`` (``csrc/torchext``): torch helpers that release the GIL, e.g.
+    ``empty(shape, like)``.  Loaded after ``import torch`` (it links torch's libraries)."""
+    global _torch_ext
+    if _torch_ext is not None:
+        return _torch_ext
+    with _lock:
+        if _torch_ext is None:
+            import torch  # noqa: F401
+
+            if _auto_build():
+                _build.build_torch_ext()
+            spec = importlib.util.spec_from_file_location("_tpi_torch", _build.TORCH_EXT)
+            if spec is None or spec.loader is None:
+                raise ImportError("_tpi_torch not found at %s (run __graft_entry__.build())"
+                                  % _build.TORCH_EXT)
+            module = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(module)
+            _torch_ext = module
+    return _torch_ext
 
 
 class HipError(RuntimeError):
@@ -76,6 +101,8 @@ class HipLib:
             "tpi_copy_segments": (i32, [vp, vp, vp, i32, u64, u64, c.POINTER(u64), vp]),
             "tpi_restore_stream": (i32, [vp, vp, i32, u64, vp, vp, vp, vp, c.c_double, u64,
                                          c.POINTER(u64), c.POINTER(i64), vp]),
+            "tpi_restore_stream_at": (i32, [vp, vp, i32, u64, vp, vp, vp, vp, u64, c.c_double,
+                                            u64, c.POINTER(u64), c.POINTER(i64), vp]),
             "tpi_save": (i32, [vp, vp, i32, u64, vp, vp, i32, u64, vp]),
             "tpi_restore": (i32, [vp, vp, i32, u64, vp, vp, i32, u64, c.POINTER(u64),
                                   c.POINTER(i64), vp]),

@@ -472,3 +472,93 @@ def test_save_refuses_a_slot_a_live_foreign_writer_still_streams(tmp_path, monke
     finally:
         if writer.poll() is None:
             writer.kill()
+
+
+@pytest.mark.parametrize("codec,slots", [("none", 1), ("tpz1", 1), ("none", 2), ("tpz1", 2)])
+@pytest.mark.parametrize("group_bytes", [1, 40_000, 1 << 30])
+def test_materialize_allocates_and_restores_group_by_group(tmp_path, codec, slots, group_bytes):
+    """Checkpointer.materialize() rebuilds a region's tensors without being handed any: one
+    tensor per group, groups sharing boundary tiles, or everything at once; the checkpointer
+    it returns is bound to them and saves again into the same region."""
+    path = str(tmp_path / "spill.bin")
+    src = _model(5)
+    ref = {k: v.clone() for k, v in src.items()}
+    with Checkpointer(src, path=path, tile_bytes=4096, codec=codec, slots=slots) as ck:
+        ck.save({"step": 1})
+        if slots == 2:  # the newest of two complete copies is the one materialized
+            for v in src.values():
+                v.mul_(2) if v.is_floating_point() else v.add_(1)
+            ref = {k: v.clone() for k, v in src.items()}
+            ck.save({"step": 2})
+    ck2, tensors, res = Checkpointer.materialize(path, "cpu", group_bytes=group_bytes)
+    try:
+        assert res.bad_tiles == 0 and res.bytes == ck2.plan.total
+        assert ck2.materialize_stats["alloc"] == "nogil"  # the _tpi_torch extension is built
+        assert list(tensors) == list(ref)
+        for k in ref:
+            assert tensors[k].is_contiguous() and torch.equal(tensors[k], ref[k]), k
+        expect_groups = len(ref) if group_bytes == 1 else (1 if group_bytes > 1e6 else None)
+        if expect_groups is not None:
+            assert ck2.materialize_stats["groups"] == expect_groups
+        assert ck2.header()["metadata"]["step"] == (2 if slots == 2 else 1)
+        # the device engine needs every (sub-)plan to start with a segment at offset 0
+        lead = torch.empty(4096, dtype=torch.uint8)
+        for lo, hi in ck2._groups(1):
+            sub, ta, tb = ck2._sub_plan(lo, hi, [tensors[e.name] for e in
+                                                 ck2.plan.entries[lo:hi]], lead)
+            assert sub.entries[0].offset == 0 and 0 <= ta < tb <= ck2.plan.ntiles
+            assert sub.total <= (tb - ta) * 4096
+        tensors["w1"].fill_(0.5)
+        ck2.save({"step": 9})
+    finally:
+        ck2.close()
+    fresh = {k: torch.zeros_like(v) for k, v in ref.items()}
+    with Checkpointer(fresh, path=path, tile_bytes=4096, codec=codec, slots=slots) as ck3:
+        ck3.restore()
+        assert ck3.header()["metadata"]["step"] == 9
+    assert torch.equal(fresh["w1"], torch.full_like(fresh["w1"], 0.5))
+    assert torch.equal(fresh["embed"], ref["embed"])
+
+
+def test_materialize_reports_corruption_and_missing_checkpoints(tmp_path):
+    path = str(tmp_path / "spill.bin")
+    with Checkpointer(_model(6), path=path, tile_bytes=4096) as ck:
+        ck.save()
+        stream_at = ck.stream_offset
+    with open(path, "r+b") as f:  # flip one byte of the stream
+        f.seek(stream_at + 5000)
+        b = f.read(1)
+        f.seek(stream_at + 5000)
+        f.write(bytes([b[0] ^ 0xFF]))
+    with pytest.raises(CheckpointError, match="corrupt tile"):
+        Checkpointer.materialize(path, "cpu", group_bytes=1)
+    empty = str(tmp_path / "empty.bin")
+    with open(empty, "wb") as f:
+        f.write(b"\0" * 8192)
+    with pytest.raises(CheckpointError, match="no checkpoint header"):
+        Checkpointer.materialize(empty, "cpu")
+
+
+def test_preemption_materialize_journals_and_tells_the_supervisor(tmp_path, monkeypatch):
+    from terraform_provider_iterative_amd.checkpoint import preemption
+
+    events = tmp_path / "events.jsonl"
+    monkeypatch.setenv("TPI_EVENTS_FILE", str(events))
+    rfd, wfd = os.pipe()
+    monkeypatch.setenv("TPI_NOTIFY_FD", str(wfd))
+    try:
+        assert preemption.materialize(str(tmp_path / "missing.spill"), "cpu") is None
+        path = str(tmp_path / "spill.bin")
+        ref = _model(7)
+        with Checkpointer(ref, path=path, tile_bytes=4096, codec="tpz1") as ck:
+            ck.save({"step": 41})
+        ck2, tensors, meta = preemption.materialize(path, "cpu", group_bytes=1)
+        ck2.close()
+        assert meta["step"] == 41
+        assert all(torch.equal(tensors[k], ref[k]) for k in ref)
+        assert os.read(rfd, 64) == b"restored\n"
+    finally:
+        os.close(rfd)
+        os.close(wfd)
+    text = events.read_text()
+    assert "checkpoint-restored" in text and "materialized in 5 groups" in text

@@ -688,3 +688,71 @@ def test_prewarmed_engine_is_taken_by_the_next_checkpointer():
     ck.restore()
     assert torch.equal(t["a"], want)
     ck.close()
+
+
+@pytest.mark.parametrize("codec", ["none", "tpz1"])
+def test_materialize_streams_groups_behind_a_writer(codec, tmp_path):
+    """Checkpointer.materialize() on the GPU: while the writer publishes its stream chunk by
+    chunk, a successor thread allocates and restores the state group by group
+    (tpi_restore_stream_at: each group waits for its own tiles of the whole stream); then
+    once more from the complete copy, one tensor per group."""
+    import threading
+    import time
+
+    from terraform_provider_iterative_amd.checkpoint import Checkpointer
+    from terraform_provider_iterative_amd.checkpoint import checkpointer as ckmod
+
+    g = torch.Generator().manual_seed(12)
+    src = {"a": torch.randn(3 << 20, generator=g).to(torch.bfloat16).cuda(),
+           "b": torch.randn(5 << 20, generator=g).mul(1e-3).cuda(),
+           "t": torch.randn(640, 1000, generator=g).cuda().t(),
+           "c": torch.randn(777_777, generator=g).cuda(),
+           "d": torch.randint(0, 1 << 30, (2 << 20,), generator=g).cuda()}
+    path = str(tmp_path / "spill")
+    kw = dict(tile_bytes=1 << 16, chunk_bytes=1 << 20, nbuf=2, codec=codec)
+    writer = Checkpointer(src, path=path, **kw)
+    writer.save({"step": 2})
+    # turn the complete checkpoint back into one "being streamed" (as in
+    # test_streamed_restore_follows_the_writers_progress), published below chunk by chunk
+    slot = writer.slots[0]
+    header = writer.header()
+    header.update(complete=False, streaming=True)
+    writer._write_header(slot, header)
+    prog = slot.progress
+    prog[1], prog[2], prog[3], prog[4] = header["generation"], 0, 0, ckmod.STREAM_RUNNING
+    prog[5] = os.getpid()
+    prog[0] = ckmod.PROGRESS_MAGIC
+    box = {}
+
+    def successor():
+        try:
+            box["out"] = Checkpointer.materialize(path, "cuda", group_bytes=6 << 20,
+                                                  stream_timeout=20, chunk_bytes=1 << 20, nbuf=2)
+        except BaseException as error:  # surfaced below
+            box["err"] = error
+
+    th = threading.Thread(target=successor)
+    th.start()
+    per = 16  # tiles (1 MiB) per publication, every 20 ms
+    for tiles in range(per, writer.plan.ntiles + per, per):
+        time.sleep(0.02)
+        prog[2] = min(tiles, writer.plan.ntiles)
+    header.update(complete=True, streaming=False)
+    writer._write_header(slot, header)
+    prog[4] = ckmod.STREAM_COMPLETE
+    th.join(60)
+    assert "err" not in box, box.get("err")
+    ck, tensors, res = box["out"]
+    assert res.bad_tiles == 0 and ck.materialize_stats["streamed"]
+    assert ck.materialize_stats["groups"] >= 3 and ck.materialized_metadata["step"] == 2
+    torch.cuda.synchronize()
+    for k in src:
+        assert tensors[k].is_cuda and torch.equal(tensors[k], src[k]), k
+    ck.close()
+    ck2, tensors2, _ = Checkpointer.materialize(path, "cuda", group_bytes=1,
+                                                chunk_bytes=1 << 20, nbuf=2)
+    assert not ck2.materialize_stats["streamed"] and ck2.materialize_stats["groups"] == len(src)
+    for k in src:
+        assert torch.equal(tensors2[k], src[k]), k
+    ck2.close()
+    writer.close()
