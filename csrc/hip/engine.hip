@@ -1322,6 +1322,30 @@ int tpi_engine_set_host_region(tpi_engine* e, void* base, uint64_t bytes, uint64
   return 0;
 }
 
+// Allocate now what the pipelines would allocate on first use (segment descriptors, tile
+// CRCs, the codec's decode buffers): a successor that restores while its predecessor frees
+// HBM must not meet a hipMalloc that waits for the driver to clear that memory.
+int tpi_engine_reserve(tpi_engine* e, int nsegs, uint64_t ntiles, int codec) {
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_OK(hipSetDevice(e->device));
+  if ((size_t)nsegs > e->seg_cap) {
+    if (e->d_segs) HIP_OK(hipFree(e->d_segs));
+    e->d_segs = nullptr;
+    e->seg_cap = 0;
+    HIP_OK(hipMalloc(&e->d_segs, (size_t)nsegs * sizeof(tpi_seg)));
+    e->seg_cap = nsegs;
+  }
+  if (ntiles > e->crc_cap) {
+    if (e->d_crcs) HIP_OK(hipFree(e->d_crcs));
+    e->d_crcs = nullptr;
+    e->crc_cap = 0;
+    HIP_OK(hipMalloc(&e->d_crcs, ntiles * sizeof(uint32_t)));
+    e->crc_cap = ntiles;
+  }
+  if (codec && prepare_codec(e, ntiles)) return -1;
+  return 0;
+}
+
 int tpi_engine_set_progress(tpi_engine* e, uint64_t* words) {
   std::lock_guard<std::mutex> lk(e->mu);
   e->progress = words;

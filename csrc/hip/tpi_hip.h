@@ -57,7 +57,7 @@ typedef struct tpi_stats {
 } tpi_stats;
 
 // Bumped whenever a signature below changes (ops/_loader.py checks it).
-#define TPI_ABI_VERSION 5
+#define TPI_ABI_VERSION 6
 
 // Library / device
 const char* tpi_last_error(void);
@@ -175,6 +175,9 @@ int tpi_host_pin_release(tpi_pinner* p);
 // words[1] = stream bytes in host memory, then words[0] = tiles whose bytes and CRCs (and
 // blob sizes) are there, both release-stored.  NULL stops publishing.
 int tpi_engine_set_progress(tpi_engine* e, uint64_t* words);
+// Allocate the buffers the pipelines would otherwise allocate on first use, for up to
+// `nsegs` segments and `ntiles` tiles (and the codec's decode buffers when `codec`).
+int tpi_engine_reserve(tpi_engine* e, int nsegs, uint64_t ntiles, int codec);
 // Restore while another process is still writing the region: chunk k is copied once words[0]
 // covers its tiles; `timeout_s` without progress fails the call.  csizes == NULL: raw stream.
 int tpi_restore_stream(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total,

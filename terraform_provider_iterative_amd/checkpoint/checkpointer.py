@@ -170,6 +170,11 @@ class DeviceEngine:
         return TransferResult(plan.total, time.perf_counter() - t0, int(st.chunks),
                               int(bad.value), wire_bytes=0)
 
+    def reserve(self, nsegs: int, ntiles: int, codec: bool) -> None:
+        """Allocate now the device buffers the first save/restore of that size would."""
+        self.lib.check(self.lib.tpi_engine_reserve(self.handle, nsegs, ntiles, 1 if codec else 0),
+                       "tpi_engine_reserve")
+
     def set_progress(self, words_addr: int) -> None:
         self.lib.check(self.lib.tpi_engine_set_progress(self.handle,
                                                         ctypes.c_void_p(words_addr or None)),
@@ -242,6 +247,8 @@ class DeviceEngine:
             pass
 
 
+PREWARM_SEGS, PREWARM_TILES = 4096, 1 << 18
+
 # Engines created ahead of the Checkpointer that takes them (prewarm_engine).
 _engine_pool: Dict[Tuple[int, int, int, int], List[DeviceEngine]] = {}
 _engine_pool_lock = threading.Lock()
@@ -261,6 +268,10 @@ def prewarm_engine(device_index: Optional[int] = None, chunk_bytes: int = 256 <<
 
             device_index = torch.cuda.current_device()
         engine = DeviceEngine(device_index, chunk_bytes, nbuf, tile_bytes)
+        # a successor's first restore then allocates nothing (PREWARM_TILES: 256 GB of 1 MiB
+        # tiles, a few MB of descriptors); allocating under its predecessor's release of HBM
+        # waits for the driver's clearing (profiles/round4/materialize_170g.md)
+        engine.reserve(PREWARM_SEGS, PREWARM_TILES, True)
     except Exception:
         return False
     with _engine_pool_lock:
@@ -1075,6 +1086,8 @@ class Checkpointer:
             if ck._entries_digest != layout["entries_sha256"] or ck.size != layout["size"]:
                 raise CheckpointError("%s: region layout not reproducible from its entries"
                                       % path)
+            if ck.engine is not None:  # before the predecessor's freeing makes hipMalloc slow
+                ck.engine.reserve(len(entries) + 1, plan.ntiles, layout["codec"] == "tpz1")
             tensors, res = ck._materialize(dev, group_bytes, stream_timeout, memory_timeout)
         except BaseException:
             ck.close()
