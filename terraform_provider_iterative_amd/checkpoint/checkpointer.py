@@ -272,11 +272,37 @@ def prewarm_engine(device_index: Optional[int] = None, chunk_bytes: int = 256 <<
         # tiles, a few MB of descriptors); allocating under its predecessor's release of HBM
         # waits for the driver's clearing (profiles/round4/materialize_170g.md)
         engine.reserve(PREWARM_SEGS, PREWARM_TILES, True)
+        _warm_engine(engine, device_index, tile_bytes)
     except Exception:
         return False
     with _engine_pool_lock:
         _engine_pool.setdefault((device_index, chunk_bytes, nbuf, tile_bytes), []).append(engine)
     return True
+
+
+def _warm_engine(engine: DeviceEngine, device_index: int, tile_bytes: int) -> None:
+    """One tiny save + restore through every pipeline (raw and TPZ1; contiguous and
+    transposed tensors): the first launch of each kernel loads its code object, which
+    allocates device memory -- under a predecessor's release of HBM that waits seconds for
+    the driver's clearing (profiles/round4/materialize_170g.md)."""
+    import torch
+
+    dev = torch.device("cuda", device_index)
+    tensors = {"a": torch.ones(4096, device=dev), "t": torch.ones(64, 48, device=dev).t()}
+    plan = PackPlan.from_tensors(tensors, tile_bytes)
+    region = HostRegion(align_up(2 * max(plan.total, tpz.bound(plan.total, tile_bytes)), 4096),
+                        device=True, populate=True)
+    try:
+        crcs = np.zeros(plan.ntiles, np.uint32)
+        csizes = np.zeros(plan.ntiles, np.uint32)
+        sig = torch.cuda.current_stream(dev).cuda_stream
+        engine.save(plan, region.addr, crcs, MODES["sdma"], sig)
+        engine.restore(plan, region.addr, crcs, MODES["sdma"], sig)
+        engine.save_z(plan, region.addr, crcs, csizes, sig)
+        engine.restore_z(plan, region.addr, crcs, csizes, sig)
+        torch.cuda.synchronize(dev)
+    finally:
+        region.close()
 
 
 def _take_engine(device_index: int, chunk_bytes: int, nbuf: int,
