@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../common/tpz.h"
+#include "sysmem.h"
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -306,6 +307,7 @@ __global__ __launch_bounds__(CWG) void k_tpz_encode(const uint8_t* __restrict__ 
                                                     const uint8_t* __restrict__ hlen,
                                                     const uint32_t* __restrict__ hwords,
                                                     const uint32_t* __restrict__ csize,
+                                                    uint32_t* __restrict__ csize_host,
                                                     uint8_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) tpz_plane hdr[4];
   __shared__ uint8_t rank[4][256];
@@ -319,6 +321,8 @@ __global__ __launch_bounds__(CWG) void k_tpz_encode(const uint8_t* __restrict__ 
   const uint8_t* t = raw + tbase;
   const uint64_t n = tlen / 4, ngroups = tpz_ngroups(tlen);
 
+  // the host learns the blob sizes here, without a copy (engine.hip meta_view)
+  if (tid == 0 && csize_host) tpi_sys_store(&csize_host[blockIdx.x], csize[blockIdx.x]);
   uint64_t part = 0;
   for (uint64_t i = tid; i < blockIdx.x; i += CWG) part += csize[i];
   uint64_t obase;
@@ -531,7 +535,9 @@ __global__ __launch_bounds__(CWG) void k_tpz_decode(const uint8_t* __restrict__ 
   const uint64_t tlen = cmin64(tile, len - tbase);
   uint8_t* t = raw + tbase;
   const uint64_t n = tlen / 4, ngroups = tpz_ngroups(tlen);
-  const uint64_t b0 = coff[blockIdx.x] - comp_base, b1 = coff[blockIdx.x + 1] - comp_base;
+  // coff may be the host's pinned offset array itself (engine.hip meta_view)
+  const uint64_t b0 = tpi_sys_load(&coff[blockIdx.x]) - comp_base;
+  const uint64_t b1 = tpi_sys_load(&coff[blockIdx.x + 1]) - comp_base;
   const uint8_t* blob = comp + b0;
   const uint64_t avail = b1 - b0;
 
@@ -688,8 +694,8 @@ __global__ __launch_bounds__(CWG) void k_tpz_decode(const uint8_t* __restrict__ 
 // ---- launchers ------------------------------------------------------------------------------------
 
 extern "C" hipError_t tpi_launch_tpz_encode(const void* raw, uint64_t len, uint64_t tile,
-                                            void* meta, uint32_t* csize, void* out,
-                                            hipStream_t stream) {
+                                            void* meta, uint32_t* csize, uint32_t* csize_host,
+                                            void* out, hipStream_t stream) {
   if (len == 0) return hipSuccess;
   const unsigned ntiles = (unsigned)((len + tile - 1) / tile);
   // meta (tpz_meta_bytes(ntiles)): plane headers | HUF code lengths | HUF substream words
@@ -701,7 +707,8 @@ extern "C" hipError_t tpi_launch_tpz_encode(const void* raw, uint64_t len, uint6
                      tile, planes, hlen, hwords, csize);
   hipLaunchKernelGGL(k_tpz_encode, dim3(ntiles), dim3(CWG), 0, stream, (const uint8_t*)raw, len,
                      tile, (const tpz_plane*)planes, (const uint8_t*)hlen,
-                     (const uint32_t*)hwords, (const uint32_t*)csize, (uint8_t*)out);
+                     (const uint32_t*)hwords, (const uint32_t*)csize, csize_host,
+                     (uint8_t*)out);
   return hipGetLastError();
 }
 

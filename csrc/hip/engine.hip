@@ -71,8 +71,8 @@ extern "C" hipError_t tpi_launch_stream_copy_hash(const tpi_seg* src, const tpi_
                                                   unsigned long long* bad, hipStream_t stream);
 
 extern "C" hipError_t tpi_launch_tpz_encode(const void* raw, uint64_t len, uint64_t tile,
-                                            void* meta, uint32_t* csize, void* out,
-                                            hipStream_t stream);
+                                            void* meta, uint32_t* csize, uint32_t* csize_host,
+                                            void* out, hipStream_t stream);
 extern "C" hipError_t tpi_launch_tpz_decode(const void* comp, const uint64_t* coff,
                                             uint64_t comp_base, uint64_t len, uint64_t tile,
                                             void* raw, hipStream_t stream);
@@ -366,8 +366,9 @@ int publish_chunk(tpi_engine* e, const std::vector<ChunkMark>& marks, uint64_t j
   }
   const uint64_t t_end = marks[j].tile_end;
   if (t_end > *tiles_published) {
-    HIP_OK(hipMemcpy(crcs_out + *tiles_published, e->d_crcs + *tiles_published,
-                     (t_end - *tiles_published) * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (crcs_out)  // else the kernels stored the CRCs in host memory themselves (meta_view)
+      HIP_OK(hipMemcpy(crcs_out + *tiles_published, e->d_crcs + *tiles_published,
+                       (t_end - *tiles_published) * sizeof(uint32_t), hipMemcpyDeviceToHost));
     *tiles_published = t_end;
   }
   __atomic_store_n(&e->progress[1], marks[j].byte_end, __ATOMIC_RELEASE);
@@ -601,6 +602,40 @@ void* device_view(void* host) {
   return d;
 }
 
+// Streamed saves and restores keep per-tile metadata (CRCs, blob sizes, blob offsets) where
+// the other side reads it -- the kernels store it straight into registered host memory and
+// load it from there (sysmem.h) -- instead of one small copy per chunk in each direction.
+// Those copies ran as HIP blit kernels on a queue of their own, the only work in flight during
+// the ~3 ms stalls of both pipelines traced in profiles/hw_queues_round3.md.  Returns the
+// device address of `bytes` at `host`, or nullptr when the kernels cannot reach it (not
+// registered, split over two registration windows) or TPI_DIRECT_META=0: then the copies.
+// TPI_DIRECT_META: "save" (default) the saves only, "1" both sides, "restore" the restores
+// only, "0" none.  Measured with bench.py on MI355X (profiles/round4/direct_meta.md): saves
+// +1.4 % (no synchronous CRC copy at publish, no blob-size copy per chunk); restores reading
+// CRCs and blob offsets over PCIe from their kernels -0.5 to -1 %, so they keep the copies.
+void* meta_view(tpi_engine* e, const void* host, uint64_t bytes, bool restore_side) {
+  static const int sides = [] {  // bit 0: saves, bit 1: restores
+    const char* v = getenv("TPI_DIRECT_META");
+    if (!v || !strcmp(v, "save")) return 1;
+    if (!strcmp(v, "0") || !strcmp(v, "false") || !strcmp(v, "no")) return 0;
+    if (!strcmp(v, "restore")) return 2;
+    return 3;
+  }();
+  if (!(sides & (restore_side ? 2 : 1)) || !host || !bytes) return nullptr;
+  const uint8_t* h = (const uint8_t*)host;
+  if (e->hwin && h >= e->hbase && h < e->hbase + e->hbytes) {
+    const uint64_t at = (uint64_t)(h - e->hbase);
+    if (at / e->hwin != (at + bytes - 1) / e->hwin) return nullptr;
+    if (e->pinner && !wait_pinned(e->pinner, std::min(e->hbytes, at + bytes))) return nullptr;
+  }
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, const_cast<void*>(host), 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return d;
+}
+
 }  // namespace
 
 extern "C" {
@@ -620,6 +655,7 @@ int tpi_save(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* ho
   const uint32_t init_full = init_for(tile);
   const uint32_t init_last = init_for(total % tile ? total % tile : tile);
   uint64_t nchunks = 0;
+  bool direct_crcs = false;
   if (mode == TPI_MODE_DIRECT) {
     HIP_OK(tpi_launch_stream_crc(0, e->d_segs, n, 0, total, device_view(host_dst), tile,
                                  e->tables, e->d_crcs, init_full, init_last, nullptr, 0,
@@ -629,29 +665,38 @@ int tpi_save(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* ho
     uint8_t* dst = (uint8_t*)host_dst;
     std::vector<ChunkMark> marks;
     uint64_t published = 0;
+    // streamed: the CRC kernel stores each tile's CRC in crcs_out itself (meta_view)
+    uint32_t* crc_host =
+        e->progress ? (uint32_t*)meta_view(e, crcs_out, (total + tile - 1) / tile *
+                                                            sizeof(uint32_t), false)
+                    : nullptr;
+    uint32_t* crc_dst = crc_host ? crc_host : e->d_crcs;
     for (uint64_t base = 0, k = 0; base < total; base += e->chunk, ++k) {
       const int b = (int)(k % e->nbuf);
       const uint64_t len = std::min(e->chunk, total - base);
       if (k >= (uint64_t)e->nbuf && staging_free(e, b, e->compute)) return -1;
       HIP_OK(tpi_launch_transposes(segs, n, base, len, e->staging[b], 0, e->compute));
       HIP_OK(tpi_launch_stream_crc(0, e->d_segs, n, base, len, e->staging[b], tile, e->tables,
-                                   e->d_crcs, init_full, init_last, nullptr, 1, e->compute));
+                                   crc_dst, init_full, init_last, nullptr, 1, e->compute));
       if (staging_ready(e, b, e->compute) || staging_d2h(e, b, dst + base, e->staging[b], len) ||
           staging_sent(e, b))
         return -1;
       marks.push_back({(base + len + tile - 1) / tile, base + len});
       // chunk k is queued behind chunk k-1 on the engine: publishing k-1 keeps it busy
-      if (e->progress && k >= 1 && publish_chunk(e, marks, k - 1, &published, crcs_out))
+      if (e->progress && k >= 1 &&
+          publish_chunk(e, marks, k - 1, &published, crc_host ? nullptr : crcs_out))
         return -1;
       nchunks = k + 1;
     }
     if (e->progress && !marks.empty() &&
-        publish_chunk(e, marks, marks.size() - 1, &published, crcs_out))
+        publish_chunk(e, marks, marks.size() - 1, &published, crc_host ? nullptr : crcs_out))
       return -1;
+    if (crc_host) direct_crcs = true;
   }
   const uint64_t ntiles = (total + tile - 1) / tile;
-  HIP_OK(region_copy(e, crcs_out, e->d_crcs, ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                        e->compute));
+  if (!direct_crcs)
+    HIP_OK(region_copy(e, crcs_out, e->d_crcs, ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                       e->compute));
   if (drain_d2h(e)) return -1;
   HIP_OK(hipStreamSynchronize(e->compute));
   if (stats) {
@@ -882,6 +927,13 @@ int tpi_save_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* 
   uint8_t* dst = (uint8_t*)host_dst;
   uint64_t out = 0, nchunks = 0, published = 0;
   std::vector<ChunkMark> marks;
+  // streamed: the kernels store CRCs and blob sizes in the host arrays themselves (meta_view)
+  uint32_t* crc_host =
+      e->progress ? (uint32_t*)meta_view(e, crcs_out, ntiles * sizeof(uint32_t), false)
+                  : nullptr;
+  uint32_t* csz_host =
+      crc_host ? (uint32_t*)meta_view(e, csizes_out, ntiles * sizeof(uint32_t), false) : nullptr;
+  if (!csz_host) crc_host = nullptr;
   for (uint64_t base = 0, k = 0; base < total; base += e->chunk, ++k) {
     const int b = (int)(k % e->nbuf);
     const uint64_t len = std::min(e->chunk, total - base);
@@ -889,11 +941,13 @@ int tpi_save_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* 
     if (k >= (uint64_t)e->nbuf && staging_free(e, b, e->compute)) return -1;
     HIP_OK(tpi_launch_transposes(segs, n, base, len, e->zraw, 0, e->compute));
     HIP_OK(tpi_launch_stream_crc(0, e->d_segs, n, base, len, e->zraw, tile, e->tables,
-                                 e->d_crcs, init_full, init_last, nullptr, 1, e->compute));
+                                 crc_host ? crc_host : e->d_crcs, init_full, init_last, nullptr,
+                                 1, e->compute));
     HIP_OK(tpi_launch_tpz_encode(e->zraw, len, tile, e->d_meta, e->d_csize + t0i,
-                                 e->staging[b], e->compute));
-    HIP_OK(region_copy(e, csizes_out + t0i, e->d_csize + t0i, nt * sizeof(uint32_t),
-                          hipMemcpyDeviceToHost, e->compute));
+                                 csz_host ? csz_host + t0i : nullptr, e->staging[b], e->compute));
+    if (!csz_host)
+      HIP_OK(region_copy(e, csizes_out + t0i, e->d_csize + t0i, nt * sizeof(uint32_t),
+                         hipMemcpyDeviceToHost, e->compute));
     HIP_OK(hipEventRecord(e->ev_a[b], e->compute));
     HIP_OK(hipEventSynchronize(e->ev_a[b]));
     uint64_t clen = 0;
@@ -902,15 +956,17 @@ int tpi_save_z(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void* 
     if (staging_d2h(e, b, dst + out, e->staging[b], clen) || staging_sent(e, b)) return -1;
     out += clen;
     marks.push_back({t0i + nt, out});
-    if (e->progress && k >= 1 && publish_chunk(e, marks, k - 1, &published, crcs_out))
+    if (e->progress && k >= 1 &&
+        publish_chunk(e, marks, k - 1, &published, crc_host ? nullptr : crcs_out))
       return -1;
     nchunks = k + 1;
   }
   if (e->progress && !marks.empty() &&
-      publish_chunk(e, marks, marks.size() - 1, &published, crcs_out))
+      publish_chunk(e, marks, marks.size() - 1, &published, crc_host ? nullptr : crcs_out))
     return -1;
-  HIP_OK(region_copy(e, crcs_out, e->d_crcs, ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                        e->compute));
+  if (!crc_host)
+    HIP_OK(region_copy(e, crcs_out, e->d_crcs, ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                       e->compute));
   if (drain_d2h(e)) return -1;
   HIP_OK(hipStreamSynchronize(e->compute));
   *stream_bytes = out;
@@ -986,7 +1042,7 @@ int tpi_spill(tpi_engine* e, const void* dev_src, const uint32_t* dev_crcs, uint
       const uint64_t t0i = base / tile, nt = (len + tile - 1) / tile;
       if (k >= (uint64_t)e->nbuf && staging_free(e, b, e->compute)) return -1;
       HIP_OK(tpi_launch_tpz_encode(src + base, len, tile, e->d_meta, e->d_csize + t0i,
-                                   e->staging[b], e->compute));
+                                   nullptr, e->staging[b], e->compute));
       HIP_OK(region_copy(e, csizes_out + t0i, e->d_csize + t0i, nt * sizeof(uint32_t),
                             hipMemcpyDeviceToHost, e->compute));
       HIP_OK(hipEventRecord(e->ev_a[b], e->compute));
@@ -1094,7 +1150,8 @@ int tpi_tpz_encode_device(const void* raw, uint64_t len, uint64_t tile, void* me
                           uint32_t* csize, void* out, uint64_t stream) {
   if (tile == 0 || tile % TPI_ROW_BYTES) return fail("tile must be k*4096");
   if (len % 16) return fail("length must be a multiple of 16");
-  HIP_OK(tpi_launch_tpz_encode(raw, len, tile, meta_scratch, csize, out, (hipStream_t)stream));
+  HIP_OK(tpi_launch_tpz_encode(raw, len, tile, meta_scratch, csize, nullptr, out,
+                               (hipStream_t)stream));
   return 0;
 }
 
@@ -1399,6 +1456,16 @@ int tpi_restore_stream_at(tpi_engine* e, const tpi_seg* segs, int n, uint64_t to
     coff = raw_coff.data();
   }
   coff[0] = 0;
+  // the kernels read the writer's CRCs and the blob offsets where they are (meta_view), so no
+  // per-chunk uploads on the aux stream
+  const uint32_t* crc_host =
+      (const uint32_t*)meta_view(e, crcs, ntiles * sizeof(uint32_t), true);
+  const uint64_t* coff_host =
+      zipped && crc_host
+          ? (const uint64_t*)meta_view(e, e->h_coff, (ntiles + 1) * sizeof(uint64_t), true)
+          : nullptr;
+  const bool direct = crc_host && (!zipped || coff_host);
+  uint32_t* crc_src = direct ? (uint32_t*)crc_host : e->d_crcs;
   const uint8_t* src = (const uint8_t*)host_src;
   uint64_t nchunks = 0;
   const uint64_t chunk_tiles = e->chunk / tile;
@@ -1444,12 +1511,14 @@ int tpi_restore_stream_at(tpi_engine* e, const tpi_seg* segs, int n, uint64_t to
     // link idle ~1 ms per chunk (rocprofv3 memory-copy trace of bench.py).  Slices of
     // different chunks are disjoint (the shared boundary offset is rewritten with the same
     // value).
-    if (zipped)
-      HIP_OK(hipMemcpyAsync(e->d_coff + t0i, coff + t0i, (nt + 1) * sizeof(uint64_t),
-                            hipMemcpyHostToDevice, e->aux));
-    HIP_OK(region_copy(e, e->d_crcs + t0i, crcs + t0i, nt * sizeof(uint32_t),
-                       hipMemcpyHostToDevice, e->aux));
-    HIP_OK(hipEventRecord(e->ev_c[b], e->aux));
+    if (!direct) {
+      if (zipped)
+        HIP_OK(hipMemcpyAsync(e->d_coff + t0i, coff + t0i, (nt + 1) * sizeof(uint64_t),
+                              hipMemcpyHostToDevice, e->aux));
+      HIP_OK(region_copy(e, e->d_crcs + t0i, crcs + t0i, nt * sizeof(uint32_t),
+                         hipMemcpyHostToDevice, e->aux));
+      HIP_OK(hipEventRecord(e->ev_c[b], e->aux));
+    }
     if (k >= (uint64_t)e->nbuf) HIP_OK(hipStreamWaitEvent(e->copy, e->ev_b[b], 0));
     // halves split on a 64 KiB boundary of the wire stream (chunks under 128 KiB stay whole)
     const uint64_t mid = split && cend - cbeg >= (128ull << 10)
@@ -1466,18 +1535,18 @@ int tpi_restore_stream_at(tpi_engine* e, const tpi_seg* segs, int n, uint64_t to
       HIP_OK(hipStreamWaitEvent(e->compute, e->ev_d[b], 0));
       ++e->split_chunks;
     }
-    HIP_OK(hipStreamWaitEvent(e->compute, e->ev_c[b], 0));
+    if (!direct) HIP_OK(hipStreamWaitEvent(e->compute, e->ev_c[b], 0));
     HIP_OK(hipStreamWaitEvent(e->compute, e->ev_a[b], 0));
     if (zipped) {
-      HIP_OK(tpi_launch_tpz_decode(e->staging[b], e->d_coff + t0i, cbeg, len, tile, e->zraw,
-                                   e->compute));
+      HIP_OK(tpi_launch_tpz_decode(e->staging[b], (direct ? coff_host : e->d_coff) + t0i, cbeg,
+                                   len, tile, e->zraw, e->compute));
       HIP_OK(hipEventRecord(e->ev_b[b], e->compute));
       HIP_OK(tpi_launch_stream_crc(1, e->d_segs, n, base, len, e->zraw, tile, e->tables,
-                                   e->d_crcs, init_full, init_last, e->d_bad, 1, e->compute));
+                                   crc_src, init_full, init_last, e->d_bad, 1, e->compute));
       HIP_OK(tpi_launch_transposes(segs, n, base, len, e->zraw, 1, e->compute));
     } else {
       HIP_OK(tpi_launch_stream_crc(1, e->d_segs, n, base, len, e->staging[b], tile, e->tables,
-                                   e->d_crcs, init_full, init_last, e->d_bad, 1, e->compute));
+                                   crc_src, init_full, init_last, e->d_bad, 1, e->compute));
       HIP_OK(tpi_launch_transposes(segs, n, base, len, e->staging[b], 1, e->compute));
       HIP_OK(hipEventRecord(e->ev_b[b], e->compute));
     }

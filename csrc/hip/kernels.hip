@@ -31,6 +31,7 @@
 
 #include "../common/crc32c.h"
 #include "../common/xxh64.h"
+#include "sysmem.h"
 #include "tpi_hip.h"
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -525,12 +526,12 @@ __global__ __launch_bounds__(WG) void k_stream_crc(TileArgs a) {
     const uint32_t crc = raw ^ init ^ 0xFFFFFFFFu;
     const uint64_t gtile = geom.gtile;
     if (MODE == MODE_UNPACK || MODE == MODE_VERIFY) {
-      if (crc != a.crcs[gtile]) {
+      if (crc != tpi_sys_load(&a.crcs[gtile])) {
         atomicAdd(&a.bad[0], 1ull);
         atomicMin(&a.bad[1], (unsigned long long)gtile);
       }
     } else {
-      a.crcs[gtile] = crc;
+      tpi_sys_store(&a.crcs[gtile], crc);
     }
   }
 }
@@ -671,7 +672,8 @@ __global__ __launch_bounds__(CRC_WG) void k_crc_tiles(TileArgs a) {
     if (lane == 0 && t < ntiles) {
       const uint32_t* r = s_red + (WG / 64) * half;
       const uint32_t init = (tile_len == a.tile_bytes) ? a.init_full : a.init_last;
-      a.crcs[a.stream_base / a.tile_bytes + t] = r[0] ^ r[1] ^ r[2] ^ r[3] ^ init ^ 0xFFFFFFFFu;
+      tpi_sys_store(&a.crcs[a.stream_base / a.tile_bytes + t],
+                    r[0] ^ r[1] ^ r[2] ^ r[3] ^ init ^ 0xFFFFFFFFu);
     }
   }
 }

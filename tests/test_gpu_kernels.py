@@ -756,3 +756,52 @@ def test_materialize_streams_groups_behind_a_writer(codec, tmp_path):
         assert torch.equal(tensors2[k], src[k]), k
     ck2.close()
     writer.close()
+
+
+def test_direct_metadata_modes_give_identical_checkpoints(tmp_path):
+    """TPI_DIRECT_META (read once per process): the streamed save's kernels store tile CRCs
+    and blob sizes straight in the host region, the streamed restore's kernels read CRCs and
+    blob offsets from host memory -- or both sides use per-chunk copies.  Every mode must write
+    the same region and restore the same bytes."""
+    import hashlib
+    import subprocess
+    import sys
+
+    script = r'''
+import hashlib, json, sys, threading, torch
+sys.path.insert(0, %r)
+from terraform_provider_iterative_amd.checkpoint import Checkpointer
+g = torch.Generator().manual_seed(21)
+src = {"a": torch.randn(3 << 20, generator=g).to(torch.bfloat16).cuda(),
+       "b": torch.randn(5 << 20, generator=g).mul(1e-3).cuda(),
+       "t": torch.randn(640, 1000, generator=g).cuda().t()}
+dst = {k: torch.zeros_like(v) for k, v in src.items()}
+dst["t"] = torch.zeros(640, 1000, device="cuda").t()
+out = {}
+for codec in ("none", "tpz1"):
+    path = sys.argv[1] + "." + codec
+    kw = dict(tile_bytes=1 << 16, chunk_bytes=1 << 20, nbuf=2, codec=codec)
+    writer, reader = Checkpointer(src, path=path, **kw), Checkpointer(dst, path=path, **kw)
+    box = {}
+    th = threading.Thread(target=lambda: box.update(res=reader.restore(stream_timeout=20)))
+    writer.save({"step": 1}, on_stream=th.start)
+    th.join(60)
+    torch.cuda.synchronize()
+    assert box["res"].bad_tiles == 0
+    assert all(torch.equal(dst[k], src[k]) for k in src)
+    slot = writer.slots[0]
+    out[codec] = hashlib.sha256(slot.crcs.tobytes() + slot.csizes.tobytes()).hexdigest()
+    for v in dst.values():
+        v.zero_()
+    reader.close()
+    writer.close()
+print(json.dumps(out))
+''' % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    seen = {}
+    for mode in ("0", "save", "restore", "1"):
+        env = dict(os.environ, TPI_DIRECT_META=mode)
+        proc = subprocess.run([sys.executable, "-c", script, str(tmp_path / ("r" + mode))],
+                              env=env, capture_output=True, text=True, timeout=180)
+        assert proc.returncode == 0, (mode, proc.stderr[-2000:])
+        seen[mode] = proc.stdout.strip().splitlines()[-1]
+    assert len(set(seen.values())) == 1, seen
