@@ -256,7 +256,8 @@ class TrainingState:
     def __init__(self, model, optimizer=None, extra: Optional[Dict[str, Any]] = None,
                  path: Optional[str] = None, device=None, *, lr_scheduler=None, scaler=None,
                  rng: bool = True, generators: Optional[Dict[str, Any]] = None,
-                 stateful: Optional[Dict[str, Any]] = None, **checkpointer_kwargs):
+                 stateful: Optional[Dict[str, Any]] = None,
+                 checkpointer: Optional[Checkpointer] = None, **checkpointer_kwargs):
         tensors, self.host = collect(model, optimizer, extra, device)
         if not tensors:
             raise ValueError("nothing to checkpoint on the model's device")
@@ -267,9 +268,72 @@ class TrainingState:
         self.generators: Dict[str, Any] = dict(generators or {})
         self.stateful: Dict[str, Any] = dict(stateful or {})
         self.host_metadata()  # anything the header cannot carry fails here, not at SIGTERM
-        self.checkpointer = Checkpointer(tensors, path=path, **checkpointer_kwargs)
-        self.path = path
+        if checkpointer is not None:  # from_materialized(): already bound to these tensors
+            bound = getattr(checkpointer.plan, "_bound", [])
+            if (len(bound) != len(tensors) or
+                    [e.name for e in checkpointer.plan.entries] != list(tensors) or
+                    any(a.data_ptr() != b.data_ptr() for a, b in zip(bound, tensors.values()))):
+                raise ValueError("the checkpointer is not bound to this model's and "
+                                 "optimizer's tensors")
+            self.checkpointer = checkpointer
+        else:
+            self.checkpointer = Checkpointer(tensors, path=path, **checkpointer_kwargs)
+        self.path = path if path is not None else checkpointer.path if checkpointer else None
         self.step_value: Optional[int] = None  # last step reported (or restored)
+
+    @classmethod
+    def from_materialized(cls, materialized, model, make_optimizer=None, *,
+                          make_lr_scheduler=None, scaler=None, rng: bool = True,
+                          generators: Optional[Dict[str, Any]] = None,
+                          stateful: Optional[Dict[str, Any]] = None) -> "TrainingState":
+        """Resume around the tensors of :func:`.preemption.materialize` instead of restoring
+        into tensors allocated beforehand (a state too big to allocate next to its
+        predecessor's; see :meth:`Checkpointer.materialize`).
+
+        ``model`` is built without storage (``with torch.device("meta"): model = Net()``);
+        its parameters and buffers become the materialized tensors
+        (``load_state_dict(assign=True)``).  ``make_optimizer(model)`` then creates the
+        optimizer over them, whose per-parameter state is set to the materialized tensors and
+        the small host tensors of the checkpoint header (Adam's step counters);
+        ``make_lr_scheduler(optimizer)`` likewise.  Everything else -- param-group
+        hyper-parameters, scheduler, ``scaler``, RNGs, ``generators``, ``stateful`` objects --
+        is restored as :meth:`resume` does.  The model and optimizer must be built the way the
+        saving process built them (same parameter order).  Tied parameters are not re-tied.
+        """
+        import torch
+
+        ck, tensors, meta = materialized
+        blobs = (meta or {}).get("host_tensors", {})
+
+        def host_tensor(name):
+            blob = blobs[name]
+            return torch.tensor(blob["data"], dtype=getattr(torch, blob["dtype"])).reshape(
+                blob["shape"])
+
+        module = getattr(model, "module", model)
+        state = {k[len("model."):]: v for k, v in tensors.items() if k.startswith("model.")}
+        for name in blobs:
+            if name.startswith("model."):
+                state[name[len("model."):]] = host_tensor(name)
+        module.load_state_dict(state, strict=True, assign=True)
+        optimizer = make_optimizer(model) if make_optimizer is not None else None
+        if optimizer is not None:
+            params = [p for group in optimizer.param_groups for p in group["params"]]
+            for source in (tensors, blobs):
+                for name in source:
+                    if not name.startswith("optim."):
+                        continue
+                    index, key = name[len("optim."):].split(".", 1)
+                    value = tensors[name] if source is tensors else host_tensor(name)
+                    optimizer.state[params[int(index)]][key] = value
+        extra = {k[len("extra."):]: v for k, v in tensors.items() if k.startswith("extra.")}
+        lr_scheduler = make_lr_scheduler(optimizer) if make_lr_scheduler is not None else None
+        out = cls(model, optimizer, extra or None, lr_scheduler=lr_scheduler, scaler=scaler,
+                  rng=rng, generators=generators, stateful=stateful, checkpointer=ck)
+        out.restore_host(meta or {})
+        if isinstance((meta or {}).get("step"), int):
+            out.step_value = meta["step"]
+        return out
 
     def register(self, name: str, obj: Any) -> None:
         """Carry ``obj.state_dict()`` in every checkpoint and ``load_state_dict`` it on resume
