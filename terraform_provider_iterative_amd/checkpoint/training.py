@@ -316,6 +316,13 @@ class TrainingState:
             if name.startswith("model."):
                 state[name[len("model."):]] = host_tensor(name)
         module.load_state_dict(state, strict=True, assign=True)
+        left = [n for n, t in list(module.named_parameters()) + list(module.named_buffers())
+                if t.is_meta]
+        if left:  # non-persistent buffers are not in any state_dict: the caller rebuilds them
+            import warnings
+
+            warnings.warn("still on the meta device after from_materialized (not in the "
+                          "checkpoint; rebuild them): %s" % ", ".join(left[:8]), stacklevel=2)
         optimizer = make_optimizer(model) if make_optimizer is not None else None
         if optimizer is not None:
             params = [p for group in optimizer.param_groups for p in group["params"]]

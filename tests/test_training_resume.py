@@ -251,3 +251,27 @@ def test_from_materialized_resumes_bit_identically(tmp_path):
 @pytest.mark.gpu
 def test_from_materialized_resumes_bit_identically_on_the_gpu(tmp_path):
     _materialize_round_trip(tmp_path, "cuda")
+
+
+def test_from_materialized_warns_about_non_persistent_buffers(tmp_path):
+    import torch
+
+    from terraform_provider_iterative_amd.checkpoint import TrainingState, preemption
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.lin = torch.nn.Linear(8, 8)
+            self.register_buffer("cache", torch.arange(8.0), persistent=False)
+
+    net = Net()
+    path = str(tmp_path / "spill")
+    state = TrainingState(net, path=path, tile_bytes=4096)
+    state.save({"step": 1})
+    state.close()
+    with torch.device("meta"):
+        fresh = Net()
+    with pytest.warns(UserWarning, match="cache"):
+        resumed = TrainingState.from_materialized(preemption.materialize(path, "cpu"), fresh)
+    assert torch.equal(fresh.lin.weight, net.lin.weight) and fresh.cache.is_meta
+    resumed.close()
