@@ -1097,6 +1097,7 @@ class Checkpointer:
         """
         import torch
 
+        t0 = time.perf_counter()
         layout = _region_layout(path)
         dev = torch.device(device if device is not None else "cuda")
         if dev.type == "cuda" and dev.index is None:
@@ -1106,14 +1107,18 @@ class Checkpointer:
         plan.device = str(dev)
         plan._bound = []
         kwargs.setdefault("codec", layout["codec"])
+        t1 = time.perf_counter()
         ck = cls(None, path, tile_bytes=layout["tile_bytes"], slots=layout["slots"], _plan=plan,
                  **kwargs)
         try:
             if ck._entries_digest != layout["entries_sha256"] or ck.size != layout["size"]:
                 raise CheckpointError("%s: region layout not reproducible from its entries"
                                       % path)
+            t2 = time.perf_counter()
             if ck.engine is not None:  # before the predecessor's freeing makes hipMalloc slow
                 ck.engine.reserve(len(entries) + 1, plan.ntiles, layout["codec"] == "tpz1")
+            ck._setup_times = {"layout": round(t1 - t0, 4), "checkpointer": round(t2 - t1, 4),
+                               "reserve": round(time.perf_counter() - t2, 4)}
             tensors, res = ck._materialize(dev, group_bytes, stream_timeout, memory_timeout)
         except BaseException:
             ck.close()
@@ -1236,7 +1241,10 @@ class Checkpointer:
             except BaseException as error:  # surfaced by the restoring thread
                 ready.put(error)
 
+        t_lead = time.perf_counter()
         lead = torch.empty(self.plan.tile_bytes, dtype=torch.uint8, device=dev)
+        setup = dict(getattr(self, "_setup_times", {}), lead=round(time.perf_counter() - t_lead, 4),
+                     find=round(t_lead - t_start, 4))
         worker = threading.Thread(target=allocate, name="tpi-materialize-alloc", daemon=True)
         worker.start()
         tensors: Dict[str, Any] = {}
@@ -1303,7 +1311,7 @@ class Checkpointer:
             native().crc32c_combine_tiles_ptr(slot.crcs.ctypes.data, self.plan.ntiles,
                                               self.plan.tile_bytes, self.plan.total)
         self.materialize_stats = {"groups": len(groups), "alloc_wait_s": round(waited[0], 4),
-                                  "streamed": streaming, "trace": trace,
+                                  "streamed": streaming, "trace": trace, "setup": setup,
                                   "alloc": "nogil" if empty_nogil is not None else "torch"}
         self.materialized_metadata = header.get("metadata", {})
         self.last_restore = total
