@@ -61,7 +61,9 @@ def _digest(cmd: Sequence[str], deps: Sequence[str]) -> str:
     h = hashlib.sha256()
     h.update("\0".join(c.replace(ROOT, "@ROOT@") for c in cmd if ".tmp." not in c).encode())
     for dep in sorted(set(deps)):
-        h.update(b"\0" + os.path.relpath(dep, ROOT).encode() + b"\0")
+        # outside the tree (torch's version file): the absolute path, the same on every box
+        name = os.path.relpath(dep, ROOT) if dep.startswith(ROOT + os.sep) else dep
+        h.update(b"\0" + name.encode() + b"\0")
         with open(dep, "rb") as handle:
             h.update(handle.read())
     return h.hexdigest()

@@ -57,7 +57,8 @@ def test_stamps_survive_moving_the_tree(tmp_path):
 
     _build.build_native()
     _build.build_supervisor()
-    copy = tmp_path / "elsewhere"
+    _build.build_torch_ext()  # depends on a file outside the tree (torch's version.py)
+    copy = tmp_path / "elsewhere" / "at" / "another" / "depth"
     shutil.copytree(os.path.join(ROOT, "csrc"), copy / "csrc")
     shutil.copytree(os.path.join(ROOT, "terraform_provider_iterative_amd"),
                     copy / "terraform_provider_iterative_amd",
@@ -69,7 +70,9 @@ def test_stamps_survive_moving_the_tree(tmp_path):
             "cmd = [__import__('os').environ.get('CXX', 'g++'), '-O2', '-std=c++17', '-Wall', "
             "'-pthread', b._define_version(), *srcs, '-o', '@OUT@']\n"
             "assert not b._stale(b.SUPERVISOR, cmd, srcs + b._sources('supervisor/*.h'))\n"
+            "import torch  # (build_torch_ext imports it; not part of the timing)\n"
             "import time; t = time.time(); b.build_native(); b.build_supervisor()\n"
+            "b.build_torch_ext()\n"
             "assert time.time() - t < 2, 'rebuilt'\n" % str(copy))
     res = subprocess.run([sys.executable, "-c", code], cwd=str(copy), capture_output=True,
                          text=True, timeout=120)
