@@ -203,6 +203,17 @@ def main():
             time.sleep(0.2)
         if not any("ready" in l for l in task.logs()):
             raise SystemExit("rank never became ready: %s" % task.logs())
+        if args.hot:
+            # a hot standby maps and pins the whole spill once the rank has created it; a
+            # preemption hours into training finds it pinned, so wait for that here too
+            # (recorded as standby_pinned_s) instead of racing the pinning
+            t_wait = time.time()
+            while time.time() - t_wait < 300 and not any(
+                    e.code == "standby-pinned" for e in task.events()):
+                time.sleep(0.1)
+            result["standby_pinned_wait_s"] = round(time.time() - t_wait, 3)
+            result["standby_pinned"] = next((e.description for e in task.events()
+                                             if e.code == "standby-pinned"), None)
         t_preempt = time.time()
         task.preempt()
         status = task.wait(args.timeout)

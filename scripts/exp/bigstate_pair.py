@@ -64,6 +64,9 @@ torch.cuda.set_device(dev)
 torch.empty(1, device=dev)
 prewarm_engine(0)
 prefetch(%(spill)r)
+if "--racing" not in sys.argv:  # a hot standby has long pinned the spill when a preemption comes
+    from terraform_provider_iterative_amd.checkpoint.host import wait_pinned
+    say("pinned in %%.3f s" %% wait_pinned(%(spill)r))
 say("standing by")
 print("ready", flush=True)
 sys.stdin.readline()
@@ -101,6 +104,8 @@ def main():
     p.add_argument("--gb", type=float, default=170.0)
     p.add_argument("--mode", choices=("materialize", "upfront"), default="materialize")
     p.add_argument("--spill", default="/dev/shm/tpi-bigstate-pair-%d.spill" % os.getpid())
+    p.add_argument("--racing", action="store_true",
+                   help="the successor starts restoring while it is still pinning the spill")
     args = p.parse_args()
     t0 = time.time()
     sub = {"root": ROOT, "spill": args.spill}
@@ -111,8 +116,8 @@ def main():
     try:
         assert pred.stdout.readline().strip() == "ready"
         succ = subprocess.Popen([sys.executable, "-c", SUCC % sub, str(args.gb), str(t0),
-                                 args.mode], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
-                                text=True, env=env)
+                                 args.mode] + (["--racing"] if args.racing else []),
+                                stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=env)
         assert succ.stdout.readline().strip() == "ready"
         t_sig = time.time()
         pred.stdin.write("\n")

@@ -253,6 +253,34 @@ def watch_prefetch(path: str, cancel: threading.Event, poll: float = 0.2) -> thr
     return thread
 
 
+def wait_pinned(path: str, timeout: float = 600.0, cancel: Optional[threading.Event] = None,
+                poll: float = 0.01) -> Optional[float]:
+    """Seconds until the prefetched region of ``path`` is mapped and pinned whole (None: no
+    prefetch of ``path``, it failed, ``timeout`` passed or ``cancel`` was set).  A hot standby
+    pins a 170 GB spill in a few seconds; until then its restore waits window by window."""
+    import time
+
+    t0 = time.monotonic()
+    with _prefetch_lock:
+        entry = _prefetched.get(path)
+    if entry is None:
+        return None
+    thread, box = entry
+    if thread is not None:  # early_prefetch(): registered whole when its thread is done
+        thread.join(timeout)
+    region = box.get("region")
+    if region is None:
+        return None
+    pinner = region.pinner
+    if pinner:
+        lib = hip()
+        while lib.tpi_host_pin_ready(pinner) < region.size:
+            if (cancel is not None and cancel.is_set()) or time.monotonic() - t0 > timeout:
+                return None
+            time.sleep(poll)
+    return time.monotonic() - t0
+
+
 def adopt(path: str, size: int) -> Optional[HostRegion]:
     """The prefetched region of ``path`` if it has exactly ``size`` bytes (waits for it)."""
     with _prefetch_lock:

@@ -398,12 +398,25 @@ def standby(prefetch_path: Optional[str] = None, materialize: bool = False) -> b
 
         prewarm_engine(torch.cuda.current_device())
     if prefetch_path:
-        from .host import prefetch, watch_prefetch
+        from .host import prefetch, wait_pinned, watch_prefetch
 
         if not prefetch(prefetch_path):
             # hot standby (started with the rank): the spill file appears later; map and pin
             # it then, long before a preemption
             watch_prefetch(prefetch_path, cancel)
+
+        def pinned():  # journal when the whole spill is pinned: from then on a restore
+            # never waits for a window (bench/bench_preempt.py waits for this)
+            t0 = time.monotonic()
+            while not cancel.is_set():
+                took = wait_pinned(prefetch_path, cancel=cancel)
+                if took is not None:
+                    journal("standby-pinned", "%.1f GB" % (os.path.getsize(prefetch_path) / 1e9),
+                            "%.3f s after standby()" % (time.monotonic() - t0))
+                    return
+                cancel.wait(0.05)
+
+        threading.Thread(target=pinned, name="tpi-standby-pinned", daemon=True).start()
     fd = int(os.environ.get("TPI_STANDBY_FD", "4"))
     while True:
         try:
