@@ -562,3 +562,9 @@ def test_preemption_materialize_journals_and_tells_the_supervisor(tmp_path, monk
         os.close(wfd)
     text = events.read_text()
     assert "checkpoint-restored" in text and "materialized in 5 groups" in text
+
+
+def test_wait_pinned_without_a_prefetch_returns_none(tmp_path):
+    from terraform_provider_iterative_amd.checkpoint.host import wait_pinned
+
+    assert wait_pinned(str(tmp_path / "never-prefetched.spill"), timeout=0.1) is None
