@@ -39,6 +39,9 @@ def main():
     p.add_argument("--sleep", type=float, default=0.0, help="sleep per step (tests)")
     p.add_argument("--ckpt-every", type=int, default=0,
                    help="asynchronous checkpoint every N steps (0: only on SIGTERM/exit)")
+    p.add_argument("--materialize", action="store_true",
+                   help="resume by materializing the state from the spill (the model is built "
+                        "on the meta device; for ranks bigger than half of HBM; one rank)")
     args = p.parse_args()
     # first log line before the framework import (~0.5-1.5 s): the task is visibly running
     # while torch loads and the runtime stages the workdir (attach() waits for it below)
@@ -61,7 +64,8 @@ def main():
     spill = os.path.join(data_dir, ".ckpt-rank%d" % rank)
     # warm standby: a successor started while its preempted predecessor is still spilling waits
     # here (torch imported, GPU up, spill region being mapped) until the supervisor activates it
-    preemption.standby(spill if device.type == "cuda" else None)
+    materialize = args.materialize and device.type == "cuda" and world == 1
+    preemption.standby(spill if device.type == "cuda" else None, materialize=materialize)
     if world > 1:
         dist.init_process_group("nccl" if device.type == "cuda" else "gloo",
                                 **({"device_id": device} if device.type == "cuda" else {}))
@@ -92,31 +96,46 @@ def main():
 
     torch.manual_seed(1234)
     h = args.hidden
-    layers = []
-    for _ in range(args.layers):
-        layers += [torch.nn.LayerNorm(h), torch.nn.Linear(h, 4 * h), torch.nn.GELU(),
-                   torch.nn.Linear(4 * h, h)]
-    model = torch.nn.Sequential(*layers).to(device=device, dtype=torch.bfloat16)
-    opt = torch.optim.AdamW(model.parameters(), lr=1e-4)
-    if world > 1:
-        model = torch.nn.parallel.DistributedDataParallel(model)
-    step_t = torch.zeros((), dtype=torch.int64, device=device)
 
-    # Optimizer state must exist before it can be checkpointed: one warm step on zeros.
-    x = torch.zeros(args.batch, args.seq, h, device=device, dtype=torch.bfloat16)
-    model(x).float().pow(2).mean().backward()
-    opt.step()
-    opt.zero_grad(set_to_none=False)
+    def build():
+        layers = []
+        for _ in range(args.layers):
+            layers += [torch.nn.LayerNorm(h), torch.nn.Linear(h, 4 * h), torch.nn.GELU(),
+                       torch.nn.Linear(4 * h, h)]
+        return torch.nn.Sequential(*layers)
+
+    def make_opt(m):
+        return torch.optim.AdamW(m.parameters(), lr=1e-4)
+
     # the batch generator: part of the checkpoint, so a resumed run draws the batches the
     # uninterrupted one would have (not the first batches again)
     gen = torch.Generator(device=device).manual_seed(rank + 7)
-    # model + optimizer device state by reference; CPU-side Adam step counters, the optimizer
-    # hyper-parameters, every RNG and `gen` ride in the checkpoint header
-    state = TrainingState(model, opt, extra={"step": step_t}, path=spill,
-                          generators={"data": gen})
+    got = preemption.materialize(spill, device) if materialize else None
+    if got is not None:
+        # the state is created while it streams in from the predecessor: no up-front
+        # allocation of a model that would not fit next to the predecessor's
+        with torch.device("meta"):
+            model = build().to(torch.bfloat16)
+        state = TrainingState.from_materialized(got, model, make_opt, generators={"data": gen})
+        opt, step_t, meta = state.optimizer, got[1]["extra.step"], got[2]
+    else:
+        model = build().to(device=device, dtype=torch.bfloat16)
+        opt = make_opt(model)
+        if world > 1:
+            model = torch.nn.parallel.DistributedDataParallel(model)
+        step_t = torch.zeros((), dtype=torch.int64, device=device)
+        # Optimizer state must exist before it can be checkpointed: one warm step on zeros.
+        x = torch.zeros(args.batch, args.seq, h, device=device, dtype=torch.bfloat16)
+        model(x).float().pow(2).mean().backward()
+        opt.step()
+        opt.zero_grad(set_to_none=False)
+        # model + optimizer device state by reference; CPU-side Adam step counters, the
+        # optimizer hyper-parameters, every RNG and `gen` ride in the checkpoint header
+        state = TrainingState(model, opt, extra={"step": step_t}, path=spill,
+                              generators={"data": gen})
+        # ranks agree on the step to resume from (or all start fresh)
+        meta = state.resume_consistent() if world > 1 else state.resume()
     ck = state.checkpointer
-    # ranks agree on the step to resume from (or all start fresh)
-    meta = state.resume_consistent() if world > 1 else state.resume()
     start = int(step_t.item())
     log("resumed from step %d" % start if meta else "fresh start")
     state.install()

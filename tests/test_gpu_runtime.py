@@ -75,13 +75,19 @@ def test_mi355x_task_sees_its_gpu(cloud):
     task.delete()
 
 
-def test_preempt_resume_training_on_gpu(cloud, tmp_path):
+@pytest.mark.parametrize("materialize", [False, True])
+def test_preempt_resume_training_on_gpu(cloud, tmp_path, materialize):
+    """examples/train/train.py preempted mid-run resumes from its checkpoint; with
+    --materialize the successor builds its model on the meta device and resumes around the
+    materialized tensors (TrainingState.from_materialized)."""
     env = {"TPI_FRAMEWORK_ROOT": ROOT, "TPI_TASK": "true"}
     script = ("#!/bin/sh\nexec %s %s/examples/train/train.py --steps 60 --hidden 256 --layers 2 "
-              "--batch 4 --seq 64 --sleep 0.05\n" % (sys.executable, ROOT))
+              "--batch 4 --seq 64 --sleep 0.05%s\n" % (sys.executable, ROOT,
+                                                       " --materialize" if materialize else ""))
     spec = Task(size=Size(machine="m+mi355x"),
                 environment=Environment(script=script, timeout=600, variables=Variables(env)))
-    task = backends.new(cloud, new_deterministic_identifier("gpu-preempt"), spec)
+    task = backends.new(cloud, new_deterministic_identifier("gpu-preempt-%d" % materialize),
+                        spec)
     task.create()
     deadline = time.time() + 300
     while time.time() < deadline and not any("step 11" in l for l in task.logs()):
