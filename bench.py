@@ -77,9 +77,10 @@ def parse_args(argv=None):
                    help="restore after the save instead of streaming behind it")
     p.add_argument("--spill-dir", default="/dev/shm",
                    help="where the host region lives (shared by saver and restorer)")
-    p.add_argument("--allow-remote-numa", action="store_true",
-                   help="measure even when a rank's host region is not on its GPU's socket "
-                        "(default: fail before the timed steps)")
+    p.add_argument("--strict-numa", action="store_true",
+                   help="stop before the timed steps (exit 4) when a rank's host region is not "
+                        "on its GPU's socket (default: warn, measure, and name the ranks in "
+                        "rank_placement.remote_numa_ranks)")
     p.add_argument("--device", choices=("cuda", "cpu"), default="cuda",
                    help="cpu: rehearse the multi-rank control flow on CPU tensors over gloo "
                         "(tests; not a measurement of the MI355X path)")
@@ -367,11 +368,13 @@ def main(argv=None):
 
     placements = gather(mine)
     _, numa_problems = region_placement_report(placements)
-    if numa_problems and not args.allow_remote_numa:
+    if numa_problems:
         if rank == 0:
-            print("bench: host regions off their GPU's socket (--allow-remote-numa to measure "
-                  "anyway): " + "; ".join(numa_problems), file=sys.stderr, flush=True)
-        raise SystemExit(4)
+            print("bench: WARNING: host regions off their GPU's socket (their copies also "
+                  "cross the inter-socket link): " + "; ".join(numa_problems), file=sys.stderr,
+                  flush=True)
+        if args.strict_numa:
+            raise SystemExit(4)
     barrier()
 
     fault = os.environ.get("TPI_BENCH_FAULT", "")
