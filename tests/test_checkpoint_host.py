@@ -568,3 +568,40 @@ def test_wait_pinned_without_a_prefetch_returns_none(tmp_path):
     from terraform_provider_iterative_amd.checkpoint.host import wait_pinned
 
     assert wait_pinned(str(tmp_path / "never-prefetched.spill"), timeout=0.1) is None
+
+
+def test_materialize_on_host_waits_for_a_streamed_save_to_complete(tmp_path):
+    """Host tensors: materialize() of a region whose writer is still streaming waits for the
+    writer's completion (no device engine to restore behind it), then restores."""
+    import threading
+
+    from terraform_provider_iterative_amd.checkpoint import checkpointer as ckmod
+
+    path = str(tmp_path / "spill.bin")
+    src = _model(8)
+    writer = Checkpointer(src, path=path, tile_bytes=4096)
+    writer.save({"step": 4})
+    slot = writer.slots[0]
+    header = writer.header()
+    header.update(complete=False, streaming=True)
+    writer._write_header(slot, header)
+    prog = slot.progress
+    prog[1], prog[2], prog[3], prog[4] = header["generation"], 0, 0, ckmod.STREAM_RUNNING
+    prog[5] = os.getpid()
+    prog[0] = ckmod.PROGRESS_MAGIC
+    box = {}
+    th = threading.Thread(target=lambda: box.update(out=Checkpointer.materialize(
+        path, "cpu", group_bytes=1, stream_timeout=20)))
+    th.start()
+    time.sleep(0.3)
+    assert th.is_alive()  # still waiting for the writer
+    prog[2] = writer.plan.ntiles
+    header.update(complete=True, streaming=False)
+    writer._write_header(slot, header)
+    prog[4] = ckmod.STREAM_COMPLETE
+    th.join(30)
+    ck, tensors, res = box["out"]
+    assert res.bad_tiles == 0 and not ck.materialize_stats["streamed"]
+    assert all(torch.equal(tensors[k], src[k]) for k in src)
+    ck.close()
+    writer.close()
