@@ -248,6 +248,7 @@ class DeviceEngine:
 
 
 PREWARM_SEGS, PREWARM_TILES = 4096, 1 << 18
+ALLOC_HEADROOM = 512 << 20  # materialize(): free HBM beyond a tensor's size before allocating it
 
 # Engines created ahead of the Checkpointer that takes them (prewarm_engine).
 _engine_pool: Dict[Tuple[int, int, int, int], List[DeviceEngine]] = {}
@@ -1221,6 +1222,18 @@ class Checkpointer:
                         while True:
                             if stop.is_set():
                                 return
+                            # ask before allocating: a hipMalloc that has to wait for memory
+                            # the predecessor is still freeing blocks for up to a second
+                            # inside the HIP runtime, and holds up this process's
+                            # hipMemcpyAsync calls -- the restore's -- all that time (HIP API
+                            # trace, profiles/round4/materialize_170g.md)
+                            if (dev.type == "cuda" and time.monotonic() - last <= memory_timeout
+                                    and torch.cuda.mem_get_info(dev)[0]
+                                    < e.nbytes + ALLOC_HEADROOM):
+                                t = time.monotonic()
+                                stop.wait(0.002)
+                                waited[0] += time.monotonic() - t
+                                continue
                             try:
                                 out.append(empty(e))
                                 break
