@@ -249,6 +249,7 @@ class DeviceEngine:
 
 PREWARM_SEGS, PREWARM_TILES = 4096, 1 << 18
 ALLOC_HEADROOM = 512 << 20  # materialize(): free HBM beyond a tensor's size before allocating it
+ALLOC_LOOKAHEAD = 3  # materialize(): groups allocated ahead of the restore once HBM runs short
 
 # Engines created ahead of the Checkpointer that takes them (prewarm_engine).
 _engine_pool: Dict[Tuple[int, int, int, int], List[DeviceEngine]] = {}
@@ -1210,11 +1211,29 @@ class Checkpointer:
                 like = likes[e.dtype] = torch.empty(0, dtype=dtype, device=dev)
             return empty_nogil(list(e.shape), like)
 
+        restored = [0]  # groups restored so far (the main thread counts)
+        # groups that fit in the HBM free right now are allocated at once; the rest -- memory
+        # the predecessor has yet to free -- only ALLOC_LOOKAHEAD groups ahead of the restore:
+        # by then that memory has long been freed, and its hipMalloc does not block the
+        # restore's copies (see the gate below)
+        budget = (torch.cuda.mem_get_info(dev)[0] - ALLOC_HEADROOM) if dev.type == "cuda" \
+            else float("inf")
+        upfront = 0
+        for lo, hi in groups:
+            size = sum(e.nbytes for e in entries[lo:hi])
+            if size > budget:
+                break
+            budget -= size
+            upfront += 1
+
         def allocate():  # runs ahead of the restores, as far as the device has room
             try:
                 if dev.type == "cuda":
                     torch.cuda.set_device(dev)
-                for lo, hi in groups:
+                for gi, (lo, hi) in enumerate(groups):
+                    while (gi >= upfront and restored[0] + ALLOC_LOOKAHEAD < gi
+                           and not stop.is_set()):
+                        stop.wait(0.002)
                     out = []
                     t_group = time.perf_counter()
                     for e in entries[lo:hi]:
@@ -1313,6 +1332,7 @@ class Checkpointer:
                         total.first_bad = ta + res.first_bad
                 for e, t in zip(entries[lo:hi], item):
                     tensors[e.name] = t
+                restored[0] = gi + 1
                 trace[gi] += [
                     round(t_group - t_start, 4), round(time.perf_counter() - t_start, 4)]
         finally:
@@ -1323,7 +1343,8 @@ class Checkpointer:
         total.crc = int(header.get("crc32c", 0)) if not streaming else \
             native().crc32c_combine_tiles_ptr(slot.crcs.ctypes.data, self.plan.ntiles,
                                               self.plan.tile_bytes, self.plan.total)
-        self.materialize_stats = {"groups": len(groups), "alloc_wait_s": round(waited[0], 4),
+        self.materialize_stats = {"groups": len(groups), "upfront_groups": upfront,
+                                  "alloc_wait_s": round(waited[0], 4),
                                   "streamed": streaming, "trace": trace, "setup": setup,
                                   "alloc": "nogil" if empty_nogil is not None else "torch"}
         self.materialized_metadata = header.get("metadata", {})
