@@ -1174,10 +1174,18 @@ class Checkpointer:
             raise CheckpointError("no checkpoint to materialize in %s" % self.path)
         slot, header = found
         self._check_compatible(header)
+        early_fallback = None
         if streaming and self.engine is None:
             streaming = False  # host tensors: wait for the whole spill first
-            self._restore_streaming_wait(slot, stream_timeout)
-            header = self._slot_header(slot) or header
+            try:
+                self._restore_streaming_wait(slot, stream_timeout)
+                header = self._slot_header(slot) or header
+            except CheckpointError as error:  # a two-slot region's older copy, if any
+                older = self._active()
+                if older is None:
+                    raise
+                slot, header = older
+                early_fallback = str(error)
         zipped = header.get("codec", "none") == "tpz1"
         if stream_timeout is None:
             stream_timeout = float(os.environ.get("TPI_STREAM_TIMEOUT", "30"))
@@ -1280,56 +1288,89 @@ class Checkpointer:
         worker = threading.Thread(target=allocate, name="tpi-materialize-alloc", daemon=True)
         worker.start()
         tensors: Dict[str, Any] = {}
-        stream_base = self.region.addr + slot.base + self.stream_offset
         total = TransferResult(self.plan.total, 0.0, wire_bytes=0)
+        src = {"slot": slot, "header": header, "zipped": zipped, "streaming": streaming}
+        done: List[Tuple[int, int, List[Any]]] = []  # restored groups, for a fallback
+        fallback = early_fallback
+
+        def restore_group(lo: int, hi: int, item: List[Any]) -> TransferResult:
+            slot, zipped = src["slot"], src["zipped"]
+            sub, ta, tb = self._sub_plan(lo, hi, item, lead)
+            crcs = slot.crcs[ta:tb]
+            csizes = slot.csizes[ta:tb] if zipped else None
+            # earlier tiles are in host memory: the previous group waited for them
+            start = int(slot.csizes[:ta].sum(dtype=np.uint64)) if zipped \
+                else ta * self.plan.tile_bytes
+            stream_base = self.region.addr + slot.base + self.stream_offset
+            if self.engine is not None:
+                sig = torch.cuda.current_stream(dev).cuda_stream
+                if src["streaming"]:
+                    from ..ops._loader import HipError
+
+                    try:
+                        res = self.engine.restore_stream(
+                            sub, stream_base + start, crcs, csizes,
+                            slot.progress.ctypes.data + 16, stream_timeout, sig, tile_base=ta)
+                    except HipError as error:
+                        raise CheckpointError(str(error)) from error
+                elif zipped:
+                    res = self.engine.restore_z(sub, stream_base + start, crcs, csizes, sig)
+                else:
+                    res = self.engine.restore(sub, stream_base + start, crcs, self.mode, sig)
+            else:
+                t0 = time.perf_counter()
+                if zipped:
+                    nbytes = int(csizes.sum(dtype=np.uint64))
+                    stream, _ = tpz.decode(self.region.array(
+                        slot.base + self.stream_offset + start, nbytes),
+                        csizes, sub.total, self.plan.tile_bytes)
+                else:
+                    nbytes = sub.total
+                    stream = self.region.array(slot.base + self.stream_offset + start,
+                                               sub.total)
+                bad, first = host_unpack(sub, stream, crcs)
+                res = TransferResult(sub.total, time.perf_counter() - t0, 0, bad, first,
+                                     wire_bytes=nbytes)
+            if res.bad_tiles:
+                res.first_bad += ta
+            return res
+
         try:
             for gi, (lo, hi) in enumerate(groups):
                 item = ready.get()
                 if isinstance(item, BaseException):
                     raise item
                 t_group = time.perf_counter()
-                sub, ta, tb = self._sub_plan(lo, hi, item, lead)
-                crcs = slot.crcs[ta:tb]
-                csizes = slot.csizes[ta:tb] if zipped else None
-                # earlier tiles are in host memory: the previous group waited for them
-                start = int(slot.csizes[:ta].sum(dtype=np.uint64)) if zipped \
-                    else ta * self.plan.tile_bytes
-                if self.engine is not None:
-                    sig = torch.cuda.current_stream(dev).cuda_stream
-                    if streaming:
-                        from ..ops._loader import HipError
-
-                        try:
-                            res = self.engine.restore_stream(
-                                sub, stream_base + start, crcs, csizes,
-                                slot.progress.ctypes.data + 16, stream_timeout, sig,
-                                tile_base=ta)
-                        except HipError as error:
-                            raise CheckpointError(str(error)) from error
-                    elif zipped:
-                        res = self.engine.restore_z(sub, stream_base + start, crcs, csizes, sig)
-                    else:
-                        res = self.engine.restore(sub, stream_base + start, crcs, self.mode, sig)
-                else:
-                    t0 = time.perf_counter()
-                    if zipped:
-                        nbytes = int(csizes.sum(dtype=np.uint64))
-                        stream, _ = tpz.decode(self.region.array(
-                            slot.base + self.stream_offset + start, nbytes),
-                            csizes, sub.total, self.plan.tile_bytes)
-                    else:
-                        nbytes = sub.total
-                        stream = self.region.array(slot.base + self.stream_offset + start,
-                                                   sub.total)
-                    bad, first = host_unpack(sub, stream, crcs)
-                    res = TransferResult(sub.total, time.perf_counter() - t0, 0, bad, first,
-                                         wire_bytes=nbytes)
+                try:
+                    res = restore_group(lo, hi, item)
+                except CheckpointError as error:
+                    # the predecessor's streamed save failed (or its writer died): fall back
+                    # to the complete copy a two-slot region still holds -- every group
+                    # again, so the state is one generation throughout
+                    older = self._active() if src["streaming"] else None
+                    if older is None:
+                        raise
+                    self._check_compatible(older[1])
+                    fallback = str(error)
+                    src.update(slot=older[0], header=older[1], streaming=False,
+                               zipped=older[1].get("codec", "none") == "tpz1")
+                    total = TransferResult(self.plan.total, 0.0, wire_bytes=0)
+                    for lo2, hi2, item2 in done:
+                        again = restore_group(lo2, hi2, item2)
+                        total.chunks += again.chunks
+                        total.wire_bytes += again.wire_bytes
+                        if again.bad_tiles:
+                            total.bad_tiles += again.bad_tiles
+                            total.first_bad = again.first_bad if total.first_bad < 0 \
+                                else total.first_bad
+                    res = restore_group(lo, hi, item)
                 total.chunks += res.chunks
                 total.wire_bytes += res.wire_bytes
                 if res.bad_tiles:
                     total.bad_tiles += res.bad_tiles
                     if total.first_bad < 0:
-                        total.first_bad = ta + res.first_bad
+                        total.first_bad = res.first_bad
+                done.append((lo, hi, item))
                 for e, t in zip(entries[lo:hi], item):
                     tensors[e.name] = t
                 restored[0] = gi + 1
@@ -1338,6 +1379,7 @@ class Checkpointer:
         finally:
             stop.set()
             worker.join()
+        slot, header, streaming = src["slot"], src["header"], src["streaming"]
         self.plan.bind(tensors)
         total.seconds = time.perf_counter() - t_start
         total.crc = int(header.get("crc32c", 0)) if not streaming else \
@@ -1346,6 +1388,7 @@ class Checkpointer:
         self.materialize_stats = {"groups": len(groups), "upfront_groups": upfront,
                                   "alloc_wait_s": round(waited[0], 4),
                                   "streamed": streaming, "trace": trace, "setup": setup,
+                                  "fallback": fallback,
                                   "alloc": "nogil" if empty_nogil is not None else "torch"}
         self.materialized_metadata = header.get("metadata", {})
         self.last_restore = total

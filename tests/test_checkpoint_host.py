@@ -605,3 +605,38 @@ def test_materialize_on_host_waits_for_a_streamed_save_to_complete(tmp_path):
     assert all(torch.equal(tensors[k], src[k]) for k in src)
     ck.close()
     writer.close()
+
+
+def test_materialize_falls_back_to_the_older_copy_when_the_stream_fails(tmp_path):
+    """slots=2: the predecessor's streamed save of generation 2 fails; materialize() restores
+    generation 1, the complete copy the region still holds (and says so)."""
+    import threading
+
+    from terraform_provider_iterative_amd.checkpoint import checkpointer as ckmod
+
+    path = str(tmp_path / "spill.bin")
+    src = _model(9)
+    ref = {k: v.clone() for k, v in src.items()}
+    writer = Checkpointer(src, path=path, tile_bytes=4096, slots=2)
+    writer.save({"step": 1})
+    slot, generation = writer._target()  # the slot a second save would stream into
+    header = writer._header(False, 0, {"step": 2}, "none", None, generation)
+    header["streaming"] = True
+    writer._write_header(slot, header)
+    prog = slot.progress
+    prog[1], prog[2], prog[3], prog[4] = generation, 0, 0, ckmod.STREAM_RUNNING
+    prog[5] = os.getpid()
+    prog[0] = ckmod.PROGRESS_MAGIC
+    box = {}
+    th = threading.Thread(target=lambda: box.update(out=Checkpointer.materialize(
+        path, "cpu", group_bytes=1, stream_timeout=20)))
+    th.start()
+    time.sleep(0.3)
+    prog[4] = ckmod.STREAM_FAILED
+    th.join(30)
+    ck, tensors, res = box["out"]
+    assert res.bad_tiles == 0 and ck.materialized_metadata["step"] == 1
+    assert "failed" in ck.materialize_stats["fallback"]
+    assert all(torch.equal(tensors[k], ref[k]) for k in ref)
+    ck.close()
+    writer.close()

@@ -805,3 +805,58 @@ print(json.dumps(out))
         assert proc.returncode == 0, (mode, proc.stderr[-2000:])
         seen[mode] = proc.stdout.strip().splitlines()[-1]
     assert len(set(seen.values())) == 1, seen
+
+
+def test_materialize_falls_back_when_the_writers_stream_fails(tmp_path):
+    """Device path: the predecessor's streamed save of generation 2 fails after publishing
+    some tiles; materialize() re-restores every group from generation 1, the complete copy a
+    two-slot region still holds, so the state is one generation throughout."""
+    import threading
+    import time
+
+    from terraform_provider_iterative_amd.checkpoint import Checkpointer
+    from terraform_provider_iterative_amd.checkpoint import checkpointer as ckmod
+
+    g = torch.Generator().manual_seed(13)
+    src = {"a": torch.randn(3 << 20, generator=g).cuda(),
+           "b": torch.randn(5 << 20, generator=g).to(torch.bfloat16).cuda()}
+    ref = {k: v.clone() for k, v in src.items()}
+    path = str(tmp_path / "spill")
+    kw = dict(tile_bytes=1 << 16, chunk_bytes=1 << 20, nbuf=2, codec="tpz1", slots=2)
+    writer = Checkpointer(src, path=path, **kw)
+    writer.save({"step": 1})  # generation 1, complete
+    for v in src.values():
+        v.mul_(-1)
+    writer.save({"step": 2})  # generation 2 ...
+    slot, header = writer._active()
+    header.update(complete=False, streaming=True)  # ... turned back into a stream
+    writer._write_header(slot, header)
+    prog = slot.progress
+    prog[1], prog[2], prog[3], prog[4] = header["generation"], 0, 0, ckmod.STREAM_RUNNING
+    prog[5] = os.getpid()
+    prog[0] = ckmod.PROGRESS_MAGIC
+    box = {}
+
+    def successor():
+        try:
+            box["out"] = Checkpointer.materialize(path, "cuda", group_bytes=4 << 20,
+                                                  stream_timeout=20, chunk_bytes=1 << 20, nbuf=2)
+        except BaseException as error:  # surfaced below
+            box["err"] = error
+
+    th = threading.Thread(target=successor)
+    th.start()
+    time.sleep(0.2)
+    prog[2] = 40  # some tiles of generation 2 arrive, then the writer fails
+    time.sleep(0.2)
+    prog[4] = ckmod.STREAM_FAILED
+    th.join(60)
+    assert "err" not in box, box.get("err")
+    ck, tensors, res = box["out"]
+    assert res.bad_tiles == 0 and ck.materialized_metadata["step"] == 1
+    assert ck.materialize_stats["fallback"]
+    torch.cuda.synchronize()
+    for k in ref:
+        assert torch.equal(tensors[k], ref[k]), k
+    ck.close()
+    writer.close()
