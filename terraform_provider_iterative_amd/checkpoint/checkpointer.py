@@ -1234,12 +1234,14 @@ class Checkpointer:
             budget -= size
             upfront += 1
 
+        lookahead = int(os.environ.get("TPI_ALLOC_LOOKAHEAD", ALLOC_LOOKAHEAD))
+
         def allocate():  # runs ahead of the restores, as far as the device has room
             try:
                 if dev.type == "cuda":
                     torch.cuda.set_device(dev)
                 for gi, (lo, hi) in enumerate(groups):
-                    while (gi >= upfront and restored[0] + ALLOC_LOOKAHEAD < gi
+                    while (gi >= upfront and restored[0] + lookahead < gi
                            and not stop.is_set()):
                         stop.wait(0.002)
                     out = []
