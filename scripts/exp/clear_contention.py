@@ -12,7 +12,6 @@ engine.  Prints one JSON line.
 """
 import argparse
 import json
-import os
 import subprocess
 import sys
 import time

@@ -1,5 +1,5 @@
 """Experiment: what a 100 GB rank's exit and a successor's host-region setup cost."""
-import ctypes, json, os, subprocess, sys, time
+import json, os, subprocess, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 GB = float(os.environ.get("GB", "100"))
