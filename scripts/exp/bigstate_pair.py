@@ -104,6 +104,8 @@ def main():
     p.add_argument("--gb", type=float, default=170.0)
     p.add_argument("--mode", choices=("materialize", "upfront"), default="materialize")
     p.add_argument("--spill", default="/dev/shm/tpi-bigstate-pair-%d.spill" % os.getpid())
+    p.add_argument("--successor-env", action="append", default=[], metavar="KEY=VALUE",
+                   help="environment of the successor only (e.g. HSA_ENABLE_SDMA=0)")
     p.add_argument("--racing", action="store_true",
                    help="the successor starts restoring while it is still pinning the spill")
     args = p.parse_args()
@@ -115,9 +117,11 @@ def main():
     succ = None
     try:
         assert pred.stdout.readline().strip() == "ready"
+        succ_env = dict(env, **dict(kv.split("=", 1) for kv in args.successor_env))
         succ = subprocess.Popen([sys.executable, "-c", SUCC % sub, str(args.gb), str(t0),
                                  args.mode] + (["--racing"] if args.racing else []),
-                                stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=env)
+                                stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True,
+                                env=succ_env)
         assert succ.stdout.readline().strip() == "ready"
         t_sig = time.time()
         pred.stdin.write("\n")
