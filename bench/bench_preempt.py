@@ -179,7 +179,7 @@ def main():
     for knob in ("TPI_D2H_ENGINE", "TPI_STREAM_TIMEOUT", "TPI_LINGER_SECONDS",
                  "TPI_HBM_HANDOFF", "TPI_RELEASE_HBM", "TPI_EXPLICIT_TEARDOWN",
                  "HSA_ENABLE_SDMA", "GPU_MAX_HW_QUEUES", "TPI_DIRECT_META",
-                 "TPI_ALLOC_LOOKAHEAD"):
+                 "TPI_ALLOC_LOOKAHEAD", "TPI_MATERIALIZE_H2D"):
         if os.environ.get(knob):
             rank_env[knob] = os.environ[knob]
     spec = Task(size=Size(machine="m+mi355x"),

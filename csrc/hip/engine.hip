@@ -233,6 +233,10 @@ struct tpi_engine {
   // D2H on an SDMA engine (sdma.cpp), one lane per staging buffer + one for direct spills;
   // nullptr = hipMemcpyAsync on the copy stream (TPI_D2H_ENGINE=blit, or no engine)
   tpi_sdma* sdma = nullptr;
+  // H2D of streamed restores on an SDMA engine of their own (tpi_engine_set_h2d_sdma), host
+  // driven like the saves' D2H: off HIP's H2D engine, which the driver's clears of freed HBM
+  // share (profiles/round4/materialize_170g.md); nullptr = hipMemcpyAsync
+  tpi_sdma* sdma_in = nullptr;
   // streaming hand-off: a save publishes {tiles, stream bytes} already in host memory here
   // (tpi_engine_set_progress); a reader in another process restores behind it
   uint64_t* progress = nullptr;
@@ -303,6 +307,23 @@ int sdma_region_d2h(tpi_engine* e, int lane, void* dst, const void* src, size_t 
       return fail("host region pinning failed");
     if (tpi_sdma_d2h(e->sdma, lane, (uint8_t*)dst + done, (const uint8_t*)src + done, len))
       return -1;
+    done += len;
+  }
+  return 0;
+}
+
+// H2D of one piece on the restore's SDMA lane `lane`, split at pinned-window boundaries.
+int sdma_region_h2d(tpi_engine* e, int lane, void* dst, const void* src, size_t n) {
+  const uint8_t* h = (const uint8_t*)src;
+  if (!e->hwin || h < e->hbase || h >= e->hbase + e->hbytes)
+    return tpi_sdma_h2d(e->sdma_in, lane, dst, src, n);
+  uint64_t off = (uint64_t)(h - e->hbase), done = 0;
+  while (done < n) {
+    const uint64_t at = off + done;
+    const uint64_t len = std::min<uint64_t>(n - done, (at / e->hwin + 1) * e->hwin - at);
+    if (e->pinner && !wait_pinned(e->pinner, std::min(e->hbytes, at + len)))
+      return fail("host region pinning failed");
+    if (tpi_sdma_h2d(e->sdma_in, lane, (uint8_t*)dst + done, h + done, len)) return -1;
     done += len;
   }
   return 0;
@@ -535,6 +556,7 @@ void tpi_engine_destroy(tpi_engine* e) {
   if (e->aux) (void)hipStreamSynchronize(e->aux);
   if (e->copy2) (void)hipStreamSynchronize(e->copy2);
   tpi_sdma_close(e->sdma);  // waits for copies still in flight
+  tpi_sdma_close(e->sdma_in);
   for (void* p : e->staging)
     if (p) (void)hipFree(p);
   for (hipEvent_t ev : e->ev_a)
@@ -1403,6 +1425,17 @@ int tpi_engine_reserve(tpi_engine* e, int nsegs, uint64_t ntiles, int codec) {
   return 0;
 }
 
+int tpi_engine_set_h2d_sdma(tpi_engine* e, int on) {
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (!on) {
+    tpi_sdma_close(e->sdma_in);
+    e->sdma_in = nullptr;
+    return 0;
+  }
+  if (!e->sdma_in) e->sdma_in = tpi_sdma_open_h2d(e->device, e->nbuf);
+  return e->sdma_in ? (int)(31 - __builtin_clz(tpi_sdma_engine(e->sdma_in))) : -1;
+}
+
 int tpi_engine_set_progress(tpi_engine* e, uint64_t* words) {
   std::lock_guard<std::mutex> lk(e->mu);
   e->progress = words;
@@ -1471,6 +1504,33 @@ int tpi_restore_stream_at(tpi_engine* e, const tpi_seg* segs, int n, uint64_t to
   const uint64_t chunk_tiles = e->chunk / tile;
   std::vector<bool> was_split(e->nbuf, false);
   e->split_chunks = 0;
+  // H2D on the engine's own SDMA lanes (tpi_engine_set_h2d_sdma): the host issues chunk k's
+  // copy, then waits for chunk k-1's and queues its kernels (a HIP stream cannot wait on the
+  // lane's signal); needs two staging buffers at least
+  const bool sdma_in = e->sdma_in != nullptr && e->nbuf >= 2;
+  struct Pending {
+    bool valid;
+    int b;
+    uint64_t base, len, t0i, cbeg;
+  } pending{false, 0, 0, 0, 0, 0};
+  auto kernels = [&](const Pending& c) -> int {
+    if (!direct) HIP_OK(hipStreamWaitEvent(e->compute, e->ev_c[c.b], 0));
+    if (zipped) {
+      HIP_OK(tpi_launch_tpz_decode(e->staging[c.b], (direct ? coff_host : e->d_coff) + c.t0i,
+                                   c.cbeg, c.len, tile, e->zraw, e->compute));
+      HIP_OK(hipEventRecord(e->ev_b[c.b], e->compute));
+      HIP_OK(tpi_launch_stream_crc(1, e->d_segs, n, c.base, c.len, e->zraw, tile, e->tables,
+                                   crc_src, init_full, init_last, e->d_bad, 1, e->compute));
+      HIP_OK(tpi_launch_transposes(segs, n, c.base, c.len, e->zraw, 1, e->compute));
+    } else {
+      HIP_OK(tpi_launch_stream_crc(1, e->d_segs, n, c.base, c.len, e->staging[c.b], tile,
+                                   e->tables, crc_src, init_full, init_last, e->d_bad, 1,
+                                   e->compute));
+      HIP_OK(tpi_launch_transposes(segs, n, c.base, c.len, e->staging[c.b], 1, e->compute));
+      HIP_OK(hipEventRecord(e->ev_b[c.b], e->compute));
+    }
+    return 0;
+  };
   for (uint64_t base = 0, k = 0; base < total; base += e->chunk, ++k) {
     const int b = (int)(k % e->nbuf);
     const uint64_t len = std::min(e->chunk, total - base);
@@ -1481,13 +1541,14 @@ int tpi_restore_stream_at(tpi_engine* e, const tpi_seg* segs, int n, uint64_t to
       (void)hipStreamSynchronize(e->copy2);
       (void)hipStreamSynchronize(e->aux);
       (void)hipStreamSynchronize(e->compute);
+      if (sdma_in) (void)tpi_sdma_wait_all(e->sdma_in);
       return -1;
     }
     // How far the restore trails the writer.  The host may run at most nbuf chunks ahead of
     // the copies (wait for chunk k - nbuf's H2D), so the chunks published past this one are
     // the copies' real backlog.  A backlog of split_lead chunks means the save is taking the
     // larger share of the link: split this chunk's H2D over two streams (two SDMA engines).
-    if (k >= (uint64_t)e->nbuf) {
+    if (k >= (uint64_t)e->nbuf && !sdma_in) {
       HIP_OK(hipEventSynchronize(e->ev_a[b]));
       if (was_split[b]) HIP_OK(hipEventSynchronize(e->ev_d[b]));
     }
@@ -1519,6 +1580,23 @@ int tpi_restore_stream_at(tpi_engine* e, const tpi_seg* segs, int n, uint64_t to
                          hipMemcpyHostToDevice, e->aux));
       HIP_OK(hipEventRecord(e->ev_c[b], e->aux));
     }
+    if (sdma_in) {
+      // staging[b] is free once chunk k - nbuf's kernels have read it
+      if (k >= (uint64_t)e->nbuf) HIP_OK(hipEventSynchronize(e->ev_b[b]));
+      if (sdma_region_h2d(e, b, e->staging[b], src + cbeg, cend - cbeg)) {
+        (void)tpi_sdma_wait_all(e->sdma_in);
+        return -1;
+      }
+      if (pending.valid) {
+        if (tpi_sdma_wait(e->sdma_in, pending.b) || kernels(pending)) {
+          (void)tpi_sdma_wait_all(e->sdma_in);
+          return -1;
+        }
+      }
+      pending = Pending{true, b, base, len, t0i, cbeg};
+      nchunks = k + 1;
+      continue;
+    }
     if (k >= (uint64_t)e->nbuf) HIP_OK(hipStreamWaitEvent(e->copy, e->ev_b[b], 0));
     // halves split on a 64 KiB boundary of the wire stream (chunks under 128 KiB stay whole)
     const uint64_t mid = split && cend - cbeg >= (128ull << 10)
@@ -1535,22 +1613,15 @@ int tpi_restore_stream_at(tpi_engine* e, const tpi_seg* segs, int n, uint64_t to
       HIP_OK(hipStreamWaitEvent(e->compute, e->ev_d[b], 0));
       ++e->split_chunks;
     }
-    if (!direct) HIP_OK(hipStreamWaitEvent(e->compute, e->ev_c[b], 0));
     HIP_OK(hipStreamWaitEvent(e->compute, e->ev_a[b], 0));
-    if (zipped) {
-      HIP_OK(tpi_launch_tpz_decode(e->staging[b], (direct ? coff_host : e->d_coff) + t0i, cbeg,
-                                   len, tile, e->zraw, e->compute));
-      HIP_OK(hipEventRecord(e->ev_b[b], e->compute));
-      HIP_OK(tpi_launch_stream_crc(1, e->d_segs, n, base, len, e->zraw, tile, e->tables,
-                                   crc_src, init_full, init_last, e->d_bad, 1, e->compute));
-      HIP_OK(tpi_launch_transposes(segs, n, base, len, e->zraw, 1, e->compute));
-    } else {
-      HIP_OK(tpi_launch_stream_crc(1, e->d_segs, n, base, len, e->staging[b], tile, e->tables,
-                                   crc_src, init_full, init_last, e->d_bad, 1, e->compute));
-      HIP_OK(tpi_launch_transposes(segs, n, base, len, e->staging[b], 1, e->compute));
-      HIP_OK(hipEventRecord(e->ev_b[b], e->compute));
-    }
+    if (kernels(Pending{true, b, base, len, t0i, cbeg})) return -1;
     nchunks = k + 1;
+  }
+  if (sdma_in && pending.valid) {
+    if (tpi_sdma_wait(e->sdma_in, pending.b) || kernels(pending)) {
+      (void)tpi_sdma_wait_all(e->sdma_in);
+      return -1;
+    }
   }
   unsigned long long bad[2];
   HIP_OK(region_copy(e, bad, e->d_bad, sizeof(bad), hipMemcpyDeviceToHost, e->compute));

@@ -22,5 +22,9 @@ tpi_sdma* tpi_sdma_open(int device, int lanes);
 void tpi_sdma_close(tpi_sdma* s);
 uint32_t tpi_sdma_engine(const tpi_sdma* s);
 int tpi_sdma_d2h(tpi_sdma* s, int lane, void* host_dst, const void* dev_src, size_t n);
+// Host -> device lanes on an engine off HIP's own H2D engine and the saves' D2H engine
+// (TPI_H2D_ENGINE=sdma<i> pins one); nullptr when none is free.
+tpi_sdma* tpi_sdma_open_h2d(int device, int lanes);
+int tpi_sdma_h2d(tpi_sdma* s, int lane, void* dev_dst, const void* host_src, size_t n);
 int tpi_sdma_wait(tpi_sdma* s, int lane);
 int tpi_sdma_wait_all(tpi_sdma* s);

@@ -188,6 +188,58 @@ tpi_sdma* tpi_sdma_open(int device, int lanes) {
   return s;
 }
 
+// Host -> device lanes for a restore that must keep off the engines the runtime uses: the
+// H2D engine HIP itself would pick (preferred H2D, else engine 0, which the kernel driver's
+// own buffer clears share) and the D2H engine tpi_sdma_open picks for saves.
+// TPI_H2D_ENGINE=sdma<i> pins an engine.  nullptr when no such engine is free.
+tpi_sdma* tpi_sdma_open_h2d(int device, int lanes) {
+  const Hsa& h = hsa();
+  if (!h.ok) return nullptr;
+  hipDeviceProp_t p;
+  if (hipGetDeviceProperties(&p, device) != hipSuccess) return nullptr;
+  AgentQuery q;
+  q.bdf = (uint32_t)((p.pciBusID << 8) | (p.pciDeviceID << 3));
+  q.domain = (uint32_t)p.pciDomainID;
+  h.iterate_agents(match_agent, &q);
+  if (!q.found) return nullptr;
+  uint32_t avail = 0, pref = 0, h2d = 0;
+  if (h.engine_status(q.gpu, q.cpu, &avail) != HSA_STATUS_SUCCESS || !avail) return nullptr;
+  if (h.preferred_engine(q.cpu, q.gpu, &pref) != HSA_STATUS_SUCCESS) pref = 0;
+  if (h.preferred_engine(q.gpu, q.cpu, &h2d) != HSA_STATUS_SUCCESS) h2d = 0;
+  uint32_t d2h_pick = (pref & avail) ? (pref & avail) : (avail & 0xEu);
+  d2h_pick &= ~(h2d ? h2d : 0x1u);
+  const uint32_t d2h = d2h_pick ? 1u << (31 - __builtin_clz(d2h_pick)) : 0;
+  uint32_t pick = avail & 0xEu & ~(h2d ? h2d : 0x1u) & ~d2h;  // host-facing engines 1-3
+  uint32_t engine = pick ? (pick & (~pick + 1)) : 0;         // lowest candidate
+  const char* env = getenv("TPI_H2D_ENGINE");
+  if (env && strncmp(env, "sdma", 4) == 0 && env[4]) {
+    const int id = atoi(env + 4);
+    if (id >= 0 && id < 16 && (avail & (1u << id))) engine = 1u << id;
+  }
+  if (!engine) return nullptr;
+  tpi_sdma* s = new tpi_sdma();
+  s->gpu = q.gpu;
+  s->cpu = q.cpu;
+  s->engine = engine;
+  s->lanes.resize(lanes > 0 ? lanes : 1);
+  return s;
+}
+
+int tpi_sdma_h2d(tpi_sdma* s, int lane, void* dev_dst, const void* host_src, size_t n) {
+  if (!n) return 0;
+  hsa_signal_t sig;
+  if (take_signal(s, &sig)) return -1;
+  hsa_status_t st = hsa().copy_on_engine(dev_dst, s->gpu, host_src, s->cpu, n, 0, nullptr, sig,
+                                         (hsa_amd_sdma_engine_id_t)s->engine, true);
+  if (st != HSA_STATUS_SUCCESS) {
+    hsa().signal_add(sig, -1);
+    s->pool.push_back(sig);
+    return tpi_fail("hsa_amd_memory_async_copy_on_engine (H2D): " + hsa_error(st));
+  }
+  s->lanes[lane % s->lanes.size()].push_back(sig);
+  return 0;
+}
+
 void tpi_sdma_close(tpi_sdma* s) {
   if (!s) return;
   tpi_sdma_wait_all(s);

@@ -57,7 +57,7 @@ typedef struct tpi_stats {
 } tpi_stats;
 
 // Bumped whenever a signature below changes (ops/_loader.py checks it).
-#define TPI_ABI_VERSION 6
+#define TPI_ABI_VERSION 7
 
 // Library / device
 const char* tpi_last_error(void);
@@ -175,6 +175,10 @@ int tpi_host_pin_release(tpi_pinner* p);
 // words[1] = stream bytes in host memory, then words[0] = tiles whose bytes and CRCs (and
 // blob sizes) are there, both release-stored.  NULL stops publishing.
 int tpi_engine_set_progress(tpi_engine* e, uint64_t* words);
+// Streamed restores (tpi_restore_stream[_at]) copy host -> device on an SDMA engine of their
+// own, driven from the host (on != 0), instead of hipMemcpyAsync.  Returns the engine index,
+// or -1 when no engine is free (the restores then keep hipMemcpyAsync).
+int tpi_engine_set_h2d_sdma(tpi_engine* e, int on);
 // Allocate the buffers the pipelines would otherwise allocate on first use, for up to
 // `nsegs` segments and `ntiles` tiles (and the codec's decode buffers when `codec`).
 int tpi_engine_reserve(tpi_engine* e, int nsegs, uint64_t ntiles, int codec);

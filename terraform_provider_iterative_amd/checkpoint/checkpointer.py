@@ -175,6 +175,11 @@ class DeviceEngine:
         self.lib.check(self.lib.tpi_engine_reserve(self.handle, nsegs, ntiles, 1 if codec else 0),
                        "tpi_engine_reserve")
 
+    def set_h2d_sdma(self, on: bool) -> int:
+        """Streamed restores copy host -> device on an SDMA engine of their own (host
+        driven), off HIP's H2D engine; returns the engine index, -1 when none is free."""
+        return int(self.lib.tpi_engine_set_h2d_sdma(self.handle, 1 if on else 0))
+
     def set_progress(self, words_addr: int) -> None:
         self.lib.check(self.lib.tpi_engine_set_progress(self.handle,
                                                         ctypes.c_void_p(words_addr or None)),
@@ -1119,6 +1124,10 @@ class Checkpointer:
             t2 = time.perf_counter()
             if ck.engine is not None:  # before the predecessor's freeing makes hipMalloc slow
                 ck.engine.reserve(len(entries) + 1, plan.ntiles, layout["codec"] == "tpz1")
+                # TPI_MATERIALIZE_H2D=sdma: the restore's host-to-device copies on an SDMA
+                # engine of their own (profiles/round4/materialize_170g.md)
+                ck.h2d_engine = ck.engine.set_h2d_sdma(
+                    os.environ.get("TPI_MATERIALIZE_H2D", "hip") == "sdma")
             ck._setup_times = {"layout": round(t1 - t0, 4), "checkpointer": round(t2 - t1, 4),
                                "reserve": round(time.perf_counter() - t2, 4)}
             tensors, res = ck._materialize(dev, group_bytes, stream_timeout, memory_timeout)
@@ -1391,6 +1400,7 @@ class Checkpointer:
                                   "alloc_wait_s": round(waited[0], 4),
                                   "streamed": streaming, "trace": trace, "setup": setup,
                                   "fallback": fallback,
+                                  "h2d_engine": getattr(self, "h2d_engine", None),
                                   "alloc": "nogil" if empty_nogil is not None else "torch"}
         self.materialized_metadata = header.get("metadata", {})
         self.last_restore = total

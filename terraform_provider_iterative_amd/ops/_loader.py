@@ -15,7 +15,7 @@ from typing import Optional
 
 from .. import _build
 
-ABI_VERSION = 6  # TPI_ABI_VERSION of csrc/hip/tpi_hip.h
+ABI_VERSION = 7  # TPI_ABI_VERSION of csrc/hip/tpi_hip.h
 
 _lock = threading.Lock()
 _native = None
@@ -97,6 +97,7 @@ class HipLib:
             "tpi_engine_split_chunks": (u64, [vp]),
             "tpi_engine_set_progress": (i32, [vp, vp]),
             "tpi_engine_reserve": (i32, [vp, i32, u64, i32]),
+            "tpi_engine_set_h2d_sdma": (i32, [vp, i32]),
             "tpi_ipc_export": (i32, [vp, vp, c.POINTER(u64), c.POINTER(u64)]),
             "tpi_mem_range": (i32, [vp, c.POINTER(u64), c.POINTER(u64)]),
             "tpi_copy_segments": (i32, [vp, vp, vp, i32, u64, u64, c.POINTER(u64), vp]),

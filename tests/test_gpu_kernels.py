@@ -860,3 +860,46 @@ def test_materialize_falls_back_when_the_writers_stream_fails(tmp_path):
         assert torch.equal(tensors[k], ref[k]), k
     ck.close()
     writer.close()
+
+
+@pytest.mark.parametrize("codec", ["none", "tpz1"])
+def test_streamed_restore_on_its_own_sdma_engine(codec, tmp_path):
+    """tpi_engine_set_h2d_sdma: a restore streaming behind a concurrent save copies host ->
+    device on an SDMA engine of its own (host-driven lanes, kernels queued per landed chunk),
+    for every staging buffer reused twice; the bytes match."""
+    import threading
+
+    from terraform_provider_iterative_amd.checkpoint import Checkpointer
+
+    g = torch.Generator().manual_seed(14)
+    src = {"a": torch.randn(3 << 20, generator=g).to(torch.bfloat16).cuda(),
+           "b": torch.randn(5 << 20, generator=g).mul(1e-3).cuda(),
+           "t": torch.randn(640, 1000, generator=g).cuda().t()}
+    dst = {k: torch.zeros_like(v) for k, v in src.items()}
+    dst["t"] = torch.zeros(640, 1000, device="cuda").t()
+    path = str(tmp_path / "spill")
+    kw = dict(tile_bytes=1 << 16, chunk_bytes=1 << 20, nbuf=2, codec=codec)
+    writer = Checkpointer(src, path=path, **kw)
+    reader = Checkpointer(dst, path=path, **kw)
+    engine = reader.engine.set_h2d_sdma(True)
+    if engine < 0:
+        pytest.skip("no free SDMA engine for host-to-device lanes on this device")
+    box = {}
+
+    def restore():
+        try:
+            box["res"] = reader.restore(stream_timeout=20)
+        except BaseException as error:  # surfaced below
+            box["err"] = error
+
+    th = threading.Thread(target=restore)
+    writer.save({"step": 1}, on_stream=th.start)
+    th.join(60)
+    assert "err" not in box, box.get("err")
+    assert box["res"].bad_tiles == 0
+    torch.cuda.synchronize()
+    for k in src:
+        assert torch.equal(dst[k], src[k]), k
+    assert reader.engine.set_h2d_sdma(False) == 0
+    reader.close()
+    writer.close()
