@@ -774,6 +774,10 @@ class NodeTask(Task):
                 directory, "data", storage.transfer_rules(self.spec.environment.exclude_list))
             log.info("Uploaded %d files to %s", stats["files"], self.remote_conn)
             return
+        if os.environ.get("TPI_PUSH_LINK", "") in ("1", "true", "yes"):
+            # hard links instead of copies (no snapshot: see storage.link_tree)
+            storage.link_tree(directory, self.data_dir, self.spec.environment.exclude_list)
+            return
         storage.transfer(directory, self.data_dir, self.spec.environment.exclude_list)
 
     def _restore_remote(self) -> None:

@@ -11,6 +11,7 @@ import json
 import logging
 import os
 import posixpath
+import shutil
 from typing import Dict, Iterable, List, Optional
 
 from ..utils.record import field, record
@@ -83,6 +84,37 @@ def _copy_threads() -> int:
     except (AttributeError, OSError):
         cpus = os.cpu_count() or 8
     return max(8, min(16, cpus))
+
+
+def link_tree(source: str, destination: str, exclude: Optional[Iterable[str]] = None) -> Dict:
+    """Hard-link ``source``'s files (rclone filter rules as :func:`transfer`) into
+    ``destination`` instead of copying them: an apply of a 10 GB workdir then costs metadata
+    operations only.  Opt-in (``TPI_PUSH_LINK=1``) because a link is not a snapshot: a file
+    the user edits in place after the apply, or the task rewrites in place, is the same file
+    on both sides (a file replaced by rename -- what most editors and the task's output
+    sync do -- is not).  Files on another filesystem, or where links are refused, are
+    copied.  Returns ``{"linked", "copied", "bytes"}``."""
+    src, dst = _local_path(source), _local_path(destination)
+    flt = make_filter(transfer_rules(exclude))
+    linked = copied = nbytes = 0
+    os.makedirs(dst, exist_ok=True)
+    for rel, size, _mtime, _mode, is_dir in native().walk(src, flt):
+        target = os.path.join(dst, rel)
+        if is_dir:
+            os.makedirs(target, exist_ok=True)
+            continue
+        os.makedirs(os.path.dirname(target), exist_ok=True)
+        if os.path.lexists(target):
+            os.remove(target)
+        try:
+            os.link(os.path.join(src, rel), target)
+            linked += 1
+        except OSError:  # EXDEV, EPERM, ...: copy this one
+            shutil.copy2(os.path.join(src, rel), target)
+            copied += 1
+        nbytes += size
+    log.info("Linked %d files (%s), copied %d", linked, human_size(nbytes), copied)
+    return {"linked": linked, "copied": copied, "bytes": nbytes}
 
 
 def transfer(source: str, destination: str, exclude: Optional[Iterable[str]] = None,

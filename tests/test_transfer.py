@@ -142,3 +142,23 @@ def test_existing_bucket_connection_strings():
     az = tr.Connection.existing_bucket("az", "container", "sub",
                                        {"account": "a", "key": "k"})
     assert str(az) == ":azureblob,account='a',key='k':container/sub"
+
+
+def test_link_tree_hard_links_with_the_transfer_filters(tmp_path):
+    """TPI_PUSH_LINK=1's push: files become hard links (same inode, no bytes copied), the
+    default excludes and user rules apply, and an existing target is replaced."""
+    from terraform_provider_iterative_amd.storage.transfer import link_tree
+
+    src, dst = tmp_path / "src", tmp_path / "dst"
+    (src / "sub").mkdir(parents=True)
+    (src / "train.py").write_text("print(1)\n")
+    (src / "sub" / "data.bin").write_bytes(b"x" * 4096)
+    (src / "main.tf").write_text("resource {}\n")          # default exclude
+    (src / "skip.log").write_text("no\n")                  # user exclude
+    (dst).mkdir()
+    (dst / "train.py").write_text("stale\n")
+    stats = link_tree(str(src), str(dst), ["skip.log"])
+    assert stats["linked"] == 2 and stats["copied"] == 0 and stats["bytes"] == 4096 + 9
+    assert os.stat(dst / "sub" / "data.bin").st_ino == os.stat(src / "sub" / "data.bin").st_ino
+    assert (dst / "train.py").read_text() == "print(1)\n"
+    assert not (dst / "main.tf").exists() and not (dst / "skip.log").exists()
