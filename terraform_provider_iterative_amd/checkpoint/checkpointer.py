@@ -1838,6 +1838,9 @@ def _region_layout(path: str) -> Dict[str, Any]:
             slots = 2 if size >= 2 * slot_bytes else 1
             if base and slots != 2:
                 continue
+            if size < slot_end:  # a persisted file holds one slot, cut after its stream
+                raise CheckpointError("%s is a persisted checkpoint, not a spill region: "
+                                      "restore it with Checkpointer.load()" % path)
             return {"entries": json.loads(blob),
                     "entries_sha256": hashlib.sha256(blob).hexdigest(),
                     "total": header["total"], "tile_bytes": header["tile_bytes"],

@@ -640,3 +640,16 @@ def test_materialize_falls_back_to_the_older_copy_when_the_stream_fails(tmp_path
     assert all(torch.equal(tensors[k], ref[k]) for k in ref)
     ck.close()
     writer.close()
+
+
+def test_materialize_refuses_a_persisted_file(tmp_path):
+    """A persisted checkpoint is one slot cut after its stream, not a spill region: mapping
+    it as a region would grow the file, so materialize() says to use load() instead."""
+    persisted = str(tmp_path / "ckpt.tpi")
+    with Checkpointer(_model(10), tile_bytes=4096) as ck:
+        ck.save()
+        ck.persist(persisted)
+    size = os.path.getsize(persisted)
+    with pytest.raises(CheckpointError, match="persisted checkpoint"):
+        Checkpointer.materialize(persisted, "cpu")
+    assert os.path.getsize(persisted) == size
