@@ -137,6 +137,12 @@ def build_parser(defaults: Dict[str, Any]) -> argparse.ArgumentParser:
     preempt.add_argument("name")
     preempt.add_argument("--rank", type=int, default=None,
                          help="preempt only this rank (its gang follows when coupled)")
+    events = sub.add_parser("events", help=argparse.SUPPRESS)
+    events.add_argument("name")
+    events.add_argument("--since", default=None, metavar="CODE",
+                        help="times relative to the first event with this code (e.g. "
+                             "preempt-signal); default: the task's first event")
+    events.add_argument("--json", action="store_true", help="one JSON object per event")
     checkpoint = sub.add_parser("checkpoint", help=argparse.SUPPRESS)
     checkpoint.add_argument("path")
     checkpoint.add_argument("--verify", action="store_true",
@@ -304,6 +310,38 @@ def cmd_preempt(args, cloud: Cloud) -> int:
     return 0
 
 
+def cmd_events(args, cloud: Cloud) -> int:
+    """The task's phase journal (``supervisor/events.jsonl``: placement, rank starts, first
+    output, preemption phases, hand-offs, exits) as a timeline in seconds."""
+    import json
+
+    task = backends.new(cloud, parse_identifier(args.name), TaskSpec())
+    events = task.events()
+
+    def seconds(event) -> float:
+        t = event.time
+        return t.timestamp() if hasattr(t, "timestamp") else float(t)
+
+    if not events:
+        sys.stderr.write("Error: no events for %s\n" % args.name)
+        return 1
+    origin = seconds(events[0])
+    if args.since:
+        marks = [seconds(e) for e in events if e.code == args.since]
+        if not marks:
+            sys.stderr.write("Error: no %s event\n" % args.since)
+            return 1
+        origin = marks[0]
+    for event in events:
+        dt = seconds(event) - origin
+        if args.json:
+            print(json.dumps({"t": round(dt, 4), "code": event.code,
+                              "description": list(event.description)}))
+        else:
+            print("%+10.4f s  %-28s %s" % (dt, event.code, " | ".join(event.description)))
+    return 0
+
+
 def cmd_destroy_runner(args, cloud: Cloud) -> int:
     from ..provider.resources import machine_delete
 
@@ -314,7 +352,8 @@ def cmd_destroy_runner(args, cloud: Cloud) -> int:
 
 
 COMMANDS = {"create": cmd_create, "read": cmd_read, "list": cmd_list, "delete": cmd_delete,
-            "stop": cmd_stop, "destroy-runner": cmd_destroy_runner, "preempt": cmd_preempt}
+            "stop": cmd_stop, "destroy-runner": cmd_destroy_runner, "preempt": cmd_preempt,
+            "events": cmd_events}
 
 
 def main(argv: Optional[List[str]] = None) -> int:

@@ -178,6 +178,26 @@ def test_leo_read_exit_code_on_failure(tmp_path, env):
     run(base + ["delete", ident], str(tmp_path), env)
 
 
+def test_leo_events_prints_the_phase_journal(tmp_path, env):
+    base = LEO + ["--cloud", "local"]
+    r = run(base + ["create", "--workdir", str(tmp_path), "--", "sh", "-c", "echo hi"],
+            str(tmp_path), env)
+    ident = r.stdout.strip().splitlines()[-1]
+    run(base + ["read", "--follow", ident], str(tmp_path), env, timeout=60)
+    text = run(base + ["events", ident], str(tmp_path), env).stdout
+    lines = text.strip().splitlines()
+    assert lines and lines[0].lstrip().startswith("+0.0000 s")
+    assert any("rank-start" in l for l in lines) and any("rank-exit" in l for l in lines), text
+    rows = [json.loads(l) for l in run(base + ["events", "--json", "--since", "rank-start",
+                                               ident], str(tmp_path), env).stdout.splitlines()]
+    start = next(r for r in rows if r["code"] == "rank-start")
+    assert start["t"] == 0 and all(r["t"] >= 0 for r in rows if r["code"] == "rank-exit")
+    missing = run(base + ["events", "--since", "no-such-code", ident], str(tmp_path), env,
+                  check=False)
+    assert missing.returncode == 1
+    run(base + ["delete", ident], str(tmp_path), env)
+
+
 def test_leo_reads_main_tf_defaults(tmp_path, env):
     from terraform_provider_iterative_amd.cli.leo import config_defaults
 
