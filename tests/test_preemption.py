@@ -201,12 +201,16 @@ def test_hot_standby_gang_of_two(cloud, monkeypatch):
     task = backends.new(cloud, new_deterministic_identifier("preempt-hot-gang"), spec)
     task.create()
     _wait_for(task, "step 3")
-    deadline = time.time() + 30
+    # each rank's hot standby starts once the rank has announced itself from standby(); under
+    # a loaded machine (the suite on 8 workers) that can take longer than the steps do
+    deadline = time.time() + 120
     while time.time() < deadline and \
             sum(e.code == "standby-start" for e in task.events()) < 2:
         time.sleep(0.05)
+    assert sum(e.code == "standby-start" for e in task.events()) == 2, \
+        [e.code for e in task.events()]
     task.preempt(rank=1)
-    status = task.wait(120)
+    status = task.wait(180)
     logs = task.logs()
     assert status["succeeded"] == 2, (status, logs)
     finished = [l for l in logs if "activated" in l and "final 30 30" in l]
