@@ -46,10 +46,11 @@ def cloud(tmp_path):
                  credentials=Credentials(node=NodeCredentials(state_root=str(tmp_path / "st"))))
 
 
-def _wait_for(task, text, timeout=60):
+def _wait_for(task, text, timeout=60, ranks=1):
+    """Until ``text`` is in the logs of ``ranks`` ranks."""
     deadline = time.time() + timeout
     while time.time() < deadline:
-        if any(text in log for log in task.logs()):
+        if sum(text in log for log in task.logs()) >= ranks:
             return True
         time.sleep(0.05)
     raise AssertionError("%r never appeared in logs: %s" % (text, task.logs()))
@@ -200,7 +201,9 @@ def test_hot_standby_gang_of_two(cloud, monkeypatch):
                                         variables=Variables({"TPI_TASK": "true"})))
     task = backends.new(cloud, new_deterministic_identifier("preempt-hot-gang"), spec)
     task.create()
-    _wait_for(task, "step 3")
+    # both ranks in their loops (handler installed): a rank still starting up when the gang
+    # is preempted dies without a save, and its standby rightly starts fresh
+    _wait_for(task, "step 3", ranks=2)
     # each rank's hot standby starts once the rank has announced itself from standby(); under
     # a loaded machine (the suite on 8 workers) that can take longer than the steps do
     deadline = time.time() + 120
@@ -216,8 +219,9 @@ def test_hot_standby_gang_of_two(cloud, monkeypatch):
     finished = [l for l in logs if "activated" in l and "final 30 30" in l]
     assert len(finished) == 2, logs
     codes = [e.code for e in task.events()]
-    assert codes.count("standby-activated") == 2, codes
-    assert codes.count("checkpoint-streaming") + codes.count("checkpoint-released") >= 2, codes
+    trail = "\n".join("%s %s" % (e.code, " ".join(e.description)) for e in task.events())
+    assert codes.count("standby-activated") == 2, trail
+    assert codes.count("checkpoint-streaming") + codes.count("checkpoint-released") >= 2, trail
     task.delete()
 
 
