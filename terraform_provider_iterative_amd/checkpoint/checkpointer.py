@@ -255,6 +255,11 @@ class DeviceEngine:
 PREWARM_SEGS, PREWARM_TILES = 4096, 1 << 18
 ALLOC_HEADROOM = 512 << 20  # materialize(): free HBM beyond a tensor's size before allocating it
 ALLOC_LOOKAHEAD = 3  # materialize(): groups allocated ahead of the restore once HBM runs short
+# export_hbm(): the largest PyTorch allocation offered through HIP IPC.  On the MI355X boxes
+# (ROCm 7.2, PyTorch 2.10) hipIpcOpenMemHandle never returns for a caching-allocator block of
+# 2 GiB or more (2040 MiB opens at once), so a state holding one takes the host path instead of
+# hanging its successor (profiles/round4/ipc_lifetime.md).  TPI_IPC_MAX_ALLOC overrides.
+IPC_MAX_ALLOC = 2 << 30
 
 # Engines created ahead of the Checkpointer that takes them (prewarm_engine).
 _engine_pool: Dict[Tuple[int, int, int, int], List[DeviceEngine]] = {}
@@ -1434,7 +1439,8 @@ class Checkpointer:
         (:meth:`restore_hbm`) while this process is still spilling it to host memory.  The
         caller must keep the tensors unchanged (and this process alive) until the successor
         has restored -- the preemption handler does (it lingers until ``restored``).
-        ``metadata``: that of the save this export accompanies; a successor resuming from the
+        Raises CheckpointError, writing nothing, when a tensor lives in an allocation of
+        ``IPC_MAX_ALLOC`` or more.  ``metadata``: that of the save this export accompanies; a successor resuming from the
         HBM gets it even when the host copy failed."""
         manifest = self._hbm_manifest_path()
         if manifest is None:
@@ -1447,6 +1453,7 @@ class Checkpointer:
         handles, where = [], []
         handle = ctypes.create_string_buffer(64)
         base, size, offset = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
+        limit = int(os.environ.get("TPI_IPC_MAX_ALLOC", IPC_MAX_ALLOC))
         for seg in self.plan.segs:
             ptr = int(seg["ptr"])
             if int(seg["nbytes"]) == 0 or ptr == 0:
@@ -1457,6 +1464,12 @@ class Checkpointer:
             lib.check(lib.tpi_mem_range(ctypes.c_void_p(ptr), ctypes.byref(base),
                                         ctypes.byref(size)), "tpi_mem_range")
             key = int(base.value)
+            if key not in allocations and int(size.value) >= limit:
+                raise CheckpointError(
+                    "no HBM hand-off: tensor %d lives in a %.2f GiB allocation, and IPC imports "
+                    "of allocations >= %.2f GiB block (TPI_IPC_MAX_ALLOC); the successor "
+                    "restores from the host copy" % (len(where), int(size.value) / 2 ** 30,
+                                                     limit / 2 ** 30))
             if key not in allocations:
                 lib.check(lib.tpi_ipc_export(ctypes.c_void_p(ptr), handle, ctypes.byref(offset),
                                              ctypes.byref(size)), "tpi_ipc_export")

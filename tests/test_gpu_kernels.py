@@ -669,6 +669,36 @@ def test_hbm_handoff_copies_a_live_predecessors_tensors(tmp_path, monkeypatch, r
         child.wait(60)
 
 
+def test_hbm_export_refuses_allocations_at_the_ipc_limit(tmp_path, monkeypatch):
+    """IPC imports of PyTorch allocations of 2 GiB or more block in hipIpcOpenMemHandle
+    (profiles/round4/ipc_lifetime.md), so export_hbm refuses a state holding one before it
+    publishes anything: the successor sees no hand-off and restores from the host copy.  The
+    limit is lowered here so that small tensors exercise it."""
+    from terraform_provider_iterative_amd.checkpoint import CheckpointError, Checkpointer
+    from terraform_provider_iterative_amd.checkpoint import checkpointer as ckmod
+
+    import ctypes
+
+    from terraform_provider_iterative_amd.ops import hip
+
+    assert ckmod.IPC_MAX_ALLOC == 2 << 30
+    t = {"a": torch.randn(1 << 18, device="cuda"), "b": torch.randn(4 << 20, device="cuda")}
+    base, size = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    largest = 0  # the caching allocator decides which allocations hold them
+    for v in t.values():
+        hip().check(hip().tpi_mem_range(ctypes.c_void_p(v.data_ptr()), ctypes.byref(base),
+                                        ctypes.byref(size)), "tpi_mem_range")
+        largest = max(largest, int(size.value))
+    ck = Checkpointer(t, path=str(tmp_path / "spill"), tile_bytes=1 << 20, chunk_bytes=4 << 20)
+    monkeypatch.setenv("TPI_IPC_MAX_ALLOC", str(largest))
+    with pytest.raises(CheckpointError, match="no HBM hand-off"):
+        ck.export_hbm()
+    assert not __import__("os").path.exists(str(tmp_path / "spill") + ".hbm")
+    monkeypatch.setenv("TPI_IPC_MAX_ALLOC", str(largest + 1))
+    assert ck.export_hbm()
+    ck.close()
+
+
 def test_prewarmed_engine_is_taken_by_the_next_checkpointer():
     """A warm standby pre-creates the device engine (preemption.standby -> prewarm_engine);
     the Checkpointer built after activation takes it instead of creating one."""
