@@ -364,15 +364,23 @@ uint64_t remove_tree(const std::string& path) {
   if (lstat(path.c_str(), &st)) return 0;
   uint64_t n = 0;
   if (S_ISDIR(st.st_mode)) {
-    DIR* d = opendir(path.c_str());
-    if (d) {
-      std::vector<std::string> names;
-      while (struct dirent* de = readdir(d))
-        if (strcmp(de->d_name, ".") && strcmp(de->d_name, "..")) names.emplace_back(de->d_name);
-      closedir(d);
-      for (auto& nme : names) n += remove_tree(join(path, nme));
+    // a few passes: a writer that is still appending (a settled supervisor journalling the
+    // exit of a released process) may re-create a file between the scan and the rmdir
+    for (int pass = 0; pass < 4; ++pass) {
+      DIR* d = opendir(path.c_str());
+      if (d) {
+        std::vector<std::string> names;
+        while (struct dirent* de = readdir(d))
+          if (strcmp(de->d_name, ".") && strcmp(de->d_name, "..")) names.emplace_back(de->d_name);
+        closedir(d);
+        for (auto& nme : names) n += remove_tree(join(path, nme));
+      }
+      if (rmdir(path.c_str()) == 0) {
+        ++n;
+        break;
+      }
+      if (errno != ENOTEMPTY && errno != EEXIST) break;
     }
-    if (rmdir(path.c_str()) == 0) ++n;
   } else if (unlink(path.c_str()) == 0) {
     ++n;
   }

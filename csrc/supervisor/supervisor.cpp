@@ -395,6 +395,11 @@ class Supervisor {
       // queued task or an on-demand reclaim would wait for it (tpl:10-15: the group scales to
       // 0 right after the task's exit).
       if (!resources_released_ && ranks_settled()) release_resources();
+      // ... and the task is over for its users at the same moment: final sync, final state,
+      // control socket closed.  Released processes still tearing down (a 100 GB pinned region
+      // can take 10-18 s to unmap after a hot hand-off) are traced and reaped by this process
+      // behind that, on no user-visible path (tpl:10-15,51: status, then scale to 0).
+      if (!settled_ && resources_released_) settle();
       if (all_finished()) break;
       double timeout = 2.0;
       if (s_.deadline > 0 && !timed_out_) timeout = std::min(timeout, s_.deadline - t);
@@ -469,6 +474,7 @@ class Supervisor {
   bool stop_ = false, timed_out_ = false, dirty_ = true;
   bool resources_released_ = false;  // leases gone; released processes may still be exiting
   bool requeued_ = false;            // the queue waiter was started (it owns state.json)
+  bool settled_ = false;  // final sync + final state written; only reaping released processes
   int total_restarts_ = 0;
   pid_t stager_pid_ = -1;
   bool staged_ = false;
@@ -1064,7 +1070,7 @@ class Supervisor {
   }
 
   void write_state(const char* phase = nullptr) {
-    if (requeued_) return;  // the queue waiter owns state.json now
+    if (requeued_ || settled_) return;  // the queue waiter owns state.json / it is final
     atomic_write(s_.state_path, state_json(phase));
   }
 
@@ -1994,21 +2000,35 @@ class Supervisor {
     for (auto& d : detached_) exiting += d.pid > 0;
     event("resources-released", {std::to_string(unlinked) + " lease file(s)",
                                  std::to_string(exiting) + " released process(es) still exiting"});
-    if (requeue_ && !stop_ && !timed_out_) {
-      bool pending = false;  // a rank that has not finished on its own
-      for (auto& r : ranks_)
-        if (r.reason == TermReason::REQUEUE && !(r.exit_signal == 0 && r.exit_code == 0))
-          pending = true;
-      if (pending) {
-        close_control();  // the next incarnation binds the same socket path
-        requeued_ = spawn_requeue();
-      }
-    }
     dirty_ = true;
   }
 
-  int finish() {
-    // Ranks are gone; give lingering writers (daemonized children) a moment, then close.
+  // Every rank is down and the resources are back: finish the task for its users now --
+  // drain the ranks' logs, run the final (awaited) off-node sync, then either put the task
+  // back into the queue or write the final state -- instead of after the last released
+  // process has been reaped.  The final sync runs before the requeue, so the next
+  // incarnation never mirrors a container this one is still writing.
+  void settle() {
+    if (settled_) return;
+    drain_rank_logs();
+    final_sync();  // the logs and statuses of every rank are written by now
+    bool pending = false;  // a reclaimed rank that has not finished on its own
+    if (requeue_ && !stop_ && !timed_out_)
+      for (auto& r : ranks_)
+        if (r.reason == TermReason::REQUEUE && !(r.exit_signal == 0 && r.exit_code == 0))
+          pending = true;
+    close_control();  // the next incarnation (requeued or restarted) binds the same path
+    if (pending) requeued_ = spawn_requeue();
+    int exiting = 0;
+    for (auto& d : detached_) exiting += d.pid > 0;
+    event("supervisor-settled", {requeued_ ? "requeued" : stop_ ? "stopped" : "all ranks finished",
+                                 std::to_string(exiting) + " released process(es) still exiting"});
+    if (!requeued_) write_state("stopped");
+    settled_ = true;
+  }
+
+  // Ranks are gone; give lingering writers (daemonized children) a moment, then close.
+  void drain_rank_logs() {
     double until = now() + 0.5;
     while (now() < until) {
       bool open_fd = false;
@@ -2033,12 +2053,13 @@ class Supervisor {
       }
       close_log(r);
     }
+  }
+
+  int finish() {
     release_resources();
+    settle();
     remove_cgroups();
-    final_sync();  // the logs and statuses of every rank are written by now
-    if (!requeued_) close_control();
     event("supervisor-exit", {requeued_ ? "requeued" : stop_ ? "stopped" : "all ranks finished"});
-    if (!requeued_) write_state("stopped");
     signal_ready();
     return 0;
   }

@@ -658,7 +658,10 @@ class NodeTask(Task):
 
     def _alive_pids(self) -> List[int]:
         state = self._state()
-        pids = [int(state.get("pid", 0) or 0), int(state.get("stager_pid", 0) or 0)]
+        # a settled supervisor ("stopped") holds nothing: it only reaps released processes
+        # still tearing down (their kernel unmaps of a pinned region), behind the task's end
+        sup = int(state.get("pid", 0) or 0) if state.get("phase") != "stopped" else 0
+        pids = [sup, int(state.get("stager_pid", 0) or 0)]
         pids += [int(r.get("pid", 0) or 0) for r in state.get("ranks") or []]
         return [p for p in pids if p > 0 and pid_alive(p)]
 
@@ -742,7 +745,10 @@ class NodeTask(Task):
             except ProcessLookupError:
                 return
         deadline = _now() + wait
-        while _now() < deadline and pid_alive(pid):
+        # the task is over once the supervisor has settled (final sync and state written);
+        # it may live on a while, reaping released processes that are still exiting
+        while (_now() < deadline and pid_alive(pid)
+               and self._state().get("phase") != "stopped"):
             time.sleep(0.02)
 
     def _stop_marker(self) -> str:

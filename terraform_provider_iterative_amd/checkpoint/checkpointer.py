@@ -1552,26 +1552,37 @@ class Checkpointer:
         path = self._hbm_claim_path()
         if path is None:
             return False
-        for _ in range(3):
-            try:
-                fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_EXCL, 0o600)
-            except FileExistsError:
-                owner = self.hbm_claim_owner()
-                if owner == os.getpid():
+        # The claim appears with its pid already in it: the pid goes into a private file that
+        # is then hard-linked to the claim path (link fails if the claim exists).  A reader
+        # can therefore never see an empty claim and take it for a dead holder's.
+        tmp = "%s.%d.tmp" % (path, os.getpid())
+        with open(tmp, "w") as f:
+            f.write(str(os.getpid()))
+        try:
+            for _ in range(3):
+                try:
+                    os.link(tmp, path)
                     return True
-                if owner is not None and _writer_alive(owner):
-                    return False
-                try:  # its holder died: the claim is void
-                    os.remove(path)
-                except OSError:
-                    pass
-                continue
+                except FileExistsError:
+                    owner = self.hbm_claim_owner()
+                    if owner == os.getpid():
+                        return True
+                    if owner is None:
+                        continue  # released in between: try again
+                    if owner == 0 or _writer_alive(owner):
+                        # empty (never produced by this writer; treated as being written) or
+                        # a live holder: the claim is taken
+                        return False
+                    try:  # its holder died: the claim is void
+                        os.remove(path)
+                    except OSError:
+                        pass
+            return False
+        finally:
             try:
-                os.write(fd, str(os.getpid()).encode())
-            finally:
-                os.close(fd)
-            return True
-        return False
+                os.remove(tmp)
+            except OSError:
+                pass
 
     def release_hbm_claim(self) -> None:
         """Drop this process's claim (after its IPC mappings are closed)."""
@@ -1821,6 +1832,8 @@ class Checkpointer:
             self.slots = []
             self.region.close()
             self.region = None
+        if self.plan is not None and hasattr(self.plan, "unbind"):
+            self.plan.unbind()  # the tensors' HBM can go with the caller's references
 
     def __enter__(self):
         return self

@@ -131,6 +131,7 @@ def checkpoint_all(metadata: Optional[Dict] = None, on_stream=None,
     meta.update(metadata or {})
     t_cb = time.perf_counter() - t0
     rates = []
+    _phase["released-behind-bytes"] = 0
     for ck in _registered:
         if (on_stream is not None and len(_registered) == 1 and _hbm_handoff()
                 and not release_behind):  # memory freed behind the spill is no hand-off
@@ -150,6 +151,7 @@ def checkpoint_all(metadata: Optional[Dict] = None, on_stream=None,
         rates.append(res.gbps)
         journal("checkpoint-saved", *_describe(res))
         if getattr(res, "released_bytes", 0):
+            _phase["released-behind-bytes"] += int(res.released_bytes)
             journal("device-memory-released", "%.1f GB behind the spill" % (
                 res.released_bytes / 1e9))
         path = _persist_paths.get(id(ck))
@@ -520,6 +522,8 @@ def _await_successor(ck: Checkpointer) -> str:
                 how = "withdrawn"
             else:
                 how = None
+        elif owner == 0:  # a claim without a pid: taken for a live claimer, never a dead one
+            how = ("timeout with an unreadable claim" if waited >= hard else None)
         elif not _writer_alive(owner):
             how = "successor died"
         elif waited >= hard:
@@ -630,8 +634,12 @@ def _save_and_exit(consistency: str, ordinal: Optional[int] = None) -> None:
     if ordinal is not None:
         meta["boundary"] = ordinal
     code = 1
+    # may _teardown free the HBM explicitly?  At a boundary, yes.  From a signal-time save on
+    # the main thread only when no process group exists: the script is mid-step there, and a
+    # collective whose peer is already gone would block hipFree until SIGKILL.
     at_boundary = consistency == "boundary" or (
-        consistency == "signal" and threading.current_thread() is threading.main_thread())
+        consistency == "signal" and threading.current_thread() is threading.main_thread()
+        and not _process_group_active())
     # a reclaim, or a state too big for a successor's copy next to ours: every tensor's HBM
     # goes back as soon as it is in host memory, so the driver clears it under the spill
     release_behind = (consistency == "boundary" and _release_hbm_enabled() and not stream_ok
@@ -654,7 +662,11 @@ def _save_and_exit(consistency: str, ordinal: Optional[int] = None) -> None:
             freed = _release_device_memory()
             journal("device-memory-released", "%.1f GB" % (freed / 1e9),
                     "%.3f s" % (time.perf_counter() - t1))
-        if not released and (safe or freed) and os.environ.get("TPI_NOTIFY_FD"):
+        # release_behind: the save itself already gave the tensors' HBM back (freed above
+        # measures ~0 then), so the GPU may go just the same
+        freed += int(_phase.get("released-behind-bytes", 0))
+        if (not released and (safe or freed)
+                and os.environ.get("TPI_NOTIFY_FD")):
             if _notify(b"released\n"):
                 released.append(True)
                 journal("checkpoint-released", "reclaim: the GPU may go" if requeue
@@ -672,6 +684,16 @@ def _save_and_exit(consistency: str, ordinal: Optional[int] = None) -> None:
     _withdraw_handoffs()
     sys.stdout.flush()
     _teardown(code, at_boundary)
+
+
+def _process_group_active() -> bool:
+    """A torch.distributed process group is initialised in this process (never imports
+    torch.distributed itself)."""
+    dist = sys.modules.get("torch.distributed")
+    try:
+        return bool(dist is not None and dist.is_available() and dist.is_initialized())
+    except Exception:
+        return True  # unknown: the conservative answer
 
 
 def _withdraw_handoffs() -> None:
@@ -728,7 +750,10 @@ def _teardown(code: int, release_device: bool = True) -> None:
             journal("predecessor-teardown", *phases)
     except Exception as error:  # never keep a preempted process alive over its teardown
         journal("predecessor-teardown-failed", str(error))
-    sys.stdout.flush()
+    try:
+        sys.stdout.flush()
+    except Exception:  # nobody reads our output any more (e.g. a killed supervisor)
+        pass
     os._exit(code)
 
 

@@ -165,6 +165,13 @@ class PackPlan:
         self._bound = [t for _, t in named]  # descriptors hold raw pointers: keep them alive
         return self
 
+    def unbind(self) -> None:
+        """Drop the bound tensors (their memory may go once the caller's references do); the
+        descriptors' pointers are cleared with them."""
+        self._bound = []
+        self._dev_segs = None
+        self.segs["ptr"] = 0
+
     @property
     def on_device(self) -> bool:
         return self.device is not None and self.device.startswith("cuda")

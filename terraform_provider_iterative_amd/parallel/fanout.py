@@ -43,6 +43,9 @@ def write_workdir(path: str, nbytes: int, nfiles: int = 10, block: int = 256 << 
                 left -= n
 
 
+XGMI_LINK_GBPS = 153.0  # one MI355X xGMI link, per direction (7 per GPU on an 8-GPU node)
+
+
 def measure_workdir_fanout(nbytes: int, rank: int, world: int, device, barrier: Callable,
                            allmax: Callable[[float], float], workdir: Optional[str] = None,
                            methods=METHODS, numa_node: int = -1) -> Dict[str, dict]:
@@ -82,7 +85,9 @@ def measure_workdir_fanout(nbytes: int, rank: int, world: int, device, barrier: 
     image = torch.empty(total, dtype=torch.uint8, device=device)
     comm = TaskComm.from_group(device=device.index) if world > 1 else None
     out: Dict[str, dict] = {"bytes": total, "files": len(files),
-                            "requested_bytes": requested}
+                            "requested_bytes": requested,
+                            # the RCCL communicator the runtime built over the task's ranks
+                            "task_comm_world": comm.world if comm is not None else 1}
     try:
         with Loader(device.index, chunk_bytes=64 << 20, nbuf=4, threads=16,
                     numa_node=numa_node) as loader:
@@ -97,9 +102,13 @@ def measure_workdir_fanout(nbytes: int, rank: int, world: int, device, barrier: 
                     shard = total // world
                     loader.load(workdir, files, rank * shard, (rank + 1) * shard,
                                 image.data_ptr())
+                    torch.cuda.synchronize(device)
                     t1 = time.perf_counter()
                     if comm is not None:
+                        barrier()  # time the all-gather alone, all ranks' shards loaded
+                        ta = time.perf_counter()
                         comm.allgather_inplace(image, shard)
+                        gather_s = allmax(time.perf_counter() - ta)
                 elif method == "broadcast":
                     if rank == 0:
                         loader.load(workdir, files, 0, total, image.data_ptr())
@@ -123,6 +132,15 @@ def measure_workdir_fanout(nbytes: int, rank: int, world: int, device, barrier: 
                                "GBps_per_rank": round(total / elapsed / 1e9, 2),
                                "GBps_aggregate": round(world * total / elapsed / 1e9, 2),
                                "verified": verified}
+                if method == "sharded" and comm is not None:
+                    # all-gather bus bandwidth (each rank receives (N-1)/N of the image), next
+                    # to what one xGMI link carries: a single ring is bound by it, so a bus
+                    # rate above it means RCCL spread the rings over several links
+                    busbw = total * (world - 1) / world / gather_s / 1e9
+                    out[method].update({"allgather_s": round(gather_s, 4),
+                                        "allgather_busbw_GBps": round(busbw, 2),
+                                        "xgmi_link_GBps": XGMI_LINK_GBPS,
+                                        "busbw_over_one_link": round(busbw / XGMI_LINK_GBPS, 2)})
     finally:
         if comm is not None:
             comm.close()

@@ -225,6 +225,48 @@ def test_exporter_withdraws_after_the_linger_timeout(exporter, monkeypatch):
     assert time.monotonic() - t0 >= 0.3
 
 
+def test_an_empty_claim_is_never_taken_for_a_dead_holder(exporter, monkeypatch):
+    #  a claim file seen between its creation and its pid being written must not
+    # read as "holder died": neither a second claimer nor the exporter may act on it
+    with open(exporter._hbm_claim_path(), "w"):
+        pass
+    assert exporter.hbm_claim_owner() == 0
+    assert not exporter.claim_hbm()
+    assert os.path.exists(exporter._hbm_claim_path())
+    monkeypatch.setenv("TPI_HANDOFF_CLOSE_TIMEOUT", "0.3")
+    preemption._usr2.set()
+    how = preemption._await_successor(exporter)
+    assert how.startswith("timeout"), how
+
+
+CLAIM_RACE = r'''
+import os, sys, time
+sys.path.insert(0, %(root)r)
+from tests.test_handoff_protocol import _FakeHandoff
+ck = _FakeHandoff(%(path)r)
+while time.time() < %(start)r:
+    pass
+got = ck.claim_hbm()
+owner = ck.hbm_claim_owner()
+print(int(got), owner, flush=True)
+time.sleep(0.5)  # stay alive: a live holder
+'''
+
+
+def test_concurrent_claims_have_exactly_one_winner_who_is_the_recorded_owner(tmp_path):
+    path = str(tmp_path / "spill")
+    start = time.time() + 1.5
+    procs = [subprocess.Popen([sys.executable, "-c", CLAIM_RACE % {
+        "root": ROOT, "path": path, "start": start}], stdout=subprocess.PIPE, text=True)
+        for _ in range(8)]
+    rows = [p.communicate(timeout=30)[0].split() for p in procs]
+    winners = [p.pid for p, (got, _) in zip(procs, rows) if got == "1"]
+    assert len(winners) == 1, rows
+    # every loser already saw the winner's pid in the claim (never an empty file)
+    assert all(int(owner) == winners[0] for _, owner in rows), (winners, rows)
+    assert not [n for n in os.listdir(tmp_path) if n.endswith(".tmp")]
+
+
 EXPORTER = r'''
 import os, sys, time
 sys.path.insert(0, %(root)r)
@@ -359,3 +401,47 @@ def test_reclaimed_gpu_goes_to_the_on_demand_task_before_the_victim_is_reaped(tm
     assert "final 30" in logs[-1], logs
     od.delete()
     spot.delete()
+
+
+RELEASING = r'''
+import os, sys, time
+sys.path.insert(0, %(root)r)
+from terraform_provider_iterative_amd.checkpoint import preemption
+from tests.test_handoff_protocol import _FakeHandoff
+
+class Res:
+    bytes = wire_bytes = 1000
+    seconds = 0.1
+    gbps = 1e-5
+    released_bytes = 10 ** 9  # the save freed every tensor's HBM behind the spill
+
+class ReleasingBehind(_FakeHandoff):
+    def save(self, metadata, on_stream=None, release_behind=False, **kw):
+        assert release_behind and on_stream is None
+        return Res()
+
+preemption.register(ReleasingBehind(%(path)r))
+preemption.install()
+preemption._save_and_exit("boundary")
+'''
+
+
+def test_a_save_that_released_behind_the_spill_still_says_released(tmp_path):
+    """(ADVICE r4) a state too big for two copies (not safe) is freed by the save itself
+    (release_behind); "released" must still go out, before the exit, so the supervisor hands
+    the GPU on without waiting for the process to be reaped."""
+    r, w = os.pipe()
+    env = dict(os.environ, TPI_NOTIFY_FD=str(w), TPI_LINGER_SECONDS="1.0",
+               TPI_EARLY_HANDOFF="0", TPI_EVENTS_FILE=str(tmp_path / "events.jsonl"))
+    env.pop("TPI_REQUEUE_FILE", None)
+    proc = subprocess.Popen([sys.executable, "-c", RELEASING % {
+        "root": ROOT, "path": str(tmp_path / "spill")}], env=env, pass_fds=(w,))
+    os.close(w)
+    try:
+        assert os.read(r, 64) == b"released\n"
+        assert proc.poll() is None, "released must come before the exit"
+        assert proc.wait(10) == preemption.PREEMPTED_EXIT_CODE
+    finally:
+        if proc.poll() is None:
+            proc.kill()
+        os.close(r)

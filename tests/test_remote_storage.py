@@ -136,3 +136,76 @@ def test_task_data_lives_in_the_container_and_survives_delete(tmp_path, fake_ssh
         res = ck.load(url)
         assert res.bad_tiles == 0 and ck.header()["metadata"] == {"run": "1"}
     assert torch.equal(state["w"], torch.arange(5000, dtype=torch.float64))
+
+
+# A rank that is preempted, releases its GPU ("released" on the notify pipe) and then takes 20 s
+# to exit after the supervisor's exit request -- the kernel teardown of a 100 GB pinned region
+# after a hot hand-off took 10-18 s on MI355X.  Its successor finishes
+# at once.  Reference: the status is written and the group scaled to 0 right after the task's
+# exit (machine-script.sh.tpl:10-15,51).
+LINGERING = r'''#!%(python)s
+import os, signal, sys, time
+restart = int(os.environ["TPI_RESTART_COUNT"])
+fd = int(os.environ["TPI_NOTIFY_FD"])
+if restart == 0:
+    signal.pthread_sigmask(signal.SIG_BLOCK, {signal.SIGTERM, signal.SIGUSR2})
+    open(os.environ["PRED_PID_FILE"], "w").write(str(os.getpid()))
+    print("ready", flush=True)
+    signal.sigwait({signal.SIGTERM})
+    os.write(fd, b"released\n")
+    signal.sigwait({signal.SIGUSR2})
+    time.sleep(20.0)
+    os._exit(143)
+os.makedirs("output", exist_ok=True)
+with open("output/result.txt", "w") as f:
+    f.write("successor done\n")
+print("successor done", flush=True)
+'''
+
+
+def test_delete_does_not_wait_for_a_lingering_released_process(tmp_path, fake_ssh):
+    import time
+
+    from terraform_provider_iterative_amd.parallel.placement import pid_alive
+
+    bucket = tmp_path / "bucket"
+    container = "storage-node:%s" % bucket
+    work = tmp_path / "work"
+    work.mkdir()
+    pid_file = tmp_path / "pred.pid"
+    cloud = Cloud(provider="local",
+                  credentials=Credentials(node=NodeCredentials(state_root=str(tmp_path / "st"))))
+    spec = Task(environment=Environment(
+        script=LINGERING % {"python": sys.executable}, timeout=120, directory=str(work),
+        directory_out="output",
+        variables=Variables({"TPI_TASK": "true", "PRED_PID_FILE": str(pid_file),
+                             "FAKE_SSH_STATE_ROOT": os.environ["FAKE_SSH_STATE_ROOT"],
+                             "TPI_SYNC_INTERVAL": "0"})),
+        remote_storage=RemoteStorage(container, "", {}))
+    task = backends.new(cloud, new_deterministic_identifier("lingering"), spec)
+    task.create()
+    deadline = time.time() + 60
+    while time.time() < deadline and "ready" not in "".join(task.logs()):
+        time.sleep(0.05)
+    pred = int(pid_file.read_text())
+    task.preempt()
+    status = task.wait(30)  # returns when the task is over for its users
+    t_over = time.time()
+    assert status["succeeded"] == 1, task.logs()
+    assert pid_alive(pred), "the released predecessor should still be exiting"
+    events = task.events()
+    codes = [e.code for e in events]
+    # the final awaited sync ran at the ranks' exit, before the released process was reaped
+    synced = [e for e in events if e.code == "remote-synced" and "final" in e.description]
+    assert synced and "supervisor-settled" in codes and "rank-released-exit" not in codes, codes
+    assert (bucket / "data" / "output" / "result.txt").read_text() == "successor done\n"
+    assert any(p.name.startswith("status-") for p in (bucket / "reports").iterdir())
+    t0 = time.time()
+    task.delete()
+    took = time.time() - t0
+    assert took < 3.0, took
+    assert pid_alive(pred), "delete must not wait for (or need) the predecessor's exit"
+    assert (work / "output" / "result.txt").read_text() == "successor done\n"
+    assert not os.path.exists(task.root)
+    assert time.time() - t_over < 10.0  # everything above, well inside the 20 s linger
+    os.kill(pred, 9)
