@@ -245,6 +245,7 @@ struct Spec {
   uint64_t cgroup_headroom_kb = 0;  // checkpoint regions (shm pages charge the first toucher)
   std::string regions_path;         // checkpoint regions announced by the ranks (host.py)
   double memory_interval = 1.0, disk_interval = 10.0;
+  double memory_fast_interval = 0.02;  // statm poll of the ranks' process trees (s)
   // spot reclaim: after `requeue` the task goes back to the node queue through this command
   std::vector<std::string> requeue_argv;
   // off-node storage.container mirror (storage/remote.py): run every sync_interval s while
@@ -308,6 +309,7 @@ Spec load_spec(const std::string& path) {
   s.rank_memory_kb = (uint64_t)lim["rank_memory_mb"].num(0) * 1024;
   s.disk_limit_bytes = (uint64_t)(lim["disk_gb"].num(0) * 1e9);
   s.memory_interval = lim["memory_interval"].num(1.0);
+  s.memory_fast_interval = lim["memory_fast_interval"].num(0.02);
   s.cgroup = lim["cgroup"].str("auto");
   s.cgroup_version = (int)lim["cgroup_version"].num(0);
   s.cgroup_headroom_kb = (uint64_t)lim["cgroup_headroom_mb"].num(0) * 1024;
@@ -677,7 +679,13 @@ class Supervisor {
   void setup_cgroups() {
     cg_dirs_.assign(s_.parallelism, "");
     cg_oom_.assign(s_.parallelism, 0);
-    if (!s_.rank_memory_kb || s_.cgroup.empty() || s_.cgroup == "off") return;
+    if (!s_.rank_memory_kb) return;
+    if (s_.cgroup.empty() || s_.cgroup == "off") {
+      memory_guard_ = "poll " + std::to_string((int)(s_.memory_fast_interval * 1000)) + " ms";
+      event("memory-guard", {memory_guard_, "cgroup off",
+                             "limit " + std::to_string(s_.rank_memory_kb / 1024) + " MB"});
+      return;
+    }
     std::string root, why;
     int ver = s_.cgroup_version;
     struct stat st;
@@ -724,11 +732,15 @@ class Supervisor {
           rmdir(d.c_str());
           d.clear();
         }
+      memory_guard_ = "poll " + std::to_string((int)(s_.memory_fast_interval * 1000)) + " ms";
       event("memory-cgroup-unavailable", {why, "the /proc poll enforces the limit"});
+      event("memory-guard", {memory_guard_, "statm of each rank's process tree",
+                             "limit " + std::to_string(s_.rank_memory_kb / 1024) + " MB"});
       return;
     }
     cg_version_ = ver;
     cg_root_ = root;
+    memory_guard_ = "cgroup v" + std::to_string(ver);
     event("memory-cgroup", {"v" + std::to_string(ver), root,
                             "cap " + std::to_string(bytes >> 20) + " MB per rank",
                             "limit " + std::to_string(s_.rank_memory_kb / 1024) + " MB (poll)"});
@@ -762,23 +774,105 @@ class Supervisor {
     return du_total_;
   }
 
+  // ---- the fast guard (no cgroup) -----------------------------------------------------------
+  // Where the kernel cap is refused (an unprivileged box), the limit is only as good as the
+  // poll.  Every memory_fast_interval (20 ms) each rank's process tree -- the rank and its
+  // descendants, from /proc/<pid>/task/<tid>/children, plus the process-group members of the
+  // last full /proc scan (orphans reparented away from the tree) -- is summed from statm
+  // (microseconds per process).  The expensive proportional split runs only when that bound,
+  // advanced from the last split by the growth of the resident set since, passes the limit.
+  struct MemTrack {
+    long pid = 0;
+    uint64_t rss_at = 0, counted_at = 0;  // resident set and counted PSS at the last split
+    bool valid = false;
+    std::vector<long> members;  // process-group members seen by the last full scan
+  };
+  std::vector<MemTrack> mem_;
+  double next_memory_scan_ = 0;
+  std::string memory_guard_;
+
+  static void tree_pids(long root, std::vector<long>& out, int depth = 0) {
+    out.push_back(root);
+    if (depth > 16) return;
+    char path[64];
+    snprintf(path, sizeof(path), "/proc/%ld/task", root);
+    DIR* d = opendir(path);
+    if (!d) return;
+    std::vector<long> kids;
+    while (struct dirent* e = readdir(d)) {
+      if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
+      char cpath[96], buf[4096];
+      snprintf(cpath, sizeof(cpath), "/proc/%ld/task/%s/children", root, e->d_name);
+      if (!read_small(cpath, buf, sizeof(buf))) continue;
+      char* p = buf;
+      while (*p) {
+        char* end = nullptr;
+        long c = strtol(p, &end, 10);
+        if (end == p) break;
+        if (c > 0) kids.push_back(c);
+        p = end;
+      }
+    }
+    closedir(d);
+    for (long c : kids) tree_pids(c, out, depth + 1);
+  }
+
+  static uint64_t resident_kb(const std::vector<long>& pids) {
+    static const uint64_t page_kb = (uint64_t)sysconf(_SC_PAGESIZE) / 1024;
+    uint64_t kb = 0;
+    char path[64], buf[256];
+    for (long pid : pids) {
+      snprintf(path, sizeof(path), "/proc/%ld/statm", pid);
+      if (!read_small(path, buf, sizeof(buf))) continue;
+      unsigned long long size = 0, resident = 0;
+      if (sscanf(buf, "%llu %llu", &size, &resident) == 2) kb += resident * page_kb;
+    }
+    return kb;
+  }
+
   void check_limits(double t) {
     if (s_.rank_memory_kb && t >= next_memory_check_) {
-      next_memory_check_ = t + s_.memory_interval;
-      std::set<long> pgids;
-      for (auto& r : ranks_)
-        if (r.state == Rank::RUNNING && r.pid > 0 && !r.killed) pgids.insert(r.pid);
-      const auto groups = pgids.empty() ? std::map<long, GroupMemory>() : groups_memory(pgids);
+      const bool fast = cg_version_ == 0 && s_.memory_fast_interval > 0;
+      next_memory_check_ = t + (fast ? std::min(s_.memory_fast_interval, s_.memory_interval)
+                                     : s_.memory_interval);
+      if ((int)mem_.size() != s_.parallelism) mem_.assign(s_.parallelism, MemTrack());
+      const bool full = t >= next_memory_scan_;
+      std::map<long, GroupMemory> groups;
+      if (full) {
+        next_memory_scan_ = t + s_.memory_interval;
+        std::set<long> pgids;
+        for (auto& r : ranks_)
+          if (r.state == Rank::RUNNING && r.pid > 0 && !r.killed) pgids.insert(r.pid);
+        if (!pgids.empty()) groups = groups_memory(pgids);
+      }
+      std::vector<Region> regions;
+      bool regions_loaded = false;
       for (auto& r : ranks_) {
         if (r.state != Rank::RUNNING || r.pid <= 0 || r.killed) continue;
-        auto g = groups.find(r.pid);
-        if (g == groups.end()) continue;
-        // quick bound: resident set minus the regions' share measured last time
-        const uint64_t known = region_kb_[r.index];
-        if (g->second.rss_kb <= s_.rank_memory_kb + known) continue;
-        const auto split = pss_split_kb(g->second.pids, load_regions());
+        MemTrack& m = mem_[r.index];
+        if (m.pid != r.pid) m = MemTrack(), m.pid = r.pid;
+        if (full) {
+          auto g = groups.find(r.pid);
+          m.members = g == groups.end() ? std::vector<long>() : g->second.pids;
+        }
+        std::vector<long> pids;
+        tree_pids(r.pid, pids);
+        for (long p : m.members)
+          if (std::find(pids.begin(), pids.end(), p) == pids.end()) pids.push_back(p);
+        const uint64_t rss = resident_kb(pids);
+        // quick bound: the counted size at the last split plus any growth since (new
+        // resident pages are at most new private pages); before any split, the resident set
+        // minus the regions' share measured last time
+        const uint64_t bound = m.valid ? m.counted_at + (rss > m.rss_at ? rss - m.rss_at : 0)
+                                       : (rss > region_kb_[r.index] ? rss - region_kb_[r.index] : 0);
+        if (bound <= s_.rank_memory_kb) continue;
+        if (!regions_loaded) regions = load_regions(), regions_loaded = true;
+        const auto split = pss_split_kb(pids, regions);
         region_kb_[r.index] = split.second;
         const uint64_t kb = split.first - std::min(split.first, split.second);
+        m.rss_at = rss;
+        m.counted_at = kb;
+        m.valid = true;
         if (kb <= s_.rank_memory_kb) continue;
         // like a container OOM kill: no grace, the rank fails (no respawn)
         r.reason = TermReason::OOM;
@@ -1087,7 +1181,8 @@ class Supervisor {
                       ", \"heartbeat\": " + std::to_string(now()) +
                       ", \"running\": " + std::to_string(running()) +
                       ", \"restarts\": " + std::to_string(total_restarts_) +
-                      ", \"stager_pid\": " + std::to_string(stager_pid_) + ", \"ranks\": [";
+                      ", \"stager_pid\": " + std::to_string(stager_pid_) +
+                      ", \"memory_guard\": " + quote(memory_guard_) + ", \"ranks\": [";
     for (size_t i = 0; i < ranks_.size(); ++i) {
       auto& r = ranks_[i];
       out += std::string(i ? ", " : "") + "{\"rank\": " + std::to_string(r.index) +

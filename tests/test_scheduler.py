@@ -374,3 +374,33 @@ def test_fast_allocation_over_the_limit_is_stopped_by_the_kernel(tmp_path):
     assert json.load(open(os.path.join(task.reports_dir, reports[0])))["result"] == "oom"
     task.delete()
     assert not [d for d in os.listdir("/sys/fs/cgroup/memory") if d.startswith("tpi-" + task.id)]
+
+
+def test_fast_allocation_is_stopped_by_the_fast_poll_without_a_cgroup(tmp_path):
+    """where the kernel cap is refused (the MI355X box), the statm poll of each
+    rank's process tree (20 ms) is the guard.  machine 1-1000 (1 GB), cgroup forced off: a rank
+    writing 2 GB as fast as it can is killed before it passes 1.5 GB."""
+    cloud = _cloud(tmp_path, "local")
+    progress = tmp_path / "progress"
+    script = ("#!%s\nimport os, time\nfd = os.open(%r, os.O_WRONLY | os.O_CREAT, 0o644)\n"
+              "print('up', flush=True)\nkeep, t = [], time.time()\n"
+              "for i in range(32):\n"
+              "    keep.append(b'\\x01' * (64 << 20))\n"
+              "    os.pwrite(fd, b'%%012d' %% ((i + 1) * (64 << 20)), 0)\n"
+              "print('survived %%.3f s' %% (time.time() - t), flush=True)\ntime.sleep(5)\n"
+              % (sys.executable, str(progress)))
+    task = _task(cloud, "poll-oom", script, machine="1-1000",
+                 env={"TPI_MEMORY_CGROUP": "off"})
+    task.create()
+    status = task.wait(30)
+    logs = "".join(task.logs())
+    assert status["failed"] == 1 and "survived" not in logs, (status, logs)
+    reached = int(progress.read_text())
+    print("reached %.2f GB" % (reached / 1e9))
+    assert reached < 1.5e9, reached
+    events = task.events()
+    guard = [e for e in events if e.code == "memory-guard"]
+    assert guard and guard[0].description[0] == "poll 20 ms", guard
+    assert task._state().get("memory_guard") == "poll 20 ms"
+    assert [e for e in events if e.code == "rank-oom-killed"]
+    task.delete()
