@@ -1638,8 +1638,52 @@ class Checkpointer:
             self.hbm_close_s = time.perf_counter() - t1
             self.release_hbm_claim()  # nothing of the predecessor is mapped any more
 
+        def open_all() -> None:
+            # Bounded: an import that never returns (round 4: hipIpcOpenMemHandle on some
+            # allocations blocked forever) must not strand this successor holding the claim
+            # while its predecessor waits on it -- past TPI_IPC_OPEN_TIMEOUT the HBM route is
+            # given up (the caller restores from the host copy).  The openers are daemon
+            # threads: one stuck in the driver cannot hold up this process's exit.
+            try:
+                limit = float(os.environ.get("TPI_IPC_OPEN_TIMEOUT", "10"))
+            except ValueError:
+                limit = 10.0
+            todo = list(range(len(bases)))
+            lock = threading.Lock()
+            errors: List[BaseException] = []
+
+            def worker() -> None:
+                while True:
+                    with lock:
+                        if not todo or errors:
+                            return
+                        i = todo.pop()
+                    try:
+                        open_one(i)
+                    except BaseException as error:  # re-raised by the caller
+                        with lock:
+                            errors.append(error)
+                        return
+
+            workers = [threading.Thread(target=worker, name="tpi-ipc-open", daemon=True)
+                       for _ in range(min(8, len(bases)) or 1)]
+            for w in workers:
+                w.start()
+            deadline = time.monotonic() + limit
+            for w in workers:
+                w.join(max(0.0, deadline - time.monotonic()))
+            if errors:
+                raise errors[0]
+            if any(w.is_alive() for w in workers):
+                with lock:
+                    todo.clear()
+                    errors.append(CheckpointError("timed out"))
+                raise CheckpointError(
+                    "HIP IPC import of the predecessor's HBM did not return within %.1f s "
+                    "(TPI_IPC_OPEN_TIMEOUT); restoring from the host copy" % limit)
+
         try:
-            each(open_one)
+            open_all()
             self.hbm_open_s = time.perf_counter() - t0
             src = np.frombuffer(bytes.fromhex(doc["segs"]), dtype=self.plan.segs.dtype).copy()
             if len(src) != len(self.plan.segs):

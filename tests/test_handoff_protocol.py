@@ -19,13 +19,14 @@ import os
 import signal
 import subprocess
 import sys
+import threading
 import time
 
 import pytest
 
 from terraform_provider_iterative_amd import _build
 from terraform_provider_iterative_amd.checkpoint import preemption
-from terraform_provider_iterative_amd.checkpoint.checkpointer import Checkpointer
+from terraform_provider_iterative_amd.checkpoint.checkpointer import CheckpointError, Checkpointer
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -445,3 +446,41 @@ def test_a_save_that_released_behind_the_spill_still_says_released(tmp_path):
         if proc.poll() is None:
             proc.kill()
         os.close(r)
+
+
+def test_a_stuck_ipc_import_gives_up_the_hbm_route_and_the_claim(tmp_path, monkeypatch):
+    """ hipIpcOpenMemHandle that never returns: restore_hbm raises after
+    TPI_IPC_OPEN_TIMEOUT (the caller restores from the host copy) and drops its claim, so the
+    predecessor is not kept waiting for a successor that will never close."""
+    from terraform_provider_iterative_amd.checkpoint import checkpointer as ckmod
+
+    stuck = threading.Event()
+
+    class FakeLib:
+        def tpi_ipc_open(self, handle, device, out):
+            if handle == b"\x02":
+                stuck.wait(60)  # the import that never returns
+            return 0
+
+        def tpi_ipc_close(self, ptr):
+            return 0
+
+        def check(self, rc, what):
+            assert rc == 0, what
+
+    class Successor(_FakeHandoff):
+        device_index = 0
+        restore_hbm = Checkpointer.restore_hbm
+
+        def _hbm_doc(self):
+            return {"allocations": ["01", "02", "03"], "where": [], "segs": ""}
+
+    monkeypatch.setattr(ckmod, "hip", lambda *a, **k: FakeLib())
+    monkeypatch.setenv("TPI_IPC_OPEN_TIMEOUT", "0.5")
+    ck = Successor(str(tmp_path / "spill"))
+    t0 = time.monotonic()
+    with pytest.raises(CheckpointError, match="did not return within"):
+        ck.restore_hbm()
+    assert time.monotonic() - t0 < 5.0
+    assert ck.hbm_claim_owner() is None  # the claim is gone: the predecessor may go
+    stuck.set()
