@@ -47,6 +47,11 @@ struct Hsa {
   decltype(&hsa_amd_memory_copy_engine_status) engine_status = nullptr;
   decltype(&hsa_amd_memory_get_preferred_copy_engine) preferred_engine = nullptr;
   decltype(&hsa_amd_memory_async_copy_on_engine) copy_on_engine = nullptr;
+  // dma-buf hand-off (optional: absent symbols only disable that route)
+  decltype(&hsa_amd_portable_export_dmabuf) export_dmabuf = nullptr;
+  decltype(&hsa_amd_portable_close_dmabuf) close_dmabuf = nullptr;
+  decltype(&hsa_amd_interop_map_buffer) interop_map = nullptr;
+  decltype(&hsa_amd_interop_unmap_buffer) interop_unmap = nullptr;
 };
 
 int find_hsa(struct dl_phdr_info* info, size_t, void* data) {
@@ -86,6 +91,10 @@ const Hsa& hsa() {
     BIND(preferred_engine, hsa_amd_memory_get_preferred_copy_engine);
     BIND(copy_on_engine, hsa_amd_memory_async_copy_on_engine);
 #undef BIND
+    h.export_dmabuf = (decltype(h.export_dmabuf))dlsym(lib, "hsa_amd_portable_export_dmabuf");
+    h.close_dmabuf = (decltype(h.close_dmabuf))dlsym(lib, "hsa_amd_portable_close_dmabuf");
+    h.interop_map = (decltype(h.interop_map))dlsym(lib, "hsa_amd_interop_map_buffer");
+    h.interop_unmap = (decltype(h.interop_unmap))dlsym(lib, "hsa_amd_interop_unmap_buffer");
     // Reference-counted: HIP already initialised the runtime, this only keeps it alive for
     // as long as we hold signals.
     h.ok = h.init() == HSA_STATUS_SUCCESS;
@@ -289,3 +298,86 @@ int tpi_sdma_wait_all(tpi_sdma* s) {
     if (tpi_sdma_wait(s, (int)i)) rc = -1;
   return rc;
 }
+
+// ---- HBM hand-off over dma-buf ------------------------------------------------------------
+// hipIpcOpenMemHandle never returns for allocations of 2 GiB or more on this stack (round 5,
+// profiles/round5/ipc_cause.md: the importer spins at 100 % CPU while the exporter's IPC
+// server thread still waits in accept(); plain hipMalloc and PyTorch blocks alike).  The
+// hand-off therefore moves its allocations as dma-buf file descriptors: the predecessor
+// exports each allocation (DRM PRIME, any size), passes the descriptors over a Unix socket
+// (SCM_RIGHTS, checkpoint/checkpointer.py), and the successor maps them into its own GPU
+// address space with hsa_amd_interop_map_buffer.  A mapping holds its own reference to the
+// memory, so it stays valid whatever the exporter does.
+
+namespace {
+
+bool device_agent(int device, hsa_agent_t* out) {
+  static std::mutex mu;
+  static std::vector<std::pair<int, hsa_agent_t>> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  for (auto& c : cache)
+    if (c.first == device) {
+      *out = c.second;
+      return true;
+    }
+  hipDeviceProp_t p;
+  if (hipGetDeviceProperties(&p, device) != hipSuccess) return false;
+  AgentQuery q;
+  q.bdf = (uint32_t)((p.pciBusID << 8) | (p.pciDeviceID << 3));
+  q.domain = (uint32_t)p.pciDomainID;
+  hsa().iterate_agents(match_agent, &q);
+  if (!q.found) return false;
+  cache.push_back({device, q.gpu});
+  *out = q.gpu;
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tpi_dmabuf_available() {
+  const Hsa& h = hsa();
+  return h.ok && h.export_dmabuf && h.close_dmabuf && h.interop_map && h.interop_unmap;
+}
+
+int tpi_dmabuf_export(const void* ptr, uint64_t size, int* fd_out, uint64_t* offset_out) {
+  if (!tpi_dmabuf_available()) return tpi_fail("dma-buf export: HSA entry points unavailable");
+  int fd = -1;
+  uint64_t off = 0;
+  hsa_status_t st = hsa().export_dmabuf(ptr, (size_t)size, &fd, &off);
+  if (st != HSA_STATUS_SUCCESS) return tpi_fail("hsa_amd_portable_export_dmabuf: " + hsa_error(st));
+  *fd_out = fd;
+  *offset_out = off;
+  return 0;
+}
+
+int tpi_dmabuf_close(int fd) {
+  if (!tpi_dmabuf_available()) return tpi_fail("dma-buf close: HSA entry points unavailable");
+  hsa_status_t st = hsa().close_dmabuf(fd);
+  if (st != HSA_STATUS_SUCCESS) return tpi_fail("hsa_amd_portable_close_dmabuf: " + hsa_error(st));
+  return 0;
+}
+
+int tpi_dmabuf_import(int device, int fd, void** ptr_out, uint64_t* size_out) {
+  if (!tpi_dmabuf_available()) return tpi_fail("dma-buf import: HSA entry points unavailable");
+  hsa_agent_t agent;
+  if (!device_agent(device, &agent)) return tpi_fail("dma-buf import: no HSA agent for device");
+  size_t size = 0;
+  void* ptr = nullptr;
+  hsa_handle_t handle = fd;  // Linux: the dma-buf file descriptor itself
+  hsa_status_t st = hsa().interop_map(1, &agent, handle, 0, &size, &ptr, nullptr, nullptr);
+  if (st != HSA_STATUS_SUCCESS) return tpi_fail("hsa_amd_interop_map_buffer: " + hsa_error(st));
+  *ptr_out = ptr;
+  *size_out = size;
+  return 0;
+}
+
+int tpi_dmabuf_unmap(void* ptr) {
+  if (!tpi_dmabuf_available()) return tpi_fail("dma-buf unmap: HSA entry points unavailable");
+  hsa_status_t st = hsa().interop_unmap(ptr);
+  if (st != HSA_STATUS_SUCCESS) return tpi_fail("hsa_amd_interop_unmap_buffer: " + hsa_error(st));
+  return 0;
+}
+
+}  // extern "C"

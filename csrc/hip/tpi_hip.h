@@ -209,6 +209,14 @@ int tpi_ipc_export(const void* ptr, void* handle_out, uint64_t* offset_out,
 int tpi_copy_segments(tpi_engine* e, const tpi_seg* src, const tpi_seg* dst, int n,
                       uint64_t total, uint64_t signal_stream, uint64_t* bad_tiles,
                       tpi_stats* stats);
+// The hand-off's default route (sdma.cpp): an allocation as a dma-buf file descriptor (any
+// size; `offset_out` = ptr's offset in the buffer), mapped by another process into its GPU
+// address space (tpi_dmabuf_import: base and size of the mapping) and unmapped again.
+int tpi_dmabuf_available(void);
+int tpi_dmabuf_export(const void* ptr, uint64_t size, int* fd_out, uint64_t* offset_out);
+int tpi_dmabuf_close(int fd);
+int tpi_dmabuf_import(int device, int fd, void** ptr_out, uint64_t* size_out);
+int tpi_dmabuf_unmap(void* ptr);
 int tpi_engine_set_host_region(tpi_engine* e, void* base, uint64_t bytes, uint64_t window,
                                tpi_pinner* pinner);
 // hipMemcpyAsync host -> device on `stream` (0 = legacy default stream).

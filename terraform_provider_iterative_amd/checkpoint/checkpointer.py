@@ -35,6 +35,7 @@ import hashlib
 import json
 import os
 import queue
+import socket
 import struct
 import tempfile
 import threading
@@ -260,6 +261,12 @@ ALLOC_LOOKAHEAD = 3  # materialize(): groups allocated ahead of the restore once
 # 2 GiB or more (2040 MiB opens at once), so a state holding one takes the host path instead of
 # hanging its successor (profiles/round4/ipc_lifetime.md).  TPI_IPC_MAX_ALLOC overrides.
 IPC_MAX_ALLOC = 2 << 30
+# The hand-off's route (TPI_HBM_ROUTE): "dmabuf" (default) passes every allocation as a dma-buf
+# descriptor over a Unix socket and maps it with hsa_amd_interop_map_buffer -- any size
+# (profiles/round5/ipc_cause.md); "ipc" keeps hipIpcGetMemHandle / hipIpcOpenMemHandle, with the
+# size guard above.
+HBM_ROUTES = ("dmabuf", "ipc")
+FDS_PER_MESSAGE = 200  # SCM_RIGHTS batch (the kernel's limit is 253 per message)
 
 # Engines created ahead of the Checkpointer that takes them (prewarm_engine).
 _engine_pool: Dict[Tuple[int, int, int, int], List[DeviceEngine]] = {}
@@ -1434,13 +1441,18 @@ class Checkpointer:
         return self.path + ".hbm" if self.path and self.engine is not None else None
 
     def export_hbm(self, metadata: Optional[Dict] = None) -> Optional[str]:
-        """Preempted rank: publish HIP IPC handles of the bound tensors next to the spill file
-        (``<path>.hbm``), so a successor on the same GPU can copy the state device to device
-        (:meth:`restore_hbm`) while this process is still spilling it to host memory.  The
-        caller must keep the tensors unchanged (and this process alive) until the successor
-        has restored -- the preemption handler does (it lingers until ``restored``).
-        Raises CheckpointError, writing nothing, when a tensor lives in an allocation of
-        ``IPC_MAX_ALLOC`` or more.  ``metadata``: that of the save this export accompanies; a successor resuming from the
+        """Preempted rank: publish the bound tensors' device allocations next to the spill
+        file (``<path>.hbm``), so a successor on the same GPU can copy the state device to
+        device (:meth:`restore_hbm`) while this process is still spilling it to host memory.
+        The caller must keep the tensors unchanged (and this process alive) until the successor
+        has restored -- the preemption handler does (it lingers until ``closed``).
+
+        Route ``dmabuf`` (default, :data:`HBM_ROUTES`): each allocation is exported as a
+        dma-buf descriptor and served to the successor over an abstract Unix socket named in
+        the manifest (same uid only); any allocation size.  Route ``ipc``: HIP IPC handles in
+        the manifest; raises CheckpointError, writing nothing, when a tensor lives in an
+        allocation of ``IPC_MAX_ALLOC`` or more (those imports never return).
+        ``metadata``: that of the save this export accompanies; a successor resuming from the
         HBM gets it even when the host copy failed."""
         manifest = self._hbm_manifest_path()
         if manifest is None:
@@ -1449,47 +1461,129 @@ class Checkpointer:
 
         torch.cuda.synchronize(self.device_index)  # no queued kernel may still write them
         lib = hip()
-        allocations: Dict[int, int] = {}  # allocation base -> index in `handles`
-        handles, where = [], []
-        handle = ctypes.create_string_buffer(64)
-        base, size, offset = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
+        route = os.environ.get("TPI_HBM_ROUTE", "dmabuf").strip().lower()
+        if route not in HBM_ROUTES:
+            raise CheckpointError("TPI_HBM_ROUTE must be one of %s" % (HBM_ROUTES,))
+        if route == "dmabuf" and not lib.tpi_dmabuf_available():
+            route = "ipc"  # this runtime cannot export dma-bufs: the IPC route, guarded
+        allocations: Dict[int, int] = {}  # allocation base -> index
+        bases: List[Tuple[int, int]] = []  # (base, size) per allocation
+        where = []
+        base, size = ctypes.c_uint64(0), ctypes.c_uint64(0)
         limit = int(os.environ.get("TPI_IPC_MAX_ALLOC", IPC_MAX_ALLOC))
         for seg in self.plan.segs:
             ptr = int(seg["ptr"])
             if int(seg["nbytes"]) == 0 or ptr == 0:
                 where.append(None)
                 continue
-            # one IPC handle per allocation (hipIpcGetMemHandle is the slow call; tensors
-            # of one caching-allocator segment share it)
+            # one handle per allocation (tensors of one caching-allocator segment share it)
             lib.check(lib.tpi_mem_range(ctypes.c_void_p(ptr), ctypes.byref(base),
                                         ctypes.byref(size)), "tpi_mem_range")
             key = int(base.value)
-            if key not in allocations and int(size.value) >= limit:
-                raise CheckpointError(
-                    "no HBM hand-off: tensor %d lives in a %.2f GiB allocation, and IPC imports "
-                    "of allocations >= %.2f GiB block (TPI_IPC_MAX_ALLOC); the successor "
-                    "restores from the host copy" % (len(where), int(size.value) / 2 ** 30,
-                                                     limit / 2 ** 30))
             if key not in allocations:
-                lib.check(lib.tpi_ipc_export(ctypes.c_void_p(ptr), handle, ctypes.byref(offset),
-                                             ctypes.byref(size)), "tpi_ipc_export")
-                allocations[key] = len(handles)
-                handles.append(handle.raw.hex())
+                if route == "ipc" and int(size.value) >= limit:
+                    raise CheckpointError(
+                        "no HBM hand-off: tensor %d lives in a %.2f GiB allocation, and IPC "
+                        "imports of allocations >= %.2f GiB block (TPI_IPC_MAX_ALLOC); the "
+                        "successor restores from the host copy" % (
+                            len(where), int(size.value) / 2 ** 30, limit / 2 ** 30))
+                allocations[key] = len(bases)
+                bases.append((key, int(size.value)))
             where.append([allocations[key], ptr - key])
-        bus = ctypes.create_string_buffer(64)
-        lib.tpi_device_pci_bus_id(self.device_index, bus, 64)
-        doc = {"format": "tpi-hbm-1", "pid": os.getpid(), "device": bus.value.decode(),
+        doc = {"format": "tpi-hbm-1", "route": route, "pid": os.getpid(),
                "entries_sha256": self._entries_digest, "total": self.plan.total,
-               "tile_bytes": self.plan.tile_bytes, "allocations": handles, "where": where,
+               "tile_bytes": self.plan.tile_bytes, "where": where,
                "segs": self.plan.segs.tobytes().hex(), "created": time.time(),
                "metadata": metadata or {},
                # the generation the save that follows this export will write
                "generation": self._target()[1]}
+        if route == "ipc":
+            handle = ctypes.create_string_buffer(64)
+            offset = ctypes.c_uint64(0)
+            handles = []
+            for key, _ in bases:
+                lib.check(lib.tpi_ipc_export(ctypes.c_void_p(key), handle, ctypes.byref(offset),
+                                             ctypes.byref(size)), "tpi_ipc_export")
+                handles.append(handle.raw.hex())
+            doc["allocations"] = handles
+        else:
+            doc["allocations"] = [sz for _, sz in bases]
+            doc["socket"] = self._serve_dmabufs(bases)
+        bus = ctypes.create_string_buffer(64)
+        lib.tpi_device_pci_bus_id(self.device_index, bus, 64)
+        doc["device"] = bus.value.decode()
         tmp = manifest + ".tmp"
         with open(tmp, "w") as handle_file:
             json.dump(doc, handle_file)
         os.replace(tmp, manifest)
         return manifest
+
+    def _serve_dmabufs(self, bases: List[Tuple[int, int]]) -> str:
+        """Export every ``(base, size)`` allocation as a dma-buf and serve the descriptors, in
+        order, to each process of this uid that connects to the returned abstract socket
+        name (messages of ``FDS_PER_MESSAGE`` descriptors: ``{"first", "offsets"}`` + fds,
+        then ``{"end": n}``).  A daemon thread; it lives as long as this process."""
+        lib = hip()
+        fds: List[int] = []
+        offsets: List[int] = []
+        fd, off = ctypes.c_int(-1), ctypes.c_uint64(0)
+        try:
+            for key, sz in bases:
+                lib.check(lib.tpi_dmabuf_export(ctypes.c_void_p(key), sz, ctypes.byref(fd),
+                                                ctypes.byref(off)), "tpi_dmabuf_export")
+                fds.append(fd.value)
+                offsets.append(int(off.value))
+        except BaseException:
+            for f in fds:
+                os.close(f)
+            raise
+        name = "tpi-hbm-%d-%s" % (os.getpid(), os.urandom(6).hex())
+        server = socket.socket(socket.AF_UNIX, socket.SOCK_SEQPACKET)
+        server.bind("\0" + name)
+        server.listen(4)
+        uid = os.getuid()
+
+        def serve() -> None:
+            while True:
+                try:
+                    conn, _ = server.accept()
+                except OSError:
+                    return
+                try:
+                    cred = conn.getsockopt(socket.SOL_SOCKET, socket.SO_PEERCRED,
+                                           struct.calcsize("3i"))
+                    if struct.unpack("3i", cred)[1] != uid:
+                        continue  # another user's process: nothing to see
+                    for i in range(0, len(fds), FDS_PER_MESSAGE):
+                        chunk = fds[i:i + FDS_PER_MESSAGE]
+                        msg = json.dumps({"first": i, "offsets": offsets[i:i + len(chunk)]})
+                        socket.send_fds(conn, [msg.encode()], chunk)
+                    conn.send(json.dumps({"end": len(fds)}).encode())
+                except OSError:
+                    pass
+                finally:
+                    conn.close()
+
+        self._dmabuf_server = (server, fds)
+        threading.Thread(target=serve, name="tpi-dmabuf-serve", daemon=True).start()
+        return name
+
+    def _close_dmabuf_server(self) -> None:
+        served = getattr(self, "_dmabuf_server", None)
+        if served is None:
+            return
+        self._dmabuf_server = None
+        server, fds = served
+        try:
+            server.shutdown(socket.SHUT_RDWR)
+        except OSError:
+            pass
+        server.close()
+        for f in fds:
+            try:
+                os.close(f)
+            except OSError:
+                pass
 
     def _hbm_doc(self) -> Optional[Dict]:
         manifest = self._hbm_manifest_path()
@@ -1594,8 +1688,9 @@ class Checkpointer:
 
     def restore_hbm(self, strict: bool = True) -> TransferResult:
         """Copy the state of a preempted predecessor on the same GPU straight from its HBM
-        (HIP IPC; one fused copy pass + a read-back verify, every tile's digest checked) into the
-        bound tensors."""
+        (its allocations mapped here over dma-buf, or HIP IPC for an ``ipc`` export; one
+        fused copy pass + a read-back verify, every tile's digest checked) into the bound
+        tensors."""
         if not self.claim_hbm():
             raise CheckpointError("the HBM hand-off is claimed by another process (withdrawn "
                                   "by its exporter, or taken by another successor)")
@@ -1606,30 +1701,77 @@ class Checkpointer:
         import torch
 
         lib = hip()
-        bases: List[Optional[int]] = [None] * len(doc["allocations"])
+        route = doc.get("route", "ipc")
+        n = len(doc["allocations"])
+        bases: List[Optional[int]] = [None] * n   # each allocation's base in this process
+        mapped: List[Optional[int]] = [None] * n  # what to unmap (dma-buf: the mapping)
         t0 = time.perf_counter()
+        try:
+            limit = float(os.environ.get("TPI_IPC_OPEN_TIMEOUT", "10"))
+        except ValueError:
+            limit = 10.0
 
-        def open_one(i: int) -> None:
+        def open_ipc(i: int) -> None:
             base = ctypes.c_void_p()
             lib.check(lib.tpi_ipc_open(bytes.fromhex(doc["allocations"][i]), self.device_index,
                                        ctypes.byref(base)), "tpi_ipc_open")
-            bases[i] = base.value
+            bases[i] = mapped[i] = base.value
+
+        def open_dmabufs() -> None:
+            # the predecessor's server sends the descriptors in order, in batches; each is
+            # mapped here and closed at once (the mapping keeps its own reference)
+            sock = socket.socket(socket.AF_UNIX, socket.SOCK_SEQPACKET)
+            sock.settimeout(limit)
+            ptr, size = ctypes.c_void_p(), ctypes.c_uint64(0)
+            with sock:
+                sock.connect("\0" + doc["socket"])
+                while True:
+                    msg, fds, _, _ = socket.recv_fds(sock, 1 << 16, FDS_PER_MESSAGE)
+                    try:
+                        if not msg:
+                            raise CheckpointError("the predecessor closed the hand-off socket")
+                        head = json.loads(msg)
+                        if "end" in head:
+                            if head["end"] != n or any(b is None for b in bases):
+                                raise CheckpointError("hand-off socket sent %s of %d "
+                                                      "allocations" % (head["end"], n))
+                            return
+                        for k, fd in enumerate(fds):
+                            i = int(head["first"]) + k
+                            lib.check(lib.tpi_dmabuf_import(self.device_index, fd,
+                                                            ctypes.byref(ptr),
+                                                            ctypes.byref(size)),
+                                      "tpi_dmabuf_import")
+                            mapped[i] = ptr.value
+                            off = int(head["offsets"][k])
+                            if int(size.value) < off + int(doc["allocations"][i]):
+                                # never let a kernel read past what was mapped
+                                raise CheckpointError(
+                                    "dma-buf %d maps %d bytes, the allocation needs %d" % (
+                                        i, int(size.value), off + int(doc["allocations"][i])))
+                            bases[i] = ptr.value + off
+                    finally:
+                        for fd in fds:
+                            os.close(fd)
 
         def close_one(i: int) -> None:
-            if bases[i] is not None:
-                lib.tpi_ipc_close(ctypes.c_void_p(bases[i]))
-                bases[i] = None
+            if mapped[i] is not None:
+                if route == "dmabuf":
+                    lib.tpi_dmabuf_unmap(ctypes.c_void_p(mapped[i]))
+                else:
+                    lib.tpi_ipc_close(ctypes.c_void_p(mapped[i]))
+                mapped[i] = bases[i] = None
 
         def each(fn) -> None:
             # one mapping per predecessor allocation (a model's state is hundreds of them);
             # opens and closes are independent driver calls, so 8 threads overlap them
-            if len(bases) > 8:
+            if n > 8:
                 from concurrent.futures import ThreadPoolExecutor
 
                 with ThreadPoolExecutor(8) as pool:
-                    list(pool.map(fn, range(len(bases))))
+                    list(pool.map(fn, range(n)))
             else:
-                for i in range(len(bases)):
+                for i in range(n):
                     fn(i)
 
         def close_all() -> None:
@@ -1639,16 +1781,12 @@ class Checkpointer:
             self.release_hbm_claim()  # nothing of the predecessor is mapped any more
 
         def open_all() -> None:
-            # Bounded: an import that never returns (round 4: hipIpcOpenMemHandle on some
-            # allocations blocked forever) must not strand this successor holding the claim
-            # while its predecessor waits on it -- past TPI_IPC_OPEN_TIMEOUT the HBM route is
-            # given up (the caller restores from the host copy).  The openers are daemon
-            # threads: one stuck in the driver cannot hold up this process's exit.
-            try:
-                limit = float(os.environ.get("TPI_IPC_OPEN_TIMEOUT", "10"))
-            except ValueError:
-                limit = 10.0
-            todo = list(range(len(bases)))
+            # Bounded: an import that never returns (round 4: hipIpcOpenMemHandle on
+            # allocations of 2 GiB or more spins forever) must not strand this successor
+            # holding the claim while its predecessor waits on it -- past TPI_IPC_OPEN_TIMEOUT
+            # the HBM route is given up (the caller restores from the host copy).  The openers
+            # are daemon threads: one stuck in the driver cannot hold up this process's exit.
+            todo = list(range(n))
             lock = threading.Lock()
             errors: List[BaseException] = []
 
@@ -1659,14 +1797,23 @@ class Checkpointer:
                             return
                         i = todo.pop()
                     try:
-                        open_one(i)
+                        open_ipc(i)
                     except BaseException as error:  # re-raised by the caller
                         with lock:
                             errors.append(error)
                         return
 
-            workers = [threading.Thread(target=worker, name="tpi-ipc-open", daemon=True)
-                       for _ in range(min(8, len(bases)) or 1)]
+            def receiver() -> None:
+                try:
+                    open_dmabufs()
+                except BaseException as error:
+                    with lock:
+                        errors.append(error)
+
+            workers = ([threading.Thread(target=receiver, name="tpi-dmabuf-open", daemon=True)]
+                       if route == "dmabuf" else
+                       [threading.Thread(target=worker, name="tpi-ipc-open", daemon=True)
+                        for _ in range(min(8, n) or 1)])
             for w in workers:
                 w.start()
             deadline = time.monotonic() + limit
@@ -1876,6 +2023,7 @@ class Checkpointer:
             self.slots = []
             self.region.close()
             self.region = None
+        self._close_dmabuf_server()
         if self.plan is not None and hasattr(self.plan, "unbind"):
             self.plan.unbind()  # the tensors' HBM can go with the caller's references
 

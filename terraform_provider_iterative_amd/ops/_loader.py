@@ -142,6 +142,11 @@ class HipLib:
             "tpi_ipc_handle": (i32, [vp, c.c_char_p]),
             "tpi_ipc_open": (i32, [c.c_char_p, i32, c.POINTER(vp)]),
             "tpi_ipc_close": (i32, [vp]),
+            "tpi_dmabuf_available": (i32, []),
+            "tpi_dmabuf_export": (i32, [vp, u64, c.POINTER(i32), c.POINTER(u64)]),
+            "tpi_dmabuf_close": (i32, [i32]),
+            "tpi_dmabuf_import": (i32, [i32, i32, c.POINTER(vp), c.POINTER(u64)]),
+            "tpi_dmabuf_unmap": (i32, [vp]),
             "tpi_comm_unique_id": (i32, [c.c_char_p]),
             "tpi_comm_init_rank": (vp, [c.c_char_p, i32, i32, i32]),
             "tpi_comm_init_all": (i32, [i32, c.POINTER(i32), c.POINTER(vp)]),

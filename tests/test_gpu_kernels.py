@@ -626,17 +626,21 @@ sys.stdin.readline()  # hold the memory until the successor is done
 '''
 
 
-@pytest.mark.parametrize("route", ["fused", "staged"])
-def test_hbm_handoff_copies_a_live_predecessors_tensors(tmp_path, monkeypatch, route):
-    """Same-GPU hand-off: the predecessor exports IPC handles of its tensors; the successor
-    copies them device to device, CRC-verified, with no host copy.  The default route is the
-    fused tensor-to-tensor copy plus a read-back verify; TPI_HANDOFF_COPY=staged selects pack +
-    unpack through a staging buffer.  Transposed and strided views take the element-wise path."""
+@pytest.mark.parametrize("route,hbm_route", [("fused", "dmabuf"), ("staged", "dmabuf"),
+                                             ("fused", "ipc")])
+def test_hbm_handoff_copies_a_live_predecessors_tensors(tmp_path, monkeypatch, route, hbm_route):
+    """Same-GPU hand-off: the predecessor exports its tensors' allocations (dma-buf
+    descriptors over a Unix socket by default, HIP IPC handles with TPI_HBM_ROUTE=ipc); the
+    successor copies them device to device, digest-verified, with no host copy.  The default
+    copy is the fused tensor-to-tensor copy plus a read-back verify; TPI_HANDOFF_COPY=staged
+    selects pack + unpack through a staging buffer.  Transposed and strided views take the
+    element-wise path."""
     import subprocess
     import sys
 
     if route == "staged":
         monkeypatch.setenv("TPI_HANDOFF_COPY", "staged")
+    monkeypatch.setenv("TPI_HBM_ROUTE", hbm_route)
 
     root = __import__("os").path.dirname(__import__("os").path.dirname(__file__))
     path = str(tmp_path / "spill")
@@ -669,11 +673,76 @@ def test_hbm_handoff_copies_a_live_predecessors_tensors(tmp_path, monkeypatch, r
         child.wait(60)
 
 
+BIG_EXPORTER = r'''
+import sys, torch
+sys.path.insert(0, %(root)r)
+from terraform_provider_iterative_amd.checkpoint import Checkpointer
+g = torch.Generator(device="cuda").manual_seed(5)
+t = {"emb": torch.empty(int(4.2 * 2 ** 30) // 4, device="cuda"),
+     "w": torch.empty(int(2.5 * 2 ** 30) // 2, device="cuda", dtype=torch.bfloat16),
+     "n": torch.randn(4096, device="cuda", generator=g)}
+t["emb"].normal_(generator=g)
+t["w"].normal_(generator=g)
+ck = Checkpointer(t, path=%(path)r, tile_bytes=1 << 20, chunk_bytes=256 << 20)
+print("exported", ck.export_hbm(), flush=True)
+sys.stdin.readline()  # hold the memory until the successor is done
+'''
+
+
+def test_hbm_handoff_of_allocations_beyond_the_ipc_limit(tmp_path, monkeypatch):
+    """VERDICT r4 #1: a state holding 4.2 GiB and 2.5 GiB tensors -- the fp32 embedding / Adam
+    moments of a large vocabulary -- hands off device to device over the dma-buf route,
+    bit-exact (HIP IPC imports of such allocations never return,
+    profiles/round5/ipc_cause.md)."""
+    import os
+    import subprocess
+    import sys
+
+    monkeypatch.setenv("TPI_HBM_ROUTE", "dmabuf")
+    monkeypatch.setenv("TPI_IPC_OPEN_TIMEOUT", "30")
+    root = os.path.dirname(os.path.dirname(__file__))
+    path = str(tmp_path / "spill")
+    child = subprocess.Popen([sys.executable, "-c", BIG_EXPORTER % {"root": root, "path": path}],
+                             stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+    try:
+        line = child.stdout.readline()
+        assert line.startswith("exported"), line
+        with open(path + ".hbm") as f:
+            doc = __import__("json").load(f)
+        assert doc["route"] == "dmabuf" and max(doc["allocations"]) >= 4 << 30, doc["allocations"]
+        dst = {"emb": torch.zeros(int(4.2 * 2 ** 30) // 4, device="cuda"),
+               "w": torch.zeros(int(2.5 * 2 ** 30) // 2, device="cuda", dtype=torch.bfloat16),
+               "n": torch.zeros(4096, device="cuda")}
+        from terraform_provider_iterative_amd.checkpoint import Checkpointer
+
+        ck = Checkpointer(dst, path=path, tile_bytes=1 << 20, chunk_bytes=256 << 20)
+        assert ck.hbm_ready()
+        res = ck.restore_hbm()
+        torch.cuda.synchronize()
+        assert res.bad_tiles == 0
+        ck.wait_hbm_close()
+        g = torch.Generator(device="cuda").manual_seed(5)  # the exporter's draw order
+        assert torch.equal(dst["n"], torch.randn(4096, device="cuda", generator=g))
+        want = torch.empty(int(4.2 * 2 ** 30) // 4, device="cuda")
+        want.normal_(generator=g)
+        assert torch.equal(dst["emb"], want)
+        del want
+        w = torch.empty(int(2.5 * 2 ** 30) // 2, device="cuda", dtype=torch.bfloat16)
+        w.normal_(generator=g)
+        assert torch.equal(dst["w"], w)
+        del w
+        ck.close()
+    finally:
+        child.stdin.write("\n")
+        child.stdin.flush()
+        child.wait(60)
+
+
 def test_hbm_export_refuses_allocations_at_the_ipc_limit(tmp_path, monkeypatch):
-    """IPC imports of PyTorch allocations of 2 GiB or more block in hipIpcOpenMemHandle
-    (profiles/round4/ipc_lifetime.md), so export_hbm refuses a state holding one before it
-    publishes anything: the successor sees no hand-off and restores from the host copy.  The
-    limit is lowered here so that small tensors exercise it."""
+    """The IPC route (TPI_HBM_ROUTE=ipc): imports of allocations of 2 GiB or more never return
+    in hipIpcOpenMemHandle (profiles/round5/ipc_cause.md), so export_hbm refuses a state holding
+    one before it publishes anything: the successor sees no hand-off and restores from the host
+    copy.  The limit is lowered here so that small tensors exercise it."""
     from terraform_provider_iterative_amd.checkpoint import CheckpointError, Checkpointer
     from terraform_provider_iterative_amd.checkpoint import checkpointer as ckmod
 
@@ -681,6 +750,7 @@ def test_hbm_export_refuses_allocations_at_the_ipc_limit(tmp_path, monkeypatch):
 
     from terraform_provider_iterative_amd.ops import hip
 
+    monkeypatch.setenv("TPI_HBM_ROUTE", "ipc")
     assert ckmod.IPC_MAX_ALLOC == 2 << 30
     t = {"a": torch.randn(1 << 18, device="cuda"), "b": torch.randn(4 << 20, device="cuda")}
     base, size = ctypes.c_uint64(0), ctypes.c_uint64(0)

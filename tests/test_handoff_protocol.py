@@ -484,3 +484,195 @@ def test_a_stuck_ipc_import_gives_up_the_hbm_route_and_the_claim(tmp_path, monke
     assert time.monotonic() - t0 < 5.0
     assert ck.hbm_claim_owner() is None  # the claim is gone: the predecessor may go
     stuck.set()
+
+
+# -- the hand-off state machine, one row per mode (docs/ARCHITECTURE.md "Hand-off modes") -------
+# A rank that speaks the notify protocol for every supervisor-visible mode.  Incarnation 0 is
+# preempted: "released", then it waits for the supervisor's exit request (SIGUSR2).  The
+# successor -- a fresh process (cold), or a standby activated by "go" (warm: started at the
+# preemption; hot: started with the rank) -- reports what a real successor reports.
+MODE_RANK = r'''#!%(python)s
+import os, signal, sys, time
+out, mode = %(out)r, %(mode)r
+fd = int(os.environ["TPI_NOTIFY_FD"])
+def note(name):
+    with open(os.path.join(out, name), "w") as f:
+        f.write(repr(time.time()))
+if mode in ("warm", "hot"):
+    os.write(fd, b"standby\n")  # preemption.standby(): standbys are welcome
+if os.environ.get("TPI_STANDBY") == "1":
+    msg = os.read(int(os.environ["TPI_STANDBY_FD"]), 64)
+    if not msg.startswith(b"go"):
+        os._exit(0)  # discarded
+    note("activated")
+if int(os.environ["TPI_RESTART_COUNT"]) == 0:
+    signal.pthread_sigmask(signal.SIG_BLOCK, {signal.SIGTERM, signal.SIGUSR2})
+    print("ready", flush=True)
+    signal.sigwait({signal.SIGTERM})
+    os.write(fd, b"released\n")
+    signal.sigwait({signal.SIGUSR2})
+    note("usr2")
+    os._exit(143)
+if mode.startswith("hbm"):
+    os.write(fd, b"restored hbm\n")
+    time.sleep(0.5)
+    if mode == "hbm-successor-dies":
+        note("successor-exit")
+        os._exit(0)
+    note("closed")
+    os.write(fd, b"closed\n")
+else:
+    note("restored")
+    os.write(fd, b"restored\n")
+time.sleep(0.2)
+print("successor done", flush=True)
+'''
+
+# mode -> (spec extras, the predecessor's release reason, the successor's start, the note
+# the predecessor's SIGUSR2 may not precede)
+HANDOFF_MODES = {
+    "cold": ({}, "successor restored", "fresh", "restored"),
+    "warm": ({"standby": True}, "successor restored", "warm standby", "restored"),
+    "hot": ({"standby": True, "standby_hot": True}, "successor restored", "warm standby",
+            "restored"),
+    "hbm": ({}, "successor closed the HBM hand-off",
+            "fresh", "closed"),
+    "hbm-successor-dies": ({}, "successor exited", "fresh", "successor-exit"),
+}
+
+
+@pytest.mark.parametrize("mode", sorted(HANDOFF_MODES))
+def test_handoff_mode_row(binary, tmp_path, mode):
+    extra, why, start, gate = HANDOFF_MODES[mode]
+    out = tmp_path / "out"
+    out.mkdir()
+    script = MODE_RANK % {"python": sys.executable, "out": str(out), "mode": mode}
+    task, spec = _spec(tmp_path, script, **extra)
+    sup = subprocess.Popen([binary, spec], stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    try:
+        deadline = time.time() + 30
+        while time.time() < deadline and not any(
+                "ready" in (task / "reports" / n).read_text()
+                for n in os.listdir(task / "reports") if n.startswith("task-")):
+            time.sleep(0.02)
+        if mode == "hot":  # the hot standby is up before the preemption
+            while time.time() < deadline and "standby-start" not in [
+                    e["code"] for e in _events(task)]:
+                time.sleep(0.02)
+        sup.send_signal(signal.SIGUSR1)  # preempt
+        _, err = sup.communicate(timeout=60)
+    finally:
+        if sup.poll() is None:
+            sup.kill()
+    assert sup.returncode == 0, err[-2000:]
+    events = _events(task)
+    codes = [e["code"] for e in events]
+    t = lambda code: next(e["time"] for e in events if e["code"] == code)  # noqa: E731
+    # released -> the successor runs -> it lets the predecessor go -> the task settles and ends
+    for a, b in (("preempt-requested", "rank-released"),
+                 ("rank-released", "predecessor-exit-requested"),
+                 ("predecessor-exit-requested", "supervisor-settled"),
+                 ("supervisor-settled", "supervisor-exit")):
+        assert t(a) <= t(b), (a, b, codes)
+    req = [e for e in events if e["code"] == "predecessor-exit-requested"]
+    assert len(req) == 1 and req[0]["description"][-1] == why, req
+    # the predecessor is never told to go before the successor is done with it
+    assert float((out / "usr2").read_text()) >= float((out / gate).read_text())
+    starts = [e for e in events if e["code"] == "rank-start"]
+    assert len(starts) == 2, starts
+    assert (starts[1]["description"][-1] == "warm standby") == (start == "warm standby"), starts
+    if mode == "hot":
+        assert t("standby-start") < t("preempt-requested")
+    if mode == "warm":
+        assert t("preempt-requested") <= t("standby-start")
+    status = [n for n in os.listdir(task / "reports") if n.startswith("status-")]
+    assert len(status) == 1, status  # the successor's; the predecessor's release is no status
+
+
+def test_dmabuf_route_hands_every_allocation_over_the_socket(tmp_path, monkeypatch):
+    """The default hand-off route (round 5): the exporter serves one dma-buf descriptor per
+    allocation over an abstract Unix socket (batches of FDS_PER_MESSAGE, SCM_RIGHTS); the
+    successor maps each, points the source segments at base + offset + the tensor's place in
+    the allocation, copies, and unmaps them all behind the restore.  Descriptors are stand-ins
+    (/dev/null) and mappings fake addresses: no GPU."""
+    import numpy as np
+
+    import torch
+
+    from terraform_provider_iterative_amd.checkpoint import checkpointer as ckmod
+    from terraform_provider_iterative_amd.ops.packing import SEG_DTYPE
+
+    n_alloc = ckmod.FDS_PER_MESSAGE + 37  # two batches
+    sizes = [(3 << 30) + i * 4096 for i in range(n_alloc)]  # >= 2 GiB: the IPC route's limit
+    exported, imported, unmapped = [], {}, []
+
+    class FakeLib:
+        def tpi_dmabuf_export(self, ptr, size, fd, off):
+            fd._obj.value = os.open(os.devnull, os.O_RDONLY)
+            off._obj.value = 4096 if len(exported) % 2 else 0
+            exported.append((ptr.value, size))
+            return 0
+
+        def tpi_dmabuf_import(self, device, fd, ptr, size):
+            os.fstat(fd)  # a live descriptor arrived
+            ptr._obj.value = 0x7000_0000_0000 + len(imported) * (1 << 36)
+            size._obj.value = (1 << 35)
+            imported[ptr._obj.value] = fd
+            return 0
+
+        def tpi_dmabuf_unmap(self, ptr):
+            unmapped.append(ptr.value)
+            return 0
+
+        def check(self, rc, what):
+            assert rc == 0, what
+
+    monkeypatch.setattr(ckmod, "hip", lambda *a, **k: FakeLib())
+
+    class Exporter:
+        _serve_dmabufs = Checkpointer._serve_dmabufs
+        _close_dmabuf_server = Checkpointer._close_dmabuf_server
+
+    exporter = Exporter()
+    bases = [(0x1000_0000_0000 + i * (1 << 33), sz) for i, sz in enumerate(sizes)]
+    name = exporter._serve_dmabufs(bases)
+    assert len(exporter._dmabuf_server[1]) == n_alloc
+
+    segs = np.zeros(n_alloc, dtype=SEG_DTYPE)
+    where = [[i, 512 * i] for i in range(n_alloc)]
+    copied = {}
+
+    class Engine:
+        def copy_segments(self, src, plan, sig):
+            copied["src"] = src.copy()
+
+            class Res:
+                bad_tiles = 0
+            return Res()
+
+    class Successor(_FakeHandoff):
+        device_index = 0
+        engine = Engine()
+        restore_hbm = Checkpointer.restore_hbm
+
+        class plan:
+            pass
+
+        def _hbm_doc(self):
+            return {"route": "dmabuf", "socket": name, "allocations": sizes, "where": where,
+                    "segs": segs.tobytes().hex()}
+
+    Successor.plan.segs = segs
+    monkeypatch.setattr(torch.cuda, "current_stream",
+                        lambda *a: type("S", (), {"cuda_stream": 0})())
+    ck = Successor(str(tmp_path / "spill"))
+    ck.restore_hbm()
+    ck._hbm_closer.join(10)
+    src = copied["src"]
+    maps = sorted(imported)
+    for i in range(n_alloc):
+        off = 4096 if i % 2 else 0
+        assert int(src[i]["ptr"]) == maps[i] + off + 512 * i
+    assert sorted(unmapped) == maps  # every mapping released, after the copy
+    assert ck.hbm_claim_owner() is None
+    exporter._close_dmabuf_server()
