@@ -1723,6 +1723,10 @@ int tpi_copy_segments(tpi_engine* e, const tpi_seg* src, const tpi_seg* dst, int
                       "hipMalloc(digests)");
     if (good) e->digest_cap = std::max<uint64_t>(ntiles, 1024);
   }
+  // TPI_HANDOFF_VERIFY=none skips the read-back pass (measurement only: the copy is then
+  // unverified; profiles/round5/handoff_kernels.md)
+  const char* verify_env = getenv("TPI_HANDOFF_VERIFY");
+  const bool readback = !(verify_env && strcmp(verify_env, "none") == 0);
   uint64_t nchunks = 0;
   // No staging buffer bounds the fused route's spans: 4 GiB (4096 one-MiB tiles, 16
   // workgroups per CU) keeps the chip full, where a 256 MB chunk is one workgroup per CU.
@@ -1733,9 +1737,10 @@ int tpi_copy_segments(tpi_engine* e, const tpi_seg* src, const tpi_seg* dst, int
       good = ok(tpi_launch_stream_copy_hash(d_src, e->d_segs, n, base, len, total, tile,
                                             TPI_SYNC_SEED, e->d_digest, nullptr, e->compute),
                 "copy") &&
-             ok(tpi_launch_stream_copy_hash(e->d_segs, nullptr, n, base, len, total, tile,
-                                            TPI_SYNC_SEED, e->d_digest, e->d_bad, e->compute),
-                "verify");
+             (!readback ||
+              ok(tpi_launch_stream_copy_hash(e->d_segs, nullptr, n, base, len, total, tile,
+                                             TPI_SYNC_SEED, e->d_digest, e->d_bad, e->compute),
+                 "verify"));
     else
       good = ok(tpi_launch_stream_copy(d_src, e->d_segs, n, base, len, tile, e->tables,
                                        e->d_crcs, init_full, init_last, nullptr, e->compute),
