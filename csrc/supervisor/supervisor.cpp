@@ -1658,6 +1658,35 @@ class Supervisor {
   static constexpr double kTraceInterval = 0.1;
   static constexpr int kTraceMax = 64;  // events per process
 
+  static std::string thread_waits(pid_t pid) {
+    std::string out;
+    char path[96], buf[512];
+    snprintf(path, sizeof(path), "/proc/%d/task", (int)pid);
+    DIR* d = opendir(path);
+    if (!d) return "-";
+    while (struct dirent* e = readdir(d)) {
+      if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
+      std::string one = e->d_name;
+      snprintf(path, sizeof(path), "/proc/%d/task/%s/stat", (int)pid, e->d_name);
+      if (read_small(path, buf, sizeof(buf))) {
+        const char* rp = strrchr(buf, ')');
+        one += std::string(":") + (rp && rp[1] == ' ' ? rp[2] : '?');
+      }
+      snprintf(path, sizeof(path), "/proc/%d/task/%s/wchan", (int)pid, e->d_name);
+      if (read_small(path, buf, sizeof(buf)) && buf[0]) one += std::string(":") + buf;
+      snprintf(path, sizeof(path), "/proc/%d/task/%s/stack", (int)pid, e->d_name);
+      if (read_small(path, buf, sizeof(buf))) {  // "[<0>] func+0x../0x..\n..."
+        std::string top(buf);
+        top = top.substr(0, top.find('\n'));
+        const size_t sp = top.find(' ');
+        one += ":" + (sp == std::string::npos ? top : top.substr(sp + 1));
+      }
+      out += (out.empty() ? "" : " ") + one;
+    }
+    closedir(d);
+    return out.empty() ? "-" : out;
+  }
+
   void trace_exits(double t) {
     if (!s_.exit_trace) return;
     for (auto& d : detached_) {
@@ -1690,10 +1719,17 @@ class Supervisor {
       ++d.trace_events;
       char el[48];
       snprintf(el, sizeof(el), "+%.3f s", t - d.exit_requested_at);
-      event("exit-trace", {"rank " + std::to_string(d.index), "machine " + d.uuid,
-                           "pid " + std::to_string(d.pid), el, std::string("state ") + state,
-                           std::string("wchan ") + wchan, "rss " + std::to_string(rss_mb) + " MB",
-                           "threads " + std::to_string(threads)});
+      std::vector<std::string> desc = {"rank " + std::to_string(d.index), "machine " + d.uuid,
+                                       "pid " + std::to_string(d.pid), el,
+                                       std::string("state ") + state,
+                                       std::string("wchan ") + wchan,
+                                       "rss " + std::to_string(rss_mb) + " MB",
+                                       "threads " + std::to_string(threads)};
+      // The last threads of an exiting process (the leader already a zombie): where each one
+      // waits in the kernel, and the top of its kernel stack where /proc lets us read it
+      // (root only) -- the teardown's slow path, named.
+      if (threads > 0 && threads <= 4) desc.push_back("tasks " + thread_waits(d.pid));
+      event("exit-trace", desc);
     }
   }
 
