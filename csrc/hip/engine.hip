@@ -1730,7 +1730,11 @@ int tpi_copy_segments(tpi_engine* e, const tpi_seg* src, const tpi_seg* dst, int
   uint64_t nchunks = 0;
   // No staging buffer bounds the fused route's spans: 4 GiB (4096 one-MiB tiles, 16
   // workgroups per CU) keeps the chip full, where a 256 MB chunk is one workgroup per CU.
-  const uint64_t span = std::max<uint64_t>(e->chunk, ((4ull << 30) / tile) * tile);
+  // TPI_HANDOFF_SPAN_MB: bytes per launch (0: the whole state in one copy + one verify launch)
+  uint64_t span_bytes = 4ull << 30;
+  if (const char* v = getenv("TPI_HANDOFF_SPAN_MB"))
+    span_bytes = strtoull(v, nullptr, 10) ? strtoull(v, nullptr, 10) << 20 : total;
+  const uint64_t span = std::max<uint64_t>(e->chunk, std::max<uint64_t>(span_bytes / tile, 1) * tile);
   for (uint64_t base = 0, k = 0; good && fused && base < total; base += span, ++k) {
     const uint64_t len = std::min(span, total - base);
     if (xxh)

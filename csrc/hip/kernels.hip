@@ -768,7 +768,7 @@ __global__ __launch_bounds__(WG) void k_shard_hash(const uint8_t* __restrict__ d
 // (profiles/handoff_hash_round3.md).  Workgroup i handles tile tile0 + i.
 enum { HASH_ONLY = 0, HASH_COPY = 1, HASH_VERIFY = 2 };
 
-template <int KIND>
+template <int KIND, int U = UNROLL>
 __global__ __launch_bounds__(WG) void k_stream_hash(const tpi_seg* __restrict__ segs,
                                                     const tpi_seg* __restrict__ dsegs, int nseg,
                                                     uint64_t tile0, uint64_t total,
@@ -789,28 +789,28 @@ __global__ __launch_bounds__(WG) void k_stream_hash(const tpi_seg* __restrict__ 
   uint64_t nwords = 0;
   const uint64_t full_rows = len / TPI_ROW_BYTES;
   uint64_t row = 0;
-  for (; row + UNROLL <= full_rows; row += UNROLL) {
-    u32x4 w[UNROLL];
+  for (; row + U <= full_rows; row += U) {
+    u32x4 w[U];
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
+    for (int u = 0; u < U; ++u) {
       const uint64_t pos = gbase + (row + u) * TPI_ROW_BYTES + lane * 16;
       advance(segs, nseg, pos, cur);
       w[u] = gather16(segs, cur, pos, nullptr, false);
     }
     if (KIND == HASH_COPY) {
 #pragma unroll
-      for (int u = 0; u < UNROLL; ++u) {
+      for (int u = 0; u < U; ++u) {
         const uint64_t pos = gbase + (row + u) * TPI_ROW_BYTES + lane * 16;
         advance(dsegs, nseg, pos, dcur);
         scatter16(dsegs, dcur, pos, w[u], false);
       }
     }
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
+    for (int u = 0; u < U; ++u) {
       va = tpi_xxh_round(va, ((uint64_t)w[u].y << 32) | w[u].x);
       vb = tpi_xxh_round(vb, ((uint64_t)w[u].w << 32) | w[u].z);
     }
-    nwords += UNROLL;
+    nwords += U;
   }
   for (uint64_t rel = row * TPI_ROW_BYTES + lane * 16; rel < len; rel += TPI_ROW_BYTES) {
     advance(segs, nseg, gbase + rel, cur);
@@ -1004,12 +1004,27 @@ extern "C" hipError_t tpi_launch_stream_copy_hash(const tpi_seg* src, const tpi_
   if (stream_base % tile_bytes || stream_base + len > total) return hipErrorInvalidValue;
   const uint64_t tile0 = stream_base / tile_bytes;
   const dim3 grid((unsigned)((len + tile_bytes - 1) / tile_bytes)), block(WG);
-  if (dst)
-    hipLaunchKernelGGL(k_stream_hash<HASH_COPY>, grid, block, 0, stream, src, dst, nseg, tile0,
-                       total, tile_bytes, seed, digests, bad);
-  else
-    hipLaunchKernelGGL(k_stream_hash<HASH_VERIFY>, grid, block, 0, stream, src, nullptr, nseg,
-                       tile0, total, tile_bytes, seed, digests, bad);
+  // rows in flight per lane (16 B each): TPI_HANDOFF_UNROLL=16 doubles the bytes each lane
+  // keeps in flight (profiles/round5/handoff_kernels.md)
+  static const int unroll = [] {
+    const char* v = getenv("TPI_HANDOFF_UNROLL");
+    return v && atoi(v) == 16 ? 16 : (v && atoi(v) == 4 ? 4 : UNROLL);
+  }();
+#define TPI_HASH_LAUNCH(UU)                                                                   \
+  if (dst)                                                                                   \
+    hipLaunchKernelGGL((k_stream_hash<HASH_COPY, UU>), grid, block, 0, stream, src, dst, nseg, \
+                       tile0, total, tile_bytes, seed, digests, bad);                         \
+  else                                                                                       \
+    hipLaunchKernelGGL((k_stream_hash<HASH_VERIFY, UU>), grid, block, 0, stream, src, nullptr, \
+                       nseg, tile0, total, tile_bytes, seed, digests, bad);
+  if (unroll == 16) {
+    TPI_HASH_LAUNCH(16)
+  } else if (unroll == 4) {
+    TPI_HASH_LAUNCH(4)
+  } else {
+    TPI_HASH_LAUNCH(UNROLL)
+  }
+#undef TPI_HASH_LAUNCH
   return hipGetLastError();
 }
 
