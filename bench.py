@@ -146,7 +146,8 @@ def first_log_latency(timeout: float = 60.0, parallelism: int = 1):
 
 E2E_KEYS = ("ok", "verified", "status", "signal_to_restored_s", "save_s",
             "rank_start_to_restored_s", "saved_to_restored_s", "signal_to_durable_s", "streamed",
-            "warm_standby_activated", "hot_standby", "standby_pinned_wait_s", "restore_journal")
+            "warm_standby_activated", "hot_standby", "standby_pinned_wait_s", "restore_journal",
+            "extra_tensors_gib")
 
 
 def preempt_e2e(total_gb: float, codec: str, timeout: float) -> dict:
@@ -160,7 +161,9 @@ def preempt_e2e(total_gb: float, codec: str, timeout: float) -> dict:
     import subprocess
 
     runs = {}
-    for name, flags in (("cold", []), ("hot", ["--hot"])):
+    # the hot run's state also holds a 4.2 GiB and a 2.5 GiB tensor (a large vocabulary's fp32
+    # embedding and moments): allocations HIP IPC cannot hand off, the dma-buf route can
+    for name, flags in (("cold", []), ("hot", ["--hot", "--extra-gib", "4.2,2.5"])):
         cmd = [sys.executable, os.path.join(ROOT, "bench", "bench_preempt.py"), "--gb",
                repr(total_gb), "--codec", codec, "--timeout", repr(timeout)] + flags
         t0 = time.perf_counter()

@@ -80,7 +80,15 @@ if resuming and materialize:
     ck.close()
     os.remove(spill)
     sys.exit(0 if ok else 3)
-tensors = synthetic_checkpoint(nbytes, 8192, dev, fill=not resuming)
+extra = %(extra)r  # GiB each: single tensors of 2 GiB or more (a large vocabulary's fp32
+                   # embedding / Adam moments), beyond what HIP IPC can hand off
+tensors = synthetic_checkpoint(nbytes - int(sum(extra) * 2 ** 30), 8192, dev, fill=not resuming)
+gen = torch.Generator(device=dev).manual_seed(77)
+for i, gib in enumerate(extra):
+    big = torch.empty(int(gib * 2 ** 30) // 4, dtype=torch.float32, device=dev)
+    if not resuming:
+        big.normal_(0, 1e-3, generator=gen)
+    tensors["embedding.%d" %% i] = big
 torch.cuda.synchronize()
 t_alloc = time.time()
 ck = Checkpointer(tensors, path=spill, codec=%(codec)r)
@@ -147,6 +155,9 @@ def main():
                         "allocated group by group while the predecessor frees its HBM")
     p.add_argument("--step-seconds", type=float, default=0.002,
                    help="duration of the rank's (idle) training step")
+    p.add_argument("--extra-gib", default="",
+                   help="comma list: also hold single fp32 tensors of these sizes (GiB) inside "
+                        "the --gb total, e.g. 4.2,2.5")
     p.add_argument("--signal-mode", action="store_true",
                    help="the rank never calls preemption.step(): save in the signal handler")
     args = p.parse_args()
@@ -173,13 +184,15 @@ def main():
                      "codec": args.codec, "prefetch": not args.no_prefetch,
                      "early": args.early_prefetch, "standby": args.standby,
                      "step_s": args.step_seconds, "boundary": not args.signal_mode,
-                     "materialize": args.materialize}
+                     "materialize": args.materialize,
+                     "extra": [float(x) for x in args.extra_gib.split(",") if x.strip()]}
     # the ranks' runtime knobs travel as task variables (the rank environment is the task's)
     rank_env = {"TPI_TASK": "true", "TPI_STREAM_HANDOFF": "0" if args.no_stream else "1"}
     for knob in ("TPI_D2H_ENGINE", "TPI_STREAM_TIMEOUT", "TPI_LINGER_SECONDS",
                  "TPI_HBM_HANDOFF", "TPI_RELEASE_HBM", "TPI_EXPLICIT_TEARDOWN",
                  "HSA_ENABLE_SDMA", "GPU_MAX_HW_QUEUES", "TPI_DIRECT_META",
-                 "TPI_ALLOC_LOOKAHEAD", "TPI_MATERIALIZE_H2D"):
+                 "TPI_ALLOC_LOOKAHEAD", "TPI_MATERIALIZE_H2D", "TPI_HBM_ROUTE",
+                 "TPI_HANDOFF_VERIFY", "TPI_HANDOFF_UNROLL", "TPI_HANDOFF_SPAN_MB"):
         if os.environ.get(knob):
             rank_env[knob] = os.environ[knob]
     spec = Task(size=Size(machine="m+mi355x"),
@@ -193,7 +206,8 @@ def main():
               "hot_standby": args.hot, "stream_handoff": not args.no_stream,
               "save_at": "signal" if args.signal_mode else "step boundary",
               "release_hbm": os.environ.get("TPI_RELEASE_HBM", "1") != "0",
-              "step_seconds": args.step_seconds, "materialize": args.materialize}
+              "step_seconds": args.step_seconds, "materialize": args.materialize,
+              "extra_tensors_gib": [float(x) for x in args.extra_gib.split(",") if x.strip()]}
     os.environ["TPI_WARM_STANDBY"] = "hot" if args.hot else ("1" if args.standby else "0")
     try:
         task.create()

@@ -158,6 +158,32 @@ int check_segments(const tpi_seg* segs, int n, uint64_t total) {
   return 0;
 }
 
+// Do the destination segments occupy disjoint memory?  Extent of a strided segment: from its
+// lowest to its highest element (negative strides included), so interleaved views of one
+// storage count as overlapping -- conservative, which only costs them the inline check.
+bool extents_disjoint(const tpi_seg* segs, int n) {
+  std::vector<std::pair<uint64_t, uint64_t>> ext;
+  ext.reserve((size_t)n);
+  for (int i = 0; i < n; ++i) {
+    if (segs[i].nbytes == 0) continue;
+    uint64_t lo = segs[i].ptr, hi = segs[i].ptr + segs[i].nbytes;
+    if (segs[i].kind != TPI_SEG_CONTIG) {
+      int64_t neg = 0, pos = 0;
+      for (int d = 0; d < segs[i].ndim && d < TPI_MAX_DIMS; ++d) {
+        const int64_t span = (segs[i].sizes[d] - 1) * segs[i].strides[d] * (int64_t)segs[i].elem;
+        (span < 0 ? neg : pos) += span;
+      }
+      lo = segs[i].ptr + neg;  // neg <= 0
+      hi = segs[i].ptr + pos + segs[i].elem;
+    }
+    ext.push_back({lo, hi});
+  }
+  std::sort(ext.begin(), ext.end());
+  for (size_t i = 1; i < ext.size(); ++i)
+    if (ext[i].first < ext[i - 1].second) return false;
+  return true;
+}
+
 }  // namespace
 
 // Error reporting for the other translation units of the library (internal.h).
@@ -1723,15 +1749,23 @@ int tpi_copy_segments(tpi_engine* e, const tpi_seg* src, const tpi_seg* dst, int
                       "hipMalloc(digests)");
     if (good) e->digest_cap = std::max<uint64_t>(ntiles, 1024);
   }
-  // TPI_HANDOFF_VERIFY=none skips the read-back pass (measurement only: the copy is then
-  // unverified; profiles/round5/handoff_kernels.md)
+  // How the destination is verified (TPI_HANDOFF_VERIFY): "readback" -- a second pass
+  // re-hashes the destination and compares digests; "inline" -- the copy kernel reads every
+  // stored word back one row group later and compares it (no second pass over HBM; needs
+  // disjoint destinations, else readback); "none" -- unverified (measurement only).
+  // profiles/round5/handoff_kernels.md
   const char* verify_env = getenv("TPI_HANDOFF_VERIFY");
-  const bool readback = !(verify_env && strcmp(verify_env, "none") == 0);
+  std::string verify = verify_env ? verify_env : "readback";
+  if (verify == "inline" && !extents_disjoint(dst, n)) verify = "readback";
+  const bool readback = verify == "readback";
+  const bool inline_check = verify == "inline";
   uint64_t nchunks = 0;
-  // No staging buffer bounds the fused route's spans: 4 GiB (4096 one-MiB tiles, 16
-  // workgroups per CU) keeps the chip full, where a 256 MB chunk is one workgroup per CU.
-  // TPI_HANDOFF_SPAN_MB: bytes per launch (0: the whole state in one copy + one verify launch)
-  uint64_t span_bytes = 4ull << 30;
+  // No staging buffer bounds the fused route's spans (a 256 MB chunk would be one workgroup
+  // per CU).
+  // TPI_HANDOFF_SPAN_MB: bytes per launch; default (0) the whole state in one copy launch and
+  // one verify launch -- no launch tails between spans (32 GB: 16.6 ms vs 17.9 ms in 4 GiB
+  // spans, profiles/round5/handoff_kernels.md)
+  uint64_t span_bytes = total;
   if (const char* v = getenv("TPI_HANDOFF_SPAN_MB"))
     span_bytes = strtoull(v, nullptr, 10) ? strtoull(v, nullptr, 10) << 20 : total;
   const uint64_t span = std::max<uint64_t>(e->chunk, std::max<uint64_t>(span_bytes / tile, 1) * tile);
@@ -1739,7 +1773,8 @@ int tpi_copy_segments(tpi_engine* e, const tpi_seg* src, const tpi_seg* dst, int
     const uint64_t len = std::min(span, total - base);
     if (xxh)
       good = ok(tpi_launch_stream_copy_hash(d_src, e->d_segs, n, base, len, total, tile,
-                                            TPI_SYNC_SEED, e->d_digest, nullptr, e->compute),
+                                            TPI_SYNC_SEED, e->d_digest,
+                                            inline_check ? e->d_bad : nullptr, e->compute),
                 "copy") &&
              (!readback ||
               ok(tpi_launch_stream_copy_hash(e->d_segs, nullptr, n, base, len, total, tile,

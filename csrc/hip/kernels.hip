@@ -766,7 +766,15 @@ __global__ __launch_bounds__(WG) void k_shard_hash(const uint8_t* __restrict__ d
 // hashed again and compared).  No table lookups: where the CRC32C verify is bound by its LDS
 // lookups at ~4.3 TB/s, this reads at the ~6 TB/s class of k_shard_hash
 // (profiles/handoff_hash_round3.md).  Workgroup i handles tile tile0 + i.
-enum { HASH_ONLY = 0, HASH_COPY = 1, HASH_VERIFY = 2 };
+//
+// HASH_COPY_CHECK copies like HASH_COPY and checks the destination inline: each lane reads back
+// the words it stored one row group earlier (the lag keeps the read-back off the stores'
+// latency) and compares them with the words it copied, so the destination is verified without
+// a second pass over HBM -- the read-back mostly hits the caches the stores just went through.
+// Overlapping destinations, the one fault an immediate read-back cannot see (a later writer
+// could still overwrite a checked word), are refused on the host before the launch
+// (tpi_copy_segments).
+enum { HASH_ONLY = 0, HASH_COPY = 1, HASH_VERIFY = 2, HASH_COPY_CHECK = 3 };
 
 template <int KIND, int U = UNROLL>
 __global__ __launch_bounds__(WG) void k_stream_hash(const tpi_seg* __restrict__ segs,
@@ -775,20 +783,27 @@ __global__ __launch_bounds__(WG) void k_stream_hash(const tpi_seg* __restrict__ 
                                                     uint64_t tile_bytes, uint64_t seed,
                                                     uint64_t* __restrict__ out,
                                                     unsigned long long* __restrict__ bad) {
+  constexpr bool COPY = KIND == HASH_COPY || KIND == HASH_COPY_CHECK;
+  constexpr bool CHECK = KIND == HASH_COPY_CHECK;
   __shared__ uint64_t red[WG / 64];
+  __shared__ int mism[WG / 64];
   const int lane = threadIdx.x;
   const uint64_t gtile = tile0 + blockIdx.x;
   const uint64_t gbase = gtile * tile_bytes;
   const uint64_t len = umin64(tile_bytes, total - gbase);
-  SegCursor cur, dcur;
+  SegCursor cur, dcur, rcur;
   seg_load(segs, nseg, seg_find(segs, nseg, gbase + lane * 16), cur);
-  if (KIND == HASH_COPY) seg_load(dsegs, nseg, seg_find(dsegs, nseg, gbase + lane * 16), dcur);
+  if (COPY) seg_load(dsegs, nseg, seg_find(dsegs, nseg, gbase + lane * 16), dcur);
+  if (CHECK) rcur = dcur;
   // two independent round chains per lane (low and high 8 bytes of each word): a single
   // chain of dependent 64-bit multiplies left the kernel latency-bound (4.8 TB/s)
   uint64_t va = seed + (uint64_t)(lane + 1) * TPI_XXH_P1, vb = va ^ TPI_XXH_P2;
   uint64_t nwords = 0;
+  uint32_t diff = 0;  // CHECK: OR of (read back ^ copied) over this lane's words
   const uint64_t full_rows = len / TPI_ROW_BYTES;
   uint64_t row = 0;
+  u32x4 prev[CHECK ? U : 1];
+  bool have_prev = false;
   for (; row + U <= full_rows; row += U) {
     u32x4 w[U];
 #pragma unroll
@@ -797,7 +812,17 @@ __global__ __launch_bounds__(WG) void k_stream_hash(const tpi_seg* __restrict__ 
       advance(segs, nseg, pos, cur);
       w[u] = gather16(segs, cur, pos, nullptr, false);
     }
-    if (KIND == HASH_COPY) {
+    if (CHECK && have_prev) {
+      __asm__ volatile("" ::: "memory");  // the stores below were issued: really read them back
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint64_t pos = gbase + (row - U + u) * TPI_ROW_BYTES + lane * 16;
+        advance(dsegs, nseg, pos, rcur);
+        const u32x4 r = gather16(dsegs, rcur, pos, nullptr, false);
+        diff |= (r.x ^ prev[u].x) | (r.y ^ prev[u].y) | (r.z ^ prev[u].z) | (r.w ^ prev[u].w);
+      }
+    }
+    if (COPY) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint64_t pos = gbase + (row + u) * TPI_ROW_BYTES + lane * 16;
@@ -809,15 +834,33 @@ __global__ __launch_bounds__(WG) void k_stream_hash(const tpi_seg* __restrict__ 
     for (int u = 0; u < U; ++u) {
       va = tpi_xxh_round(va, ((uint64_t)w[u].y << 32) | w[u].x);
       vb = tpi_xxh_round(vb, ((uint64_t)w[u].w << 32) | w[u].z);
+      if (CHECK) prev[u] = w[u];
     }
+    if (CHECK) have_prev = true;
     nwords += U;
+  }
+  if (CHECK && have_prev) {  // the last full group
+    __asm__ volatile("" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t pos = gbase + (row - U + u) * TPI_ROW_BYTES + lane * 16;
+      advance(dsegs, nseg, pos, rcur);
+      const u32x4 r = gather16(dsegs, rcur, pos, nullptr, false);
+      diff |= (r.x ^ prev[u].x) | (r.y ^ prev[u].y) | (r.z ^ prev[u].z) | (r.w ^ prev[u].w);
+    }
   }
   for (uint64_t rel = row * TPI_ROW_BYTES + lane * 16; rel < len; rel += TPI_ROW_BYTES) {
     advance(segs, nseg, gbase + rel, cur);
     const u32x4 w = gather16(segs, cur, gbase + rel, nullptr, false);
-    if (KIND == HASH_COPY) {
+    if (COPY) {
       advance(dsegs, nseg, gbase + rel, dcur);
       scatter16(dsegs, dcur, gbase + rel, w, false);
+    }
+    if (CHECK) {
+      __asm__ volatile("" ::: "memory");
+      advance(dsegs, nseg, gbase + rel, rcur);
+      const u32x4 r = gather16(dsegs, rcur, gbase + rel, nullptr, false);
+      diff |= (r.x ^ w.x) | (r.y ^ w.y) | (r.z ^ w.z) | (r.w ^ w.w);
     }
     va = tpi_xxh_round(va, ((uint64_t)w.y << 32) | w.x);
     vb = tpi_xxh_round(vb, ((uint64_t)w.w << 32) | w.z);
@@ -827,6 +870,10 @@ __global__ __launch_bounds__(WG) void k_stream_hash(const tpi_seg* __restrict__ 
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) h ^= __shfl_xor(h, o, 64);
   if ((lane & 63) == 0) red[lane >> 6] = h;
+  if (CHECK) {
+    const int any = __any(diff != 0);  // wave vote
+    if ((lane & 63) == 0) mism[lane >> 6] = any;
+  }
   __syncthreads();
   if (lane == 0) {
     const uint64_t digest = tpi_xxh_avalanche(red[0] ^ red[1] ^ red[2] ^ red[3] ^ len);
@@ -837,6 +884,10 @@ __global__ __launch_bounds__(WG) void k_stream_hash(const tpi_seg* __restrict__ 
       }
     } else {
       out[gtile] = digest;
+      if (CHECK && (mism[0] | mism[1] | mism[2] | mism[3])) {
+        atomicAdd(&bad[0], 1ull);
+        atomicMin(&bad[1], (unsigned long long)gtile);
+      }
     }
   }
 }
@@ -993,8 +1044,9 @@ extern "C" hipError_t tpi_launch_stream_hash(const tpi_seg* segs, int nseg, uint
 
 // Hand-off over the stream bytes [stream_base, stream_base + len) (tile aligned) of a plan
 // whose stream is `total` bytes: dst != nullptr copies src -> dst and records the tile
-// digests of what was read into `digests` (indexed by global tile); dst == nullptr re-hashes
-// src and counts tiles whose digest differs (bad[0]; bad[1] = first such tile).
+// digests of what was read into `digests` (indexed by global tile) -- with `bad` also reading
+// every stored word back (HASH_COPY_CHECK); dst == nullptr re-hashes src and counts tiles
+// whose digest differs (bad[0]; bad[1] = first such tile).
 extern "C" hipError_t tpi_launch_stream_copy_hash(const tpi_seg* src, const tpi_seg* dst,
                                                   int nseg, uint64_t stream_base, uint64_t len,
                                                   uint64_t total, uint64_t tile_bytes,
@@ -1004,14 +1056,18 @@ extern "C" hipError_t tpi_launch_stream_copy_hash(const tpi_seg* src, const tpi_
   if (stream_base % tile_bytes || stream_base + len > total) return hipErrorInvalidValue;
   const uint64_t tile0 = stream_base / tile_bytes;
   const dim3 grid((unsigned)((len + tile_bytes - 1) / tile_bytes)), block(WG);
-  // rows in flight per lane (16 B each): TPI_HANDOFF_UNROLL=16 doubles the bytes each lane
-  // keeps in flight (profiles/round5/handoff_kernels.md)
+  // rows in flight per lane (16 B each; TPI_HANDOFF_UNROLL 4, 8 or 16).  4 is the fastest on
+  // MI355X: more waves resident beat more bytes per wave -- 32 GB copy 11.7 ms at 4, 12.5 at 8,
+  // 22.2 at 16 (profiles/round5/handoff_kernels.md)
   static const int unroll = [] {
     const char* v = getenv("TPI_HANDOFF_UNROLL");
-    return v && atoi(v) == 16 ? 16 : (v && atoi(v) == 4 ? 4 : UNROLL);
+    return v && atoi(v) == 16 ? 16 : (v && atoi(v) == 8 ? 8 : 4);
   }();
 #define TPI_HASH_LAUNCH(UU)                                                                   \
-  if (dst)                                                                                   \
+  if (dst && bad)                                                                            \
+    hipLaunchKernelGGL((k_stream_hash<HASH_COPY_CHECK, UU>), grid, block, 0, stream, src, dst, \
+                       nseg, tile0, total, tile_bytes, seed, digests, bad);                   \
+  else if (dst)                                                                              \
     hipLaunchKernelGGL((k_stream_hash<HASH_COPY, UU>), grid, block, 0, stream, src, dst, nseg, \
                        tile0, total, tile_bytes, seed, digests, bad);                         \
   else                                                                                       \
@@ -1019,10 +1075,10 @@ extern "C" hipError_t tpi_launch_stream_copy_hash(const tpi_seg* src, const tpi_
                        nseg, tile0, total, tile_bytes, seed, digests, bad);
   if (unroll == 16) {
     TPI_HASH_LAUNCH(16)
-  } else if (unroll == 4) {
-    TPI_HASH_LAUNCH(4)
+  } else if (unroll == 8) {
+    TPI_HASH_LAUNCH(8)
   } else {
-    TPI_HASH_LAUNCH(UNROLL)
+    TPI_HASH_LAUNCH(4)
   }
 #undef TPI_HASH_LAUNCH
   return hipGetLastError();

@@ -577,15 +577,20 @@ def test_streamed_restore_gives_up_on_a_stalled_writer(tmp_path):
     writer.close()
 
 
-@pytest.mark.parametrize("digest", ["xxh", "crc32c"])
-def test_handoff_copy_verify_catches_a_bad_destination(digest, monkeypatch):
+@pytest.mark.parametrize("digest,verify", [("xxh", "readback"), ("crc32c", "readback"),
+                                           ("xxh", "inline")])
+def test_handoff_copy_verify_catches_a_bad_destination(digest, verify, monkeypatch):
     """The hand-off's fused copy records a digest per tile of what it read; the read-back pass
     must flag tiles whose destination differs.  Two destination segments aliasing the same
-    memory make the copy overwrite one tensor with another, as a wrong mapping would."""
+    memory make the copy overwrite one tensor with another, as a wrong mapping would.  With
+    TPI_HANDOFF_VERIFY=inline the copy reads every stored word back itself; aliasing
+    destinations -- which an immediate read-back could miss -- fall back to the read-back
+    pass, so the fault is still caught."""
     from terraform_provider_iterative_amd.checkpoint import Checkpointer
     from terraform_provider_iterative_amd.ops.packing import PackPlan
 
     monkeypatch.setenv("TPI_HANDOFF_HASH", digest)  # read by every tpi_copy_segments call
+    monkeypatch.setenv("TPI_HANDOFF_VERIFY", verify)
     g = torch.Generator(device="cuda").manual_seed(5)
     src = {"a": torch.randn(1 << 20, device="cuda", generator=g),
            "b": torch.randn(1 << 20, device="cuda", generator=g).to(torch.bfloat16),
