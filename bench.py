@@ -556,8 +556,9 @@ def main(argv=None):
                        "mode": args.mode, "codec": args.codec,
                        "d2h_engine": ck.engine.d2h_engine if ck.engine else None,
                        "tensors_per_rank": len(tensors),
-                       # HIP hardware queues per process: 8 for this bench (HIP's default, and
-                       # the runtime ranks', is 4; +2-3 %% here, profiles/hw_queues_round3.md)
+                       # HIP hardware queues per process, as run: the MI355X boxes export 4
+                       # (HIP's default, the runtime ranks' too); bench.py asks for 8 only
+                       # where nothing is set (+2-3 %%, profiles/hw_queues_round3.md)
                        "gpu_max_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                        # every runtime knob set in the environment, by name
                        "env_knobs": {k: v for k, v in sorted(os.environ.items())

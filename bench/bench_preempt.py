@@ -88,7 +88,7 @@ for i, gib in enumerate(extra):
     big = torch.empty(int(gib * 2 ** 30) // 4, dtype=torch.float32, device=dev)
     if not resuming:
         big.normal_(0, 1e-3, generator=gen)
-    tensors["embedding.%d" %% i] = big
+    tensors["embedding.%%d" %% i] = big
 torch.cuda.synchronize()
 t_alloc = time.time()
 ck = Checkpointer(tensors, path=spill, codec=%(codec)r)

@@ -229,3 +229,20 @@ def test_eight_ranks_report_their_placement_and_flag_off_socket_regions(tmp_path
     for r in (4, 5, 6, 7):
         assert "rank %d:" % r in strict.stderr
     assert "rank 3:" not in strict.stderr
+
+
+def test_preempt_bench_rank_script_renders():
+    """bench/bench_preempt.py's rank script is a %-template: every literal % in it must be
+    escaped, or the driver bench's preempt_e2e block dies before the task starts."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location(
+        "bench_preempt", os.path.join(ROOT, "bench", "bench_preempt.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    for extra in ([], [4.2, 2.5]):
+        text = mod.RANK % {"python": sys.executable, "root": ROOT, "spill": "/dev/shm/x",
+                           "gb": 100.0, "codec": "tpz1", "prefetch": True, "early": False,
+                           "standby": True, "step_s": 0.002, "boundary": True,
+                           "materialize": False, "extra": extra}
+        compile(text, "rank", "exec")

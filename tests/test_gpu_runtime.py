@@ -434,6 +434,10 @@ def test_save_releases_device_memory_behind_the_spill(tmp_path):
     host copy is complete and restores into fresh tensors."""
     from terraform_provider_iterative_amd.checkpoint import Checkpointer
 
+    # fresh segments for the state: a large free block cached by an earlier test would be split
+    # between the state and `ref` below, and a segment with a live block never goes back
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
     g = torch.Generator(device="cuda").manual_seed(21)
     src = {"w%d" % i: torch.randn(64 << 20, device="cuda", generator=g) for i in range(6)}
     src["view_a"] = src["w5"][: 1 << 20]
