@@ -273,10 +273,20 @@ def main():
         result["durability"] = next((c for c, _, _ in events if c in (
             "checkpoint-durable", "checkpoint-not-durable", "checkpoint-durability-unknown")), None)
         result["verified"] = any("verified True" in l for l in logs)
+        t_settled, _ = first("supervisor-settled")
+        t_exit, _ = first("rank-exit", t_respawn or 0.0)
+        if t_settled and t_exit:  # the successor's exit -> final sync + final state
+            result["rank_exit_to_settled_s"] = round(t_settled - t_exit, 3)
+        result["released_exit_pending_at_settle"] = first("rank-released-exit")[0] is None
         result["ok"] = bool(status.get("succeeded") == 1 and result["verified"])
     finally:
         try:
+            # the task is over for its users once the supervisor settled; a released
+            # predecessor may still be tearing down its pinned region:
+            # delete must not wait for it
+            t_del = time.time()
             task.delete()
+            result["delete_s"] = round(time.time() - t_del, 3)
         finally:
             shutil.rmtree(state, ignore_errors=True)
             if os.path.exists(spill):
