@@ -261,11 +261,14 @@ ALLOC_LOOKAHEAD = 3  # materialize(): groups allocated ahead of the restore once
 # 2 GiB or more (2040 MiB opens at once), so a state holding one takes the host path instead of
 # hanging its successor (profiles/round4/ipc_lifetime.md).  TPI_IPC_MAX_ALLOC overrides.
 IPC_MAX_ALLOC = 2 << 30
-# The hand-off's route (TPI_HBM_ROUTE): "dmabuf" (default) passes every allocation as a dma-buf
-# descriptor over a Unix socket and maps it with hsa_amd_interop_map_buffer -- any size
-# (profiles/round5/ipc_cause.md); "ipc" keeps hipIpcGetMemHandle / hipIpcOpenMemHandle, with the
-# size guard above.
-HBM_ROUTES = ("dmabuf", "ipc")
+# The hand-off's route per allocation (TPI_HBM_ROUTE): "auto" (default) -- HIP IPC handles for
+# allocations below IPC_MAX_ALLOC (exported and opened in microseconds each), dma-buf
+# descriptors over a Unix socket, mapped with hsa_amd_interop_map_buffer, for the larger ones
+# that HIP IPC cannot open (profiles/round5/ipc_cause.md; a dma-buf export + map costs ~1.5 ms
+# per allocation next to a live 100 GB state, so not for hundreds of small ones); "dmabuf" --
+# every allocation as a dma-buf; "ipc" -- every allocation over HIP IPC, refusing a state with
+# an allocation of IPC_MAX_ALLOC or more.
+HBM_ROUTES = ("auto", "dmabuf", "ipc")
 FDS_PER_MESSAGE = 200  # SCM_RIGHTS batch (the kernel's limit is 253 per message)
 
 # Engines created ahead of the Checkpointer that takes them (prewarm_engine).
@@ -1447,13 +1450,12 @@ class Checkpointer:
         The caller must keep the tensors unchanged (and this process alive) until the successor
         has restored -- the preemption handler does (it lingers until ``closed``).
 
-        Route ``dmabuf`` (default, :data:`HBM_ROUTES`): each allocation is exported as a
-        dma-buf descriptor and served to the successor over an abstract Unix socket named in
-        the manifest (same uid only); any allocation size.  Route ``ipc``: HIP IPC handles in
-        the manifest; raises CheckpointError, writing nothing, when a tensor lives in an
-        allocation of ``IPC_MAX_ALLOC`` or more (those imports never return).
-        ``metadata``: that of the save this export accompanies; a successor resuming from the
-        HBM gets it even when the host copy failed."""
+        Each allocation goes either as a HIP IPC handle in the manifest or as a dma-buf
+        descriptor served to the successor over an abstract Unix socket named in the manifest
+        (same uid only), per :data:`HBM_ROUTES`.  With ``TPI_HBM_ROUTE=ipc`` a state holding
+        an allocation of ``IPC_MAX_ALLOC`` or more raises CheckpointError, writing nothing
+        (such imports never return).  ``metadata``: that of the save this export accompanies;
+        a successor resuming from the HBM gets it even when the host copy failed."""
         manifest = self._hbm_manifest_path()
         if manifest is None:
             return None
@@ -1461,16 +1463,15 @@ class Checkpointer:
 
         torch.cuda.synchronize(self.device_index)  # no queued kernel may still write them
         lib = hip()
-        route = os.environ.get("TPI_HBM_ROUTE", "dmabuf").strip().lower()
+        route = os.environ.get("TPI_HBM_ROUTE", "auto").strip().lower()
         if route not in HBM_ROUTES:
             raise CheckpointError("TPI_HBM_ROUTE must be one of %s" % (HBM_ROUTES,))
-        if route == "dmabuf" and not lib.tpi_dmabuf_available():
-            route = "ipc"  # this runtime cannot export dma-bufs: the IPC route, guarded
+        dmabuf_ok = bool(lib.tpi_dmabuf_available())
+        limit = int(os.environ.get("TPI_IPC_MAX_ALLOC", IPC_MAX_ALLOC))
         allocations: Dict[int, int] = {}  # allocation base -> index
         bases: List[Tuple[int, int]] = []  # (base, size) per allocation
         where = []
         base, size = ctypes.c_uint64(0), ctypes.c_uint64(0)
-        limit = int(os.environ.get("TPI_IPC_MAX_ALLOC", IPC_MAX_ALLOC))
         for seg in self.plan.segs:
             ptr = int(seg["ptr"])
             if int(seg["nbytes"]) == 0 or ptr == 0:
@@ -1481,34 +1482,46 @@ class Checkpointer:
                                         ctypes.byref(size)), "tpi_mem_range")
             key = int(base.value)
             if key not in allocations:
-                if route == "ipc" and int(size.value) >= limit:
-                    raise CheckpointError(
-                        "no HBM hand-off: tensor %d lives in a %.2f GiB allocation, and IPC "
-                        "imports of allocations >= %.2f GiB block (TPI_IPC_MAX_ALLOC); the "
-                        "successor restores from the host copy" % (
-                            len(where), int(size.value) / 2 ** 30, limit / 2 ** 30))
                 allocations[key] = len(bases)
                 bases.append((key, int(size.value)))
             where.append([allocations[key], ptr - key])
-        doc = {"format": "tpi-hbm-1", "route": route, "pid": os.getpid(),
+        # which allocations travel as dma-bufs
+        if route == "dmabuf" and dmabuf_ok:
+            as_dmabuf = list(range(len(bases)))
+        elif route == "ipc" or not dmabuf_ok:
+            as_dmabuf = []
+            big = [i for i, (_, sz) in enumerate(bases) if sz >= limit]
+            if big:
+                raise CheckpointError(
+                    "no HBM hand-off: %d allocation(s) of %.2f GiB or more (the largest %.2f "
+                    "GiB), and HIP IPC imports of such allocations never return "
+                    "(TPI_IPC_MAX_ALLOC%s); the successor restores from the host copy" % (
+                        len(big), limit / 2 ** 30, max(bases[i][1] for i in big) / 2 ** 30,
+                        "" if dmabuf_ok else "; this runtime cannot export dma-bufs"))
+        else:
+            as_dmabuf = [i for i, (_, sz) in enumerate(bases) if sz >= limit]
+        doc = {"format": "tpi-hbm-2", "pid": os.getpid(),
                "entries_sha256": self._entries_digest, "total": self.plan.total,
                "tile_bytes": self.plan.tile_bytes, "where": where,
                "segs": self.plan.segs.tobytes().hex(), "created": time.time(),
                "metadata": metadata or {},
+               "allocations": [sz for _, sz in bases],
                # the generation the save that follows this export will write
                "generation": self._target()[1]}
-        if route == "ipc":
-            handle = ctypes.create_string_buffer(64)
-            offset = ctypes.c_uint64(0)
-            handles = []
-            for key, _ in bases:
-                lib.check(lib.tpi_ipc_export(ctypes.c_void_p(key), handle, ctypes.byref(offset),
-                                             ctypes.byref(size)), "tpi_ipc_export")
-                handles.append(handle.raw.hex())
-            doc["allocations"] = handles
-        else:
-            doc["allocations"] = [sz for _, sz in bases]
-            doc["socket"] = self._serve_dmabufs(bases)
+        handle = ctypes.create_string_buffer(64)
+        offset = ctypes.c_uint64(0)
+        ipc: Dict[str, str] = {}
+        dmabuf_set = set(as_dmabuf)
+        for i, (key, _) in enumerate(bases):
+            if i in dmabuf_set:
+                continue
+            lib.check(lib.tpi_ipc_export(ctypes.c_void_p(key), handle, ctypes.byref(offset),
+                                         ctypes.byref(size)), "tpi_ipc_export")
+            ipc[str(i)] = handle.raw.hex()
+        doc["ipc"] = ipc
+        if as_dmabuf:
+            doc["socket"], doc["dmabuf"] = self._serve_dmabufs(
+                [(i, bases[i][0], bases[i][1]) for i in as_dmabuf])
         bus = ctypes.create_string_buffer(64)
         lib.tpi_device_pci_bus_id(self.device_index, bus, 64)
         doc["device"] = bus.value.decode()
@@ -1518,25 +1531,37 @@ class Checkpointer:
         os.replace(tmp, manifest)
         return manifest
 
-    def _serve_dmabufs(self, bases: List[Tuple[int, int]]) -> str:
-        """Export every ``(base, size)`` allocation as a dma-buf and serve the descriptors, in
-        order, to each process of this uid that connects to the returned abstract socket
-        name (messages of ``FDS_PER_MESSAGE`` descriptors: ``{"first", "offsets"}`` + fds,
-        then ``{"end": n}``).  A daemon thread; it lives as long as this process."""
+    def _serve_dmabufs(self, allocs: List[Tuple[int, int, int]]) -> Tuple[str, Dict[str, Any]]:
+        """Export every ``(index, base, size)`` allocation as a dma-buf and serve the
+        descriptors, in order, to each process of this uid that connects to the returned
+        abstract socket name (messages of up to ``FDS_PER_MESSAGE`` descriptors:
+        ``{"index", "offsets"}`` + fds, then ``{"end": n}``).  Returns the name and, per
+        allocation index, the exported buffer's size and offset (checked against the
+        allocation here and again by the importer).  A daemon thread serves as long as this
+        process lives."""
         lib = hip()
         fds: List[int] = []
         offsets: List[int] = []
+        info: Dict[str, Any] = {}
         fd, off = ctypes.c_int(-1), ctypes.c_uint64(0)
         try:
-            for key, sz in bases:
+            for i, key, sz in allocs:
                 lib.check(lib.tpi_dmabuf_export(ctypes.c_void_p(key), sz, ctypes.byref(fd),
                                                 ctypes.byref(off)), "tpi_dmabuf_export")
                 fds.append(fd.value)
                 offsets.append(int(off.value))
+                buf = os.lseek(fd.value, 0, os.SEEK_END)  # a dma-buf's size
+                os.lseek(fd.value, 0, os.SEEK_SET)
+                if buf < int(off.value) + sz:
+                    raise CheckpointError(
+                        "dma-buf export of allocation %d (%d bytes at %#x) gave a %d-byte "
+                        "buffer at offset %d" % (i, sz, key, buf, int(off.value)))
+                info[str(i)] = [buf, int(off.value)]
         except BaseException:
             for f in fds:
                 os.close(f)
             raise
+        index = [i for i, _, _ in allocs]
         name = "tpi-hbm-%d-%s" % (os.getpid(), os.urandom(6).hex())
         server = socket.socket(socket.AF_UNIX, socket.SOCK_SEQPACKET)
         server.bind("\0" + name)
@@ -1554,9 +1579,10 @@ class Checkpointer:
                                            struct.calcsize("3i"))
                     if struct.unpack("3i", cred)[1] != uid:
                         continue  # another user's process: nothing to see
-                    for i in range(0, len(fds), FDS_PER_MESSAGE):
-                        chunk = fds[i:i + FDS_PER_MESSAGE]
-                        msg = json.dumps({"first": i, "offsets": offsets[i:i + len(chunk)]})
+                    for k in range(0, len(fds), FDS_PER_MESSAGE):
+                        chunk = fds[k:k + FDS_PER_MESSAGE]
+                        msg = json.dumps({"index": index[k:k + len(chunk)],
+                                          "offsets": offsets[k:k + len(chunk)]})
                         socket.send_fds(conn, [msg.encode()], chunk)
                     conn.send(json.dumps({"end": len(fds)}).encode())
                 except OSError:
@@ -1566,7 +1592,7 @@ class Checkpointer:
 
         self._dmabuf_server = (server, fds)
         threading.Thread(target=serve, name="tpi-dmabuf-serve", daemon=True).start()
-        return name
+        return name, info
 
     def _close_dmabuf_server(self) -> None:
         served = getattr(self, "_dmabuf_server", None)
@@ -1594,7 +1620,7 @@ class Checkpointer:
                 doc = json.load(f)
         except (OSError, ValueError):
             return None
-        if (doc.get("format") != "tpi-hbm-1" or doc.get("pid") == os.getpid()
+        if (doc.get("format") != "tpi-hbm-2" or doc.get("pid") == os.getpid()
                 or doc.get("entries_sha256") != self._entries_digest
                 or doc.get("total") != self.plan.total):
             return None
@@ -1701,10 +1727,12 @@ class Checkpointer:
         import torch
 
         lib = hip()
-        route = doc.get("route", "ipc")
         n = len(doc["allocations"])
+        ipc = {int(i): h for i, h in (doc.get("ipc") or {}).items()}
+        sizes = [int(x) for x in doc["allocations"]]
         bases: List[Optional[int]] = [None] * n   # each allocation's base in this process
-        mapped: List[Optional[int]] = [None] * n  # what to unmap (dma-buf: the mapping)
+        mapped: List[Optional[int]] = [None] * n  # what to unmap / close
+        via_dmabuf = [False] * n
         t0 = time.perf_counter()
         try:
             limit = float(os.environ.get("TPI_IPC_OPEN_TIMEOUT", "10"))
@@ -1713,16 +1741,18 @@ class Checkpointer:
 
         def open_ipc(i: int) -> None:
             base = ctypes.c_void_p()
-            lib.check(lib.tpi_ipc_open(bytes.fromhex(doc["allocations"][i]), self.device_index,
+            lib.check(lib.tpi_ipc_open(bytes.fromhex(ipc[i]), self.device_index,
                                        ctypes.byref(base)), "tpi_ipc_open")
             bases[i] = mapped[i] = base.value
 
         def open_dmabufs() -> None:
-            # the predecessor's server sends the descriptors in order, in batches; each is
-            # mapped here and closed at once (the mapping keeps its own reference)
+            # the predecessor's server sends the descriptors in batches; each is checked
+            # (size), mapped here and closed at once (the mapping keeps its own reference)
             sock = socket.socket(socket.AF_UNIX, socket.SOCK_SEQPACKET)
             sock.settimeout(limit)
             ptr, size = ctypes.c_void_p(), ctypes.c_uint64(0)
+            want = doc.get("dmabuf") or {}
+            got = 0
             with sock:
                 sock.connect("\0" + doc["socket"])
                 while True:
@@ -1732,31 +1762,41 @@ class Checkpointer:
                             raise CheckpointError("the predecessor closed the hand-off socket")
                         head = json.loads(msg)
                         if "end" in head:
-                            if head["end"] != n or any(b is None for b in bases):
+                            if head["end"] != len(want) or got != len(want):
                                 raise CheckpointError("hand-off socket sent %s of %d "
-                                                      "allocations" % (head["end"], n))
+                                                      "dma-bufs" % (head["end"], len(want)))
                             return
+                        if len(fds) != len(head["index"]):
+                            raise CheckpointError("hand-off message lost descriptors")
                         for k, fd in enumerate(fds):
-                            i = int(head["first"]) + k
+                            i = int(head["index"][k])
+                            off = int(head["offsets"][k])
+                            buf = os.lseek(fd, 0, os.SEEK_END)
+                            if buf < off + sizes[i] or [buf, off] != want.get(str(i)):
+                                raise CheckpointError(
+                                    "dma-buf for allocation %d is %d bytes at offset %d; the "
+                                    "exporter announced %s for %d bytes" % (
+                                        i, buf, off, want.get(str(i)), sizes[i]))
                             lib.check(lib.tpi_dmabuf_import(self.device_index, fd,
                                                             ctypes.byref(ptr),
                                                             ctypes.byref(size)),
                                       "tpi_dmabuf_import")
                             mapped[i] = ptr.value
-                            off = int(head["offsets"][k])
-                            if int(size.value) < off + int(doc["allocations"][i]):
+                            via_dmabuf[i] = True
+                            if int(size.value) < off + sizes[i]:
                                 # never let a kernel read past what was mapped
                                 raise CheckpointError(
                                     "dma-buf %d maps %d bytes, the allocation needs %d" % (
-                                        i, int(size.value), off + int(doc["allocations"][i])))
+                                        i, int(size.value), off + sizes[i]))
                             bases[i] = ptr.value + off
+                            got += 1
                     finally:
                         for fd in fds:
                             os.close(fd)
 
         def close_one(i: int) -> None:
             if mapped[i] is not None:
-                if route == "dmabuf":
+                if via_dmabuf[i]:
                     lib.tpi_dmabuf_unmap(ctypes.c_void_p(mapped[i]))
                 else:
                     lib.tpi_ipc_close(ctypes.c_void_p(mapped[i]))
@@ -1781,12 +1821,13 @@ class Checkpointer:
             self.release_hbm_claim()  # nothing of the predecessor is mapped any more
 
         def open_all() -> None:
-            # Bounded: an import that never returns (round 4: hipIpcOpenMemHandle on
-            # allocations of 2 GiB or more spins forever) must not strand this successor
-            # holding the claim while its predecessor waits on it -- past TPI_IPC_OPEN_TIMEOUT
-            # the HBM route is given up (the caller restores from the host copy).  The openers
-            # are daemon threads: one stuck in the driver cannot hold up this process's exit.
-            todo = list(range(n))
+            # Bounded: an import that never returns (hipIpcOpenMemHandle on an allocation of
+            # 2 GiB or more spins forever, profiles/round5/ipc_cause.md) must not strand this
+            # successor holding the claim while its predecessor waits on it -- past
+            # TPI_IPC_OPEN_TIMEOUT the HBM route is given up (the caller restores from the
+            # host copy).  The openers are daemon threads: one stuck in the driver cannot hold
+            # up this process's exit.  IPC handles and dma-bufs are opened side by side.
+            todo = sorted(ipc)
             lock = threading.Lock()
             errors: List[BaseException] = []
 
@@ -1810,10 +1851,11 @@ class Checkpointer:
                     with lock:
                         errors.append(error)
 
-            workers = ([threading.Thread(target=receiver, name="tpi-dmabuf-open", daemon=True)]
-                       if route == "dmabuf" else
-                       [threading.Thread(target=worker, name="tpi-ipc-open", daemon=True)
-                        for _ in range(min(8, n) or 1)])
+            workers = [threading.Thread(target=worker, name="tpi-ipc-open", daemon=True)
+                       for _ in range(min(8, len(todo)))]
+            if doc.get("socket"):
+                workers.append(threading.Thread(target=receiver, name="tpi-dmabuf-open",
+                                                daemon=True))
             for w in workers:
                 w.start()
             deadline = time.monotonic() + limit
@@ -1828,6 +1870,8 @@ class Checkpointer:
                 raise CheckpointError(
                     "HIP IPC import of the predecessor's HBM did not return within %.1f s "
                     "(TPI_IPC_OPEN_TIMEOUT); restoring from the host copy" % limit)
+            if any(b is None for b in bases):
+                raise CheckpointError("the HBM hand-off left allocations unmapped")
 
         try:
             open_all()

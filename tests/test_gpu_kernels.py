@@ -631,11 +631,12 @@ sys.stdin.readline()  # hold the memory until the successor is done
 '''
 
 
-@pytest.mark.parametrize("route,hbm_route", [("fused", "dmabuf"), ("staged", "dmabuf"),
-                                             ("fused", "ipc")])
+@pytest.mark.parametrize("route,hbm_route", [("fused", "auto"), ("fused", "dmabuf"),
+                                             ("staged", "dmabuf"), ("fused", "ipc")])
 def test_hbm_handoff_copies_a_live_predecessors_tensors(tmp_path, monkeypatch, route, hbm_route):
-    """Same-GPU hand-off: the predecessor exports its tensors' allocations (dma-buf
-    descriptors over a Unix socket by default, HIP IPC handles with TPI_HBM_ROUTE=ipc); the
+    """Same-GPU hand-off: the predecessor exports its tensors' allocations (HIP IPC handles,
+    dma-buf descriptors over a Unix socket for allocations of 2 GiB or more; all dma-bufs with
+    TPI_HBM_ROUTE=dmabuf, all IPC with TPI_HBM_ROUTE=ipc); the
     successor copies them device to device, digest-verified, with no host copy.  The default
     copy is the fused tensor-to-tensor copy plus a read-back verify; TPI_HANDOFF_COPY=staged
     selects pack + unpack through a staging buffer.  Transposed and strided views take the
@@ -703,7 +704,7 @@ def test_hbm_handoff_of_allocations_beyond_the_ipc_limit(tmp_path, monkeypatch):
     import subprocess
     import sys
 
-    monkeypatch.setenv("TPI_HBM_ROUTE", "dmabuf")
+    monkeypatch.setenv("TPI_HBM_ROUTE", "auto")
     monkeypatch.setenv("TPI_IPC_OPEN_TIMEOUT", "30")
     root = os.path.dirname(os.path.dirname(__file__))
     path = str(tmp_path / "spill")
@@ -714,7 +715,9 @@ def test_hbm_handoff_of_allocations_beyond_the_ipc_limit(tmp_path, monkeypatch):
         assert line.startswith("exported"), line
         with open(path + ".hbm") as f:
             doc = __import__("json").load(f)
-        assert doc["route"] == "dmabuf" and max(doc["allocations"]) >= 4 << 30, doc["allocations"]
+        assert max(doc["allocations"]) >= 4 << 30, doc["allocations"]
+        # auto route: the two big allocations as dma-bufs, the small one over HIP IPC
+        assert len(doc["dmabuf"]) == 2 and len(doc["ipc"]) >= 1, doc
         dst = {"emb": torch.zeros(int(4.2 * 2 ** 30) // 4, device="cuda"),
                "w": torch.zeros(int(2.5 * 2 ** 30) // 2, device="cuda", dtype=torch.bfloat16),
                "n": torch.zeros(4096, device="cuda")}

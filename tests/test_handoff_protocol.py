@@ -473,7 +473,8 @@ def test_a_stuck_ipc_import_gives_up_the_hbm_route_and_the_claim(tmp_path, monke
         restore_hbm = Checkpointer.restore_hbm
 
         def _hbm_doc(self):
-            return {"allocations": ["01", "02", "03"], "where": [], "segs": ""}
+            return {"allocations": [1 << 20] * 3, "ipc": {"0": "01", "1": "02", "2": "03"},
+                    "where": [], "segs": ""}
 
     monkeypatch.setattr(ckmod, "hip", lambda *a, **k: FakeLib())
     monkeypatch.setenv("TPI_IPC_OPEN_TIMEOUT", "0.5")
@@ -590,11 +591,12 @@ def test_handoff_mode_row(binary, tmp_path, mode):
 
 
 def test_dmabuf_route_hands_every_allocation_over_the_socket(tmp_path, monkeypatch):
-    """The default hand-off route (round 5): the exporter serves one dma-buf descriptor per
-    allocation over an abstract Unix socket (batches of FDS_PER_MESSAGE, SCM_RIGHTS); the
-    successor maps each, points the source segments at base + offset + the tensor's place in
-    the allocation, copies, and unmaps them all behind the restore.  Descriptors are stand-ins
-    (/dev/null) and mappings fake addresses: no GPU."""
+    """The hand-off's mixed route (round 5): allocations below IPC_MAX_ALLOC travel as HIP IPC
+    handles in the manifest, the larger ones as dma-buf descriptors the exporter serves over an
+    abstract Unix socket (batches of FDS_PER_MESSAGE, SCM_RIGHTS), each buffer's size checked
+    on both sides.  The successor maps each, points the source segments at base + offset + the
+    tensor's place in the allocation, copies, and unmaps them all behind the restore.  Buffers
+    are sparse memfds and mappings fake addresses: no GPU."""
     import numpy as np
 
     import torch
@@ -602,44 +604,92 @@ def test_dmabuf_route_hands_every_allocation_over_the_socket(tmp_path, monkeypat
     from terraform_provider_iterative_amd.checkpoint import checkpointer as ckmod
     from terraform_provider_iterative_amd.ops.packing import SEG_DTYPE
 
-    n_alloc = ckmod.FDS_PER_MESSAGE + 37  # two batches
-    sizes = [(3 << 30) + i * 4096 for i in range(n_alloc)]  # >= 2 GiB: the IPC route's limit
-    exported, imported, unmapped = [], {}, []
+    n_alloc = ckmod.FDS_PER_MESSAGE + 37  # two batches of dma-bufs ...
+    n_small = 5                           # ... and a few IPC handles
+    sizes = [(3 << 30) + i * 4096 for i in range(n_alloc)] + [1 << 20] * n_small
+    imported, opened, unmapped, closed = {}, {}, [], []
 
     class FakeLib:
+        def tpi_mem_range(self, ptr, base, size):
+            i = (ptr.value - 0x1000_0000_0000) // (1 << 33)
+            base._obj.value, size._obj.value = 0x1000_0000_0000 + i * (1 << 33), sizes[i]
+            return 0
+
+        def tpi_dmabuf_available(self):
+            return 1
+
         def tpi_dmabuf_export(self, ptr, size, fd, off):
-            fd._obj.value = os.open(os.devnull, os.O_RDONLY)
-            off._obj.value = 4096 if len(exported) % 2 else 0
-            exported.append((ptr.value, size))
+            f = os.memfd_create("fake-dmabuf")
+            os.ftruncate(f, size + 4096)
+            fd._obj.value = f
+            off._obj.value = 4096
+            return 0
+
+        def tpi_ipc_export(self, ptr, handle, off, size):
+            handle.raw = ("%064x" % ptr.value).encode()[:64]
             return 0
 
         def tpi_dmabuf_import(self, device, fd, ptr, size):
-            os.fstat(fd)  # a live descriptor arrived
             ptr._obj.value = 0x7000_0000_0000 + len(imported) * (1 << 36)
-            size._obj.value = (1 << 35)
+            size._obj.value = os.lseek(fd, 0, os.SEEK_END)
             imported[ptr._obj.value] = fd
+            return 0
+
+        def tpi_ipc_open(self, handle, device, out):
+            out._obj.value = 0x6000_0000_0000 + len(opened) * (1 << 30)
+            opened[out._obj.value] = handle
             return 0
 
         def tpi_dmabuf_unmap(self, ptr):
             unmapped.append(ptr.value)
             return 0
 
+        def tpi_ipc_close(self, ptr):
+            closed.append(ptr.value)
+            return 0
+
+        def tpi_device_pci_bus_id(self, dev, buf, n):
+            buf.value = b"0000:75:00.0"
+            return 0
+
         def check(self, rc, what):
             assert rc == 0, what
 
     monkeypatch.setattr(ckmod, "hip", lambda *a, **k: FakeLib())
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a: None)
+    monkeypatch.setattr(torch.cuda, "current_stream",
+                        lambda *a: type("S", (), {"cuda_stream": 0})())
+    monkeypatch.delenv("TPI_HBM_ROUTE", raising=False)
 
-    class Exporter:
+    n = n_alloc + n_small
+    segs = np.zeros(n, dtype=SEG_DTYPE)
+    segs["ptr"] = [0x1000_0000_0000 + i * (1 << 33) + 512 * i for i in range(n)]
+    segs["nbytes"] = 4096
+
+    class Plan:
+        pass
+
+    Plan.segs, Plan.total, Plan.tile_bytes = segs, 1 << 30, 1 << 20
+
+    class Exporter(_FakeHandoff):
+        device_index = 0
+        engine = object()
+        plan = Plan
+        _entries_digest = "d"
+        export_hbm = Checkpointer.export_hbm
         _serve_dmabufs = Checkpointer._serve_dmabufs
         _close_dmabuf_server = Checkpointer._close_dmabuf_server
 
-    exporter = Exporter()
-    bases = [(0x1000_0000_0000 + i * (1 << 33), sz) for i, sz in enumerate(sizes)]
-    name = exporter._serve_dmabufs(bases)
-    assert len(exporter._dmabuf_server[1]) == n_alloc
+        def _target(self):
+            return None, 3
 
-    segs = np.zeros(n_alloc, dtype=SEG_DTYPE)
-    where = [[i, 512 * i] for i in range(n_alloc)]
+    exporter = Exporter(str(tmp_path / "spill"))
+    manifest = exporter.export_hbm({"step": 9})
+    with open(manifest) as f:
+        doc = json.load(f)
+    assert len(doc["ipc"]) == n_small and len(doc["dmabuf"]) == n_alloc, doc.keys()
+    assert sorted(int(i) for i in doc["ipc"]) == list(range(n_alloc, n))
+
     copied = {}
 
     class Engine:
@@ -653,26 +703,22 @@ def test_dmabuf_route_hands_every_allocation_over_the_socket(tmp_path, monkeypat
     class Successor(_FakeHandoff):
         device_index = 0
         engine = Engine()
+        plan = Plan
         restore_hbm = Checkpointer.restore_hbm
 
-        class plan:
-            pass
-
         def _hbm_doc(self):
-            return {"route": "dmabuf", "socket": name, "allocations": sizes, "where": where,
-                    "segs": segs.tobytes().hex()}
+            return doc
 
-    Successor.plan.segs = segs
-    monkeypatch.setattr(torch.cuda, "current_stream",
-                        lambda *a: type("S", (), {"cuda_stream": 0})())
     ck = Successor(str(tmp_path / "spill"))
     ck.restore_hbm()
     ck._hbm_closer.join(10)
     src = copied["src"]
     maps = sorted(imported)
-    for i in range(n_alloc):
-        off = 4096 if i % 2 else 0
-        assert int(src[i]["ptr"]) == maps[i] + off + 512 * i
-    assert sorted(unmapped) == maps  # every mapping released, after the copy
+    for i in range(n_alloc):  # the dma-bufs, in the exporter's order
+        assert int(src[i]["ptr"]) == maps[i] + 4096 + 512 * i
+    ipc_bases = {int(h.decode(), 16): b for b, h in opened.items()}
+    for i in range(n_alloc, n):
+        assert int(src[i]["ptr"]) == ipc_bases[0x1000_0000_0000 + i * (1 << 33)] + 512 * i
+    assert sorted(unmapped) == maps and sorted(closed) == sorted(opened)
     assert ck.hbm_claim_owner() is None
     exporter._close_dmabuf_server()
