@@ -45,6 +45,12 @@ def test_two_rank_rehearsal_prints_one_json_line(tmp_path):
     assert abs(d["value"] - expect) / expect < 0.02
     assert d["restore_verified"] is True
     assert "CPU rehearsal" in d["data"]
+    # N > 1 evidence: every rank's process-group size; RCCL's fields null under gloo
+    comm = d["comm"]
+    assert [c["rank"] for c in comm["ranks"]] == [0, 1]
+    assert all(c["torch_pg_size"] == 2 and c["backend"] == "gloo" for c in comm["ranks"])
+    assert comm["pg_sizes_match"] is True and comm["rccl_nranks_match"] is None
+    assert d["config"]["gpu_max_hw_queues"] >= 1 and "env_knobs" in d["config"]
 
 
 def test_side_measurement_watchdog_keeps_the_headline(tmp_path):
