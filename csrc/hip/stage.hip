@@ -417,6 +417,26 @@ int tpi_ipc_close(void* dev_ptr) {
   return 0;
 }
 
+// One plain hipMalloc outside PyTorch's caching allocator (whose cached segments can be split
+// into a request, leaving it inside a larger allocation): the hand-off relocates tensors of
+// allocations HIP IPC cannot open into such blocks (checkpoint/checkpointer.py).
+int tpi_dev_alloc(uint64_t bytes, void** out) {
+  TPI_HIP(hipMalloc(out, (size_t)bytes));
+  return 0;
+}
+
+int tpi_dev_free(void* ptr) {
+  TPI_HIP(hipFree(ptr));
+  return 0;
+}
+
+// Device-to-device copy on `stream` (0: the null stream), synchronous.
+int tpi_d2d(void* dst, const void* src, uint64_t bytes, uint64_t stream) {
+  TPI_HIP(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  TPI_HIP(hipStreamSynchronize((hipStream_t)stream));
+  return 0;
+}
+
 }  // extern "C"
 
 // ---- task communicator (RCCL) ----------------------------------------------------------------

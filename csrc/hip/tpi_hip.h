@@ -217,6 +217,10 @@ int tpi_dmabuf_export(const void* ptr, uint64_t size, int* fd_out, uint64_t* off
 int tpi_dmabuf_close(int fd);
 int tpi_dmabuf_import(int device, int fd, void** ptr_out, uint64_t* size_out);
 int tpi_dmabuf_unmap(void* ptr);
+// Plain device allocations (hipMalloc / hipFree) and a synchronous device-to-device copy.
+int tpi_dev_alloc(uint64_t bytes, void** out);
+int tpi_dev_free(void* ptr);
+int tpi_d2d(void* dst, const void* src, uint64_t bytes, uint64_t stream);
 int tpi_engine_set_host_region(tpi_engine* e, void* base, uint64_t bytes, uint64_t window,
                                tpi_pinner* pinner);
 // hipMemcpyAsync host -> device on `stream` (0 = legacy default stream).

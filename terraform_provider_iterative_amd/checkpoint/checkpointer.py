@@ -47,7 +47,7 @@ import numpy as np
 
 from ..ops import codec as tpz
 from ..ops import hip, native
-from ..ops.packing import PackPlan, TensorEntry, align_up
+from ..ops.packing import SEG_CONTIG, PackPlan, TensorEntry, align_up
 from ..ops.packing import pack as host_pack, unpack as host_unpack
 from . import host
 from .host import HostRegion
@@ -160,12 +160,19 @@ class DeviceEngine:
         return TransferResult(plan.total, time.perf_counter() - t0, int(st.chunks),
                               int(bad.value), int(first.value), wire_bytes=int(st.bytes))
 
-    def copy_segments(self, src: np.ndarray, plan: PackPlan, signal_stream: int) -> TransferResult:
+    def copy_segments(self, src: np.ndarray, plan: PackPlan, signal_stream: int,
+                      dst: Optional[np.ndarray] = None) -> TransferResult:
+        """``src`` -> ``plan``'s tensors (or the descriptors ``dst``: the same stream, possibly
+        split into more segments than the plan has, like ``src``)."""
         st = _Stats()
         bad = ctypes.c_uint64(0)
         t0 = time.perf_counter()
-        rc = self.lib.tpi_copy_segments(self.handle, src.ctypes.data, plan.segs.ctypes.data,
-                                        len(plan.entries), plan.total, signal_stream,
+        dst = plan.segs if dst is None else dst
+        if len(dst) != len(src):
+            raise CheckpointError("copy_segments: %d source and %d destination segments"
+                                  % (len(src), len(dst)))
+        rc = self.lib.tpi_copy_segments(self.handle, src.ctypes.data, dst.ctypes.data,
+                                        len(dst), plan.total, signal_stream,
                                         ctypes.byref(bad), ctypes.byref(st))
         self.lib.check(rc, "tpi_copy_segments")
         return TransferResult(plan.total, time.perf_counter() - t0, int(st.chunks),
@@ -261,14 +268,19 @@ ALLOC_LOOKAHEAD = 3  # materialize(): groups allocated ahead of the restore once
 # 2 GiB or more (2040 MiB opens at once), so a state holding one takes the host path instead of
 # hanging its successor (profiles/round4/ipc_lifetime.md).  TPI_IPC_MAX_ALLOC overrides.
 IPC_MAX_ALLOC = 2 << 30
-# The hand-off's route per allocation (TPI_HBM_ROUTE): "auto" (default) -- HIP IPC handles for
-# allocations below IPC_MAX_ALLOC (exported and opened in microseconds each), dma-buf
-# descriptors over a Unix socket, mapped with hsa_amd_interop_map_buffer, for the larger ones
-# that HIP IPC cannot open (profiles/round5/ipc_cause.md; a dma-buf export + map costs ~1.5 ms
-# per allocation next to a live 100 GB state, so not for hundreds of small ones); "dmabuf" --
-# every allocation as a dma-buf; "ipc" -- every allocation over HIP IPC, refusing a state with
-# an allocation of IPC_MAX_ALLOC or more.
+# The hand-off's route (TPI_HBM_ROUTE):
+# * "auto" (default): every allocation over HIP IPC (exported and opened in microseconds).
+#   Tensors in an allocation of IPC_MAX_ALLOC or more -- which HIP IPC cannot open -- are first
+#   copied (device to device, ~1 ms per 5 GB) into plain hipMalloc blocks of RELOCATE_CHUNK
+#   bytes, and those travel instead (profiles/round5/ipc_cause.md);
+# * "dmabuf" (experimental): allocations of IPC_MAX_ALLOC or more as dma-buf descriptors over a
+#   Unix socket, mapped with hsa_amd_interop_map_buffer.  Bit-exact when the exporter idles,
+#   but a 100 GB hot hand-off faulted the GPU while the exporter's spill ran (round 5, r5f);
+#   a dma-buf export + map also costs ~1.5 ms per allocation next to a live 100 GB state;
+# * "ipc": HIP IPC only; a state with an allocation of IPC_MAX_ALLOC or more is refused (the
+#   successor restores from the host copy).
 HBM_ROUTES = ("auto", "dmabuf", "ipc")
+RELOCATE_CHUNK = 1 << 30
 FDS_PER_MESSAGE = 200  # SCM_RIGHTS batch (the kernel's limit is 253 per message)
 
 # Engines created ahead of the Checkpointer that takes them (prewarm_engine).
@@ -1450,12 +1462,12 @@ class Checkpointer:
         The caller must keep the tensors unchanged (and this process alive) until the successor
         has restored -- the preemption handler does (it lingers until ``closed``).
 
-        Each allocation goes either as a HIP IPC handle in the manifest or as a dma-buf
-        descriptor served to the successor over an abstract Unix socket named in the manifest
-        (same uid only), per :data:`HBM_ROUTES`.  With ``TPI_HBM_ROUTE=ipc`` a state holding
-        an allocation of ``IPC_MAX_ALLOC`` or more raises CheckpointError, writing nothing
-        (such imports never return).  ``metadata``: that of the save this export accompanies;
-        a successor resuming from the HBM gets it even when the host copy failed."""
+        Allocations travel as HIP IPC handles in the manifest; how those of ``IPC_MAX_ALLOC``
+        or more travel depends on ``TPI_HBM_ROUTE`` (:data:`HBM_ROUTES`): relocated into plain
+        blocks (default), as dma-buf descriptors, or not at all (CheckpointError, nothing
+        written: the successor restores from the host copy).  ``metadata``: that of the save
+        this export accompanies; a successor resuming from the HBM gets it even when the host
+        copy failed."""
         manifest = self._hbm_manifest_path()
         if manifest is None:
             return None
@@ -1466,53 +1478,62 @@ class Checkpointer:
         route = os.environ.get("TPI_HBM_ROUTE", "auto").strip().lower()
         if route not in HBM_ROUTES:
             raise CheckpointError("TPI_HBM_ROUTE must be one of %s" % (HBM_ROUTES,))
-        dmabuf_ok = bool(lib.tpi_dmabuf_available())
         limit = int(os.environ.get("TPI_IPC_MAX_ALLOC", IPC_MAX_ALLOC))
-        allocations: Dict[int, int] = {}  # allocation base -> index
-        bases: List[Tuple[int, int]] = []  # (base, size) per allocation
-        where = []
+        sizes: Dict[int, int] = {}  # allocation base -> size
+        raw_where: List[Optional[Tuple[int, int]]] = []  # (allocation base, offset) per segment
         base, size = ctypes.c_uint64(0), ctypes.c_uint64(0)
         for seg in self.plan.segs:
             ptr = int(seg["ptr"])
             if int(seg["nbytes"]) == 0 or ptr == 0:
-                where.append(None)
+                raw_where.append(None)
                 continue
             # one handle per allocation (tensors of one caching-allocator segment share it)
             lib.check(lib.tpi_mem_range(ctypes.c_void_p(ptr), ctypes.byref(base),
                                         ctypes.byref(size)), "tpi_mem_range")
-            key = int(base.value)
-            if key not in allocations:
-                allocations[key] = len(bases)
-                bases.append((key, int(size.value)))
-            where.append([allocations[key], ptr - key])
-        # which allocations travel as dma-bufs
-        if route == "dmabuf" and dmabuf_ok:
-            as_dmabuf = list(range(len(bases)))
-        elif route == "ipc" or not dmabuf_ok:
-            as_dmabuf = []
-            big = [i for i, (_, sz) in enumerate(bases) if sz >= limit]
-            if big:
-                raise CheckpointError(
-                    "no HBM hand-off: %d allocation(s) of %.2f GiB or more (the largest %.2f "
-                    "GiB), and HIP IPC imports of such allocations never return "
-                    "(TPI_IPC_MAX_ALLOC%s); the successor restores from the host copy" % (
-                        len(big), limit / 2 ** 30, max(bases[i][1] for i in big) / 2 ** 30,
-                        "" if dmabuf_ok else "; this runtime cannot export dma-bufs"))
-        else:
-            as_dmabuf = [i for i, (_, sz) in enumerate(bases) if sz >= limit]
+            sizes.setdefault(int(base.value), int(size.value))
+            raw_where.append((int(base.value), ptr - int(base.value)))
+        big = {key for key, sz in sizes.items() if sz >= limit}
+        if big and (route == "ipc" or (route == "dmabuf" and not lib.tpi_dmabuf_available())):
+            raise CheckpointError(
+                "no HBM hand-off: %d allocation(s) of %.2f GiB or more (the largest %.2f GiB), "
+                "and HIP IPC imports of such allocations never return (TPI_IPC_MAX_ALLOC); the "
+                "successor restores from the host copy" % (
+                    len(big), limit / 2 ** 30, max(sizes[k] for k in big) / 2 ** 30))
+        pieces: Dict[str, List[List[int]]] = {}
+        if big and route == "auto":
+            pieces = self._relocate(raw_where, big)  # segment -> [[block base, 0, n], ...]
+        # the allocations the successor maps, in order
+        keys: List[int] = []
+        index: Dict[int, int] = {}
+
+        def idx(key: int) -> int:
+            if key not in index:
+                index[key] = len(keys)
+                keys.append(key)
+            return index[key]
+
+        where: List[Optional[List[int]]] = []
+        for si, w in enumerate(raw_where):
+            if w is None or str(si) in pieces:
+                where.append(None)
+            else:
+                where.append([idx(w[0]), w[1]])
+        for si in pieces:
+            pieces[si] = [[idx(p[0]), p[1], p[2]] for p in pieces[si]]
+        alloc_sizes = [sizes.get(k) or self._relocated_size[k] for k in keys]
+        as_dmabuf = [i for i, k in enumerate(keys) if k in big] if route == "dmabuf" else []
         doc = {"format": "tpi-hbm-2", "pid": os.getpid(),
                "entries_sha256": self._entries_digest, "total": self.plan.total,
-               "tile_bytes": self.plan.tile_bytes, "where": where,
+               "tile_bytes": self.plan.tile_bytes, "where": where, "pieces": pieces,
                "segs": self.plan.segs.tobytes().hex(), "created": time.time(),
-               "metadata": metadata or {},
-               "allocations": [sz for _, sz in bases],
+               "metadata": metadata or {}, "allocations": alloc_sizes,
                # the generation the save that follows this export will write
                "generation": self._target()[1]}
         handle = ctypes.create_string_buffer(64)
         offset = ctypes.c_uint64(0)
         ipc: Dict[str, str] = {}
         dmabuf_set = set(as_dmabuf)
-        for i, (key, _) in enumerate(bases):
+        for i, key in enumerate(keys):
             if i in dmabuf_set:
                 continue
             lib.check(lib.tpi_ipc_export(ctypes.c_void_p(key), handle, ctypes.byref(offset),
@@ -1521,7 +1542,7 @@ class Checkpointer:
         doc["ipc"] = ipc
         if as_dmabuf:
             doc["socket"], doc["dmabuf"] = self._serve_dmabufs(
-                [(i, bases[i][0], bases[i][1]) for i in as_dmabuf])
+                [(i, keys[i], alloc_sizes[i]) for i in as_dmabuf])
         bus = ctypes.create_string_buffer(64)
         lib.tpi_device_pci_bus_id(self.device_index, bus, 64)
         doc["device"] = bus.value.decode()
@@ -1530,6 +1551,54 @@ class Checkpointer:
             json.dump(doc, handle_file)
         os.replace(tmp, manifest)
         return manifest
+
+    def _relocate(self, raw_where: List[Optional[Tuple[int, int]]],
+                  big: set) -> Dict[str, List[List[int]]]:
+        """Copy every tensor living in one of the ``big`` allocations (HIP IPC cannot open
+        them) into plain hipMalloc blocks of at most ``RELOCATE_CHUNK`` bytes, device to
+        device; returns, per segment index, its pieces ``[block base, 0, bytes]`` in stream
+        order.  The blocks stay allocated until this process exits (the successor maps them).
+        Raises CheckpointError when such a tensor is not contiguous or the device has no room
+        for the copies -- the successor then restores from the host copy."""
+        import torch
+
+        lib = hip()
+        todo = [si for si, w in enumerate(raw_where) if w is not None and w[0] in big]
+        need = sum(int(self.plan.segs[si]["nbytes"]) for si in todo)
+        free, _ = torch.cuda.mem_get_info(self.device_index)
+        if free < need + (1 << 30):
+            raise CheckpointError("no HBM hand-off: relocating %.2f GB out of allocations HIP "
+                                  "IPC cannot open needs that much free HBM (%.2f GB free)"
+                                  % (need / 1e9, free / 1e9))
+        blocks: List[int] = []
+        self._relocated_size: Dict[int, int] = getattr(self, "_relocated_size", {})
+        self._relocated = getattr(self, "_relocated", [])
+        out: Dict[str, List[List[int]]] = {}
+        stream = torch.cuda.current_stream(self.device_index).cuda_stream
+        ptr = ctypes.c_void_p()
+        try:
+            for si in todo:
+                seg = self.plan.segs[si]
+                if int(seg["kind"]) != SEG_CONTIG:
+                    raise CheckpointError(
+                        "no HBM hand-off: a non-contiguous tensor lives in an allocation HIP "
+                        "IPC cannot open")
+                nbytes, src = int(seg["nbytes"]), int(seg["ptr"])
+                parts = []
+                for k in range(0, nbytes, RELOCATE_CHUNK):
+                    n = min(RELOCATE_CHUNK, nbytes - k)
+                    lib.check(lib.tpi_dev_alloc(n, ctypes.byref(ptr)), "tpi_dev_alloc")
+                    blocks.append(ptr.value)
+                    lib.check(lib.tpi_d2d(ptr, ctypes.c_void_p(src + k), n, stream), "tpi_d2d")
+                    self._relocated_size[ptr.value] = n
+                    parts.append([ptr.value, 0, n])
+                out[str(si)] = parts
+        except BaseException:
+            for b in blocks:
+                lib.tpi_dev_free(ctypes.c_void_p(b))
+            raise
+        self._relocated.extend(blocks)
+        return out
 
     def _serve_dmabufs(self, allocs: List[Tuple[int, int, int]]) -> Tuple[str, Dict[str, Any]]:
         """Export every ``(index, base, size)`` allocation as a dma-buf and serve the
@@ -1881,8 +1950,11 @@ class Checkpointer:
                 raise CheckpointError("HBM hand-off describes a different tensor set")
             for i, w in enumerate(doc["where"]):
                 src[i]["ptr"] = 0 if w is None else bases[w[0]] + w[1]
+            dst = None
+            if doc.get("pieces"):
+                src, dst = _split_relocated(src, self.plan.segs, doc["pieces"], bases)
             sig = torch.cuda.current_stream(self.device_index).cuda_stream
-            res = self.engine.copy_segments(src, self.plan, sig)  # synchronous: copy done
+            res = self.engine.copy_segments(src, self.plan, sig, dst)  # synchronous: copy done
         except BaseException:
             close_all()
             raise
@@ -2026,6 +2098,21 @@ class Checkpointer:
                 storage = t.untyped_storage()
                 freed += storage.nbytes()
                 storage.resize_(0)
+        freed += self._free_relocated()
+        return freed
+
+    def _free_relocated(self) -> int:
+        """Free the blocks an HBM export relocated tensors into (:meth:`_relocate`); only once
+        no successor maps them any more (the hand-off protocol has ended)."""
+        blocks = getattr(self, "_relocated", None)
+        if not blocks:
+            return 0
+        self._relocated = []
+        lib = hip()
+        freed = 0
+        for b in blocks:
+            lib.tpi_dev_free(ctypes.c_void_p(b))
+            freed += self._relocated_size.pop(b, 0)
         return freed
 
     def wait_hbm_close(self) -> None:
@@ -2068,6 +2155,7 @@ class Checkpointer:
             self.region.close()
             self.region = None
         self._close_dmabuf_server()
+        self._free_relocated()
         if self.plan is not None and hasattr(self.plan, "unbind"):
             self.plan.unbind()  # the tensors' HBM can go with the caller's references
 
@@ -2076,6 +2164,38 @@ class Checkpointer:
 
     def __exit__(self, *exc):
         self.close()
+
+
+def _split_relocated(src: np.ndarray, dst: np.ndarray, pieces: Dict[str, List[List[int]]],
+                     bases: List[Optional[int]]) -> Tuple[np.ndarray, np.ndarray]:
+    """Source and destination descriptors for an HBM hand-off whose exporter relocated some
+    tensors into blocks (:meth:`Checkpointer._relocate`): each such segment becomes one
+    contiguous segment per block, the destination split at the same stream offsets.  Both
+    stay sorted by stream offset, so the copy and its verification see the same stream."""
+    out_src, out_dst = [], []
+    for i in range(len(src)):
+        parts = pieces.get(str(i))
+        if not parts:
+            out_src.append(src[i:i + 1])
+            out_dst.append(dst[i:i + 1])
+            continue
+        if int(dst[i]["kind"]) != SEG_CONTIG:
+            raise CheckpointError("HBM hand-off: a relocated tensor is not contiguous here")
+        if sum(int(p[2]) for p in parts) != int(src[i]["nbytes"]):
+            raise CheckpointError("HBM hand-off: relocated pieces do not cover tensor %d" % i)
+        done = 0
+        for alloc, off, n in parts:
+            s_part = src[i:i + 1].copy()
+            d_part = dst[i:i + 1].copy()
+            for part, ptr in ((s_part, bases[alloc] + off), (d_part, int(dst[i]["ptr"]) + done)):
+                part["ptr"] = ptr
+                part["off"] = int(src[i]["off"]) + done
+                part["nbytes"] = n
+                part["kind"], part["ndim"] = SEG_CONTIG, 0
+            out_src.append(s_part)
+            out_dst.append(d_part)
+            done += n
+    return np.concatenate(out_src), np.concatenate(out_dst)
 
 
 def _region_layout(path: str) -> Dict[str, Any]:

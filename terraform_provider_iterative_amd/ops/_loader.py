@@ -147,6 +147,9 @@ class HipLib:
             "tpi_dmabuf_close": (i32, [i32]),
             "tpi_dmabuf_import": (i32, [i32, i32, c.POINTER(vp), c.POINTER(u64)]),
             "tpi_dmabuf_unmap": (i32, [vp]),
+            "tpi_dev_alloc": (i32, [u64, c.POINTER(vp)]),
+            "tpi_dev_free": (i32, [vp]),
+            "tpi_d2d": (i32, [vp, vp, u64, u64]),
             "tpi_comm_unique_id": (i32, [c.c_char_p]),
             "tpi_comm_init_rank": (vp, [c.c_char_p, i32, i32, i32]),
             "tpi_comm_init_all": (i32, [i32, c.POINTER(i32), c.POINTER(vp)]),

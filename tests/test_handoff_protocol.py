@@ -591,7 +591,7 @@ def test_handoff_mode_row(binary, tmp_path, mode):
 
 
 def test_dmabuf_route_hands_every_allocation_over_the_socket(tmp_path, monkeypatch):
-    """The hand-off's mixed route (round 5): allocations below IPC_MAX_ALLOC travel as HIP IPC
+    """TPI_HBM_ROUTE=dmabuf (round 5): allocations below IPC_MAX_ALLOC travel as HIP IPC
     handles in the manifest, the larger ones as dma-buf descriptors the exporter serves over an
     abstract Unix socket (batches of FDS_PER_MESSAGE, SCM_RIGHTS), each buffer's size checked
     on both sides.  The successor maps each, points the source segments at base + offset + the
@@ -659,7 +659,7 @@ def test_dmabuf_route_hands_every_allocation_over_the_socket(tmp_path, monkeypat
     monkeypatch.setattr(torch.cuda, "synchronize", lambda *a: None)
     monkeypatch.setattr(torch.cuda, "current_stream",
                         lambda *a: type("S", (), {"cuda_stream": 0})())
-    monkeypatch.delenv("TPI_HBM_ROUTE", raising=False)
+    monkeypatch.setenv("TPI_HBM_ROUTE", "dmabuf")
 
     n = n_alloc + n_small
     segs = np.zeros(n, dtype=SEG_DTYPE)
@@ -693,7 +693,7 @@ def test_dmabuf_route_hands_every_allocation_over_the_socket(tmp_path, monkeypat
     copied = {}
 
     class Engine:
-        def copy_segments(self, src, plan, sig):
+        def copy_segments(self, src, plan, sig, dst=None):
             copied["src"] = src.copy()
 
             class Res:
@@ -722,3 +722,141 @@ def test_dmabuf_route_hands_every_allocation_over_the_socket(tmp_path, monkeypat
     assert sorted(unmapped) == maps and sorted(closed) == sorted(opened)
     assert ck.hbm_claim_owner() is None
     exporter._close_dmabuf_server()
+
+
+def test_auto_route_relocates_tensors_of_big_allocations(tmp_path, monkeypatch):
+    """The default route (round 5): tensors in an allocation HIP IPC cannot open (>= 2 GiB) are
+    copied device to device into plain blocks of at most RELOCATE_CHUNK bytes, which travel
+    over HIP IPC like every other allocation; the successor splits those segments -- source and
+    destination at the same stream offsets -- and copies as usual.  Fake device: no GPU."""
+    import numpy as np
+
+    import torch
+
+    from terraform_provider_iterative_amd.checkpoint import checkpointer as ckmod
+    from terraform_provider_iterative_amd.ops.packing import SEG_CONTIG, SEG_DTYPE
+
+    G = 1 << 30
+    # allocation 0: 5 GiB holding two tensors (3 GiB + 1.5 GiB); 1: a small one; 2: 2.5 GiB
+    tensors = [(0x1000_0000_0000, 0, 3 * G), (0x1000_0000_0000, 3 * G, G + G // 2),
+               (0x2000_0000_0000, 0, 1 << 20), (0x3000_0000_0000, 0, 5 * G // 2)]
+    alloc_size = {0x1000_0000_0000: 5 * G, 0x2000_0000_0000: 4 << 20, 0x3000_0000_0000: 5 * G // 2}
+    blocks, copies, opened = [], [], {}
+
+    class FakeLib:
+        def tpi_mem_range(self, ptr, base, size):
+            key = max(k for k in alloc_size if k <= ptr.value)
+            base._obj.value, size._obj.value = key, alloc_size[key]
+            return 0
+
+        def tpi_dev_alloc(self, n, out):
+            out._obj.value = 0x9000_0000_0000 + len(blocks) * (2 * G)
+            blocks.append((out._obj.value, n))
+            return 0
+
+        def tpi_d2d(self, dst, src, n, stream):
+            copies.append((dst.value, src.value, n))
+            return 0
+
+        def tpi_dev_free(self, ptr):
+            return 0
+
+        def tpi_dmabuf_available(self):
+            return 1
+
+        def tpi_ipc_export(self, ptr, handle, off, size):
+            handle.raw = ("%064x" % ptr.value).encode()[:64]
+            return 0
+
+        def tpi_ipc_open(self, handle, device, out):
+            out._obj.value = int(handle.decode(), 16) + 0x0100_0000_0000_0000  # "mapped" here
+            opened[out._obj.value] = handle
+            return 0
+
+        def tpi_ipc_close(self, ptr):
+            return 0
+
+        def tpi_device_pci_bus_id(self, dev, buf, n):
+            buf.value = b"0000:75:00.0"
+            return 0
+
+        def check(self, rc, what):
+            assert rc == 0, what
+
+    monkeypatch.setattr(ckmod, "hip", lambda *a, **k: FakeLib())
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a: None)
+    monkeypatch.setattr(torch.cuda, "mem_get_info", lambda *a: (200 * G, 288 * G))
+    monkeypatch.setattr(torch.cuda, "current_stream",
+                        lambda *a: type("S", (), {"cuda_stream": 0})())
+    monkeypatch.delenv("TPI_HBM_ROUTE", raising=False)
+
+    segs = np.zeros(len(tensors), dtype=SEG_DTYPE)
+    off = 0
+    for i, (key, o, n) in enumerate(tensors):
+        segs[i]["ptr"], segs[i]["off"], segs[i]["nbytes"] = key + o, off, n
+        segs[i]["kind"] = SEG_CONTIG
+        off += n
+
+    class Plan:
+        pass
+
+    Plan.segs, Plan.total, Plan.tile_bytes = segs, off, 1 << 20
+
+    class Exporter(_FakeHandoff):
+        device_index = 0
+        engine = object()
+        plan = Plan
+        _entries_digest = "d"
+        export_hbm = Checkpointer.export_hbm
+        _relocate = Checkpointer._relocate
+
+        def _target(self):
+            return None, 1
+
+    with open(Exporter(str(tmp_path / "spill")).export_hbm()) as f:
+        doc = json.load(f)
+    # 3 + 2 + 3 blocks of <= 1 GiB; the small allocation stays itself; nothing >= 2 GiB left
+    assert sorted(doc["pieces"]) == ["0", "1", "3"]
+    assert [len(doc["pieces"][k]) for k in ("0", "1", "3")] == [3, 2, 3]
+    assert max(doc["allocations"]) <= ckmod.RELOCATE_CHUNK and len(doc["ipc"]) == 9
+    assert sum(n for _, _, n in copies) == 3 * G + G + G // 2 + 5 * G // 2
+    assert doc["where"][2] is not None and doc["where"][0] is None
+
+    dst_base = 0x5000_0000_0000
+    dsegs = segs.copy()
+    dsegs["ptr"] = [dst_base + int(s["off"]) for s in segs]
+    seen = {}
+
+    class Engine:
+        def copy_segments(self, src, plan, sig, dst=None):
+            seen["src"], seen["dst"] = src.copy(), dst.copy()
+
+            class Res:
+                bad_tiles = 0
+            return Res()
+
+    class DstPlan:
+        pass
+
+    DstPlan.segs, DstPlan.total, DstPlan.tile_bytes = dsegs, off, 1 << 20
+
+    class Successor(_FakeHandoff):
+        device_index = 0
+        engine = Engine()
+        plan = DstPlan
+        restore_hbm = Checkpointer.restore_hbm
+
+        def _hbm_doc(self):
+            return doc
+
+    ck = Successor(str(tmp_path / "spill"))
+    ck.restore_hbm()
+    ck._hbm_closer.join(10)
+    src, dst = seen["src"], seen["dst"]
+    assert len(src) == len(dst) == 3 + 2 + 1 + 3
+    assert list(src["off"]) == list(dst["off"]) == sorted(src["off"])
+    assert list(src["nbytes"]) == list(dst["nbytes"])
+    assert all(int(d["ptr"]) == dst_base + int(d["off"]) for d in dst)  # split in place
+    # every source piece is a mapped block (or the small allocation), never a big allocation
+    mapped = set(opened)
+    assert all(any(b <= int(p) < b + 2 * G for b in mapped) for p in src["ptr"])
