@@ -1948,11 +1948,17 @@ class Checkpointer:
             src = np.frombuffer(bytes.fromhex(doc["segs"]), dtype=self.plan.segs.dtype).copy()
             if len(src) != len(self.plan.segs):
                 raise CheckpointError("HBM hand-off describes a different tensor set")
+            owner = np.full(len(src), -1, dtype=np.int64)  # mapped allocation of each segment
             for i, w in enumerate(doc["where"]):
                 src[i]["ptr"] = 0 if w is None else bases[w[0]] + w[1]
-            dst = None
+                owner[i] = -1 if w is None else w[0]
+            dst = self.plan.segs
             if doc.get("pieces"):
-                src, dst = _split_relocated(src, self.plan.segs, doc["pieces"], bases)
+                src, dst, owner = _split_relocated(src, self.plan.segs, doc["pieces"], bases,
+                                                   owner)
+            # never launch a copy that could touch memory outside what is mapped: every source
+            # segment inside its mapped allocation, every destination inside its own
+            _check_copy_ranges(src, owner, bases, sizes, dst, lib)
             sig = torch.cuda.current_stream(self.device_index).cuda_stream
             res = self.engine.copy_segments(src, self.plan, sig, dst)  # synchronous: copy done
         except BaseException:
@@ -2166,18 +2172,66 @@ class Checkpointer:
         self.close()
 
 
+def _seg_extent(seg) -> Tuple[int, int]:
+    """``[lo, hi)`` of the memory a segment descriptor touches (strided views: from their
+    lowest to their highest element)."""
+    ptr, nbytes = int(seg["ptr"]), int(seg["nbytes"])
+    if int(seg["kind"]) == SEG_CONTIG or nbytes == 0:
+        return ptr, ptr + nbytes
+    elem = int(seg["elem"])
+    neg = pos = 0
+    for d in range(int(seg["ndim"])):
+        span = (int(seg["sizes"][d]) - 1) * int(seg["strides"][d]) * elem
+        if span < 0:
+            neg += span
+        else:
+            pos += span
+    return ptr + neg, ptr + pos + elem
+
+
+def _check_copy_ranges(src: np.ndarray, owner: np.ndarray, bases: List[Optional[int]],
+                       sizes: List[int], dst: np.ndarray, lib) -> None:
+    """Host-side bounds check before the hand-off's copy kernel: each source segment must lie
+    inside the predecessor allocation it was mapped from (``owner``), each destination segment
+    inside the device allocation holding it in this process.  A descriptor that fails raises
+    CheckpointError (the caller restores from the host copy) instead of faulting the GPU."""
+    base, size = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    for i in range(len(src)):
+        if int(src[i]["nbytes"]) == 0:
+            continue
+        a = int(owner[i])
+        lo, hi = _seg_extent(src[i])
+        if a < 0 or bases[a] is None or lo < bases[a] or hi > bases[a] + sizes[a]:
+            raise CheckpointError(
+                "HBM hand-off: source segment %d [%#x, %#x) lies outside its mapped allocation "
+                "%d [%s, +%d)" % (i, lo, hi, a, None if a < 0 else bases[a],
+                                  -1 if a < 0 else sizes[a]))
+        lo, hi = _seg_extent(dst[i])
+        if lib.tpi_mem_range(ctypes.c_void_p(int(dst[i]["ptr"])), ctypes.byref(base),
+                             ctypes.byref(size)) != 0:
+            raise CheckpointError("HBM hand-off: destination segment %d is not device memory"
+                                  % i)
+        if lo < int(base.value) or hi > int(base.value) + int(size.value):
+            raise CheckpointError(
+                "HBM hand-off: destination segment %d [%#x, %#x) lies outside its allocation "
+                "[%#x, +%d)" % (i, lo, hi, int(base.value), int(size.value)))
+
+
 def _split_relocated(src: np.ndarray, dst: np.ndarray, pieces: Dict[str, List[List[int]]],
-                     bases: List[Optional[int]]) -> Tuple[np.ndarray, np.ndarray]:
+                     bases: List[Optional[int]], owner: np.ndarray
+                     ) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
     """Source and destination descriptors for an HBM hand-off whose exporter relocated some
     tensors into blocks (:meth:`Checkpointer._relocate`): each such segment becomes one
     contiguous segment per block, the destination split at the same stream offsets.  Both
-    stay sorted by stream offset, so the copy and its verification see the same stream."""
-    out_src, out_dst = [], []
+    stay sorted by stream offset, so the copy and its verification see the same stream.
+    ``owner`` (mapped allocation per segment) is expanded alongside."""
+    out_src, out_dst, out_owner = [], [], []
     for i in range(len(src)):
         parts = pieces.get(str(i))
         if not parts:
             out_src.append(src[i:i + 1])
             out_dst.append(dst[i:i + 1])
+            out_owner.append(int(owner[i]))
             continue
         if int(dst[i]["kind"]) != SEG_CONTIG:
             raise CheckpointError("HBM hand-off: a relocated tensor is not contiguous here")
@@ -2194,8 +2248,9 @@ def _split_relocated(src: np.ndarray, dst: np.ndarray, pieces: Dict[str, List[Li
                 part["kind"], part["ndim"] = SEG_CONTIG, 0
             out_src.append(s_part)
             out_dst.append(d_part)
+            out_owner.append(int(alloc))
             done += n
-    return np.concatenate(out_src), np.concatenate(out_dst)
+    return np.concatenate(out_src), np.concatenate(out_dst), np.array(out_owner, np.int64)
 
 
 def _region_layout(path: str) -> Dict[str, Any]:

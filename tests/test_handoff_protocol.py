@@ -823,6 +823,7 @@ def test_auto_route_relocates_tensors_of_big_allocations(tmp_path, monkeypatch):
     assert doc["where"][2] is not None and doc["where"][0] is None
 
     dst_base = 0x5000_0000_0000
+    alloc_size[dst_base] = off  # the successor's own allocation holding its tensors
     dsegs = segs.copy()
     dsegs["ptr"] = [dst_base + int(s["off"]) for s in segs]
     seen = {}
@@ -860,3 +861,37 @@ def test_auto_route_relocates_tensors_of_big_allocations(tmp_path, monkeypatch):
     # every source piece is a mapped block (or the small allocation), never a big allocation
     mapped = set(opened)
     assert all(any(b <= int(p) < b + 2 * G for b in mapped) for p in src["ptr"])
+
+
+def test_copy_ranges_are_checked_on_the_host_before_any_kernel():
+    """A hand-off descriptor that would read past the mapped predecessor allocation, or write
+    past the successor's own, is refused on the host (CheckpointError: restore from the host
+    copy) -- the copy kernel never sees it."""
+    import numpy as np
+
+    from terraform_provider_iterative_amd.checkpoint.checkpointer import (_check_copy_ranges,
+                                                                          _seg_extent)
+    from terraform_provider_iterative_amd.ops.packing import SEG_CONTIG, SEG_DTYPE
+
+    class Lib:
+        def tpi_mem_range(self, ptr, base, size):
+            base._obj.value, size._obj.value = 0x9000, 0x1000  # the successor's allocation
+            return 0
+
+    src = np.zeros(2, dtype=SEG_DTYPE)
+    dst = np.zeros(2, dtype=SEG_DTYPE)
+    src["kind"] = dst["kind"] = SEG_CONTIG
+    src["ptr"], src["nbytes"] = [0x1000, 0x1800], [0x800, 0x800]
+    dst["ptr"], dst["nbytes"] = [0x9000, 0x9800], [0x800, 0x800]
+    owner = np.array([0, 0])
+    _check_copy_ranges(src, owner, [0x1000], [0x1000], dst, Lib())  # fits exactly
+    with pytest.raises(CheckpointError, match="source segment 1"):
+        _check_copy_ranges(src, owner, [0x1000], [0xfff], dst, Lib())
+    dst["nbytes"][1] = 0x801
+    with pytest.raises(CheckpointError, match="destination segment 1"):
+        _check_copy_ranges(src, owner, [0x1000], [0x1000], dst, Lib())
+    # a strided view's extent runs from its lowest to its highest element
+    v = np.zeros(1, dtype=SEG_DTYPE)[0]
+    v["ptr"], v["nbytes"], v["kind"], v["elem"], v["ndim"] = 0x100, 64, 1, 4, 2
+    v["sizes"][:2], v["strides"][:2] = [4, 4], [-8, 1]
+    assert _seg_extent(v) == (0x100 - 3 * 8 * 4, 0x100 + 3 * 4 + 4)
