@@ -147,7 +147,7 @@ def first_log_latency(timeout: float = 60.0, parallelism: int = 1):
 E2E_KEYS = ("ok", "verified", "status", "signal_to_restored_s", "save_s",
             "rank_start_to_restored_s", "saved_to_restored_s", "signal_to_durable_s", "streamed",
             "warm_standby_activated", "hot_standby", "standby_pinned_wait_s", "restore_journal",
-            "extra_tensors_gib", "delete_s", "rank_exit_to_settled_s",
+            "extra_tensors_gib", "delete_s", "rank_exit_to_settled_s", "vram_before_start",
             "released_exit_pending_at_settle")
 
 

@@ -209,6 +209,11 @@ def main():
               "step_seconds": args.step_seconds, "materialize": args.materialize,
               "extra_tensors_gib": [float(x) for x in args.extra_gib.split(",") if x.strip()]}
     os.environ["TPI_WARM_STANDBY"] = "hot" if args.hot else ("1" if args.standby else "0")
+    # processes of an earlier run may still be giving back their HBM: start from an empty GPU
+    from terraform_provider_iterative_amd.parallel.placement import discover, wait_vram_drained
+
+    gpus = discover()
+    result["vram_before_start"] = wait_vram_drained(gpus[0].pci) if gpus else {}
     try:
         task.create()
         deadline = time.time() + args.timeout

@@ -1959,6 +1959,10 @@ class Checkpointer:
             # never launch a copy that could touch memory outside what is mapped: every source
             # segment inside its mapped allocation, every destination inside its own
             _check_copy_ranges(src, owner, bases, sizes, dst, lib)
+            try:  # diagnostic for the journal
+                self.hbm_free_before_copy = torch.cuda.mem_get_info(self.device_index)[0]
+            except Exception:
+                self.hbm_free_before_copy = 0
             sig = torch.cuda.current_stream(self.device_index).cuda_stream
             res = self.engine.copy_segments(src, self.plan, sig, dst)  # synchronous: copy done
         except BaseException:

@@ -949,7 +949,9 @@ def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None,
         try:  # the predecessor on this GPU is alive and exported its tensors: copy from HBM
             res = checkpointer.restore_hbm()
             journal("checkpoint-restored", "HBM hand-off", *_describe(res),
-                    "ipc open %.3f s" % getattr(checkpointer, "hbm_open_s", 0.0))
+                    "ipc open %.3f s" % getattr(checkpointer, "hbm_open_s", 0.0),
+                    "%.1f GB free at the copy" % (
+                        getattr(checkpointer, "hbm_free_before_copy", 0) / 1e9))
             notify_restored(hbm=True)
 
             def behind():  # after "restored": the unmapping, then the host copy's durability
@@ -984,7 +986,8 @@ def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None,
             # whose spill failed, and there even when no host copy completed at all
             return hbm["metadata"] or (header or {}).get("metadata", {})
         except Exception as error:  # fall back to the host region
-            journal("checkpoint-hbm-failed", str(error))
+            journal("checkpoint-hbm-failed", str(error), "%.1f GB free at the copy" % (
+                getattr(checkpointer, "hbm_free_before_copy", 0) / 1e9))
     if header is not None:
         try:
             res = checkpointer.restore(generation=generation)

@@ -18,7 +18,7 @@ import json
 import os
 import time
 from contextlib import contextmanager
-from typing import Dict, Iterator, List, Optional
+from typing import Dict, Iterator, List, Optional, Tuple
 
 from ..utils.record import field, record
 
@@ -634,6 +634,38 @@ def pin_to_numa(node: int) -> Optional[List[int]]:
         return None
     os.sched_setaffinity(0, cpus)
     return sorted(cpus)
+
+
+def vram_usage(pci: str) -> Optional[Tuple[int, int]]:
+    """``(used, total)`` bytes of a GPU's device memory from the amdgpu driver's sysfs
+    counters (no GPU context needed: readable while other processes still hold the device),
+    None when unreadable.  ``pci``: the GPU's bus id (:attr:`GPU.pci`)."""
+    base = "/sys/bus/pci/devices/%s" % pci
+    used, total = _read(base + "/mem_info_vram_used").strip(), \
+        _read(base + "/mem_info_vram_total").strip()
+    if not (used.isdigit() and total.isdigit()):
+        return None
+    return int(used), int(total)
+
+
+def wait_vram_drained(pci: str, fraction: float = 0.03, timeout: float = 120.0) -> Dict:
+    """Block until at most ``fraction`` of a GPU's memory is in use (processes of an earlier
+    task may still be tearing down, their HBM not yet back), or ``timeout``; returns what was
+    seen: ``{"used_gb_at_start", "waited_s", "used_gb"}`` (empty when sysfs is unreadable).
+    Back-to-back measurements start from an empty device this way."""
+    import time
+
+    first = vram_usage(pci) if pci else None
+    if first is None:
+        return {}
+    t0 = time.monotonic()
+    now = first
+    while now is not None and now[0] > fraction * now[1] and time.monotonic() - t0 < timeout:
+        time.sleep(0.1)
+        now = vram_usage(pci)
+    return {"used_gb_at_start": round(first[0] / 1e9, 2),
+            "waited_s": round(time.monotonic() - t0, 2),
+            "used_gb": round((now or first)[0] / 1e9, 2)}
 
 
 def pin_to_device_numa(device_index: int) -> Optional[List[int]]:
