@@ -148,6 +148,7 @@ E2E_KEYS = ("ok", "verified", "status", "signal_to_restored_s", "save_s",
             "rank_start_to_restored_s", "saved_to_restored_s", "signal_to_durable_s", "streamed",
             "warm_standby_activated", "hot_standby", "standby_pinned_wait_s", "restore_journal",
             "extra_tensors_gib", "delete_s", "rank_exit_to_settled_s", "vram_before_start",
+            "memory_guard",
             "released_exit_pending_at_settle")
 
 

@@ -278,6 +278,9 @@ def main():
         result["durability"] = next((c for c, _, _ in events if c in (
             "checkpoint-durable", "checkpoint-not-durable", "checkpoint-durability-unknown")), None)
         result["verified"] = any("verified True" in l for l in logs)
+        # the host-memory guard the supervisor runs for the ranks (cgroup, or the 20 ms poll)
+        result["memory_guard"] = next((d for c, _, d in events
+                                       if c in ("memory-cgroup", "memory-guard")), None)
         t_settled, _ = first("supervisor-settled")
         t_exit, _ = first("rank-exit", t_respawn or 0.0)
         if t_settled and t_exit:  # the successor's exit -> final sync + final state
