@@ -1566,6 +1566,11 @@ class Checkpointer:
         todo = [si for si, w in enumerate(raw_where) if w is not None and w[0] in big]
         need = sum(int(self.plan.segs[si]["nbytes"]) for si in todo)
         free, _ = torch.cuda.mem_get_info(self.device_index)
+        from ..parallel.placement import device_vram_usage
+
+        usage = device_vram_usage(self.device_index)  # the driver's count (delayed frees)
+        if usage is not None:
+            free = min(free, usage[1] - usage[0])
         if free < need + (1 << 30):
             raise CheckpointError("no HBM hand-off: relocating %.2f GB out of allocations HIP "
                                   "IPC cannot open needs that much free HBM (%.2f GB free)"

@@ -460,9 +460,17 @@ def wait_for_device_memory(spill: str, margin: float = 0.05,
     if timeout is None:
         timeout = float(os.environ.get("TPI_STREAM_TIMEOUT", "30"))
     dev = torch.cuda.current_device()
+    from ..parallel.placement import device_vram_usage
+
     t0 = time.monotonic()
     while time.monotonic() - t0 < timeout:
         free, _ = torch.cuda.mem_get_info(dev)
+        # The driver's own count too: memory an exiting process gave back can still be held
+        # (delayed frees) while the runtime already reports it free.  Filling the device on
+        # top of it made the hand-off copy fault in round 5 (profiles/round5/ipc_cause.md).
+        usage = device_vram_usage(dev)
+        if usage is not None:
+            free = min(free, usage[1] - usage[0])
         if free >= need or streaming_writer(spill) is None:
             break
         time.sleep(0.005)

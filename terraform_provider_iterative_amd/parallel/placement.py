@@ -648,6 +648,21 @@ def vram_usage(pci: str) -> Optional[Tuple[int, int]]:
     return int(used), int(total)
 
 
+def device_vram_usage(device_index: int) -> Optional[Tuple[int, int]]:
+    """:func:`vram_usage` of HIP device ``device_index`` (found through its PCI bus id)."""
+    import ctypes
+
+    from ..ops import hip
+
+    lib = hip(required=False)
+    if lib is None:
+        return None
+    bus = ctypes.create_string_buffer(64)
+    if lib.tpi_device_pci_bus_id(device_index, bus, 64) != 0:
+        return None
+    return vram_usage(bus.value.decode().lower())
+
+
 def wait_vram_drained(pci: str, fraction: float = 0.03, timeout: float = 120.0) -> Dict:
     """Block until at most ``fraction`` of a GPU's memory is in use (processes of an earlier
     task may still be tearing down, their HBM not yet back), or ``timeout``; returns what was
