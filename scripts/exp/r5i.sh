@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round 5: the GPU test suite, then the headline bench (with its new preempt_e2e block).
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/r5i
+mkdir -p $O
+cd $R
+echo "[$(date +%T)] gpu tests"
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread \
+  > $O/gpu_tests.txt 2>&1
+rc=$?
+tail -25 $O/gpu_tests.txt
+case $rc in 0|1) ;; *) echo "tests ended with $rc: stopping"; exit $rc;; esac
+echo "[$(date +%T)] bench"
+timeout -k 10 900 python -u bench.py --steps 5 --warmup 1 > $O/bench.json 2> $O/bench.log
+brc=$?
+tail -5 $O/bench.log
+cat $O/bench.json
+exit $(( rc > brc ? rc : brc ))
