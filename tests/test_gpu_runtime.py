@@ -428,34 +428,47 @@ def test_resume_consistent_takes_the_hbm_hand_off(tmp_path):
         proc.wait(60)
 
 
+RELEASE_BEHIND = r'''
+import json, sys, torch
+sys.path.insert(0, %(root)r)
+from terraform_provider_iterative_amd.checkpoint import Checkpointer
+g = torch.Generator(device="cuda").manual_seed(21)
+src = {"w%%d" %% i: torch.randn(64 << 20, device="cuda", generator=g) for i in range(6)}
+src["view_a"] = src["w5"][: 1 << 20]
+ref = {k: v.clone() for k, v in src.items()}
+torch.cuda.synchronize()
+ck = Checkpointer(src, path=%(spill)r, chunk_bytes=64 << 20, codec="tpz1")
+before = torch.cuda.memory_reserved()
+res = ck.save({"step": 1}, release_behind=True)
+out = {"released": res.released_bytes,
+       "emptied": all(t.untyped_storage().nbytes() == 0 for t in src.values()),
+       "reserved_drop": before - torch.cuda.memory_reserved()}
+ck.close()
+dst = {k: torch.zeros_like(v) for k, v in ref.items() if k != "view_a"}
+dst["view_a"] = dst["w5"][: 1 << 20]
+with Checkpointer(dst, path=%(spill)r, chunk_bytes=64 << 20, codec="tpz1") as ck2:
+    out["bad_tiles"] = ck2.restore().bad_tiles
+    out["meta"] = ck2.header()["metadata"]
+    torch.cuda.synchronize()
+out["equal"] = all(torch.equal(dst[k], ref[k]) for k in ref)
+print(json.dumps(out))
+'''
+
+
 def test_save_releases_device_memory_behind_the_spill(tmp_path):
     """Big-state preemption: with release_behind the device storages are freed while the
     spill runs (each once its tiles are in host memory) and handed back to the driver; the
-    host copy is complete and restores into fresh tensors."""
-    from terraform_provider_iterative_amd.checkpoint import Checkpointer
+    host copy is complete and restores into fresh tensors.  Run in a fresh process: in this
+    one, a tensor an earlier test still holds can pin a cached segment the state would be
+    carved from, and such a segment never goes back to the driver."""
+    import json
+    import subprocess
 
-    # fresh segments for the state: a large free block cached by an earlier test would be split
-    # between the state and `ref` below, and a segment with a live block never goes back
-    torch.cuda.synchronize()
-    torch.cuda.empty_cache()
-    g = torch.Generator(device="cuda").manual_seed(21)
-    src = {"w%d" % i: torch.randn(64 << 20, device="cuda", generator=g) for i in range(6)}
-    src["view_a"] = src["w5"][: 1 << 20]
-    ref = {k: v.clone() for k, v in src.items()}
-    spill = str(tmp_path / "spill")
-    torch.cuda.synchronize()
-    torch.cuda.empty_cache()
-    ck = Checkpointer(src, path=spill, chunk_bytes=64 << 20, codec="tpz1")
-    before = torch.cuda.memory_reserved()
-    res = ck.save({"step": 1}, release_behind=True)
-    assert res.released_bytes == 6 * (64 << 20) * 4
-    assert all(t.untyped_storage().nbytes() == 0 for t in src.values())
-    assert torch.cuda.memory_reserved() <= before - res.released_bytes
-    ck.close()
-    dst = {k: torch.zeros_like(v) for k, v in ref.items() if k != "view_a"}
-    dst["view_a"] = dst["w5"][: 1 << 20]
-    with Checkpointer(dst, path=spill, chunk_bytes=64 << 20, codec="tpz1") as ck2:
-        assert ck2.restore().bad_tiles == 0 and ck2.header()["metadata"] == {"step": 1}
-        torch.cuda.synchronize()
-    for k in ref:
-        assert torch.equal(dst[k], ref[k]), k
+    proc = subprocess.run([sys.executable, "-c", RELEASE_BEHIND % {
+        "root": ROOT, "spill": str(tmp_path / "spill")}], capture_output=True, text=True,
+        timeout=180)
+    assert proc.returncode == 0, proc.stderr[-3000:]
+    out = json.loads(proc.stdout.strip().splitlines()[-1])
+    assert out["released"] == 6 * (64 << 20) * 4 and out["emptied"], out
+    assert out["reserved_drop"] >= out["released"], out
+    assert out["bad_tiles"] == 0 and out["meta"] == {"step": 1} and out["equal"], out
