@@ -241,6 +241,8 @@ struct tpi_engine {
   // HBM hand-off: tile digests of the fused copy, checked by its read-back pass
   uint64_t* d_digest = nullptr;
   size_t digest_cap = 0;
+  tpi_seg* d_src = nullptr;  // the hand-off's source descriptors (kept: no hipFree per call)
+  size_t src_cap = 0;
   uint64_t hash_ntiles = 0;
   bool hash_valid = false;
   // TPZ1 codec: raw pack scratch (one chunk), per-tile headers of the chunk in flight,
@@ -600,6 +602,7 @@ void tpi_engine_destroy(tpi_engine* e) {
   if (e->d_bad) (void)hipFree(e->d_bad);
   if (e->d_hash) (void)hipFree(e->d_hash);
   if (e->d_digest) (void)hipFree(e->d_digest);
+  if (e->d_src) (void)hipFree(e->d_src);
   if (e->d_prev) (void)hipFree(e->d_prev);
   if (e->d_idx) (void)hipFree(e->d_idx);
   if (e->d_count) (void)hipFree(e->d_count);
@@ -1447,6 +1450,21 @@ int tpi_engine_reserve(tpi_engine* e, int nsegs, uint64_t ntiles, int codec) {
     HIP_OK(hipMalloc(&e->d_crcs, ntiles * sizeof(uint32_t)));
     e->crc_cap = ntiles;
   }
+  // the HBM hand-off's buffers as well: a successor's first copy then allocates nothing
+  if (ntiles > e->digest_cap) {
+    if (e->d_digest) HIP_OK(hipFree(e->d_digest));
+    e->d_digest = nullptr;
+    e->digest_cap = 0;
+    HIP_OK(hipMalloc(&e->d_digest, ntiles * sizeof(uint64_t)));
+    e->digest_cap = ntiles;
+  }
+  if ((size_t)nsegs > e->src_cap) {
+    if (e->d_src) HIP_OK(hipFree(e->d_src));
+    e->d_src = nullptr;
+    e->src_cap = 0;
+    HIP_OK(hipMalloc(&e->d_src, (size_t)nsegs * sizeof(tpi_seg)));
+    e->src_cap = nsegs;
+  }
   if (codec && prepare_codec(e, ntiles)) return -1;
   return 0;
 }
@@ -1711,9 +1729,15 @@ int tpi_copy_segments(tpi_engine* e, const tpi_seg* src, const tpi_seg* dst, int
   if (check_segments(src, n, total)) return -1;
   if (prepare(e, dst, n, total)) return -1;  // dst -> d_segs
   e->hash_valid = false;
-  tpi_seg* d_src = nullptr;
-  HIP_OK(hipMalloc(&d_src, (size_t)n * sizeof(tpi_seg)));
-  auto release = [&] { (void)hipFree(d_src); };
+  if ((size_t)n > e->src_cap) {  // grown, never shrunk: no allocation per hand-off
+    if (e->d_src) HIP_OK(hipFree(e->d_src));
+    e->d_src = nullptr;
+    e->src_cap = 0;
+    HIP_OK(hipMalloc(&e->d_src, std::max<size_t>(n, 64) * sizeof(tpi_seg)));
+    e->src_cap = std::max<size_t>(n, 64);
+  }
+  tpi_seg* d_src = e->d_src;
+  auto release = [&] {};
   auto ok = [&](hipError_t err, const char* what) {
     if (err == hipSuccess) return true;
     fail(std::string(what) + ": " + hipGetErrorString(err));

@@ -1061,7 +1061,7 @@ extern "C" hipError_t tpi_launch_stream_copy_hash(const tpi_seg* src, const tpi_
   // 22.2 at 16 (profiles/round5/handoff_kernels.md)
   static const int unroll = [] {
     const char* v = getenv("TPI_HANDOFF_UNROLL");
-    return v && atoi(v) == 16 ? 16 : (v && atoi(v) == 8 ? 8 : 4);
+    return v && atoi(v) == 16 ? 16 : v && atoi(v) == 8 ? 8 : v && atoi(v) == 2 ? 2 : 4;
   }();
 #define TPI_HASH_LAUNCH(UU)                                                                   \
   if (dst && bad)                                                                            \
@@ -1077,6 +1077,8 @@ extern "C" hipError_t tpi_launch_stream_copy_hash(const tpi_seg* src, const tpi_
     TPI_HASH_LAUNCH(16)
   } else if (unroll == 8) {
     TPI_HASH_LAUNCH(8)
+  } else if (unroll == 2) {
+    TPI_HASH_LAUNCH(2)
   } else {
     TPI_HASH_LAUNCH(4)
   }

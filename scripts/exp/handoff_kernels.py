@@ -25,7 +25,8 @@ def main():
     src = synthetic_checkpoint(int(gb * 1e9), 8192, dev)
     dst = synthetic_checkpoint(int(gb * 1e9), 8192, dev, fill=False)
     torch.cuda.synchronize()
-    ck = Checkpointer(dst, populate=False)  # the host region is not used here
+    tile = int(float(os.environ.get("HK_TILE_MB", "1")) * (1 << 20))
+    ck = Checkpointer(dst, populate=False, tile_bytes=tile)  # the host region is not used here
     src_segs = PackPlan.from_tensors(src, ck.plan.tile_bytes).segs.copy()
     stream = torch.cuda.current_stream().cuda_stream
     for i in range(4):

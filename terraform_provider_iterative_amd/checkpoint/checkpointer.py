@@ -334,6 +334,9 @@ def _warm_engine(engine: DeviceEngine, device_index: int, tile_bytes: int) -> No
         engine.restore(plan, region.addr, crcs, MODES["sdma"], sig)
         engine.save_z(plan, region.addr, crcs, csizes, sig)
         engine.restore_z(plan, region.addr, crcs, csizes, sig)
+        # and the HBM hand-off's copy + read-back kernels (a hot standby's first restore)
+        dst = {"a": torch.zeros(4096, device=dev), "t": torch.zeros(64, 48, device=dev).t()}
+        engine.copy_segments(plan.segs.copy(), PackPlan.from_tensors(dst, tile_bytes), sig)
         torch.cuda.synchronize(dev)
     finally:
         region.close()
