@@ -1056,12 +1056,13 @@ extern "C" hipError_t tpi_launch_stream_copy_hash(const tpi_seg* src, const tpi_
   if (stream_base % tile_bytes || stream_base + len > total) return hipErrorInvalidValue;
   const uint64_t tile0 = stream_base / tile_bytes;
   const dim3 grid((unsigned)((len + tile_bytes - 1) / tile_bytes)), block(WG);
-  // rows in flight per lane (16 B each; TPI_HANDOFF_UNROLL 4, 8 or 16).  4 is the fastest on
-  // MI355X: more waves resident beat more bytes per wave -- 32 GB copy 11.7 ms at 4, 12.5 at 8,
-  // 22.2 at 16 (profiles/round5/handoff_kernels.md)
+  // rows in flight per lane (16 B each; TPI_HANDOFF_UNROLL 2, 4, 8 or 16).  2 is the fastest
+  // on MI355X: more waves resident beat more bytes per wave -- 100 GB copy + read-back 49.7 ms
+  // at 2, 51.7 at 4; 32 GB copy 11.7 ms at 4, 12.5 at 8, 22.2 at 16
+  // (profiles/round5/handoff_kernels.md)
   static const int unroll = [] {
     const char* v = getenv("TPI_HANDOFF_UNROLL");
-    return v && atoi(v) == 16 ? 16 : v && atoi(v) == 8 ? 8 : v && atoi(v) == 2 ? 2 : 4;
+    return v && atoi(v) == 16 ? 16 : v && atoi(v) == 8 ? 8 : v && atoi(v) == 4 ? 4 : 2;
   }();
 #define TPI_HASH_LAUNCH(UU)                                                                   \
   if (dst && bad)                                                                            \
