@@ -453,6 +453,7 @@ def test_a_stuck_ipc_import_gives_up_the_hbm_route_and_the_claim(tmp_path, monke
     TPI_IPC_OPEN_TIMEOUT (the caller restores from the host copy) and drops its claim, so the
     predecessor is not kept waiting for a successor that will never close."""
     from terraform_provider_iterative_amd.checkpoint import checkpointer as ckmod
+    from terraform_provider_iterative_amd.checkpoint import handoff as hmod
 
     stuck = threading.Event()
 
@@ -476,7 +477,7 @@ def test_a_stuck_ipc_import_gives_up_the_hbm_route_and_the_claim(tmp_path, monke
             return {"allocations": [1 << 20] * 3, "ipc": {"0": "01", "1": "02", "2": "03"},
                     "where": [], "segs": ""}
 
-    monkeypatch.setattr(ckmod, "hip", lambda *a, **k: FakeLib())
+    monkeypatch.setattr(hmod, "hip", lambda *a, **k: FakeLib())
     monkeypatch.setenv("TPI_IPC_OPEN_TIMEOUT", "0.5")
     ck = Successor(str(tmp_path / "spill"))
     t0 = time.monotonic()
@@ -602,6 +603,7 @@ def test_dmabuf_route_hands_every_allocation_over_the_socket(tmp_path, monkeypat
     import torch
 
     from terraform_provider_iterative_amd.checkpoint import checkpointer as ckmod
+    from terraform_provider_iterative_amd.checkpoint import handoff as hmod
     from terraform_provider_iterative_amd.ops.packing import SEG_DTYPE
 
     n_alloc = ckmod.FDS_PER_MESSAGE + 37  # two batches of dma-bufs ...
@@ -655,7 +657,7 @@ def test_dmabuf_route_hands_every_allocation_over_the_socket(tmp_path, monkeypat
         def check(self, rc, what):
             assert rc == 0, what
 
-    monkeypatch.setattr(ckmod, "hip", lambda *a, **k: FakeLib())
+    monkeypatch.setattr(hmod, "hip", lambda *a, **k: FakeLib())
     monkeypatch.setattr(torch.cuda, "synchronize", lambda *a: None)
     monkeypatch.setattr(torch.cuda, "current_stream",
                         lambda *a: type("S", (), {"cuda_stream": 0})())
@@ -734,6 +736,7 @@ def test_auto_route_relocates_tensors_of_big_allocations(tmp_path, monkeypatch):
     import torch
 
     from terraform_provider_iterative_amd.checkpoint import checkpointer as ckmod
+    from terraform_provider_iterative_amd.checkpoint import handoff as hmod
     from terraform_provider_iterative_amd.ops.packing import SEG_CONTIG, SEG_DTYPE
 
     G = 1 << 30
@@ -783,7 +786,7 @@ def test_auto_route_relocates_tensors_of_big_allocations(tmp_path, monkeypatch):
         def check(self, rc, what):
             assert rc == 0, what
 
-    monkeypatch.setattr(ckmod, "hip", lambda *a, **k: FakeLib())
+    monkeypatch.setattr(hmod, "hip", lambda *a, **k: FakeLib())
     monkeypatch.setattr(torch.cuda, "synchronize", lambda *a: None)
     monkeypatch.setattr(torch.cuda, "mem_get_info", lambda *a: (200 * G, 288 * G))
     monkeypatch.setattr(torch.cuda, "current_stream",
@@ -869,8 +872,8 @@ def test_copy_ranges_are_checked_on_the_host_before_any_kernel():
     copy) -- the copy kernel never sees it."""
     import numpy as np
 
-    from terraform_provider_iterative_amd.checkpoint.checkpointer import (_check_copy_ranges,
-                                                                          _seg_extent)
+    from terraform_provider_iterative_amd.checkpoint.handoff import (_check_copy_ranges,
+                                                                     _seg_extent)
     from terraform_provider_iterative_amd.ops.packing import SEG_CONTIG, SEG_DTYPE
 
     class Lib:
