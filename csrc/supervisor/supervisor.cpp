@@ -72,261 +72,10 @@
 using tpi::json::quote;
 using tpi::json::Value;
 
+#include "common.h"
+#include "memory_guard.h"
+
 namespace {
-
-double now() {
-  struct timespec ts;
-  clock_gettime(CLOCK_REALTIME, &ts);
-  return ts.tv_sec + ts.tv_nsec * 1e-9;
-}
-
-std::string read_file(const std::string& path) {
-  std::ifstream in(path, std::ios::binary);
-  if (!in) throw std::runtime_error("cannot read " + path);
-  std::stringstream ss;
-  ss << in.rdbuf();
-  return ss.str();
-}
-
-void write_all(int fd, const std::string& s) {
-  const char* p = s.data();
-  size_t left = s.size();
-  while (left) {
-    ssize_t n = write(fd, p, left);
-    if (n < 0) {
-      if (errno == EINTR) continue;
-      return;
-    }
-    p += n;
-    left -= (size_t)n;
-  }
-}
-
-bool atomic_write(const std::string& path, const std::string& data) {
-  std::string tmp = path + ".tmp";
-  int fd = open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
-  if (fd < 0) return false;
-  write_all(fd, data);
-  close(fd);
-  return rename(tmp.c_str(), path.c_str()) == 0;
-}
-
-std::string uuid4() {
-  unsigned char b[16];
-  int fd = open("/dev/urandom", O_RDONLY | O_CLOEXEC);
-  if (fd < 0 || read(fd, b, 16) != 16) {
-    for (int i = 0; i < 16; ++i) b[i] = (unsigned char)(rand() & 0xff);
-  }
-  if (fd >= 0) close(fd);
-  b[6] = (b[6] & 0x0f) | 0x40;
-  b[8] = (b[8] & 0x3f) | 0x80;
-  char out[37];
-  snprintf(out, sizeof(out),
-           "%02x%02x%02x%02x-%02x%02x-%02x%02x-%02x%02x-%02x%02x%02x%02x%02x%02x", b[0], b[1],
-           b[2], b[3], b[4], b[5], b[6], b[7], b[8], b[9], b[10], b[11], b[12], b[13], b[14],
-           b[15]);
-  return out;
-}
-
-std::string utc_stamp(double t) {
-  time_t s = (time_t)t;
-  struct tm tm;
-  gmtime_r(&s, &tm);
-  char buf[32];
-  strftime(buf, sizeof(buf), "%Y-%m-%dT%H:%M:%SZ", &tm);
-  return buf;
-}
-
-const char* signame(int sig) {
-  switch (sig) {
-    case SIGTERM: return "TERM";
-    case SIGKILL: return "KILL";
-    case SIGINT: return "INT";
-    case SIGHUP: return "HUP";
-    case SIGSEGV: return "SEGV";
-    case SIGABRT: return "ABRT";
-    case SIGBUS: return "BUS";
-    case SIGFPE: return "FPE";
-    case SIGILL: return "ILL";
-    case SIGPIPE: return "PIPE";
-    case SIGQUIT: return "QUIT";
-    case SIGUSR1: return "USR1";
-    case SIGUSR2: return "USR2";
-    default: return "UNKNOWN";
-  }
-}
-
-enum class TermReason { NONE, STOP, PREEMPT, TIMEOUT, FAILFAST, REQUEUE, OOM, DISK };
-
-// --daemon: the launching parent blocks on this pipe until the ranks are spawned and the
-// first state.json is on disk, so "create returned" implies "supervisor visible".
-int g_ready_fd = -1;
-
-void signal_ready() {
-  if (g_ready_fd >= 0) {
-    write_all(g_ready_fd, "1");
-    close(g_ready_fd);
-    g_ready_fd = -1;
-  }
-}
-
-struct Rank {
-  int index = 0;
-  std::string gpus;
-  pid_t pid = -1;
-  int fd = -1;
-  int logfd = -1;
-  int nfd = -1;  // read end of the rank's notify pipe (TPI_NOTIFY_FD in the rank)
-  std::string uuid;
-  std::string partial;
-  std::string note;  // partial line read from the notify pipe
-  enum State { PENDING, RUNNING, DONE, PREEMPTED } state = PENDING;
-  int restarts = 0;
-  TermReason reason = TermReason::NONE;
-  double term_at = 0;
-  bool killed = false;
-  int exit_code = -1, exit_signal = 0;
-  double started = 0;
-  bool first_output = false;  // phase journal: first line of this incarnation seen
-  bool released = false;      // wrote "released" on its notify pipe
-  bool standby_capable = false;  // announced "standby" (calls preemption.standby())
-  int hot_spawns = 0;            // hot standbys started for this incarnation
-  int gofd = -1;                 // standby only: write end of its activation pipe
-  double hold_until = 0;  // a resuming incarnation: no new hot standby until it restored
-  // restored from its predecessor's HBM ("restored hbm"): the predecessor must stay alive
-  // until this incarnation has unmapped the IPC imports ("closed") or died
-  bool awaiting_close = false;
-  // detached (released / discarded): when it was told to go, and the exit trace so far
-  double exit_requested_at = 0;
-  std::string trace_last;
-  double trace_last_at = 0;
-  int trace_events = 0;
-};
-
-struct Spec {
-  std::string task_id, task_dir, workdir, script, shell = "/bin/bash";
-  std::vector<std::pair<std::string, std::string>> env;
-  double deadline = 0;
-  int parallelism = 1;
-  std::vector<std::string> rank_gpus;        // HIP_VISIBLE_DEVICES (the task's GPU set)
-  std::vector<std::string> rank_local_gpus;  // the rank's own GPUs, task-visible numbering
-  std::vector<std::vector<int>> rank_cpus;   // NUMA-local cores of the rank's GPUs (affinity)
-  std::string master_addr = "127.0.0.1";
-  int master_port = 29500;
-  bool gang = true, fail_fast = true, respawn_on_sigterm = true, login_shell = false;
-  bool standby = false;
-  bool standby_hot = false;  // keep the standby running before any preemption
-  int max_restarts = -1;
-  double grace = 30, respawn_delay = 0;
-  std::string reports_dir, state_path, events_path, control_path;
-  // written before a spot reclaim's SIGTERM: the ranks save without hand-off, free their HBM
-  // and leave at once (TPI_REQUEUE_FILE; nobody restores from this GPU)
-  std::string requeue_path;
-  bool exit_trace = true;  // journal state/wchan of released processes until they are reaped
-  std::vector<std::string> leases;
-  // workdir stager (spec "stager", runtime/stage.py): started before the ranks, holds the
-  // HBM copies of the workdir for the task's lifetime
-  std::vector<std::string> stager_argv;
-  std::string stager_manifest, stager_log, stager_gpus;
-  double stager_timeout = 600;
-  // false (default): ranks start while the stager loads (attach() waits for the manifest),
-  // so staging is off the first-log path; true: ranks start once the workdir is in HBM
-  bool stage_before_ranks = false;
-  // machine-type limits (resource_job.go:112-118 turns cpu/memory/disk into pod limits):
-  // host memory per rank (its process group; 0 = none) and the task's workdir size
-  uint64_t rank_memory_kb = 0;
-  uint64_t disk_limit_bytes = 0;
-  // hard cap: each rank's processes in a memory cgroup (v2 memory.max / v1
-  // memory.limit_in_bytes) of rank_memory + headroom -- "auto" (the hierarchy this process is
-  // in, when writable), "off", or a cgroup directory; the poll below keeps enforcing the limit
-  // itself (without checkpoint regions), the cgroup stops a runaway allocation between polls
-  std::string cgroup = "auto";
-  int cgroup_version = 0;
-  uint64_t cgroup_headroom_kb = 0;  // checkpoint regions (shm pages charge the first toucher)
-  std::string regions_path;         // checkpoint regions announced by the ranks (host.py)
-  double memory_interval = 1.0, disk_interval = 10.0;
-  double memory_fast_interval = 0.02;  // statm poll of the ranks' process trees (s)
-  // spot reclaim: after `requeue` the task goes back to the node queue through this command
-  std::vector<std::string> requeue_argv;
-  // off-node storage.container mirror (storage/remote.py): run every sync_interval s while
-  // ranks run (tpl:118-124) and once, awaited, when they are done (ExecStop's final copy)
-  std::vector<std::string> sync_argv;
-  double sync_interval = 10, sync_timeout = 600;
-  int restart_base = 0;  // restarts of earlier supervisors of this task (requeued incarnations)
-};
-
-Spec load_spec(const std::string& path) {
-  Value v = tpi::json::parse(read_file(path));
-  Spec s;
-  s.task_id = v["task_id"].str();
-  s.task_dir = v["task_dir"].str();
-  s.workdir = v["workdir"].str();
-  s.script = v["script"].str();
-  s.shell = v["shell"].str("/bin/bash");
-  for (auto& kv : v["env"].o) s.env.emplace_back(kv.first, kv.second.str());
-  s.deadline = v["deadline"].num(0);
-  s.parallelism = std::max(1, (int)v["parallelism"].num(1));
-  for (auto& r : v["ranks"].a) {
-    s.rank_gpus.push_back(r["gpus"].str());
-    s.rank_local_gpus.push_back(r["rank_gpus"].str());
-    std::vector<int> cpus;
-    for (auto& c : r["cpus"].a) cpus.push_back((int)c.num(-1));
-    s.rank_cpus.push_back(cpus);
-  }
-  s.rank_gpus.resize(s.parallelism);
-  s.rank_local_gpus.resize(s.parallelism);
-  s.rank_cpus.resize(s.parallelism);
-  s.master_addr = v["master_addr"].str("127.0.0.1");
-  s.master_port = (int)v["master_port"].num(29500);
-  s.gang = v["gang"].boolean(true);
-  s.fail_fast = v["fail_fast"].boolean(s.parallelism > 1);
-  s.respawn_on_sigterm = v["respawn_on_sigterm"].boolean(true);
-  s.login_shell = v["login_shell"].boolean(false);
-  s.max_restarts = (int)v["max_restarts"].num(-1);
-  s.grace = v["grace_seconds"].num(30);
-  s.respawn_delay = v["respawn_delay"].num(0);
-  s.standby = v["standby"].boolean(false);
-  s.standby_hot = s.standby && v["standby_hot"].boolean(false);
-  s.reports_dir = v["reports_dir"].str(s.task_dir + "/reports");
-  s.state_path = v["state_path"].str(s.task_dir + "/supervisor/state.json");
-  s.events_path = v["events_path"].str(s.task_dir + "/supervisor/events.jsonl");
-  s.control_path = v["control_path"].str(s.task_dir + "/supervisor/control.sock");
-  {
-    const size_t slash = s.state_path.rfind('/');
-    const std::string dir = slash == std::string::npos ? "." : s.state_path.substr(0, slash);
-    s.requeue_path = v["requeue_path"].str(dir + "/requeue");
-  }
-  s.exit_trace = v["exit_trace"].boolean(true);
-  for (auto& l : v["leases"].a) s.leases.push_back(l.str());
-  const Value& st = v["stager"];
-  for (auto& a : st["argv"].a) s.stager_argv.push_back(a.str());
-  s.stager_manifest = st["manifest"].str();
-  s.stager_log = st["log"].str(s.task_dir + "/supervisor/stager.log");
-  s.stager_gpus = st["gpus"].str();
-  s.stager_timeout = st["timeout"].num(600);
-  s.stage_before_ranks = st["before_ranks"].boolean(false);
-  const Value& lim = v["limits"];
-  s.rank_memory_kb = (uint64_t)lim["rank_memory_mb"].num(0) * 1024;
-  s.disk_limit_bytes = (uint64_t)(lim["disk_gb"].num(0) * 1e9);
-  s.memory_interval = lim["memory_interval"].num(1.0);
-  s.memory_fast_interval = lim["memory_fast_interval"].num(0.02);
-  s.cgroup = lim["cgroup"].str("auto");
-  s.cgroup_version = (int)lim["cgroup_version"].num(0);
-  s.cgroup_headroom_kb = (uint64_t)lim["cgroup_headroom_mb"].num(0) * 1024;
-  {
-    const size_t slash = s.state_path.rfind('/');
-    const std::string dir = slash == std::string::npos ? "." : s.state_path.substr(0, slash);
-    s.regions_path = v["regions_path"].str(dir + "/regions");
-  }
-  s.disk_interval = lim["disk_interval"].num(10.0);
-  for (auto& a : v["requeue_argv"].a) s.requeue_argv.push_back(a.str());
-  for (auto& a : v["sync"]["argv"].a) s.sync_argv.push_back(a.str());
-  s.sync_interval = v["sync"]["interval"].num(10);
-  s.sync_timeout = v["sync"]["timeout"].num(600);
-  s.restart_base = (int)v["restart_base"].num(0);
-  if (s.workdir.empty() || s.script.empty()) throw std::runtime_error("spec needs workdir+script");
-  return s;
-}
 
 class Supervisor {
  public:
@@ -353,7 +102,7 @@ class Supervisor {
     open_control();
     unlink(s_.requeue_path.c_str());  // a reclaimed incarnation's marker
     started_ = now();
-    setup_cgroups();
+    memory_.start();
     event("supervisor-start", {"pid " + std::to_string(getpid()),
                                "parallelism " + std::to_string(s_.parallelism)});
     if (s_.deadline > 0 && now() >= s_.deadline) {
@@ -414,7 +163,7 @@ class Supervisor {
           if (d.pid > 0 && (d.exit_requested_at > 0 || d.killed))
             timeout = std::min(timeout, kTraceInterval);
       if (respawn_at_ > 0) timeout = std::min(timeout, respawn_at_ - t);
-      if (s_.rank_memory_kb) timeout = std::min(timeout, next_memory_check_ - t);
+      if (s_.rank_memory_kb) timeout = std::min(timeout, memory_.next_check() - t);
       if (s_.disk_limit_bytes) timeout = std::min(timeout, next_disk_check_ - t);
       if (!s_.sync_argv.empty() && s_.sync_interval > 0 && sync_pid_ <= 0)
         timeout = std::min(timeout, next_sync_ - t);
@@ -481,288 +230,12 @@ class Supervisor {
   pid_t stager_pid_ = -1;
   bool staged_ = false;
   bool requeue_ = false;  // reclaimed (spot): ranks go down, the task goes back to the queue
-  double next_memory_check_ = 0, next_disk_check_ = 0;
+  double next_disk_check_ = 0;
+  MemoryGuard memory_{s_, [this](const std::string& c, const std::vector<std::string>& d) {
+    event(c, d);
+  }};
 
-  // ---- machine-type limits -------------------------------------------------------------------
-  // Host memory of the ranks' process groups, from one pass over /proc.  The resident set
-  // (/proc/<pid>/statm) is O(1) per process but counts pages shared inside a group (forked
-  // data-loader workers, a spill region mapped twice) once per member, so it is an upper bound.
-  // Only a group whose bound is over its limit pays for the proportional set size
-  // (smaps_rollup walks the page tables: tens of ms for a 100 GB pinned spill), which splits
-  // shared pages between their users and decides the OOM kill.
-  static bool read_small(const char* path, char* buf, size_t cap) {
-    int fd = open(path, O_RDONLY | O_CLOEXEC);
-    if (fd < 0) return false;
-    ssize_t n = read(fd, buf, cap - 1);
-    close(fd);
-    if (n <= 0) return false;
-    buf[n] = 0;
-    return true;
-  }
-
-  struct GroupMemory {
-    uint64_t rss_kb = 0;
-    std::vector<long> pids;
-  };
-
-  static std::map<long, GroupMemory> groups_memory(const std::set<long>& pgids) {
-    static const uint64_t page_kb = (uint64_t)sysconf(_SC_PAGESIZE) / 1024;
-    std::map<long, GroupMemory> out;
-    DIR* d = opendir("/proc");
-    if (!d) return out;
-    while (struct dirent* e = readdir(d)) {
-      char* end = nullptr;
-      long pid = strtol(e->d_name, &end, 10);
-      if (!end || *end || pid <= 0) continue;
-      char path[64], buf[512];
-      snprintf(path, sizeof(path), "/proc/%ld/stat", pid);
-      if (!read_small(path, buf, sizeof(buf))) continue;
-      const char* rp = strrchr(buf, ')');
-      long pgrp = 0, ppid = 0;
-      char state = 0;
-      if (!rp || sscanf(rp + 1, " %c %ld %ld", &state, &ppid, &pgrp) != 3 || !pgids.count(pgrp))
-        continue;
-      snprintf(path, sizeof(path), "/proc/%ld/statm", pid);
-      if (!read_small(path, buf, sizeof(buf))) continue;
-      unsigned long long size = 0, resident = 0;
-      if (sscanf(buf, "%llu %llu", &size, &resident) != 2) continue;
-      GroupMemory& g = out[pgrp];
-      g.rss_kb += resident * page_kb;
-      g.pids.push_back(pid);
-    }
-    closedir(d);
-    return out;
-  }
-
-  static uint64_t pss_kb(const std::vector<long>& pids) {
-    uint64_t total = 0;
-    for (long pid : pids) {
-      std::ifstream in("/proc/" + std::to_string(pid) + "/smaps_rollup");
-      std::string key;
-      uint64_t value;
-      while (in >> key) {
-        if (key == "Pss:" && in >> value) {
-          total += value;
-          break;
-        }
-        in.ignore(1 << 20, '\n');
-      }
-    }
-    return total;
-  }
-
-  // Checkpoint spill regions announced by the ranks (checkpoint/host.py: one line
-  // "<pid> <start> <end> <path|->" per mapping).  They mirror device state -- a rank's
-  // checkpoint of 100+ GB of HBM -- and are not its working set, so the limit leaves them out
-  // (a file-backed region matches by path in every process that maps it, an anonymous one by
-  // the announcing pid and address range).
-  struct Region {
-    long pid = 0;
-    uint64_t start = 0, end = 0;
-    std::string path;
-  };
-
-  std::vector<Region> load_regions() const {
-    std::vector<Region> out;
-    std::ifstream in(s_.regions_path);
-    std::string line;
-    while (std::getline(in, line)) {
-      Region r;
-      char path[4096] = "";
-      unsigned long long a = 0, b = 0;
-      if (sscanf(line.c_str(), "%ld %llx %llx %4095[^\n]", &r.pid, &a, &b, path) < 3) continue;
-      r.start = a;
-      r.end = b;
-      if (strcmp(path, "-") != 0) r.path = path;
-      out.push_back(r);
-    }
-    return out;
-  }
-
-  // Proportional set size of a group, and the part of it in checkpoint regions (kB).
-  static std::pair<uint64_t, uint64_t> pss_split_kb(const std::vector<long>& pids,
-                                                    const std::vector<Region>& regions) {
-    if (regions.empty()) return {pss_kb(pids), 0};
-    uint64_t total = 0, excluded = 0;
-    for (long pid : pids) {
-      std::ifstream in("/proc/" + std::to_string(pid) + "/smaps");
-      std::string line;
-      bool skip = false;
-      while (std::getline(in, line)) {
-        if (line.empty()) continue;
-        const char c = line[0];
-        if ((c >= '0' && c <= '9') || (c >= 'a' && c <= 'f')) {  // "start-end perms ... path"
-          unsigned long long a = 0, b = 0;
-          int consumed = 0;
-          skip = false;
-          if (sscanf(line.c_str(), "%llx-%llx %*s %*s %*s %*s%n", &a, &b, &consumed) < 2) continue;
-          std::string path = consumed > 0 && (size_t)consumed < line.size()
-                                 ? line.substr((size_t)consumed) : std::string();
-          path.erase(0, path.find_first_not_of(' '));
-          const std::string deleted = " (deleted)";
-          if (path.size() > deleted.size() &&
-              path.compare(path.size() - deleted.size(), deleted.size(), deleted) == 0)
-            path.resize(path.size() - deleted.size());
-          for (const Region& r : regions)
-            if ((!r.path.empty() && r.path == path) ||
-                (r.path.empty() && r.pid == pid && a < r.end && r.start < b)) {
-              skip = true;
-              break;
-            }
-        } else if (line.compare(0, 4, "Pss:") == 0) {
-          const uint64_t v = strtoull(line.c_str() + 4, nullptr, 10);
-          total += v;
-          if (skip) excluded += v;
-        }
-      }
-    }
-    return {total, excluded};
-  }
-
-  std::map<int, uint64_t> region_kb_;  // rank index -> its regions' share at the last check
-
-  // ---- memory cgroups (the hard cap) ----------------------------------------------------------
-  // k8s turns the machine type into a pod memory limit (resource_job.go:112-118): the kernel
-  // stops a container at it, however fast it allocates.  The /proc poll above sees a rank only
-  // every memory_interval; a rank that allocates faster than that could take the node down
-  // first.  So each rank also gets a memory cgroup -- v2 memory.max or v1
-  // memory.limit_in_bytes -- when the hierarchy is writable (root, or a delegated subtree),
-  // capped at limit + headroom: shm pages of a checkpoint region are charged to the cgroup of
-  // the process that first touched them, so a GPU rank gets room for its GPUs' HBM.
-  std::vector<std::string> cg_dirs_;  // per rank index; empty: no cgroup
-  std::vector<uint64_t> cg_oom_;      // kernel OOM kills seen per rank
-  int cg_version_ = 0;
-  std::string cg_root_;
-
-  static bool write_text(const std::string& path, const std::string& text, bool append = false) {
-    int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_CLOEXEC | (append ? O_APPEND : O_TRUNC),
-                  0644);
-    if (fd < 0) return false;
-    const ssize_t n = write(fd, text.data(), text.size());
-    const int saved = errno;
-    close(fd);
-    errno = saved;
-    return n == (ssize_t)text.size();
-  }
-
-  // Our own cgroup path ("" controller: the v2 entry "0::/path").
-  static std::string own_cgroup(const std::string& controller) {
-    std::ifstream in("/proc/self/cgroup");
-    std::string line;
-    while (std::getline(in, line)) {
-      const size_t a = line.find(':'), b = line.find(':', a + 1);
-      if (a == std::string::npos || b == std::string::npos) continue;
-      const std::string ctl = line.substr(a + 1, b - a - 1), path = line.substr(b + 1);
-      if (controller.empty() ? (line.compare(0, a, "0") == 0 && ctl.empty())
-                             : ("," + ctl + ",").find("," + controller + ",") != std::string::npos)
-        return path == "/" ? "" : path;
-    }
-    return "";
-  }
-
-  // cgroups of supervisors that died without cleaning up (tpi-<task>-<pid>-r<i>)
-  static void sweep_stale_cgroups(const std::string& root) {
-    DIR* d = opendir(root.c_str());
-    if (!d) return;
-    while (struct dirent* e = readdir(d)) {
-      const std::string name = e->d_name;
-      if (name.compare(0, 4, "tpi-") != 0) continue;
-      const size_t r = name.rfind("-r"), dash = r == std::string::npos ? r : name.rfind('-', r - 1);
-      if (dash == std::string::npos) continue;
-      const long pid = strtol(name.c_str() + dash + 1, nullptr, 10);
-      if (pid > 0 && kill((pid_t)pid, 0) != 0 && errno == ESRCH)
-        rmdir((root + "/" + name).c_str());
-    }
-    closedir(d);
-  }
-
-  void setup_cgroups() {
-    cg_dirs_.assign(s_.parallelism, "");
-    cg_oom_.assign(s_.parallelism, 0);
-    if (!s_.rank_memory_kb) return;
-    if (s_.cgroup.empty() || s_.cgroup == "off") {
-      memory_guard_ = "poll " + std::to_string((int)(s_.memory_fast_interval * 1000)) + " ms";
-      event("memory-guard", {memory_guard_, "cgroup off",
-                             "limit " + std::to_string(s_.rank_memory_kb / 1024) + " MB"});
-      return;
-    }
-    std::string root, why;
-    int ver = s_.cgroup_version;
-    struct stat st;
-    if (s_.cgroup == "auto") {
-      if (stat("/sys/fs/cgroup/cgroup.controllers", &st) == 0) {
-        ver = 2;
-        root = "/sys/fs/cgroup" + own_cgroup("");
-        // children need the memory controller in our subtree (granted only where the
-        // hierarchy is delegated to us)
-        write_text(root + "/cgroup.subtree_control", "+memory");
-      } else if (stat("/sys/fs/cgroup/memory/memory.limit_in_bytes", &st) == 0) {
-        ver = 1;
-        const std::string own = "/sys/fs/cgroup/memory" + own_cgroup("memory");
-        root = stat(own.c_str(), &st) == 0 ? own : "/sys/fs/cgroup/memory";
-      } else {
-        why = "no cgroup memory controller";
-      }
-    } else {
-      root = s_.cgroup;
-      if (!ver) ver = stat((root + "/cgroup.controllers").c_str(), &st) == 0 ? 2 : 1;
-    }
-    const uint64_t bytes = (s_.rank_memory_kb + s_.cgroup_headroom_kb) * 1024;
-    if (why.empty()) {
-      sweep_stale_cgroups(root);
-      for (int i = 0; i < s_.parallelism; ++i) {
-        const std::string dir = root + "/tpi-" + s_.task_id + "-" + std::to_string(getpid()) +
-                                "-r" + std::to_string(i);
-        if (mkdir(dir.c_str(), 0755) && errno != EEXIST) {
-          why = "mkdir " + dir + ": " + strerror(errno);
-          break;
-        }
-        cg_dirs_[i] = dir;
-        const std::string limit = dir + (ver == 2 ? "/memory.max" : "/memory.limit_in_bytes");
-        if (!write_text(limit, std::to_string(bytes))) {
-          why = "write " + limit + ": " + strerror(errno);
-          break;
-        }
-        if (ver == 2) write_text(dir + "/memory.swap.max", "0");
-      }
-    }
-    if (!why.empty()) {
-      for (auto& d : cg_dirs_)
-        if (!d.empty()) {
-          rmdir(d.c_str());
-          d.clear();
-        }
-      memory_guard_ = "poll " + std::to_string((int)(s_.memory_fast_interval * 1000)) + " ms";
-      event("memory-cgroup-unavailable", {why, "the /proc poll enforces the limit"});
-      event("memory-guard", {memory_guard_, "statm of each rank's process tree",
-                             "limit " + std::to_string(s_.rank_memory_kb / 1024) + " MB"});
-      return;
-    }
-    cg_version_ = ver;
-    cg_root_ = root;
-    memory_guard_ = "cgroup v" + std::to_string(ver);
-    event("memory-cgroup", {"v" + std::to_string(ver), root,
-                            "cap " + std::to_string(bytes >> 20) + " MB per rank",
-                            "limit " + std::to_string(s_.rank_memory_kb / 1024) + " MB (poll)"});
-  }
-
-  uint64_t cgroup_oom_kills(int index) {
-    if (index < 0 || index >= (int)cg_dirs_.size() || cg_dirs_[index].empty()) return 0;
-    std::ifstream in(cg_dirs_[index] + (cg_version_ == 2 ? "/memory.events" : "/memory.oom_control"));
-    std::string key;
-    uint64_t value = 0;
-    while (in >> key) {
-      if (key == "oom_kill" && in >> value) return value;
-      in.ignore(1 << 16, '\n');
-    }
-    return 0;
-  }
-
-  void remove_cgroups() {
-    for (auto& d : cg_dirs_)
-      if (!d.empty()) rmdir(d.c_str());
-  }
-
+  // ---- machine-type limits: the workdir's disk use (memory: memory_guard.h) ----------------
   static thread_local uint64_t du_total_;
   static int du_visit(const char*, const struct stat* st, int type, struct FTW*) {
     if (type == FTW_F) du_total_ += (uint64_t)st->st_blocks * 512;
@@ -774,121 +247,16 @@ class Supervisor {
     return du_total_;
   }
 
-  // ---- the fast guard (no cgroup) -----------------------------------------------------------
-  // Where the kernel cap is refused (an unprivileged box), the limit is only as good as the
-  // poll.  Every memory_fast_interval (20 ms) each rank's process tree -- the rank and its
-  // descendants, from /proc/<pid>/task/<tid>/children, plus the process-group members of the
-  // last full /proc scan (orphans reparented away from the tree) -- is summed from statm
-  // (microseconds per process).  The expensive proportional split runs only when that bound,
-  // advanced from the last split by the growth of the resident set since, passes the limit.
-  struct MemTrack {
-    long pid = 0;
-    uint64_t rss_at = 0, counted_at = 0;  // resident set and counted PSS at the last split
-    bool valid = false;
-    std::vector<long> members;  // process-group members seen by the last full scan
-  };
-  std::vector<MemTrack> mem_;
-  double next_memory_scan_ = 0;
-  std::string memory_guard_;
-
-  static void tree_pids(long root, std::vector<long>& out, int depth = 0) {
-    out.push_back(root);
-    if (depth > 16) return;
-    char path[64];
-    snprintf(path, sizeof(path), "/proc/%ld/task", root);
-    DIR* d = opendir(path);
-    if (!d) return;
-    std::vector<long> kids;
-    while (struct dirent* e = readdir(d)) {
-      if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
-      char cpath[96], buf[4096];
-      snprintf(cpath, sizeof(cpath), "/proc/%ld/task/%s/children", root, e->d_name);
-      if (!read_small(cpath, buf, sizeof(buf))) continue;
-      char* p = buf;
-      while (*p) {
-        char* end = nullptr;
-        long c = strtol(p, &end, 10);
-        if (end == p) break;
-        if (c > 0) kids.push_back(c);
-        p = end;
-      }
-    }
-    closedir(d);
-    for (long c : kids) tree_pids(c, out, depth + 1);
-  }
-
-  static uint64_t resident_kb(const std::vector<long>& pids) {
-    static const uint64_t page_kb = (uint64_t)sysconf(_SC_PAGESIZE) / 1024;
-    uint64_t kb = 0;
-    char path[64], buf[256];
-    for (long pid : pids) {
-      snprintf(path, sizeof(path), "/proc/%ld/statm", pid);
-      if (!read_small(path, buf, sizeof(buf))) continue;
-      unsigned long long size = 0, resident = 0;
-      if (sscanf(buf, "%llu %llu", &size, &resident) == 2) kb += resident * page_kb;
-    }
-    return kb;
-  }
-
   void check_limits(double t) {
-    if (s_.rank_memory_kb && t >= next_memory_check_) {
-      const bool fast = cg_version_ == 0 && s_.memory_fast_interval > 0;
-      next_memory_check_ = t + (fast ? std::min(s_.memory_fast_interval, s_.memory_interval)
-                                     : s_.memory_interval);
-      if ((int)mem_.size() != s_.parallelism) mem_.assign(s_.parallelism, MemTrack());
-      const bool full = t >= next_memory_scan_;
-      std::map<long, GroupMemory> groups;
-      if (full) {
-        next_memory_scan_ = t + s_.memory_interval;
-        std::set<long> pgids;
-        for (auto& r : ranks_)
-          if (r.state == Rank::RUNNING && r.pid > 0 && !r.killed) pgids.insert(r.pid);
-        if (!pgids.empty()) groups = groups_memory(pgids);
-      }
-      std::vector<Region> regions;
-      bool regions_loaded = false;
-      for (auto& r : ranks_) {
-        if (r.state != Rank::RUNNING || r.pid <= 0 || r.killed) continue;
-        MemTrack& m = mem_[r.index];
-        if (m.pid != r.pid) m = MemTrack(), m.pid = r.pid;
-        if (full) {
-          auto g = groups.find(r.pid);
-          m.members = g == groups.end() ? std::vector<long>() : g->second.pids;
-        }
-        std::vector<long> pids;
-        tree_pids(r.pid, pids);
-        for (long p : m.members)
-          if (std::find(pids.begin(), pids.end(), p) == pids.end()) pids.push_back(p);
-        const uint64_t rss = resident_kb(pids);
-        // quick bound: the counted size at the last split plus any growth since (new
-        // resident pages are at most new private pages); before any split, the resident set
-        // minus the regions' share measured last time
-        const uint64_t bound = m.valid ? m.counted_at + (rss > m.rss_at ? rss - m.rss_at : 0)
-                                       : (rss > region_kb_[r.index] ? rss - region_kb_[r.index] : 0);
-        if (bound <= s_.rank_memory_kb) continue;
-        if (!regions_loaded) regions = load_regions(), regions_loaded = true;
-        const auto split = pss_split_kb(pids, regions);
-        region_kb_[r.index] = split.second;
-        const uint64_t kb = split.first - std::min(split.first, split.second);
-        m.rss_at = rss;
-        m.counted_at = kb;
-        m.valid = true;
-        if (kb <= s_.rank_memory_kb) continue;
-        // like a container OOM kill: no grace, the rank fails (no respawn)
-        r.reason = TermReason::OOM;
-        if (r.term_at == 0) r.term_at = t;
-        kill(-r.pid, SIGKILL);
-        kill(r.pid, SIGKILL);
-        r.killed = true;
-        std::vector<std::string> desc = {"rank " + std::to_string(r.index),
-                                         "memory " + std::to_string(kb / 1024) + " MB",
-                                         "limit " + std::to_string(s_.rank_memory_kb / 1024) +
-                                             " MB"};
-        if (split.second)
-          desc.push_back("checkpoint regions " + std::to_string(split.second / 1024) +
-                         " MB not counted");
-        event("rank-oom-killed", desc);
-      }
+    for (auto& k : memory_.check(t, ranks_)) {
+      // like a container OOM kill: no grace, the rank fails (no respawn)
+      Rank& r = ranks_[k.index];
+      r.reason = TermReason::OOM;
+      if (r.term_at == 0) r.term_at = t;
+      kill(-r.pid, SIGKILL);
+      kill(r.pid, SIGKILL);
+      r.killed = true;
+      event("rank-oom-killed", k.desc);
     }
     if (s_.disk_limit_bytes && t >= next_disk_check_ && !stop_) {
       next_disk_check_ = t + s_.disk_interval;
@@ -1182,7 +550,7 @@ class Supervisor {
                       ", \"running\": " + std::to_string(running()) +
                       ", \"restarts\": " + std::to_string(total_restarts_) +
                       ", \"stager_pid\": " + std::to_string(stager_pid_) +
-                      ", \"memory_guard\": " + quote(memory_guard_) + ", \"ranks\": [";
+                      ", \"memory_guard\": " + quote(memory_.guard()) + ", \"ranks\": [";
     for (size_t i = 0; i < ranks_.size(); ++i) {
       auto& r = ranks_[i];
       out += std::string(i ? ", " : "") + "{\"rank\": " + std::to_string(r.index) +
@@ -1294,8 +662,7 @@ class Supervisor {
       }
     }
     std::string exec_cmd = "exec \"$0\"";
-    const std::string cg_procs = r.index < (int)cg_dirs_.size() && !cg_dirs_[r.index].empty()
-                                     ? cg_dirs_[r.index] + "/cgroup.procs" : std::string();
+    const std::string cg_procs = memory_.cgroup_procs(r.index);
     pid_t parent = getpid();
     pid_t pid = fork();
     if (pid == 0) {
@@ -2034,9 +1401,7 @@ class Supervisor {
     int sig = signaled ? WTERMSIG(st) : 0;
     int code = WIFEXITED(st) ? WEXITSTATUS(st) : -1;
     if (signaled && sig == SIGKILL && !r.killed && r.reason == TermReason::NONE) {
-      const uint64_t kills = cgroup_oom_kills(r.index);
-      if (kills > cg_oom_[r.index]) {  // the kernel stopped it at the cgroup cap
-        cg_oom_[r.index] = kills;
+      if (memory_.oom_by_cgroup(r.index)) {  // the kernel stopped it at the cgroup cap
         r.reason = TermReason::OOM;
         event("rank-oom-killed", {"rank " + std::to_string(r.index), "memory cgroup cap",
                                   "limit " + std::to_string(s_.rank_memory_kb / 1024) + " MB"});
@@ -2189,7 +1554,7 @@ class Supervisor {
   int finish() {
     release_resources();
     settle();
-    remove_cgroups();
+    memory_.cleanup();
     event("supervisor-exit", {requeued_ ? "requeued" : stop_ ? "stopped" : "all ranks finished"});
     signal_ready();
     return 0;
