@@ -23,6 +23,7 @@ class TransferResult:
     dirty_tiles: int = -1  # incremental sync: tiles that changed since the previous sync
     wire_bytes: int = -1   # bytes that crossed the link / landed in the region (codec)
     released_bytes: int = 0  # device memory freed behind the spill (save(release_behind=True))
+    device_seconds: float = -1.0  # device time of the kernels alone (HBM hand-off copy)
 
     def __post_init__(self):
         if self.wire_bytes < 0:

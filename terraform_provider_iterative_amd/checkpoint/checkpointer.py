@@ -154,7 +154,8 @@ class DeviceEngine:
                                         ctypes.byref(bad), ctypes.byref(st))
         self.lib.check(rc, "tpi_copy_segments")
         return TransferResult(plan.total, time.perf_counter() - t0, int(st.chunks),
-                              int(bad.value), wire_bytes=0)
+                              int(bad.value), wire_bytes=0,
+                              device_seconds=st.pack_ms / 1e3 if st.pack_ms >= 0 else -1.0)
 
     def reserve(self, nsegs: int, ntiles: int, codec: bool) -> None:
         """Allocate now the device buffers the first save/restore of that size would."""

@@ -958,6 +958,7 @@ def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None,
             res = checkpointer.restore_hbm()
             journal("checkpoint-restored", "HBM hand-off", *_describe(res),
                     "ipc open %.3f s" % getattr(checkpointer, "hbm_open_s", 0.0),
+                    "kernels %.4f s" % res.device_seconds,
                     "%.1f GB free at the copy" % (
                         getattr(checkpointer, "hbm_free_before_copy", 0) / 1e9))
             notify_restored(hbm=True)
