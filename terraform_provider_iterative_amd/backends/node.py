@@ -776,9 +776,10 @@ class NodeTask(Task):
         if not directory:
             return
         if self.remote_conn is not None:  # into the container; the node restores from it
-            stats = remote_storage.SSHRemote(self.remote_conn).put_tree(
+            stats = remote_storage.open_remote(self.remote_conn).put_tree(
                 directory, "data", storage.transfer_rules(self.spec.environment.exclude_list))
-            log.info("Uploaded %d files to %s", stats["files"], self.remote_conn)
+            log.info("Uploaded %d files to %s", stats["files"],
+                     remote_storage.describe(self.remote_conn))
             return
         if os.environ.get("TPI_PUSH_LINK", "") in ("1", "true", "yes"):
             # hard links instead of copies (no snapshot: see storage.link_tree)
@@ -787,9 +788,9 @@ class NodeTask(Task):
         storage.transfer(directory, self.data_dir, self.spec.environment.exclude_list)
 
     def _restore_remote(self) -> None:
-        stats = remote_storage.SSHRemote(self.remote_conn).get_tree("data", self.data_dir,
+        stats = remote_storage.open_remote(self.remote_conn).get_tree("data", self.data_dir,
                                                                     ["+ **"])
-        self._event("container-restored", str(self.remote_conn),
+        self._event("container-restored", remote_storage.describe(self.remote_conn),
                     "%d files" % stats["files"], "%d bytes" % stats["bytes"])
 
     def pull(self) -> None:
@@ -799,7 +800,7 @@ class NodeTask(Task):
         excludes = self.spec.environment.exclude_list or saved.get("exclude") or []
         rules = storage.limit_transfer(out, storage.transfer_rules(excludes))
         if self.remote_conn is not None:  # the container holds the task's final data
-            remote_storage.SSHRemote(self.remote_conn).get_tree("data", directory, rules)
+            remote_storage.open_remote(self.remote_conn).get_tree("data", directory, rules)
             return
         storage.transfer(self.data_dir, directory, rules=rules)
 

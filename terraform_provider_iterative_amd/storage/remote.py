@@ -39,6 +39,7 @@ import tempfile
 import threading
 from typing import Dict, Iterable, List, Optional, Tuple
 
+from . import objectstore
 from .transfer import Connection, make_filter, transfer_rules
 from ..ops import native
 
@@ -55,7 +56,12 @@ def parse(container: str, path: str = "", opts: Optional[Dict[str, str]] = None
           ) -> Optional[Connection]:
     """The SSH :class:`Connection` named by a ``storage.container`` value (None: not an
     off-node container).  ``opts`` (``container_opts``) may give ``host``/``port``/``user``
-    and a ``root`` that a relative directory is taken under."""
+    and a ``root`` that a relative directory is taken under.  Object-store containers
+    (``s3://``, ``gs://``, ``az://`` and rclone's forms) parse to their own connections
+    (:mod:`storage.objectstore`)."""
+    obj = objectstore.parse(container, path, opts)
+    if obj is not None:
+        return obj
     opts = dict(opts or {})
     conn = None
     m = _URL.match(container) if container.startswith("ssh://") else _SCP.match(container)
@@ -98,6 +104,8 @@ def is_remote(value: str) -> bool:
     """Does ``value`` (a container or a file path) name a location on another node?"""
     if not value:
         return False
+    if objectstore.is_object_store(value):
+        return True
     if value.startswith("ssh://"):
         return bool(_URL.match(value))
     return bool(_SCP.match(value)) or value.startswith(tuple(":%s," % b for b in BACKENDS))
@@ -260,14 +268,27 @@ class SSHRemote:
         return os.path.getsize(local)
 
 
+def open_remote(conn: Connection):
+    """The file operations of an off-node container: :class:`SSHRemote`, or an object store's
+    (:func:`storage.objectstore.open_remote`) -- the same interface."""
+    if conn.backend in BACKENDS:
+        return SSHRemote(conn)
+    return objectstore.open_remote(conn)
+
+
+def describe(conn: Connection) -> str:
+    """A container for logs and events (an object store's credentials left out)."""
+    return str(conn) if conn.backend in BACKENDS else objectstore.describe(conn)
+
+
 def split_file(location: str) -> Tuple[SSHRemote, str]:
     """(remote, file path) of a remote file location (any of the container forms)."""
     conn = parse(location)
     if conn is None:
         raise ValueError("%r is not a remote location" % location)
     directory, name = posixpath.split(conn.path)
-    conn.path = directory or "/"
-    return SSHRemote(conn), name
+    conn.path = directory or ("/" if conn.backend in BACKENDS else "")
+    return open_remote(conn), name
 
 
 def fetch(location: str, directory: Optional[str] = None) -> str:
@@ -318,7 +339,7 @@ def sync_task(task_root: str) -> int:
     conn = parse(rs.get("container", ""), rs.get("path", ""), rs.get("config") or {})
     if conn is None:
         return 0
-    remote = SSHRemote(conn)
+    remote = open_remote(conn)
     manifest_path = os.path.join(task_root, "supervisor", MANIFEST)
     try:
         with open(manifest_path) as f:
@@ -339,7 +360,7 @@ def sync_task(task_root: str) -> int:
             if gone and sub == "data":
                 remote.remove([posixpath.join(sub, p) for p in gone])
             state[sub] = now
-    except (OSError, subprocess.SubprocessError) as error:
+    except (OSError, subprocess.SubprocessError, ValueError) as error:
         print("tpi-remote-sync: %s" % error, file=__import__("sys").stderr, flush=True)
         return 1
     tmp = manifest_path + ".tmp"

@@ -217,10 +217,28 @@ class Connection:
     def parse(cls, remote: str) -> "Connection":
         if not remote.startswith(":"):
             return cls(backend="local", container=remote)
-        head, sep, rest = remote[1:].partition(":")
-        if not sep:
+        # split ``backend,k='v',...`` from the path at the first ':' outside quotes, and the
+        # options at ',' outside quotes (a quoted value may hold either, e.g. an endpoint URL)
+        parts, cur, quote, rest = [], "", "", None
+        for i, ch in enumerate(remote[1:], 1):
+            if quote:
+                if ch == quote:
+                    quote = ""
+                cur += ch
+            elif ch in "'\"":
+                quote = ch
+                cur += ch
+            elif ch == ",":
+                parts.append(cur)
+                cur = ""
+            elif ch == ":":
+                rest = remote[i + 1:]
+                break
+            else:
+                cur += ch
+        if rest is None:
             raise ValueError("malformed connection string %r" % remote)
-        parts = head.split(",")
+        parts.append(cur)
         config = {}
         for item in parts[1:]:
             key, _, value = item.partition("=")
