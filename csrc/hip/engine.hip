@@ -1800,7 +1800,10 @@ int tpi_copy_segments(tpi_engine* e, const tpi_seg* src, const tpi_seg* dst, int
   uint64_t span_bytes = total;
   if (const char* v = getenv("TPI_HANDOFF_SPAN_MB"))
     span_bytes = strtoull(v, nullptr, 10) ? strtoull(v, nullptr, 10) << 20 : total;
-  const uint64_t span = std::max<uint64_t>(e->chunk, std::max<uint64_t>(span_bytes / tile, 1) * tile);
+  // whole tiles, rounded up: the default covers the state's last partial tile in the same
+  // launch (rounded down, a second pair of 1-tile launches followed every copy)
+  const uint64_t span =
+      std::max<uint64_t>(e->chunk, std::max<uint64_t>((span_bytes + tile - 1) / tile, 1) * tile);
   for (uint64_t base = 0, k = 0; good && fused && base < total; base += span, ++k) {
     const uint64_t len = std::min(span, total - base);
     if (xxh)

@@ -47,6 +47,19 @@ def main():
     torch.cuda.synchronize()
     ck = Checkpointer(dst, populate=False)
     src_segs = PackPlan.from_tensors(src, ck.plan.tile_bytes).segs.copy()
+    if os.environ.get("FT_RESERVE"):  # what a hot standby does before the signal
+        ck.engine.reserve(len(src_segs), ck.plan.ntiles, False)
+    if os.environ.get("FT_SMALL_FIRST"):  # one small copy first: is the cost per launch size?
+        n = max(1, int(float(os.environ["FT_SMALL_FIRST"]) * (1 << 20)) // 4)  # MiB -> floats
+        small = {"a": torch.ones(n, device=dev)}
+        small_dst = {"a": torch.zeros(n, device=dev)}
+        cks = Checkpointer(small_dst, populate=False)
+        r = cks.engine.copy_segments(PackPlan.from_tensors(small, cks.plan.tile_bytes).segs.copy(),
+                                     cks.plan, stream)
+        print(json.dumps({"case": "small %s MiB first" % os.environ["FT_SMALL_FIRST"],
+                          "kernels_s": round(r.device_seconds, 4)}),
+              flush=True)
+        cks.close()
     for i in range(3):
         copy(ck, "A%d src->dst" % i)
     ck2 = Checkpointer(synthetic_checkpoint(int(gb * 1e9), 8192, dev, fill=False), populate=False)

@@ -144,14 +144,31 @@ def hipcc() -> str:
 
 
 def build_hip(force: bool = False, verbose: bool = False) -> str:
+    """``libtpi_hip.so``: every source compiled to its own object in parallel (each carries
+    its own gfx950 code object; the kernels are reached through host launch functions, so no
+    relocatable device code is needed), then one link."""
     srcs = _sources("hip/*.hip", "hip/*.cpp")
-    deps = srcs + _sources("hip/*.h", "common/*.h")
+    headers = _sources("hip/*.h", "common/*.h")
     tl = torch_lib_dir()
-    cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics", _define_version(),
-           *srcs, "-L" + tl, "-Wl,-rpath," + tl, "-L" + ROCM_LIB, "-Wl,-rpath," + ROCM_LIB,
-           "-lrccl", "-lrocprofiler-sdk-roctx", "-ldl", "-o", "@OUT@"]
-    return _build(HIP_SO, cmd, deps, force, verbose)
+    flags = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall",
+             "-Wno-unused-function", "-munsafe-fp-atomics", _define_version()]
+    objdir = os.path.join(LIB, "obj")
+    os.makedirs(objdir, exist_ok=True)
+
+    def compile_one(src: str) -> str:
+        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        return _build(obj, [hipcc(), *flags, "-c", src, "-o", "@OUT@"], [src] + headers,
+                      force, verbose)
+
+    from concurrent.futures import ThreadPoolExecutor
+
+    jobs = max(1, min(len(srcs), int(os.environ.get("MAX_JOBS", "0") or os.cpu_count() or 4)))
+    with ThreadPoolExecutor(jobs) as pool:
+        objs = list(pool.map(compile_one, srcs))
+    cmd = [hipcc(), "--offload-arch=" + ARCH, "-shared", "-fPIC", *objs, "-L" + tl,
+           "-Wl,-rpath," + tl, "-L" + ROCM_LIB, "-Wl,-rpath," + ROCM_LIB, "-lrccl",
+           "-lrocprofiler-sdk-roctx", "-ldl", "-o", "@OUT@"]
+    return _build(HIP_SO, cmd, objs, force, verbose)
 
 
 def build_supervisor(force: bool = False, verbose: bool = False) -> str:
