@@ -226,6 +226,12 @@ struct tpi_engine {
   std::vector<hipEvent_t> ev_a, ev_b;  // save: packed/copied; restore: copied/unpacked
   hipEvent_t ev_wait = nullptr, ev_done = nullptr;
   hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;  // timing: the hand-off kernels' device time
+  // The HBM hand-off's copy runs on a stream of the device's highest priority
+  // (TPI_HANDOFF_PRIORITY=high, default; "normal": on `compute`): during a hot hand-off the
+  // predecessor's save (its pack / codec kernels) shares the GPU, and its workgroups then
+  // queue behind the copy's instead of interleaving with them.
+  hipStream_t urgent = nullptr;
+  hipEvent_t ev_prio = nullptr;
   tpi_crc_tables* tables = nullptr;
   tpi_seg* d_segs = nullptr;
   size_t seg_cap = 0;
@@ -568,6 +574,18 @@ tpi_engine* tpi_engine_create(int device, uint64_t chunk_bytes, int nbuf, uint64
     return bail("hipEventCreate", err);
   if ((err = hipEventCreate(&e->ev_t0)) != hipSuccess || (err = hipEventCreate(&e->ev_t1)) != hipSuccess)
     return bail("hipEventCreate", err);
+  {
+    const char* prio = getenv("TPI_HANDOFF_PRIORITY");
+    if (!prio || strcmp(prio, "normal") != 0) {
+      int least = 0, greatest = 0;  // no priority stream: the copy stays on `compute`
+      if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+          hipStreamCreateWithPriority(&e->urgent, hipStreamNonBlocking, greatest) != hipSuccess ||
+          hipEventCreateWithFlags(&e->ev_prio, hipEventDisableTiming) != hipSuccess) {
+        if (e->urgent) (void)hipStreamDestroy(e->urgent);
+        e->urgent = nullptr;
+      }
+    }
+  }
   if ((err = hipMalloc(&e->d_bad, 2 * sizeof(unsigned long long))) != hipSuccess)
     return bail("hipMalloc(bad)", err);
   if (device_tables(device, &e->tables)) {
@@ -614,6 +632,8 @@ void tpi_engine_destroy(tpi_engine* e) {
   for (void* p : {e->zraw, e->d_meta, (void*)e->d_csize, (void*)e->d_coff})
     if (p) (void)hipFree(p);
   if (e->h_coff) (void)hipHostFree(e->h_coff);
+  if (e->urgent) (void)hipStreamDestroy(e->urgent);
+  if (e->ev_prio) (void)hipEventDestroy(e->ev_prio);
   if (e->compute) (void)hipStreamDestroy(e->compute);
   if (e->copy) (void)hipStreamDestroy(e->copy);
   if (e->aux) (void)hipStreamDestroy(e->aux);
@@ -1733,6 +1753,12 @@ int tpi_copy_segments(tpi_engine* e, const tpi_seg* src, const tpi_seg* dst, int
   auto t0 = std::chrono::steady_clock::now();
   if (check_segments(src, n, total)) return -1;
   if (prepare(e, dst, n, total)) return -1;  // dst -> d_segs
+  hipStream_t cs = e->compute;  // the stream of this copy (TPI_HANDOFF_PRIORITY)
+  if (e->urgent) {  // after the descriptor upload prepare() queued on `compute`
+    HIP_OK(hipEventRecord(e->ev_prio, e->compute));
+    HIP_OK(hipStreamWaitEvent(e->urgent, e->ev_prio, 0));
+    cs = e->urgent;
+  }
   e->hash_valid = false;
   if ((size_t)n > e->src_cap) {  // grown, never shrunk: no allocation per hand-off
     if (e->d_src) HIP_OK(hipFree(e->d_src));
@@ -1753,16 +1779,16 @@ int tpi_copy_segments(tpi_engine* e, const tpi_seg* src, const tpi_seg* dst, int
   const uint32_t init_last = init_for(total % tile ? total % tile : tile);
   unsigned long long bad_init[2] = {0ull, ~0ull}, bad[2] = {0ull, 0ull};
   bool good = ok(hipMemcpyAsync(d_src, src, (size_t)n * sizeof(tpi_seg), hipMemcpyHostToDevice,
-                                e->compute), "upload source segments") &&
+                                cs), "upload source segments") &&
               ok(hipMemcpyAsync(e->d_bad, bad_init, sizeof(bad_init), hipMemcpyHostToDevice,
-                                e->compute), "upload bad counter");
+                                cs), "upload bad counter");
   if (good && signal_stream != TPI_NO_STREAM) {  // dst tensors: after the caller's work on them
     good = ok(hipEventRecord(e->ev_wait, (hipStream_t)signal_stream), "hipEventRecord") &&
-           ok(hipStreamWaitEvent(e->compute, e->ev_wait, 0), "hipStreamWaitEvent");
+           ok(hipStreamWaitEvent(cs, e->ev_wait, 0), "hipStreamWaitEvent");
   }
   // device time of the kernels alone (stats->pack_ms): what the hand-off spends beside them
   // (descriptor uploads, host checks, synchronisation) is copy_ms - pack_ms
-  if (good) good = ok(hipEventRecord(e->ev_t0, e->compute), "hipEventRecord");
+  if (good) good = ok(hipEventRecord(e->ev_t0, cs), "hipEventRecord");
   bool fused = true;
   for (int i = 0; i < n && fused; ++i)
     fused = src[i].off == dst[i].off && src[i].nbytes == dst[i].nbytes;
@@ -1809,41 +1835,41 @@ int tpi_copy_segments(tpi_engine* e, const tpi_seg* src, const tpi_seg* dst, int
     if (xxh)
       good = ok(tpi_launch_stream_copy_hash(d_src, e->d_segs, n, base, len, total, tile,
                                             TPI_SYNC_SEED, e->d_digest,
-                                            inline_check ? e->d_bad : nullptr, e->compute),
+                                            inline_check ? e->d_bad : nullptr, cs),
                 "copy") &&
              (!readback ||
               ok(tpi_launch_stream_copy_hash(e->d_segs, nullptr, n, base, len, total, tile,
-                                             TPI_SYNC_SEED, e->d_digest, e->d_bad, e->compute),
+                                             TPI_SYNC_SEED, e->d_digest, e->d_bad, cs),
                  "verify"));
     else
       good = ok(tpi_launch_stream_copy(d_src, e->d_segs, n, base, len, tile, e->tables,
-                                       e->d_crcs, init_full, init_last, nullptr, e->compute),
+                                       e->d_crcs, init_full, init_last, nullptr, cs),
                 "copy") &&
              ok(tpi_launch_stream_copy(e->d_segs, nullptr, n, base, len, tile, e->tables,
-                                       e->d_crcs, init_full, init_last, e->d_bad, e->compute),
+                                       e->d_crcs, init_full, init_last, e->d_bad, cs),
                 "verify");
     nchunks = k + 1;
   }
   for (uint64_t base = 0, k = 0; good && !fused && base < total; base += e->chunk, ++k) {
     const uint64_t len = std::min(e->chunk, total - base);
     void* buf = e->staging[k % e->nbuf];
-    good = ok(tpi_launch_transposes(src, n, base, len, buf, 0, e->compute), "transpose in") &&
+    good = ok(tpi_launch_transposes(src, n, base, len, buf, 0, cs), "transpose in") &&
            ok(tpi_launch_stream_crc(0, d_src, n, base, len, buf, tile, e->tables, e->d_crcs,
-                                    init_full, init_last, nullptr, 1, e->compute), "pack") &&
+                                    init_full, init_last, nullptr, 1, cs), "pack") &&
            ok(tpi_launch_stream_crc(1, e->d_segs, n, base, len, buf, tile, e->tables,
-                                    e->d_crcs, init_full, init_last, e->d_bad, 1, e->compute),
+                                    e->d_crcs, init_full, init_last, e->d_bad, 1, cs),
               "unpack") &&
-           ok(tpi_launch_transposes(dst, n, base, len, buf, 1, e->compute), "transpose out");
+           ok(tpi_launch_transposes(dst, n, base, len, buf, 1, cs), "transpose out");
     nchunks = k + 1;
   }
-  if (good) good = ok(hipEventRecord(e->ev_t1, e->compute), "hipEventRecord");
+  if (good) good = ok(hipEventRecord(e->ev_t1, cs), "hipEventRecord");
   if (good)
-    good = ok(hipMemcpyAsync(bad, e->d_bad, sizeof(bad), hipMemcpyDeviceToHost, e->compute),
+    good = ok(hipMemcpyAsync(bad, e->d_bad, sizeof(bad), hipMemcpyDeviceToHost, cs),
               "bad counter") &&
-           ok(hipEventRecord(e->ev_done, e->compute), "hipEventRecord");
+           ok(hipEventRecord(e->ev_done, cs), "hipEventRecord");
   if (good && signal_stream != TPI_NO_STREAM)
     good = ok(hipStreamWaitEvent((hipStream_t)signal_stream, e->ev_done, 0), "hipStreamWaitEvent");
-  if (!ok(hipStreamSynchronize(e->compute), "hipStreamSynchronize")) good = false;
+  if (!ok(hipStreamSynchronize(cs), "hipStreamSynchronize")) good = false;
   release();
   if (!good) return -1;
   *bad_tiles = bad[0];
