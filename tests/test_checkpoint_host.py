@@ -265,7 +265,7 @@ def test_failed_streamed_save_fails_the_successor(tmp_path, monkeypatch):
 def test_engine_pool_hands_out_the_matching_engine_and_releases_the_rest(monkeypatch):
     # prewarm_engine's pool, with stand-in engines (no GPU): the first Checkpointer on a device
     # takes the engine with its parameters; the device's other prewarmed engines are closed
-    from terraform_provider_iterative_amd.checkpoint import checkpointer as ckmod
+    from terraform_provider_iterative_amd.checkpoint import engine as ckmod
 
     class FakeEngine:
         def __init__(self):

@@ -780,15 +780,15 @@ def test_prewarmed_engine_is_taken_by_the_next_checkpointer():
     """A warm standby pre-creates the device engine (preemption.standby -> prewarm_engine);
     the Checkpointer built after activation takes it instead of creating one."""
     from terraform_provider_iterative_amd.checkpoint import Checkpointer, prewarm_engine
-    from terraform_provider_iterative_amd.checkpoint import checkpointer as ckmod
+    from terraform_provider_iterative_amd.checkpoint import engine as engmod
 
     assert prewarm_engine(torch.cuda.current_device(), chunk_bytes=4 << 20, nbuf=2,
                           tile_bytes=1 << 20)
     key = (torch.cuda.current_device(), 4 << 20, 2, 1 << 20)
-    pooled = ckmod._engine_pool[key][-1]
+    pooled = engmod._engine_pool[key][-1]
     t = {"a": torch.randn(3 << 20, device="cuda")}
     ck = Checkpointer(t, chunk_bytes=4 << 20, nbuf=2)
-    assert ck.engine is pooled and not ckmod._engine_pool.get(key)
+    assert ck.engine is pooled and not engmod._engine_pool.get(key)
     want = t["a"].clone()
     ck.save()
     t["a"].zero_()
