@@ -73,6 +73,7 @@ using tpi::json::quote;
 using tpi::json::Value;
 
 #include "common.h"
+#include "container_sync.h"
 #include "memory_guard.h"
 
 namespace {
@@ -138,7 +139,7 @@ class Supervisor {
       check_grace(t);
       check_respawn(t);
       check_limits(t);
-      check_sync(t);
+      sync_.check(t);
       trace_exits(t);
       // Every rank is down (exited, or released after its save): the GPUs, cores and memory
       // go back to the node now, not when the last released process has been reaped -- its
@@ -165,8 +166,7 @@ class Supervisor {
       if (respawn_at_ > 0) timeout = std::min(timeout, respawn_at_ - t);
       if (s_.rank_memory_kb) timeout = std::min(timeout, memory_.next_check() - t);
       if (s_.disk_limit_bytes) timeout = std::min(timeout, next_disk_check_ - t);
-      if (!s_.sync_argv.empty() && s_.sync_interval > 0 && sync_pid_ <= 0)
-        timeout = std::min(timeout, next_sync_ - t);
+      timeout = sync_.timeout(t, timeout);
       if (stager_fd_ >= 0) timeout = std::min(timeout, stager_deadline_ - t);
       timeout = std::max(timeout, 0.0);
       std::vector<struct pollfd> pfds;
@@ -281,81 +281,9 @@ class Supervisor {
   bool disk_exceeded_ = false;
 
   // ---- off-node container mirror ------------------------------------------------------------
-  pid_t sync_pid_ = -1;
-  double next_sync_ = 0;
-  int sync_failures_ = 0;
-
-  pid_t spawn_sync() {
-    std::vector<char*> argv;
-    for (auto& a : s_.sync_argv) argv.push_back(const_cast<char*>(a.c_str()));
-    argv.push_back(nullptr);
-    int logfd = open((s_.events_path + ".sync.log").c_str(),
-                     O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
-    pid_t parent = getpid();
-    pid_t pid = fork();
-    if (pid == 0) {
-      setpgid(0, 0);
-      prctl(PR_SET_PDEATHSIG, SIGTERM);
-      if (getppid() != parent) _exit(127);
-      sigset_t none;
-      sigemptyset(&none);
-      sigprocmask(SIG_SETMASK, &none, nullptr);
-      int devnull = open("/dev/null", O_RDWR);
-      if (devnull >= 0) {
-        dup2(devnull, 0);
-        dup2(devnull, 1);
-      }
-      if (logfd >= 0) dup2(logfd, 2);
-      execv(argv[0], argv.data());
-      _exit(127);
-    }
-    if (logfd >= 0) close(logfd);
-    return pid;
-  }
-
-  void check_sync(double t) {
-    if (s_.sync_argv.empty() || s_.sync_interval <= 0 || sync_pid_ > 0 || t < next_sync_) return;
-    if (next_sync_ == 0) {  // the first mirror one interval after the start
-      next_sync_ = t + s_.sync_interval;
-      return;
-    }
-    next_sync_ = t + s_.sync_interval;
-    sync_pid_ = spawn_sync();
-  }
-
-  void sync_exited(int st) {
-    sync_pid_ = -1;
-    const bool ok = WIFEXITED(st) && WEXITSTATUS(st) == 0;
-    if (!ok && ++sync_failures_ <= 5)  // journal the first failures, not every retry
-      event("remote-sync-failed", {WIFSIGNALED(st) ? std::string("signal ") + signame(WTERMSIG(st))
-                                                   : "code " + std::to_string(WEXITSTATUS(st)),
-                                   "see " + s_.events_path + ".sync.log"});
-  }
-
-  // The final mirror, awaited: the task is over only once its data is in the container.
-  void final_sync() {
-    if (s_.sync_argv.empty()) return;
-    const double t0 = now();
-    int st = 0;
-    if (sync_pid_ > 0 && waitpid(sync_pid_, &st, 0) == sync_pid_) sync_exited(st);
-    pid_t pid = spawn_sync();
-    if (pid <= 0) {
-      event("remote-sync-failed", {"fork failed"});
-      return;
-    }
-    pid_t got = 0;
-    while ((got = waitpid(pid, &st, WNOHANG)) == 0 && now() - t0 < s_.sync_timeout) usleep(5000);
-    if (got == 0) {
-      kill(-pid, SIGKILL);
-      kill(pid, SIGKILL);
-      waitpid(pid, &st, 0);
-    }
-    char took[48];
-    snprintf(took, sizeof(took), "%.3f s", now() - t0);
-    const bool ok = got == pid && WIFEXITED(st) && WEXITSTATUS(st) == 0;
-    event(ok ? "remote-synced" : "remote-sync-failed",
-          {ok ? "final" : (got == 0 ? "final: timed out" : "final"), took});
-  }
+  ContainerSync sync_{s_, [this](const std::string& c, const std::vector<std::string>& d) {
+    event(c, d);
+  }};
 
   // ---- workdir stager ----------------------------------------------------------------------
   int stager_fd_ = -1;            // the stager's stdout ("staged ..." line), while staging
@@ -1344,8 +1272,8 @@ class Supervisor {
         stager_exited(st);
         continue;
       }
-      if (pid == sync_pid_) {
-        sync_exited(st);
+      if (pid == sync_.pid()) {
+        sync_.exited(st);
         continue;
       }
       for (size_t i = 0; i < detached_.size(); ++i)
@@ -1507,7 +1435,7 @@ class Supervisor {
   void settle() {
     if (settled_) return;
     drain_rank_logs();
-    final_sync();  // the logs and statuses of every rank are written by now
+    sync_.final();  // the logs and statuses of every rank are written by now
     bool pending = false;  // a reclaimed rank that has not finished on its own
     if (requeue_ && !stop_ && !timed_out_)
       for (auto& r : ranks_)
