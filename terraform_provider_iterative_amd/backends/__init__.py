@@ -6,7 +6,7 @@ from ..utils.record import replace
 from typing import List
 
 from ..models.cloud import (ALL_PROVIDERS, NODE_PROVIDERS, REMOTE_PROVIDERS, Cloud)
-from ..models.values import Task as TaskSpec
+from ..models.values import RemoteStorage, Task as TaskSpec
 from ..utils.identifier import Identifier
 from .base import Resource, Task
 from .node import NodeTask, list_tasks as _node_list
@@ -33,8 +33,27 @@ def _retarget(cloud: Cloud) -> Cloud:
     return cloud
 
 
+# A remote cloud's ``storage.container`` names one of its buckets (``ExistingS3Bucket``,
+# ``ExistingBucket``, ``ExistingBlobContainer``: task/{aws,gcp,az}/task.go); run on a node
+# runtime, the same bucket is reached over its object-store protocol (storage/objectstore.py).
+_BUCKET_SCHEMES = {"aws": "s3", "gcp": "gs", "az": "az"}
+
+
+def _bucket_container(provider: str, task: TaskSpec) -> TaskSpec:
+    rs = task.remote_storage
+    scheme = _BUCKET_SCHEMES.get(provider)
+    if rs is None or not scheme or not rs.container or "://" in rs.container \
+            or rs.container.startswith((":", "/", ".", "~")):
+        return task
+    return replace(task, remote_storage=RemoteStorage("%s://%s" % (scheme, rs.container),
+                                                      rs.path, dict(rs.config)))
+
+
 def new(cloud: Cloud, identifier: Identifier, task: TaskSpec) -> Task:
-    cloud = _retarget(cloud)
+    retargeted = _retarget(cloud)
+    if retargeted is not cloud:
+        task = _bucket_container(cloud.provider, task)
+    cloud = retargeted
     if cloud.provider in NODE_PROVIDERS:
         if is_remote(cloud):  # region = "host=...": the node runtime of another host
             return RemoteNodeTask(cloud, identifier, task)

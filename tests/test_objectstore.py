@@ -285,3 +285,32 @@ def test_task_data_lives_in_a_bucket(tmp_path, fake, backend, monkeypatch):
     assert (work / "output" / "result.txt").read_text() == "saw hello\n"
     assert "proj/data/output/result.txt" in objs  # the bucket is left in place
     assert fake.store.auth_failures == 0
+
+
+def test_a_remote_clouds_bucket_is_reached_over_its_protocol_on_a_node(tmp_path, monkeypatch):
+    """A configuration written for aws / gcp / az run on a node runtime (``TPI_REMOTE_AS``):
+    its ``storage.container`` names the cloud's bucket (the reference's ``ExistingS3Bucket``
+    etc.), so the node reaches that bucket -- not a local directory of the same name."""
+    from terraform_provider_iterative_amd import backends
+    from terraform_provider_iterative_amd.models.cloud import (Cloud, Credentials,
+                                                               NodeCredentials)
+    from terraform_provider_iterative_amd.models.values import Environment, RemoteStorage, Task
+    from terraform_provider_iterative_amd.utils.identifier import new_deterministic_identifier
+
+    monkeypatch.setenv("TPI_REMOTE_AS", "mi355x")
+    monkeypatch.delenv("TPI_REMOTE_HOST", raising=False)
+    creds = Credentials(node=NodeCredentials(state_root=str(tmp_path / "st")))
+    for provider, backend in (("aws", "s3"), ("gcp", "googlecloudstorage"), ("az", "azureblob")):
+        spec = Task(environment=Environment(script="#!/bin/sh\ntrue\n"),
+                    remote_storage=RemoteStorage("bkt", "sub/dir", {"region": "eu-west-1"}))
+        task = backends.new(Cloud(provider=provider, credentials=creds),
+                            new_deterministic_identifier("rb-" + provider), spec)
+        conn = task.remote_conn
+        assert (conn.backend, conn.container, conn.path) == (backend, "bkt", "sub/dir"), provider
+        assert conn.config["region"] == "eu-west-1"
+    # an explicit URL or a node path is left alone
+    spec = Task(environment=Environment(script="#!/bin/sh\ntrue\n"),
+                remote_storage=RemoteStorage(str(tmp_path / "dir"), "", {}))
+    task = backends.new(Cloud(provider="aws", credentials=creds),
+                        new_deterministic_identifier("rb-dir"), spec)
+    assert task.remote_conn is None
