@@ -401,6 +401,7 @@ class HbmHandoff:
         (its allocations mapped here over dma-buf, or HIP IPC for an ``ipc`` export; one
         fused copy pass + a read-back verify, every tile's digest checked) into the bound
         tensors."""
+        t_entry = time.perf_counter()
         if not self.claim_hbm():
             raise CheckpointError("the HBM hand-off is claimed by another process (withdrawn "
                                   "by its exporter, or taken by another successor)")
@@ -418,6 +419,8 @@ class HbmHandoff:
         mapped: List[Optional[int]] = [None] * n  # what to unmap / close
         via_dmabuf = [False] * n
         t0 = time.perf_counter()
+        phases = {"claim": t0 - t_entry}  # seconds per step, for the journal
+        self.hbm_phases = phases
         try:
             limit = float(os.environ.get("TPI_IPC_OPEN_TIMEOUT", "10"))
         except ValueError:
@@ -543,6 +546,15 @@ class HbmHandoff:
             for w in workers:
                 w.start()
             deadline = time.monotonic() + limit
+            try:  # meanwhile: this process's destinations (the plan's segments), checked once
+                key = self.plan.segs.tobytes()
+                if getattr(self, "_dst_checked", None) != key:
+                    _check_destinations(self.plan.segs, lib)
+                    self._dst_checked = key
+            except BaseException as error:
+                with lock:
+                    todo.clear()
+                    errors.append(error)
             for w in workers:
                 w.join(max(0.0, deadline - time.monotonic()))
             if errors:
@@ -559,7 +571,8 @@ class HbmHandoff:
 
         try:
             open_all()
-            self.hbm_open_s = time.perf_counter() - t0
+            self.hbm_open_s = phases["open"] = time.perf_counter() - t0
+            t1 = time.perf_counter()
             src = np.frombuffer(bytes.fromhex(doc["segs"]), dtype=self.plan.segs.dtype).copy()
             if len(src) != len(self.plan.segs):
                 raise CheckpointError("HBM hand-off describes a different tensor set")
@@ -573,13 +586,20 @@ class HbmHandoff:
                                                    owner)
             # never launch a copy that could touch memory outside what is mapped: every source
             # segment inside its mapped allocation, every destination inside its own
-            _check_copy_ranges(src, owner, bases, sizes, dst, lib)
+            # (relocated pieces split contiguous destination segments of the plan, whose
+            # bounds open_all checked: they need no second look)
+            _check_copy_ranges(src, owner, bases, sizes, None, lib)
+            t2 = time.perf_counter()
+            phases["plan"] = t2 - t1
             try:  # diagnostic for the journal
                 self.hbm_free_before_copy = torch.cuda.mem_get_info(self.device_index)[0]
             except Exception:
                 self.hbm_free_before_copy = 0
             sig = torch.cuda.current_stream(self.device_index).cuda_stream
+            t3 = time.perf_counter()
+            phases["meminfo"] = t3 - t2
             res = self.engine.copy_segments(src, self.plan, sig, dst)  # synchronous: copy done
+            phases["copy"] = time.perf_counter() - t3
         except BaseException:
             close_all()
             raise
@@ -637,31 +657,56 @@ def _seg_extent(seg) -> Tuple[int, int]:
 
 
 def _check_copy_ranges(src: np.ndarray, owner: np.ndarray, bases: List[Optional[int]],
-                       sizes: List[int], dst: np.ndarray, lib) -> None:
+                       sizes: List[int], dst: Optional[np.ndarray], lib) -> None:
     """Host-side bounds check before the hand-off's copy kernel: each source segment must lie
     inside the predecessor allocation it was mapped from (``owner``), each destination segment
-    inside the device allocation holding it in this process.  A descriptor that fails raises
-    CheckpointError (the caller restores from the host copy) instead of faulting the GPU."""
-    base, size = ctypes.c_uint64(0), ctypes.c_uint64(0)
-    for i in range(len(src)):
-        if int(src[i]["nbytes"]) == 0:
-            continue
+    inside the device allocation holding it in this process (``dst`` None: checked already,
+    :func:`_check_destinations`).  A descriptor that fails raises CheckpointError (the caller
+    restores from the host copy) instead of faulting the GPU."""
+    live = src["nbytes"] != 0
+    contig = live & (src["kind"] == SEG_CONTIG)
+    if np.any(owner[live] < 0):
+        i = int(np.flatnonzero(live & (owner < 0))[0])
+        raise CheckpointError("HBM hand-off: source segment %d has no mapped allocation" % i)
+    if any(bases[int(a)] is None for a in np.unique(owner[live])):
+        raise CheckpointError("HBM hand-off: a source segment's allocation is not mapped")
+    # contiguous segments (nearly all): one vector comparison against their allocations
+    base_of = np.array([0 if b is None else b for b in bases] + [0], dtype=np.uint64)
+    size_of = np.array(list(sizes) + [0], dtype=np.uint64)
+    own = np.where(owner < 0, len(bases), owner)
+    lo = src["ptr"].astype(np.uint64)
+    hi = lo + src["nbytes"].astype(np.uint64)
+    bad = contig & ((lo < base_of[own]) | (hi > base_of[own] + size_of[own]))
+    for i in list(np.flatnonzero(bad)) + list(np.flatnonzero(live & ~contig)):
         a = int(owner[i])
-        lo, hi = _seg_extent(src[i])
-        if a < 0 or bases[a] is None or lo < bases[a] or hi > bases[a] + sizes[a]:
+        lo_i, hi_i = _seg_extent(src[i])
+        if lo_i < bases[a] or hi_i > bases[a] + sizes[a]:
             raise CheckpointError(
                 "HBM hand-off: source segment %d [%#x, %#x) lies outside its mapped allocation "
-                "%d [%s, +%d)" % (i, lo, hi, a, None if a < 0 else bases[a],
-                                  -1 if a < 0 else sizes[a]))
+                "%d [%#x, +%d)" % (i, lo_i, hi_i, a, bases[a], sizes[a]))
+    if dst is not None:
+        _check_destinations(dst, lib)
+
+
+def _check_destinations(dst: np.ndarray, lib) -> None:
+    """Every destination segment inside the device allocation that holds it (one driver
+    query per allocation: segments are sorted, consecutive ones often share one)."""
+    base, size = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    known: Tuple[int, int] = (1, 0)  # [lo, hi) of the last allocation looked up
+    for i in range(len(dst)):
+        if int(dst[i]["nbytes"]) == 0:
+            continue
         lo, hi = _seg_extent(dst[i])
-        if lib.tpi_mem_range(ctypes.c_void_p(int(dst[i]["ptr"])), ctypes.byref(base),
-                             ctypes.byref(size)) != 0:
-            raise CheckpointError("HBM hand-off: destination segment %d is not device memory"
-                                  % i)
-        if lo < int(base.value) or hi > int(base.value) + int(size.value):
+        if not (known[0] <= lo and hi <= known[1]):
+            if lib.tpi_mem_range(ctypes.c_void_p(int(dst[i]["ptr"])), ctypes.byref(base),
+                                 ctypes.byref(size)) != 0:
+                raise CheckpointError("HBM hand-off: destination segment %d is not device "
+                                      "memory" % i)
+            known = (int(base.value), int(base.value) + int(size.value))
+        if lo < known[0] or hi > known[1]:
             raise CheckpointError(
                 "HBM hand-off: destination segment %d [%#x, %#x) lies outside its allocation "
-                "[%#x, +%d)" % (i, lo, hi, int(base.value), int(size.value)))
+                "[%#x, +%d)" % (i, lo, hi, known[0], known[1] - known[0]))
 
 
 def _split_relocated(src: np.ndarray, dst: np.ndarray, pieces: Dict[str, List[List[int]]],

@@ -959,6 +959,8 @@ def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None,
             journal("checkpoint-restored", "HBM hand-off", *_describe(res),
                     "ipc open %.3f s" % getattr(checkpointer, "hbm_open_s", 0.0),
                     "kernels %.4f s" % res.device_seconds,
+                    "steps " + " ".join("%s %.4f" % kv for kv in
+                                        getattr(checkpointer, "hbm_phases", {}).items()),
                     "%.1f GB free at the copy" % (
                         getattr(checkpointer, "hbm_free_before_copy", 0) / 1e9))
             notify_restored(hbm=True)

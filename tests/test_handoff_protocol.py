@@ -469,8 +469,15 @@ def test_a_stuck_ipc_import_gives_up_the_hbm_route_and_the_claim(tmp_path, monke
         def check(self, rc, what):
             assert rc == 0, what
 
+    import types
+
+    import numpy as np
+
+    from terraform_provider_iterative_amd.ops.packing import SEG_DTYPE
+
     class Successor(_FakeHandoff):
         device_index = 0
+        plan = types.SimpleNamespace(segs=np.zeros(0, dtype=SEG_DTYPE))
         restore_hbm = Checkpointer.restore_hbm
 
         def _hbm_doc(self):
@@ -893,6 +900,19 @@ def test_copy_ranges_are_checked_on_the_host_before_any_kernel():
     dst["nbytes"][1] = 0x801
     with pytest.raises(CheckpointError, match="destination segment 1"):
         _check_copy_ranges(src, owner, [0x1000], [0x1000], dst, Lib())
+    # consecutive destinations in one allocation: one driver query for all of them
+    from terraform_provider_iterative_amd.checkpoint.handoff import _check_destinations
+
+    calls = []
+
+    class CountingLib(Lib):
+        def tpi_mem_range(self, ptr, base, size):
+            calls.append(ptr.value)
+            return Lib.tpi_mem_range(self, ptr, base, size)
+
+    dst["nbytes"][1] = 0x800
+    _check_destinations(dst, CountingLib())
+    assert calls == [0x9000]
     # a strided view's extent runs from its lowest to its highest element
     v = np.zeros(1, dtype=SEG_DTYPE)[0]
     v["ptr"], v["nbytes"], v["kind"], v["elem"], v["ndim"] = 0x100, 64, 1, 4, 2
