@@ -146,7 +146,8 @@ def first_log_latency(timeout: float = 60.0, parallelism: int = 1):
 
 E2E_KEYS = ("ok", "verified", "status", "signal_to_restored_s", "save_s",
             "rank_start_to_restored_s", "saved_to_restored_s", "signal_to_durable_s", "streamed",
-            "warm_standby_activated", "hot_standby", "standby_pinned_wait_s", "restore_journal",
+            "warm_standby_activated", "hot_standby", "preload", "preloaded_wait_s",
+            "standby_pinned_wait_s", "restore_journal",
             "extra_tensors_gib", "delete_s", "rank_exit_to_settled_s", "vram_before_start",
             "memory_guard",
             "released_exit_pending_at_settle")
@@ -156,16 +157,18 @@ def preempt_e2e(total_gb: float, codec: str, timeout: float) -> dict:
     """Config 4's real path, untimed: an ``iterative_task`` on ``cloud = "mi355x"`` holding
     ``total_gb`` of state in HBM is preempted (``leo preempt``: SIGTERM to the rank), the
     supervisor respawns it and the successor restores and verifies the state
-    (``bench/bench_preempt.py``, one child process per run).  ``cold``: the successor is a
-    fresh process that restores behind the streamed spill; ``hot``: a hot standby started with
-    the rank copies the state device to device.  Signal -> restored is read from the task's
-    phase journal."""
+    (``bench/bench_preempt.py``, one child process per run).  ``cold``: no standby -- the
+    successor the default configuration gives (a preloaded interpreter, runtime/preload.py,
+    that imported PyTorch before the preemption); ``fresh``: ``TPI_PRELOAD=0``, a new process;
+    ``hot``: a hot standby started with the rank copies the state device to device.  Signal ->
+    restored is read from the task's phase journal."""
     import subprocess
 
     runs = {}
     # the hot run's state also holds a 4.2 GiB and a 2.5 GiB tensor (a large vocabulary's fp32
     # embedding and moments): allocations HIP IPC cannot hand off, the dma-buf route can
-    for name, flags in (("cold", []), ("hot", ["--hot", "--extra-gib", "4.2,2.5"])):
+    for name, flags in (("cold", []), ("hot", ["--hot", "--extra-gib", "4.2,2.5"]),
+                        ("fresh", ["--no-preload"])):
         cmd = [sys.executable, os.path.join(ROOT, "bench", "bench_preempt.py"), "--gb",
                repr(total_gb), "--codec", codec, "--timeout", repr(timeout)] + flags
         t0 = time.perf_counter()
@@ -186,6 +189,7 @@ def preempt_e2e(total_gb: float, codec: str, timeout: float) -> dict:
             file=sys.stderr, flush=True)
     return {"cold_signal_to_restored_s": runs.get("cold", {}).get("signal_to_restored_s"),
             "hot_signal_to_restored_s": runs.get("hot", {}).get("signal_to_restored_s"),
+            "fresh_signal_to_restored_s": runs.get("fresh", {}).get("signal_to_restored_s"),
             "verified": all(r.get("ok") is True for r in runs.values()),
             "gb": total_gb, "runs": runs}
 

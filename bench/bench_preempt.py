@@ -147,6 +147,11 @@ def main():
     p.add_argument("--hot", action="store_true",
                    help="hot standby (TPI_WARM_STANDBY=hot): the successor is started with the "
                         "rank, so it is ready to restore behind the streamed spill")
+    p.add_argument("--preload", action="store_true",
+                   help="TPI_PRELOAD=1 (the default): the successor is a preloaded interpreter "
+                        "(PyTorch imported before the preemption, runtime/preload.py)")
+    p.add_argument("--no-preload", action="store_true",
+                   help="TPI_PRELOAD=0: the successor is a fresh process")
     p.add_argument("--no-stream", action="store_true",
                    help="TPI_STREAM_HANDOFF=0: release the successor only after the spill")
     p.add_argument("--no-prefetch", action="store_true",
@@ -192,6 +197,10 @@ def main():
                      "extra": [float(x) for x in args.extra_gib.split(",") if x.strip()]}
     # the ranks' runtime knobs travel as task variables (the rank environment is the task's)
     rank_env = {"TPI_TASK": "true", "TPI_STREAM_HANDOFF": "0" if args.no_stream else "1"}
+    if args.preload or args.no_preload:
+        rank_env["TPI_PRELOAD"] = "0" if args.no_preload else "1"
+    preload = (not args.no_preload and not args.hot and
+               (args.preload or os.environ.get("TPI_PRELOAD", "1") not in ("0", "false", "no")))
     for knob in ("TPI_D2H_ENGINE", "TPI_STREAM_TIMEOUT", "TPI_LINGER_SECONDS",
                  "TPI_HBM_HANDOFF", "TPI_RELEASE_HBM", "TPI_EXPLICIT_TEARDOWN",
                  "HSA_ENABLE_SDMA", "GPU_MAX_HW_QUEUES", "TPI_DIRECT_META",
@@ -207,7 +216,8 @@ def main():
                         "DRAM->restore (1 x MI355X, iterative_task)" % args.gb,
               "codec": args.codec, "spill": spill, "prefetch": not args.no_prefetch,
               "early_prefetch": args.early_prefetch, "standby": args.standby,
-              "hot_standby": args.hot, "stream_handoff": not args.no_stream,
+              "hot_standby": args.hot, "preload": preload,
+              "stream_handoff": not args.no_stream,
               "save_at": "signal" if args.signal_mode else "step boundary",
               "release_hbm": os.environ.get("TPI_RELEASE_HBM", "1") != "0",
               "step_seconds": args.step_seconds, "materialize": args.materialize,
@@ -238,6 +248,16 @@ def main():
             result["standby_pinned_wait_s"] = round(time.time() - t_wait, 3)
             result["standby_pinned"] = next((e.description for e in task.events()
                                              if e.code == "standby-pinned"), None)
+        if preload:
+            # the preloaded successor is spawned 2 s after the rank and then imports PyTorch;
+            # a preemption hours into training finds it parked, so wait for that here too
+            t_wait = time.time()
+            while time.time() - t_wait < 120 and not any(
+                    e.code == "standby-start" and "preloaded" in e.description
+                    for e in task.events()):
+                time.sleep(0.1)
+            time.sleep(3.0)  # its imports (it parks on its activation pipe after them)
+            result["preloaded_wait_s"] = round(time.time() - t_wait, 3)
         t_preempt = time.time()
         task.preempt()
         status = task.wait(args.timeout)

@@ -210,6 +210,8 @@ struct Spec {
   // off-node storage.container mirror (storage/remote.py): run every sync_interval s while
   // ranks run (tpl:118-124) and once, awaited, when they are done (ExecStop's final copy)
   std::vector<std::string> sync_argv;
+  // preloaded successors (TPI_PRELOAD): the launcher; the script path is appended
+  std::vector<std::string> preload_argv;
   double sync_interval = 10, sync_timeout = 600;
   int restart_base = 0;  // restarts of earlier supervisors of this task (requeued incarnations)
 };
@@ -280,6 +282,7 @@ Spec load_spec(const std::string& path) {
   s.disk_interval = lim["disk_interval"].num(10.0);
   for (auto& a : v["requeue_argv"].a) s.requeue_argv.push_back(a.str());
   for (auto& a : v["sync"]["argv"].a) s.sync_argv.push_back(a.str());
+  for (auto& a : v["preload_argv"].a) s.preload_argv.push_back(a.str());
   s.sync_interval = v["sync"]["interval"].num(10);
   s.sync_timeout = v["sync"]["timeout"].num(600);
   s.restart_base = (int)v["restart_base"].num(0);

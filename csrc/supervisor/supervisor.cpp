@@ -165,6 +165,11 @@ class Supervisor {
             timeout = std::min(timeout, kTraceInterval);
       if (respawn_at_ > 0) timeout = std::min(timeout, respawn_at_ - t);
       if (s_.rank_memory_kb) timeout = std::min(timeout, memory_.next_check() - t);
+      if (!s_.preload_argv.empty())  // the next preloaded successor due
+        for (auto& r : ranks_)
+          if (r.state == Rank::RUNNING && r.pid > 0 && r.term_at == 0 &&
+              standby_[r.index].pid <= 0 && r.hot_spawns < 2)
+            timeout = std::min(timeout, std::max(r.hold_until, r.started + kPreloadDelay) - t);
       if (s_.disk_limit_bytes) timeout = std::min(timeout, next_disk_check_ - t);
       timeout = sync_.timeout(t, timeout);
       if (stager_fd_ >= 0) timeout = std::min(timeout, stager_deadline_ - t);
@@ -197,6 +202,7 @@ class Supervisor {
       }
       if (released) handoff_released();
       if (s_.standby_hot) keep_hot_standbys();
+      if (!s_.preload_argv.empty()) keep_preloaded();
       if (pfds[0].revents & POLLIN) handle_signals();
       if (ctl_fd_ >= 0 && nrank_fds < pfds.size() && (pfds[nrank_fds].revents & POLLIN))
         handle_control();
@@ -551,7 +557,7 @@ class Supervisor {
     return env;
   }
 
-  void spawn(Rank& r, bool standby = false) {
+  void spawn(Rank& r, bool standby = false, bool preload = false) {
     r.uuid = uuid4();
     r.partial.clear();
     r.reason = TermReason::NONE;
@@ -635,7 +641,13 @@ class Supervisor {
         dprintf(2, "tpi-supervisor: chdir %s: %s\n", s_.workdir.c_str(), strerror(errno));
         _exit(126);
       }
-      if (s_.login_shell) {
+      if (preload) {  // runtime/preload.py: imports now, runs the script once activated
+        std::vector<char*> pargv;
+        for (auto& a : s_.preload_argv) pargv.push_back(const_cast<char*>(a.c_str()));
+        pargv.push_back(const_cast<char*>(s_.script.c_str()));
+        pargv.push_back(nullptr);
+        execve(pargv[0], pargv.data(), envp.data());
+      } else if (s_.login_shell) {
         const char* argv[] = {s_.shell.c_str(), "-lc", exec_cmd.c_str(), s_.script.c_str(), nullptr};
         execve(s_.shell.c_str(), const_cast<char**>(argv), envp.data());
       } else if (shebang) {
@@ -673,22 +685,45 @@ class Supervisor {
     r.first_output = false;
     r.released = false;
     r.hold_until = (!standby && r.restarts > 0) ? r.started + kStandbyHold : 0;
-    event(standby ? "standby-start" : "rank-start",
-          {"rank " + std::to_string(r.index), "pid " + std::to_string(pid), "machine " + r.uuid,
-           "gpus " + (r.gpus.empty() ? "-" : r.gpus), "restart " + std::to_string(r.restarts)});
+    if (!standby) r.hot_spawns = 0;  // a new incarnation: its own standby budget
+    std::vector<std::string> desc = {"rank " + std::to_string(r.index), "pid " + std::to_string(pid),
+                                     "machine " + r.uuid, "gpus " + (r.gpus.empty() ? "-" : r.gpus),
+                                     "restart " + std::to_string(r.restarts)};
+    if (preload) desc.push_back("preloaded");
+    event(standby ? "standby-start" : "rank-start", desc);
   }
 
   // Warm successor of rank r, spawned while r is being preempted.
-  void spawn_standby(Rank& r) {
+  void spawn_standby(Rank& r, bool preload = false) {
     Rank& sb = standby_[r.index];
-    if (!s_.standby || !r.standby_capable || sb.pid > 0 || stop_ || timed_out_) return;
+    if (sb.pid > 0 || stop_ || timed_out_) return;
+    if (!preload && (!s_.standby || !r.standby_capable)) return;
     if (s_.max_restarts >= 0 && r.restarts >= s_.max_restarts) return;
     sb = Rank();
     sb.index = r.index;
     sb.gpus = r.gpus;
     sb.restarts = r.restarts + 1;
-    spawn(sb, true);
+    spawn(sb, true, preload);
     if (sb.state != Rank::RUNNING) sb = Rank();
+  }
+
+  // Preloaded successors (spec "preload_argv", TPI_PRELOAD=1): every running Python rank keeps
+  // a process that has imported PyTorch and this package and waits on its activation pipe
+  // (runtime/preload.py); the respawn activates it like a warm standby, so a cold successor
+  // skips the interpreter start and the imports (~1.8 s of its 1.9 s).  Started kPreloadDelay
+  // after the rank (not competing with its own start-up), at most two per incarnation.  A hot
+  // standby (which the script itself parks, GPU initialised) takes precedence.
+  static constexpr double kPreloadDelay = 2.0;
+  void keep_preloaded() {
+    const double t = now();
+    for (auto& r : ranks_) {
+      if (r.state != Rank::RUNNING || r.pid <= 0 || r.term_at > 0 ||
+          standby_[r.index].pid > 0 || r.hot_spawns >= 2 || t < r.hold_until ||
+          t < r.started + kPreloadDelay || (s_.standby_hot && r.standby_capable))
+        continue;
+      ++r.hot_spawns;
+      spawn_standby(r, true);
+    }
   }
 
   // Hot standby (spec "standby_hot"): every running, standby-capable rank keeps a successor

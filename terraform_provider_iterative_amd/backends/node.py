@@ -126,6 +126,37 @@ def _free_port(start: int) -> int:
     return start
 
 
+
+def shebang_python(script: str):
+    """``(interpreter, flags)`` when ``script``'s ``#!`` line runs this Python interpreter
+    (``#!/path/python [-u ...]`` or ``#!/usr/bin/env python3 [...]``), else None."""
+    import shutil
+
+    first = (script or "").split("\n", 1)[0]
+    if not first.startswith("#!"):
+        return None
+    words = first[2:].split()
+    if not words:
+        return None
+    if os.path.basename(words[0]) == "env" and len(words) > 1:
+        words = words[1:]
+        if words[0].startswith("-"):  # env -S / -i ...: not followed here
+            return None
+        found = shutil.which(words[0])
+        if not found:
+            return None
+        words[0] = found
+    if not os.path.basename(words[0]).startswith("python"):
+        return None
+    try:
+        same = os.path.realpath(words[0]) == os.path.realpath(sys.executable)
+    except OSError:
+        return None
+    flags = words[1:]
+    if not same or any(not f.startswith("-") or f in ("-c", "-m") for f in flags):
+        return None
+    return sys.executable, flags
+
 class NodeTask(Task):
     """Task on this node; ``provider`` selects CPU-only or GPU placement."""
 
@@ -413,7 +444,28 @@ class NodeTask(Task):
             "limits": self._limits(alloc),
             "requeue_argv": self._waiter_argv(),
             "sync": self._remote_sync(knob),
+            # a preloaded successor per Python rank (runtime/preload.py; TPI_PRELOAD=0: none)
+            "preload_argv": self._preload_argv(knob),
         }
+
+    def _preload_argv(self, knob) -> List[str]:
+        """The launcher of a preloaded successor (``runtime/preload.py``; the supervisor appends
+        the script path), or ``[]``.  On by default (``TPI_PRELOAD=0`` disables) for a script
+        that this very interpreter would run (``#!`` naming it, directly or through ``env``;
+        interpreter flags are kept), since the successor runs it in-process; off with a hot
+        standby (``TPI_WARM_STANDBY=hot``), whose parked successor has the GPU initialised."""
+        if knob("TPI_PRELOAD", "1") not in ("1", "true", "yes"):
+            return []
+        if knob("TPI_WARM_STANDBY", "1") == "hot":
+            return []
+        interp = shebang_python(self.spec.environment.script)
+        if interp is None:
+            return []
+        path, flags = interp
+        code = ("import sys; sys.path.insert(0, %r); "
+                "from terraform_provider_iterative_amd.runtime.preload import main; main()"
+                % ROOT)
+        return [path] + flags + ["-c", code]
 
     def _remote_sync(self, knob) -> Optional[Dict]:
         """The supervisor's mirror of an off-node container: every ``TPI_SYNC_INTERVAL`` s

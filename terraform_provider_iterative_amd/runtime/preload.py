@@ -1,0 +1,85 @@
+"""Preloaded successor of a Python rank: an interpreter that has already imported PyTorch and
+this package, parked until its rank is preempted, then running the rank's script in-process.
+
+A cold successor spends ~1.8 s of its 1.9 s signal -> restored starting an interpreter and
+importing PyTorch (``profiles/round5/r5p/bench.json``, ``preempt_e2e.runs.cold``).  With
+``TPI_PRELOAD=1`` the supervisor keeps one of these per rank (``preload_argv`` in its spec,
+``csrc/supervisor/supervisor.cpp`` ``keep_preloaded``): spawned with the next incarnation's
+environment once the rank has run a while, it imports and then blocks on its activation pipe
+(fd ``TPI_STANDBY_FD``, as a warm standby does).  The supervisor activates it at the respawn
+("go port=<rendezvous port>"); it then runs the script exactly as ``python script`` would:
+``__main__``, ``sys.argv``, ``sys.path[0]`` the script's directory, exit status from
+``SystemExit`` or an uncaught exception.  It never touches the GPU before activation (nothing
+here initialises HIP), so the script's own ``HIP_VISIBLE_DEVICES`` and device choices hold.
+EOF on the pipe (the rank finished, the task stopped): it exits quietly.
+
+Reference: a spot VM's replacement boots and runs the machine script from the start
+(``task/common/machine/machine-script.sh.tpl:89``); here the replacement is a process, and
+its start-up is taken off the recovery path.
+"""
+from __future__ import annotations
+
+import os
+import runpy
+import sys
+import time
+
+
+def _read_go(fd: int) -> str:
+    data = b""
+    while not data.endswith(b"\n"):
+        try:
+            chunk = os.read(fd, 256)
+        except InterruptedError:
+            continue
+        if not chunk:
+            break
+        data += chunk
+    return data.decode(errors="replace").strip()
+
+
+def main(argv=None) -> None:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if not argv:
+        raise SystemExit("usage: preload <script> [args...]")
+    added = sys.path[0] if sys.path else None  # the package root the launcher put first
+    t0 = time.time()
+    import torch  # noqa: F401  -- the point: the import a successor would wait for
+
+    import terraform_provider_iterative_amd.checkpoint  # noqa: F401
+    from terraform_provider_iterative_amd.checkpoint import preemption  # noqa: F401
+    preloaded_s = time.time() - t0
+    fd = int(os.environ.get("TPI_STANDBY_FD", "4"))
+    line = _read_go(fd)
+    try:
+        os.close(fd)
+    except OSError:
+        pass
+    if not line.startswith("go"):
+        os._exit(0)  # discarded before it was needed
+    for token in line.split()[1:]:
+        if token.startswith("port="):
+            os.environ["MASTER_PORT"] = token[5:]
+    for name in ("TPI_STANDBY", "TPI_STANDBY_FD"):
+        os.environ.pop(name, None)
+    os.environ["TPI_PRELOADED"] = "%.3f" % preloaded_s
+    if os.environ.get("TPI_DEADLINE"):  # set at spawn; the time left is that of now
+        try:
+            os.environ["TPI_REMAINING_RUN_TIME"] = str(
+                max(0, int(float(os.environ["TPI_DEADLINE"]) - time.time())))
+        except ValueError:
+            pass
+    script = os.path.abspath(argv[0])
+    # as `python script`: the script's directory first on the path, not the launcher's
+    if added is not None and sys.path and sys.path[0] == added:
+        sys.path.pop(0)
+    if sys.path and sys.path[0] in ("", os.getcwd()):
+        sys.path[0] = os.path.dirname(script)
+    else:
+        sys.path.insert(0, os.path.dirname(script))
+    sys.argv = [argv[0]] + argv[1:]
+    runpy.run_path(script, run_name="__main__")
+
+
+if __name__ == "__main__":
+    main()

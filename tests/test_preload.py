@@ -1,0 +1,126 @@
+"""Preloaded successors (``TPI_PRELOAD=1``, ``runtime/preload.py`` + the supervisor's
+``keep_preloaded``): a Python rank's successor has imported PyTorch before the preemption and
+then runs the script exactly as ``python script`` would.
+
+Reference: the replacement of a preempted spot VM runs the machine script from the start
+(``task/common/machine/machine-script.sh.tpl:89``).
+"""
+import os
+import sys
+import time
+
+import pytest
+
+from terraform_provider_iterative_amd import backends
+from terraform_provider_iterative_amd.backends.node import shebang_python
+from terraform_provider_iterative_amd.models.cloud import Cloud, Credentials, NodeCredentials
+from terraform_provider_iterative_amd.models.values import Environment, Task, Variables
+from terraform_provider_iterative_amd.utils.identifier import new_deterministic_identifier
+
+
+def test_only_scripts_of_this_interpreter_are_preloaded():
+    exe = sys.executable
+    assert shebang_python("#!%s\nprint(1)\n" % exe) == (exe, [])
+    assert shebang_python("#!%s -u\n" % exe) == (exe, ["-u"])
+    assert shebang_python("#!/bin/bash\necho hi\n") is None
+    assert shebang_python("print(1)\n") is None
+    assert shebang_python("#!%s -m mod\n" % exe) is None  # not a plain script run
+    assert shebang_python("#!/nonexistent/python3\n") is None
+    env_form = shebang_python("#!/usr/bin/env %s\n" % os.path.basename(exe))
+    import shutil
+
+    found = shutil.which(os.path.basename(exe))
+    if found and os.path.realpath(found) == os.path.realpath(exe):
+        assert env_form == (exe, [])
+    else:
+        assert env_form is None
+
+
+SCRIPT = r'''#!%(python)s
+import os, sys, time
+restart = int(os.environ["TPI_RESTART_COUNT"])
+print("incarnation %%d torch-preloaded %%s name %%s argv0 %%s path0 %%s preloaded %%s standby %%s" %% (
+    restart, "torch" in sys.modules, __name__, sys.argv[0], sys.path[0],
+    os.environ.get("TPI_PRELOADED"), os.environ.get("TPI_STANDBY")), flush=True)
+if restart == 0:
+    while True:  # preempted: SIGTERM ends it, the supervisor respawns the rank
+        time.sleep(0.05)
+sys.exit(7 if restart == 1 else 0)
+'''
+
+
+def _wait_event(task, pred, timeout):
+    deadline = time.time() + timeout
+    while time.time() < deadline:
+        for e in task.events():
+            if pred(e):
+                return e
+        time.sleep(0.1)
+    raise AssertionError("no such event; events: %s" % [(e.code, e.description)
+                                                         for e in task.events()])
+
+
+def test_a_preempted_rank_resumes_in_its_preloaded_successor(tmp_path):
+    cloud = Cloud(provider="local",
+                  credentials=Credentials(node=NodeCredentials(state_root=str(tmp_path / "st"))))
+    spec = Task(environment=Environment(
+        script=SCRIPT % {"python": sys.executable}, timeout=120,
+        variables=Variables({"TPI_TASK": "true", "TPI_PRELOAD": "1",
+                             "TPI_MAX_RESTARTS": "1"})))
+    task = backends.new(cloud, new_deterministic_identifier("preload-1"), spec)
+    task.create()
+    try:
+        started = _wait_event(task, lambda e: e.code == "standby-start" and
+                              "preloaded" in e.description, 60)
+        assert "restart 1" in started.description
+        time.sleep(4.0)  # the successor is importing torch; activated before or after, it waits
+        t0 = time.time()
+        task.preempt()
+        status = task.wait(60)
+        took = time.time() - t0
+    finally:
+        logs = "\n".join(task.logs())
+    # the second incarnation exits 7: a failure the status records
+    assert status["failed"] == 1, (status, logs)
+    assert "incarnation 0 torch-preloaded False name __main__" in logs, logs
+    line = next(l for l in logs.splitlines() if "incarnation 1" in l)
+    script_path = line.split(" argv0 ")[1].split()[0]
+    assert "torch-preloaded True" in line and "name __main__" in line, line
+    assert line.split(" path0 ")[1].split()[0] == os.path.dirname(script_path), line
+    assert "standby None" in line and "preloaded None" not in line, line
+    starts = [e for e in task.events() if e.code == "rank-start"]
+    assert any("warm standby" in e.description and "restart 1" in e.description
+               for e in starts), starts
+    assert took < 30, took
+    task.delete()
+
+
+def test_preload_is_on_by_default_and_off_on_request(tmp_path, monkeypatch):
+    monkeypatch.delenv("TPI_PRELOAD", raising=False)  # tests/conftest.py turns it off
+    cloud = Cloud(provider="local",
+                  credentials=Credentials(node=NodeCredentials(state_root=str(tmp_path / "st"))))
+
+    def argv_for(script, **env):
+        spec = Task(environment=Environment(script=script, variables=Variables(env)))
+        task = backends.new(cloud, new_deterministic_identifier("pre-%d" % len(env)), spec)
+        return task._preload_argv(lambda name, default: env.get(name, default))
+
+    python_script = "#!%s\nprint(1)\n" % sys.executable
+    argv = argv_for(python_script)
+    assert argv[0] == sys.executable and argv[1] == "-c" and "runtime.preload" in argv[2]
+    assert argv_for(python_script, TPI_PRELOAD="0") == []
+    assert argv_for(python_script, TPI_WARM_STANDBY="hot") == []  # its own parked successor
+    assert argv_for("#!/bin/sh\necho hi\n") == []
+
+
+def test_no_preload_when_disabled(tmp_path):
+    cloud = Cloud(provider="local",
+                  credentials=Credentials(node=NodeCredentials(state_root=str(tmp_path / "st"))))
+    spec = Task(environment=Environment(
+        script="#!%s\nimport time; time.sleep(3)\n" % sys.executable, timeout=60,
+        variables=Variables({"TPI_TASK": "true", "TPI_PRELOAD": "0"})))
+    task = backends.new(cloud, new_deterministic_identifier("preload-0"), spec)
+    task.create()
+    assert task.wait(60)["succeeded"] == 1
+    assert not [e for e in task.events() if e.code == "standby-start"]
+    task.delete()
