@@ -454,7 +454,8 @@ class NodeTask(Task):
         that this very interpreter would run (``#!`` naming it, directly or through ``env``;
         interpreter flags are kept), since the successor runs it in-process; off with a hot
         standby (``TPI_WARM_STANDBY=hot``), whose parked successor has the GPU initialised."""
-        if knob("TPI_PRELOAD", "1") not in ("1", "true", "yes"):
+        mode = knob("TPI_PRELOAD", "1")
+        if mode not in ("1", "true", "yes", "gpu"):
             return []
         if knob("TPI_WARM_STANDBY", "1") == "hot":
             return []
@@ -462,9 +463,10 @@ class NodeTask(Task):
         if interp is None:
             return []
         path, flags = interp
+        # TPI_PRELOAD=gpu: the parked process also initialises the GPU and prewarms an engine
         code = ("import sys; sys.path.insert(0, %r); "
-                "from terraform_provider_iterative_amd.runtime.preload import main; main()"
-                % ROOT)
+                "from terraform_provider_iterative_amd.runtime.preload import main; main(gpu=%r)"
+                % (ROOT, mode == "gpu"))
         return [path] + flags + ["-c", code]
 
     def _remote_sync(self, knob) -> Optional[Dict]:

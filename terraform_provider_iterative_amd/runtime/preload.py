@@ -10,7 +10,8 @@ environment once the rank has run a while, it imports and then blocks on its act
 ("go port=<rendezvous port>"); it then runs the script exactly as ``python script`` would:
 ``__main__``, ``sys.argv``, ``sys.path[0]`` the script's directory, exit status from
 ``SystemExit`` or an uncaught exception.  It never touches the GPU before activation (nothing
-here initialises HIP), so the script's own ``HIP_VISIBLE_DEVICES`` and device choices hold.
+here initialises HIP unless ``TPI_PRELOAD=gpu``), so the script's own ``HIP_VISIBLE_DEVICES``
+and device choices hold.
 EOF on the pipe (the rank finished, the task stopped): it exits quietly.
 
 Reference: a spot VM's replacement boots and runs the machine script from the start
@@ -38,7 +39,22 @@ def _read_go(fd: int) -> str:
     return data.decode(errors="replace").strip()
 
 
-def main(argv=None) -> None:
+def _warm_gpu() -> None:
+    """``TPI_PRELOAD=gpu``: also initialise the GPU and prewarm a checkpoint engine, as a hot
+    standby does (the successor's Checkpointer takes the engine).  Costs the parked process a
+    GPU context and the engine's staging buffers for the life of the rank."""
+    import torch
+
+    from terraform_provider_iterative_amd.checkpoint import prewarm_engine
+
+    torch.cuda.init()
+    device = torch.cuda.current_device()
+    torch.empty(1 << 20, dtype=torch.uint8, device="cuda")  # context + caching allocator
+    prewarm_engine(device)
+    torch.cuda.synchronize()
+
+
+def main(argv=None, gpu: bool = False) -> None:
     argv = list(sys.argv[1:] if argv is None else argv)
     if not argv:
         raise SystemExit("usage: preload <script> [args...]")
@@ -48,6 +64,11 @@ def main(argv=None) -> None:
 
     import terraform_provider_iterative_amd.checkpoint  # noqa: F401
     from terraform_provider_iterative_amd.checkpoint import preemption  # noqa: F401
+    if gpu:
+        try:
+            _warm_gpu()
+        except Exception as error:  # the successor initialises it itself
+            print("tpi-preload: GPU warm-up failed: %s" % error, file=sys.stderr, flush=True)
     preloaded_s = time.time() - t0
     fd = int(os.environ.get("TPI_STANDBY_FD", "4"))
     line = _read_go(fd)
