@@ -1153,25 +1153,23 @@ class Checkpointer(HbmHandoff):
 
     def persist(self, path: str) -> str:
         """Write the current checkpoint (header, CRCs, stream: one slot) to ``path``
-        atomically.  ``path`` may name a file on another node (``ssh://host/dir/file``,
-        ``host:/dir/file``: an off-node ``storage.container``, :mod:`..storage.remote`); the
-        file is written locally first, then moved there."""
+        atomically.  ``path`` may name a file on another node or in a bucket (``ssh://host/dir/
+        file``, ``host:/dir/file``, ``s3://``/``gs://``/``az://bucket/key``: an off-node
+        ``storage.container``, :mod:`..storage.remote`); the slot then goes there straight
+        from the host region, with no local temporary file."""
         from ..storage import remote
 
-        if remote.is_remote(path):
-            tmp = _local_scratch(path)
-            try:
-                self.persist(tmp)
-                remote.store(tmp, path)
-            finally:
-                if os.path.exists(tmp):
-                    os.remove(tmp)
-            return path
         self.wait_pending()
         active = self._active()
         if active is None:
             raise CheckpointError("nothing saved yet")
         slot, header = active
+        if remote.is_remote(path):
+            nbytes = self.stream_offset + int(header["stream_bytes"])
+            view = memoryview((ctypes.c_char * nbytes).from_address(
+                self.region.addr + slot.base)).cast("B")
+            remote.store_bytes(view, path)
+            return path
         tmp = path + ".tpi-partial"
         # parallel pwrite of the slot (native, GIL released) + fsync, then an atomic rename
         native().write_file_ptr(tmp, self.region.addr + slot.base,

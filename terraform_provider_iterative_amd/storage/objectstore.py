@@ -265,7 +265,11 @@ class ObjectRemote:
         raise NotImplementedError
 
     # helpers -------------------------------------------------------------------------------------
-    def _read(self, local: str, offset: int, length: int) -> bytes:
+    def _read(self, local, offset: int, length: int):
+        """``length`` bytes at ``offset`` of a file (path) or of a buffer (memoryview: a
+        slice, no copy)."""
+        if isinstance(local, memoryview):
+            return local[offset:offset + length]
         with open(local, "rb") as f:
             f.seek(offset)
             data = f.read(length)
@@ -273,15 +277,18 @@ class ObjectRemote:
             raise ObjectStoreError("%s changed size while it was uploaded" % local)
         return data
 
-    def _upload(self, key: str, local: str, pool: ThreadPoolExecutor) -> int:
-        st = os.stat(local)
-        meta = {"mtime": "%.9f" % st.st_mtime}
-        if st.st_size <= self.part:
-            with self._slots:
-                self._put(key, self._read(local, 0, st.st_size), meta)
+    def _upload(self, key: str, local, pool: ThreadPoolExecutor) -> int:
+        if isinstance(local, memoryview):
+            size, meta = local.nbytes, {"mtime": "%.9f" % time.time()}
         else:
-            self._upload_large(key, local, st.st_size, meta, pool)
-        return st.st_size
+            st = os.stat(local)
+            size, meta = st.st_size, {"mtime": "%.9f" % st.st_mtime}
+        if size <= self.part:
+            with self._slots:
+                self._put(key, self._read(local, 0, size), meta)
+        else:
+            self._upload_large(key, local, size, meta, pool)
+        return size
 
     def _download(self, key: str, size: int, local: str, pool: ThreadPoolExecutor) -> int:
         os.makedirs(os.path.dirname(os.path.abspath(local)), exist_ok=True)
@@ -334,6 +341,12 @@ class ObjectRemote:
 
     def put_file(self, local: str, rel: str) -> int:
         return self._run([lambda pool: self._upload(self.path(rel), local, pool)])
+
+    def put_bytes(self, data: memoryview, rel: str) -> int:
+        """Upload a buffer as one object (a checkpoint slot straight from its host region:
+        no temporary file)."""
+        return self._run([lambda pool: self._upload(self.path(rel), memoryview(data).cast("B"),
+                                                     pool)])
 
     def get_file(self, rel: str, local: str) -> int:
         key = self.path(rel)

@@ -254,6 +254,38 @@ class SSHRemote:
                 self.host, dest, proc.stderr.decode(errors="replace")[-1000:]))
         return os.path.getsize(local)
 
+    def put_bytes(self, data: memoryview, rel: str) -> int:
+        """Write a buffer as one file (a checkpoint slot straight from its host region)."""
+        view = memoryview(data).cast("B")
+        dest = self.path(rel)
+        tmp = dest + ".tpi-partial"
+        command = "mkdir -p %s && cat > %s && mv -f %s %s" % (
+            shlex.quote(posixpath.dirname(dest)), shlex.quote(tmp), shlex.quote(tmp),
+            shlex.quote(dest))
+        proc = subprocess.Popen(self._argv(command), stdin=subprocess.PIPE,
+                                stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+        err = b""
+
+        def drain():
+            nonlocal err
+            err = proc.stderr.read()
+
+        reader = threading.Thread(target=drain, daemon=True)
+        reader.start()
+        try:
+            for off in range(0, view.nbytes, 64 << 20):
+                proc.stdin.write(view[off:off + (64 << 20)])
+        except BrokenPipeError:
+            pass
+        finally:
+            proc.stdin.close()
+            rc = proc.wait()
+            reader.join()
+        if rc != 0:
+            raise OSError("storage node %s: writing %s failed: %s" % (
+                self.host, dest, err.decode(errors="replace")[-1000:]))
+        return view.nbytes
+
     def get_file(self, rel: str, local: str) -> int:
         src = self.path(rel)
         tmp = local + ".tpi-partial"
@@ -313,6 +345,12 @@ def file_exists(location: str) -> bool:
 def store(local: str, location: str) -> int:
     remote, name = split_file(location)
     return remote.put_file(local, name)
+
+
+def store_bytes(data: memoryview, location: str) -> int:
+    """Write a buffer to a remote file location (no local temporary file)."""
+    remote, name = split_file(location)
+    return remote.put_bytes(data, name)
 
 
 # -- the running task's mirror (the reference's 10 s data loop and its final copy) --------------

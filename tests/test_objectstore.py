@@ -314,3 +314,35 @@ def test_a_remote_clouds_bucket_is_reached_over_its_protocol_on_a_node(tmp_path,
     task = backends.new(Cloud(provider="aws", credentials=creds),
                         new_deterministic_identifier("rb-dir"), spec)
     assert task.remote_conn is None
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_checkpoint_persists_straight_into_a_bucket_and_loads_back(tmp_path, fake, backend,
+                                                                   monkeypatch):
+    """``Checkpointer.persist(url)`` uploads the slot from the host region itself (parts of
+    a buffer, no local temporary file); ``load(url)`` fetches and restores it."""
+    import torch
+
+    from terraform_provider_iterative_amd.checkpoint import Checkpointer
+
+    monkeypatch.setenv("TPI_OBJECT_PART_MB", "1")  # a multipart upload for this small state
+    opts = fake.options(backend)
+    url = ":%s,%s:ckb/runs/ck.tpi" % (
+        backend, ",".join("%s='%s'" % (k, v) for k, v in opts.items()
+                          if k != "service_account_credentials"))
+    if backend == "googlecloudstorage":
+        creds = tmp_path / "sa.json"
+        creds.write_text(opts["service_account_credentials"])
+        monkeypatch.setenv("GOOGLE_APPLICATION_CREDENTIALS", str(creds))
+    state = {"w": torch.arange(600_000, dtype=torch.float64)}
+    with Checkpointer(state, path=str(tmp_path / "spill"), tile_bytes=4096) as ck:
+        ck.save({"step": 7})
+        assert ck.persist(url) == url
+    assert not [p for p in os.listdir(tmp_path) if "tpi-partial" in p or p.startswith("tpi-")]
+    obj = fake.objects(backend, "ckb")["runs/ck.tpi"]
+    assert len(obj) > 4_800_000
+    state2 = {"w": torch.zeros(600_000, dtype=torch.float64)}
+    with Checkpointer(state2, path=str(tmp_path / "spill2"), tile_bytes=4096) as ck2:
+        res = ck2.load(url)
+        assert res.bad_tiles == 0 and ck2.header()["metadata"] == {"step": 7}
+    assert torch.equal(state2["w"], state["w"])
