@@ -104,6 +104,41 @@ def test_preempt_resume_training_on_gpu(cloud, tmp_path, materialize):
     task.delete()
 
 
+def test_preempted_training_resumes_in_a_preloaded_successor_on_gpu(cloud, tmp_path):
+    """A Python rank (examples/train/train.py behind a Python shebang) with TPI_PRELOAD=1:
+    its successor is the parked interpreter that imported PyTorch before the preemption
+    (runtime/preload.py); it resumes the training from the preemption checkpoint."""
+    env = {"TPI_FRAMEWORK_ROOT": ROOT, "TPI_TASK": "true", "TPI_PRELOAD": "1"}
+    train = os.path.join(ROOT, "examples", "train", "train.py")
+    script = ("#!%s\nimport runpy, sys\nsys.argv = [%r, '--steps', '600', '--hidden', '256', "
+              "'--layers', '2', '--batch', '4', '--seq', '64', '--sleep', '0.05']\n"
+              "sys.path.insert(0, %r)\nprint('torch preloaded', 'torch' in sys.modules, "
+              "flush=True)\nrunpy.run_path(%r, run_name='__main__')\n"
+              % (sys.executable, train, os.path.dirname(train), train))
+    spec = Task(size=Size(machine="m+mi355x"),
+                environment=Environment(script=script, timeout=600, variables=Variables(env)))
+    task = backends.new(cloud, new_deterministic_identifier("gpu-preload"), spec)
+    task.create()
+    deadline = time.time() + 300
+    while time.time() < deadline and not any(
+            e.code == "standby-start" and "preloaded" in e.description for e in task.events()):
+        time.sleep(0.1)
+    assert any(e.code == "standby-start" for e in task.events()), task.logs()
+    time.sleep(4.0)  # its imports; it then parks
+    task.preempt()
+    status = task.wait(300)
+    logs = task.logs()
+    assert status["succeeded"] == 1, logs
+    assert len(logs) == 2 and "preemption checkpoint saved" in logs[0], logs
+    assert "torch preloaded False" in logs[0] and "torch preloaded True" in logs[1], logs
+    resumed = [l for l in logs[1].splitlines() if "resumed from step" in l]
+    assert resumed and int(resumed[0].rsplit(" ", 1)[1]) >= 1, logs[1]
+    assert "done" in logs[1]
+    assert any(e.code == "rank-start" and "warm standby" in e.description
+               for e in task.events())
+    task.delete()
+
+
 def test_training_state_on_device_carries_cpu_step_counters(tmp_path):
     from terraform_provider_iterative_amd.checkpoint import TrainingState, collect
 
