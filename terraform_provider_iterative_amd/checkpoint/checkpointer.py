@@ -1185,34 +1185,50 @@ class Checkpointer(HbmHandoff):
         The stream section is read by parallel native readers in chunks that are published
         like a streamed save's (progress block), so the device restore runs behind the file
         read instead of after it.  ``path`` may name a file on another node (see
-        :meth:`persist`): it is fetched first."""
+        :meth:`persist`): an object in a bucket is read in place by ranged requests, streamed
+        the same way; a file on an SSH node is fetched first."""
         from ..storage import remote
 
+        obj = None
         if remote.is_remote(path):
-            tmp = remote.fetch(path, os.path.dirname(_local_scratch(path)))
-            try:
-                return self.load(tmp)
-            finally:
-                os.remove(tmp)
+            obj = remote.object_source(path)
+            if obj is None:
+                tmp = remote.fetch(path, os.path.dirname(_local_scratch(path)))
+                try:
+                    return self.load(tmp)
+                finally:
+                    os.remove(tmp)
         self.wait_pending()
         self._wait_writers()
         slot, generation = self._target()
-        with open(path, "rb") as f:
-            head = np.frombuffer(f.read(PREAMBLE + self.header_cap), np.uint8)
-            header = self.read_header(head)
-            self._check_compatible(header)
-            if not header.get("complete"):
-                raise CheckpointError("%s holds an incomplete checkpoint" % path)
-            size = os.fstat(f.fileno()).st_size
+        if obj is None:
+            with open(path, "rb") as f:
+                head = np.frombuffer(f.read(PREAMBLE + self.header_cap), np.uint8)
+                size = os.fstat(f.fileno()).st_size
+        else:
+            size = obj[0].size(obj[1])
+            if size is None:
+                raise CheckpointError("no checkpoint at %s" % path)
+            head = np.frombuffer(obj[0].read(obj[1], 0, min(size, PREAMBLE + self.header_cap)),
+                                 np.uint8)
+        header = self.read_header(head)
+        self._check_compatible(header)
+        if not header.get("complete"):
+            raise CheckpointError("%s holds an incomplete checkpoint" % path)
         stream_bytes = int(header["stream_bytes"])
         end = self.stream_offset + stream_bytes
         if size < end:
             raise CheckpointError("%s is truncated (%d of %d bytes)" % (path, size, end))
         self._invalidate(slot)
         # entries + CRCs + blob sizes first (small), then the stream, streamed
-        native().read_stream_ptr(path, self.region.addr + slot.base + self.entries_offset,
-                                 self.entries_offset, self.stream_offset - self.entries_offset,
-                                 FILE_THREADS, 64 << 20, 0, 0, 0)
+        if obj is None:
+            native().read_stream_ptr(path, self.region.addr + slot.base + self.entries_offset,
+                                     self.entries_offset,
+                                     self.stream_offset - self.entries_offset,
+                                     FILE_THREADS, 64 << 20, 0, 0, 0)
+        else:
+            obj[0].read_into(obj[1], self.region.addr + slot.base + self.entries_offset,
+                             self.entries_offset, self.stream_offset - self.entries_offset)
         if header.get("codec", "none") == "tpz1":
             tile_ends = np.cumsum(slot.csizes.astype(np.uint64), dtype=np.uint64)
             if len(tile_ends) and int(tile_ends[-1]) != stream_bytes:
@@ -1228,12 +1244,21 @@ class Checkpointer(HbmHandoff):
         self._write_header(slot, dict(header, complete=False, streaming=True))
         failure: list = []
 
+        def publish(done: int) -> None:  # as read_stream's words: bytes, then whole tiles
+            prog[3] = done
+            prog[2] = int(np.searchsorted(tile_ends, np.uint64(done), side="right"))
+
         def read():
             try:
-                native().read_stream_ptr(path, self.region.addr + slot.base + self.stream_offset,
-                                         self.stream_offset, stream_bytes, FILE_THREADS,
-                                         LOAD_CHUNK, prog.ctypes.data + 16,
-                                         tile_ends.ctypes.data, len(tile_ends))
+                if obj is None:
+                    native().read_stream_ptr(path,
+                                             self.region.addr + slot.base + self.stream_offset,
+                                             self.stream_offset, stream_bytes, FILE_THREADS,
+                                             LOAD_CHUNK, prog.ctypes.data + 16,
+                                             tile_ends.ctypes.data, len(tile_ends))
+                else:
+                    obj[0].read_into(obj[1], self.region.addr + slot.base + self.stream_offset,
+                                     self.stream_offset, stream_bytes, publish)
                 self._write_header(slot, header)
                 prog[4] = STREAM_COMPLETE
             except BaseException as error:  # the restore sees FAILED and raises

@@ -355,6 +355,55 @@ class ObjectRemote:
             raise FileNotFoundError("%s: no object %s" % (self, key))
         return self._run([lambda pool: self._download(key, size, local, pool)])
 
+    def size(self, rel: str) -> Optional[int]:
+        """Bytes of the object at ``rel`` (None: no such object)."""
+        return self._head(self.path(rel))
+
+    def read(self, rel: str, offset: int, n: int) -> bytes:
+        """``n`` bytes at ``offset`` of an object (one ranged request)."""
+        if n <= 0:
+            return b""
+        with self._slots:
+            data = self._get(self.path(rel), offset, offset + n - 1)
+        if len(data) != n:
+            raise ObjectStoreError("%s: short read of %s at %d" % (self, rel, offset))
+        return data
+
+    def read_into(self, rel: str, addr: int, offset: int, n: int,
+                  progress: Optional[Callable[[int], None]] = None) -> int:
+        """Bytes ``[offset, offset + n)`` of an object into memory at ``addr`` (ranged GETs,
+        ``threads`` at once); ``progress(b)`` is called, in order, each time the prefix
+        ``[0, b)`` is complete -- a streamed restore runs behind it (Checkpointer.load)."""
+        import ctypes
+
+        key = self.path(rel)
+        starts = list(range(0, n, self.part))
+        done = set()
+        lock = threading.Lock()
+        state = {"prefix": 0}
+
+        def piece(i: int) -> None:
+            a = starts[i]
+            b = min(n, a + self.part)
+            with self._slots:
+                data = self._get(key, offset + a, offset + b - 1)
+                if len(data) != b - a:
+                    raise ObjectStoreError("%s: short read of %s at %d" % (self, key, offset + a))
+                ctypes.memmove(addr + a, data, b - a)
+            with lock:
+                done.add(i)
+                advanced = False
+                while state["prefix"] < len(starts) and state["prefix"] in done:
+                    state["prefix"] += 1
+                    advanced = True
+                if advanced and progress is not None:
+                    progress(min(n, starts[state["prefix"] - 1] + self.part))
+
+        with ThreadPoolExecutor(self.threads, thread_name_prefix="tpi-obj-read") as pool:
+            for fut in [pool.submit(piece, i) for i in range(len(starts))]:
+                fut.result()
+        return n
+
     def put_tree(self, local_dir: str, rel: str, rules: Optional[List[str]] = None,
                  only: Optional[Iterable[str]] = None) -> Dict[str, int]:
         """Upload ``local_dir`` (filter ``rules``; ``only``: just these relative paths) under

@@ -347,6 +347,14 @@ def store(local: str, location: str) -> int:
     return remote.put_file(local, name)
 
 
+def object_source(location: str):
+    """``(remote, key)`` of an object-store file location, read in place by ranged requests
+    (:meth:`ObjectRemote.read_into`); None for other locations (fetched whole)."""
+    if not objectstore.is_object_store(location):
+        return None
+    return split_file(location)
+
+
 def store_bytes(data: memoryview, location: str) -> int:
     """Write a buffer to a remote file location (no local temporary file)."""
     remote, name = split_file(location)
