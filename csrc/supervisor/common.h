@@ -150,6 +150,7 @@ struct Rank {
   bool released = false;      // wrote "released" on its notify pipe
   bool standby_capable = false;  // announced "standby" (calls preemption.standby())
   int hot_spawns = 0;            // hot standbys started for this incarnation
+  bool unused_standby = false;   // a standby discarded before activation (empty log: removed)
   int gofd = -1;                 // standby only: write end of its activation pipe
   double hold_until = 0;  // a resuming incarnation: no new hot standby until it restored
   // restored from its predecessor's HBM ("restored hbm"): the predecessor must stay alive

@@ -758,6 +758,10 @@ class Supervisor {
     sb.term_at = now();
     sb.exit_requested_at = sb.term_at;
     sb.state = Rank::DONE;
+    sb.unused_standby = true;
+    struct stat st;  // nothing printed yet (a parked preloaded successor): no machine log
+    if (sb.logfd >= 0 && fstat(sb.logfd, &st) == 0 && st.st_size == 0)
+      unlink((s_.reports_dir + "/task-" + sb.uuid).c_str());
     event("standby-discarded", {"rank " + std::to_string(index), "machine " + sb.uuid, why});
     detached_.push_back(sb);
     sb = Rank();
@@ -963,8 +967,13 @@ class Supervisor {
 
   void close_log(Rank& r) {
     if (r.logfd >= 0) {
+      struct stat st;
+      // a standby that never ran the script (a preloaded one, or killed before it printed)
+      // leaves no empty machine log behind for `leo read`
+      const bool empty = r.unused_standby && fstat(r.logfd, &st) == 0 && st.st_size == 0;
       close(r.logfd);
       r.logfd = -1;
+      if (empty) unlink((s_.reports_dir + "/task-" + r.uuid).c_str());
     }
   }
 

@@ -92,6 +92,8 @@ def test_a_preempted_rank_resumes_in_its_preloaded_successor(tmp_path):
     assert any("warm standby" in e.description and "restart 1" in e.description
                for e in starts), starts
     assert took < 30, took
+    # the successor's own parked successor was discarded unused: it leaves no empty log
+    assert all(l.strip() for l in task.logs()), task.logs()
     task.delete()
 
 
