@@ -534,15 +534,30 @@ tpi_engine* tpi_engine_create(int device, uint64_t chunk_bytes, int nbuf, uint64
     return nullptr;
   };
   hipError_t err;
+  // TPI_ENGINE_TRACE=1: the time of each creation step on stderr
+  const bool trace = getenv("TPI_ENGINE_TRACE") != nullptr;
+  auto t_last = std::chrono::steady_clock::now();
+  auto step = [&](const char* what) {
+    if (!trace) return;
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "tpi_engine_create: %s %.3f ms\n", what,
+            std::chrono::duration<double, std::milli>(t - t_last).count());
+    t_last = t;
+  };
   if ((err = hipSetDevice(device)) != hipSuccess) return bail("hipSetDevice", err);
+  step("hipSetDevice");
   if ((err = hipStreamCreateWithFlags(&e->compute, hipStreamNonBlocking)) != hipSuccess)
     return bail("hipStreamCreate(compute)", err);
+  // the process's first hardware queue: ~137 ms of a cold successor's engine creation, the
+  // other streams ~5 ms each (profiles/round5/r5z/engine_create_trace.txt)
+  step("compute stream");
   if ((err = hipStreamCreateWithFlags(&e->copy, hipStreamNonBlocking)) != hipSuccess)
     return bail("hipStreamCreate(copy)", err);
   if ((err = hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking)) != hipSuccess)
     return bail("hipStreamCreate(aux)", err);
   if ((err = hipStreamCreateWithFlags(&e->copy2, hipStreamNonBlocking)) != hipSuccess)
     return bail("hipStreamCreate(copy2)", err);
+  step("3 more streams");
   if (const char* lead = getenv("TPI_H2D_SPLIT_LEAD")) {  // "off": never split
     char* end = nullptr;
     const unsigned long long v = strtoull(lead, &end, 10);
@@ -568,6 +583,7 @@ tpi_engine* tpi_engine_create(int device, uint64_t chunk_bytes, int nbuf, uint64
     if ((err = hipEventCreateWithFlags(&e->ev_b[i], hipEventDisableTiming)) != hipSuccess)
       return bail("hipEventCreate", err);
   }
+  step("staging + events");
   if ((err = hipEventCreateWithFlags(&e->ev_wait, hipEventDisableTiming)) != hipSuccess)
     return bail("hipEventCreate", err);
   if ((err = hipEventCreateWithFlags(&e->ev_done, hipEventDisableTiming)) != hipSuccess)
@@ -586,13 +602,16 @@ tpi_engine* tpi_engine_create(int device, uint64_t chunk_bytes, int nbuf, uint64
       }
     }
   }
+  step("events + priority stream");
   if ((err = hipMalloc(&e->d_bad, 2 * sizeof(unsigned long long))) != hipSuccess)
     return bail("hipMalloc(bad)", err);
   if (device_tables(device, &e->tables)) {
     tpi_engine_destroy(e);
     return nullptr;
   }
+  step("crc tables");
   e->sdma = tpi_sdma_open(device, nbuf + 1);
+  step("sdma lanes");
   return e;
 }
 
