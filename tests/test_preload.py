@@ -126,3 +126,47 @@ def test_no_preload_when_disabled(tmp_path):
     assert task.wait(60)["succeeded"] == 1
     assert not [e for e in task.events() if e.code == "standby-start"]
     task.delete()
+
+
+GANG = r'''#!%(python)s
+import os, sys, time
+restart = int(os.environ["TPI_RESTART_COUNT"])
+print("rank %%s incarnation %%d torch-preloaded %%s port %%s" %% (
+    os.environ["RANK"], restart, "torch" in sys.modules, os.environ["MASTER_PORT"]), flush=True)
+if restart == 0:
+    while True:
+        time.sleep(0.05)
+'''
+
+
+def test_a_preempted_gang_resumes_in_preloaded_successors_on_the_new_port(tmp_path):
+    """Two coupled ranks, both preempted: each resumes in its own preloaded successor, which
+    takes the new incarnation's rendezvous port from its activation ("go port=N")."""
+    cloud = Cloud(provider="local",
+                  credentials=Credentials(node=NodeCredentials(state_root=str(tmp_path / "st"))))
+    spec = Task(environment=Environment(
+        script=GANG % {"python": sys.executable}, timeout=120,
+        variables=Variables({"TPI_TASK": "true", "TPI_PRELOAD": "1", "TPI_MAX_RESTARTS": "1"})),
+        parallelism=2)
+    task = backends.new(cloud, new_deterministic_identifier("preload-gang"), spec)
+    task.create()
+    try:
+        deadline = time.time() + 60
+        while time.time() < deadline and len([
+                e for e in task.events()
+                if e.code == "standby-start" and "preloaded" in e.description]) < 2:
+            time.sleep(0.1)
+        time.sleep(4.0)
+        task.preempt()
+        status = task.wait(60)
+    finally:
+        logs = "\n".join(task.logs())
+    assert status["succeeded"] == 2, (status, logs)
+    first = {l.split()[2]: l.split()[-1] for l in logs.splitlines() if "incarnation 0" in l}
+    second = [l for l in logs.splitlines() if "incarnation 1" in l]
+    assert len(first) == 2 and len(second) == 2, logs
+    for line in second:
+        words = line.split()
+        assert "torch-preloaded True" in line, line
+        assert words[-1] != first[words[2]], (line, first)  # a fresh rendezvous port
+    task.delete()
