@@ -63,8 +63,6 @@ log = logging.getLogger("tpi")
 BACKENDS = {"s3": "s3", "googlecloudstorage": "googlecloudstorage", "gcs": "googlecloudstorage",
             "azureblob": "azureblob"}
 SCHEMES = {"s3": "s3", "gs": "googlecloudstorage", "az": "azureblob"}
-SECRET_KEYS = ("secret_access_key", "session_token", "key", "sas_url",
-               "service_account_credentials", "token", "access_key_id")
 
 
 class ObjectStoreError(OSError):

@@ -9,8 +9,6 @@ import os
 import sys
 import time
 
-import pytest
-
 from terraform_provider_iterative_amd import backends
 from terraform_provider_iterative_amd.backends.node import shebang_python
 from terraform_provider_iterative_amd.models.cloud import Cloud, Credentials, NodeCredentials
