@@ -576,10 +576,16 @@ class HbmHandoff:
             src = np.frombuffer(bytes.fromhex(doc["segs"]), dtype=self.plan.segs.dtype).copy()
             if len(src) != len(self.plan.segs):
                 raise CheckpointError("HBM hand-off describes a different tensor set")
-            owner = np.full(len(src), -1, dtype=np.int64)  # mapped allocation of each segment
-            for i, w in enumerate(doc["where"]):
-                src[i]["ptr"] = 0 if w is None else bases[w[0]] + w[1]
-                owner[i] = -1 if w is None else w[0]
+            # each segment's mapped allocation and offset in it, as arrays (-1: none)
+            where = doc["where"]
+            owner = np.array([-1 if w is None else int(w[0]) for w in where], dtype=np.int64)
+            offs = np.array([0 if w is None else int(w[1]) for w in where], dtype=np.uint64)
+            if len(owner) != len(src):
+                raise CheckpointError("HBM hand-off: %d locations for %d segments"
+                                      % (len(owner), len(src)))
+            base_of = np.array([0 if b is None else b for b in bases] + [0], dtype=np.uint64)
+            src["ptr"] = np.where(owner < 0, np.uint64(0),
+                                  base_of[np.where(owner < 0, len(bases), owner)] + offs)
             dst = self.plan.segs
             if doc.get("pieces"):
                 src, dst, owner = _split_relocated(src, self.plan.segs, doc["pieces"], bases,
@@ -716,15 +722,18 @@ def _split_relocated(src: np.ndarray, dst: np.ndarray, pieces: Dict[str, List[Li
     tensors into blocks (:meth:`Checkpointer._relocate`): each such segment becomes one
     contiguous segment per block, the destination split at the same stream offsets.  Both
     stay sorted by stream offset, so the copy and its verification see the same stream.
-    ``owner`` (mapped allocation per segment) is expanded alongside."""
+    ``owner`` (mapped allocation per segment) is expanded alongside.  The segments between
+    relocated ones are carried over as whole slices."""
     out_src, out_dst, out_owner = [], [], []
-    for i in range(len(src)):
-        parts = pieces.get(str(i))
+    prev = 0
+    for i in sorted(int(k) for k in pieces):
+        parts = pieces[str(i)]
         if not parts:
-            out_src.append(src[i:i + 1])
-            out_dst.append(dst[i:i + 1])
-            out_owner.append(int(owner[i]))
             continue
+        out_src.append(src[prev:i])
+        out_dst.append(dst[prev:i])
+        out_owner.append(owner[prev:i])
+        prev = i + 1
         if int(dst[i]["kind"]) != SEG_CONTIG:
             raise CheckpointError("HBM hand-off: a relocated tensor is not contiguous here")
         if sum(int(p[2]) for p in parts) != int(src[i]["nbytes"]):
@@ -740,6 +749,10 @@ def _split_relocated(src: np.ndarray, dst: np.ndarray, pieces: Dict[str, List[Li
                 part["kind"], part["ndim"] = SEG_CONTIG, 0
             out_src.append(s_part)
             out_dst.append(d_part)
-            out_owner.append(int(alloc))
+            out_owner.append(np.array([alloc], np.int64))
             done += n
-    return np.concatenate(out_src), np.concatenate(out_dst), np.array(out_owner, np.int64)
+    out_src.append(src[prev:])
+    out_dst.append(dst[prev:])
+    out_owner.append(owner[prev:])
+    return (np.concatenate(out_src), np.concatenate(out_dst),
+            np.concatenate(out_owner).astype(np.int64))
