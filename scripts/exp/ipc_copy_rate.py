@@ -83,6 +83,11 @@ def main():
             child.stdin.flush()
             time.sleep(0.05)
         ck.restore_hbm()
+        print(json.dumps({"case": "ipc open", "threads": os.environ.get("TPI_IPC_OPEN_THREADS", "8"),
+                          "allocations": len(getattr(ck, "_last_bases", []) or []),
+                          "open_s": round(ck.hbm_open_s, 4),
+                          "steps": {k: round(v, 4) for k, v in ck.hbm_phases.items()}}),
+              flush=True)
         ck.engine.copy_segments = orig
         ck.wait_hbm_close()
         if saving:

@@ -538,8 +538,12 @@ class HbmHandoff:
                     with lock:
                         errors.append(error)
 
+            try:  # TPI_IPC_OPEN_THREADS: concurrent imports (driver calls)
+                nthreads = max(1, int(os.environ.get("TPI_IPC_OPEN_THREADS", "8")))
+            except ValueError:
+                nthreads = 8
             workers = [threading.Thread(target=worker, name="tpi-ipc-open", daemon=True)
-                       for _ in range(min(8, len(todo)))]
+                       for _ in range(min(nthreads, len(todo)))]
             if doc.get("socket"):
                 workers.append(threading.Thread(target=receiver, name="tpi-dmabuf-open",
                                                 daemon=True))
