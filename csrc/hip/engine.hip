@@ -200,6 +200,10 @@ struct tpi_pinner {
   int device = 0;
   std::atomic<uint64_t> touched{0}, ready{0};
   std::atomic<bool> failed{false}, stop{false};
+  // held: no window is registered until released (tpi_host_pin_hold) or a copy needs one
+  // (wait_pinned): a successor copying its predecessor's HBM keeps the GPU's page-table
+  // updates for 100 GB of host pages out of its IPC imports' way
+  std::atomic<bool> held{false};
   std::thread toucher, registrar;
   std::vector<uint8_t*> registered;
   std::string error;
@@ -283,6 +287,7 @@ namespace {
 
 // Wait until the pinner has registered `end` bytes of the region (false: pinning failed).
 bool wait_pinned(tpi_pinner* p, uint64_t end) {
+  p->held.store(false, std::memory_order_release);  // a copy needs the region: pin it now
   while (p->ready.load(std::memory_order_acquire) < end) {
     if (p->failed.load()) return false;
     std::this_thread::sleep_for(std::chrono::microseconds(100));
@@ -1425,7 +1430,8 @@ tpi_pinner* tpi_host_pin_start(void* base, uint64_t bytes, uint64_t window, int 
     (void)hipSetDevice(p->device);
     for (uint64_t w = 0; w < p->bytes && !p->stop.load(); w += p->window) {
       const uint64_t end = std::min(p->bytes, w + p->window);
-      while (p->touched.load(std::memory_order_acquire) < end && !p->stop.load())
+      while ((p->touched.load(std::memory_order_acquire) < end ||
+              p->held.load(std::memory_order_acquire)) && !p->stop.load())
         std::this_thread::sleep_for(std::chrono::microseconds(100));
       if (p->stop.load()) break;
       hipError_t err = hipHostRegister(p->base + w, end - w,
@@ -1443,10 +1449,16 @@ tpi_pinner* tpi_host_pin_start(void* base, uint64_t bytes, uint64_t window, int 
 }
 
 uint64_t tpi_host_pin_ready(const tpi_pinner* p) { return p->ready.load(); }
+
+int tpi_host_pin_hold(tpi_pinner* p, int hold) {
+  p->held.store(hold != 0, std::memory_order_release);
+  return 0;
+}
 uint64_t tpi_host_pin_window(const tpi_pinner* p) { return p->window; }
 
 // Wait for the whole region (0) or report the pinning error (-1).
 int tpi_host_pin_wait(tpi_pinner* p) {
+  p->held.store(false, std::memory_order_release);
   if (p->toucher.joinable()) p->toucher.join();
   if (p->registrar.joinable()) p->registrar.join();
   if (p->failed.load()) return fail(p->error);

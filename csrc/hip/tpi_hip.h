@@ -164,6 +164,8 @@ int tpi_host_register_ro(void* ptr, uint64_t bytes);
 typedef struct tpi_pinner tpi_pinner;
 tpi_pinner* tpi_host_pin_start(void* base, uint64_t bytes, uint64_t window, int threads);
 uint64_t tpi_host_pin_ready(const tpi_pinner* p);
+// hold != 0: register no further window until released, or until a copy waits for one
+int tpi_host_pin_hold(tpi_pinner* p, int hold);
 uint64_t tpi_host_pin_window(const tpi_pinner* p);
 int tpi_host_pin_wait(tpi_pinner* p);
 int tpi_host_pin_release(tpi_pinner* p);

@@ -397,6 +397,16 @@ class HbmHandoff:
                 pass
 
     def restore_hbm(self, strict: bool = True) -> TransferResult:
+        """See :meth:`_restore_hbm`; the host region's pinning, held while the hand-off runs
+        (:func:`host.prefetch`), resumes when it ends, however it ends."""
+        try:
+            return self._restore_hbm(strict)
+        finally:
+            region = getattr(self, "region", None)
+            if region is not None and getattr(region, "pinner", None):
+                hip().tpi_host_pin_hold(region.pinner, 0)
+
+    def _restore_hbm(self, strict: bool = True) -> TransferResult:
         """Copy the state of a preempted predecessor on the same GPU straight from its HBM
         (its allocations mapped here over dma-buf, or HIP IPC for an ``ipc`` export; one
         fused copy pass + a read-back verify, every tile's digest checked) into the bound

@@ -226,6 +226,12 @@ def prefetch(path: str, device_index: Optional[int] = None, numa: bool = True,
         try:
             box["region"] = HostRegion(size, path, device=True, numa_node=node,
                                        progressive=True, window=window)
+            if os.path.exists(path + ".hbm") and box["region"].pinner:
+                # a live predecessor exported its HBM: the successor will copy from there, and
+                # registering 100 GB of host pages (GPU page-table updates) under its IPC
+                # imports slowed them 5-20x (profiles/round5/r5ad/).  Held until the hand-off
+                # is done (Checkpointer.restore_hbm) or a copy needs the region.
+                hip().tpi_host_pin_hold(box["region"].pinner, 1)
         except Exception as error:  # surfaced as "not adopted"; the caller maps itself
             box["error"] = error
         _prefetched[path] = (None, box)
@@ -274,6 +280,7 @@ def wait_pinned(path: str, timeout: float = 600.0, cancel: Optional[threading.Ev
     pinner = region.pinner
     if pinner:
         lib = hip()
+        lib.tpi_host_pin_hold(pinner, 0)  # someone waits for it: no longer held
         while lib.tpi_host_pin_ready(pinner) < region.size:
             if (cancel is not None and cancel.is_set()) or time.monotonic() - t0 > timeout:
                 return None

@@ -131,6 +131,7 @@ class HipLib:
             "tpi_d2h": (i32, [vp, vp, vp, u64]),
             "tpi_host_pin_start": (vp, [vp, u64, u64, i32]),
             "tpi_host_pin_ready": (u64, [vp]),
+            "tpi_host_pin_hold": (i32, [vp, i32]),
             "tpi_host_pin_window": (u64, [vp]),
             "tpi_host_pin_wait": (i32, [vp]),
             "tpi_host_pin_release": (i32, [vp]),

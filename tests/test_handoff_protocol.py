@@ -479,6 +479,7 @@ def test_a_stuck_ipc_import_gives_up_the_hbm_route_and_the_claim(tmp_path, monke
         device_index = 0
         plan = types.SimpleNamespace(segs=np.zeros(0, dtype=SEG_DTYPE))
         restore_hbm = Checkpointer.restore_hbm
+        _restore_hbm = Checkpointer._restore_hbm
 
         def _hbm_doc(self):
             return {"allocations": [1 << 20] * 3, "ipc": {"0": "01", "1": "02", "2": "03"},
@@ -714,6 +715,7 @@ def test_dmabuf_route_hands_every_allocation_over_the_socket(tmp_path, monkeypat
         engine = Engine()
         plan = Plan
         restore_hbm = Checkpointer.restore_hbm
+        _restore_hbm = Checkpointer._restore_hbm
 
         def _hbm_doc(self):
             return doc
@@ -856,6 +858,7 @@ def test_auto_route_relocates_tensors_of_big_allocations(tmp_path, monkeypatch):
         engine = Engine()
         plan = DstPlan
         restore_hbm = Checkpointer.restore_hbm
+        _restore_hbm = Checkpointer._restore_hbm
 
         def _hbm_doc(self):
             return doc
