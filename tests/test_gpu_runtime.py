@@ -187,6 +187,31 @@ def test_prefetched_spill_region_is_adopted(tmp_path):
     assert not prefetch(str(tmp_path / "missing"))
 
 
+def test_prefetch_holds_pinning_while_an_hbm_hand_off_is_offered(tmp_path):
+    """A spill with an HBM hand-off next to it (``<spill>.hbm``): the prefetched region is
+    mapped but not registered (GPU page-table updates would slow the successor's IPC
+    imports), until a copy needs it -- here the restore -- which releases the hold."""
+    from terraform_provider_iterative_amd.checkpoint import Checkpointer, host, prefetch
+
+    spill = str(tmp_path / "spill")
+    src = {"w": torch.randn(8 << 20, device="cuda")}
+    ref = {k: v.clone() for k, v in src.items()}
+    with Checkpointer(src, path=spill) as ck:
+        ck.save({"step": 1})
+    open(spill + ".hbm", "w").write("{}")  # an offer (its content is not read here)
+    assert prefetch(spill, window=2 << 20)
+    region = host._prefetched[spill][1]["region"]
+    time.sleep(1.0)  # touching finished long ago; registration waits for the release
+    assert ops.hip().tpi_host_pin_ready(region.pinner) == 0
+    os.remove(spill + ".hbm")
+    dst = {k: torch.zeros_like(v) for k, v in ref.items()}
+    with Checkpointer(dst, path=spill) as ck2:
+        assert ck2.restore().bad_tiles == 0  # its copies wait for their windows: released
+        torch.cuda.synchronize()
+        assert ops.hip().tpi_host_pin_ready(ck2.region.pinner) > 0
+    assert torch.equal(dst["w"], ref["w"])
+
+
 @pytest.mark.parametrize("codec", ["none", "tpz1"])
 def test_progressively_pinned_region_restores_across_windows(tmp_path, codec):
     # 2 MiB registration windows: chunks (1 MiB tiles, 3 MiB chunks) and compressed blobs
