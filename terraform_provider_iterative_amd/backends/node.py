@@ -128,8 +128,9 @@ def _free_port(start: int) -> int:
 
 
 def shebang_python(script: str):
-    """``(interpreter, flags)`` when ``script``'s ``#!`` line runs this Python interpreter
-    (``#!/path/python [-u ...]`` or ``#!/usr/bin/env python3 [...]``), else None."""
+    """``(interpreter, flags)`` when ``script``'s ``#!`` line runs this Python interpreter's
+    binary (``#!/path/python [-u ...]`` or ``#!/usr/bin/env python3 [...]``; a virtualenv's
+    link to it included, and kept as the interpreter to launch), else None."""
     import shutil
 
     first = (script or "").split("\n", 1)[0]
@@ -155,7 +156,9 @@ def shebang_python(script: str):
     flags = words[1:]
     if not same or any(not f.startswith("-") or f in ("-c", "-m") for f in flags):
         return None
-    return sys.executable, flags
+    # launched as the script names it: a virtualenv's interpreter is a link to the same binary
+    # but brings its own site-packages (pyvenv.cfg next to the link)
+    return words[0], flags
 
 class NodeTask(Task):
     """Task on this node; ``provider`` selects CPU-only or GPU placement."""

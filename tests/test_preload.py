@@ -29,9 +29,19 @@ def test_only_scripts_of_this_interpreter_are_preloaded():
 
     found = shutil.which(os.path.basename(exe))
     if found and os.path.realpath(found) == os.path.realpath(exe):
-        assert env_form == (exe, [])
+        assert env_form == (found, [])
     else:
         assert env_form is None
+
+
+def test_a_virtualenv_interpreter_is_launched_as_named(tmp_path):
+    """A venv's python is a link to the same binary; the preloaded successor must start it by
+    that path, or the venv's site-packages would be missing."""
+    venv = tmp_path / "venv" / "bin"
+    venv.mkdir(parents=True)
+    link = venv / "python3"
+    link.symlink_to(os.path.realpath(sys.executable))
+    assert shebang_python("#!%s\n" % link) == (str(link), [])
 
 
 SCRIPT = r'''#!%(python)s
