@@ -169,8 +169,8 @@ class _Http:
                 sign: Callable[[], Dict[str, str]], body: bytes = b"",
                 ok: Tuple[int, ...] = (200, 201, 204, 206)) -> Tuple[int, Dict[str, str], bytes]:
         """One request; returns (status, lowercase headers, body).  Statuses outside ``ok``
-        (after retries) raise :class:`ObjectStoreError`, except 404 (returned: callers decide
-        whether a missing object is an error)."""
+        (after retries) raise :class:`ObjectStoreError`, except a 404 of a read or a delete
+        (returned: callers decide whether a missing object is an error)."""
         url = path + ("?" + query if query else "")
         delay = 0.2
         for attempt in range(self.RETRIES):
@@ -190,7 +190,10 @@ class _Http:
                 time.sleep(delay)
                 delay *= 2
                 continue
-            if r.status in ok or r.status == 404 or r.status == 308:
+            # a missing object is the caller's call on reads and deletes; a write that finds no
+            # bucket / container / upload session has failed
+            if r.status in ok or r.status == 308 or (
+                    r.status == 404 and method in ("GET", "HEAD", "DELETE")):
                 return r.status, hdrs, data
             if (r.status >= 500 or r.status == 429) and attempt < self.RETRIES - 1:
                 time.sleep(delay)

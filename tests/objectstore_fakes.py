@@ -41,6 +41,7 @@ class Store:
         self.fail_next = 0
         self.requests = []    # (service, method, path)
         self.auth_failures = 0
+        self.missing_prefix = None  # writes into buckets with this name prefix: 404
         self.pubkey = None    # GCS: PEM of the service account's public key
         self.sa_email = ""
 
@@ -112,6 +113,9 @@ class Handler(BaseHTTPRequestHandler):
             if st.fail_next > 0:
                 st.fail_next -= 1
                 return self._reply(503, b"try again")
+        if st.missing_prefix and self.command in ("PUT", "POST") and u.path != "/token" and \
+                ("/" + st.missing_prefix) in u.path:
+            return self._reply(404, b"<Error><Code>NoSuchBucket</Code></Error>")
         if u.path.startswith("/s3/"):
             return self._s3(u, body)
         if u.path.startswith("/" + AZ_ACCOUNT + "/"):

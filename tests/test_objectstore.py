@@ -346,3 +346,16 @@ def test_checkpoint_persists_straight_into_a_bucket_and_loads_back(tmp_path, fak
         res = ck2.load(url)
         assert res.bad_tiles == 0 and ck2.header()["metadata"] == {"step": 7}
     assert torch.equal(state2["w"], state["w"])
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_a_write_into_a_missing_bucket_fails(tmp_path, fake, backend, monkeypatch):
+    """A write that finds no bucket must fail, not pass silently (the fake answers 404 for
+    every write into a bucket whose name starts with "missing")."""
+    r = remote.open_remote(remote.parse("%s://missing-b" % SCHEME[backend], "",
+                                        fake.options(backend)))
+    f = tmp_path / "f.txt"
+    f.write_text("x")
+    fake.store.missing_prefix = "missing"
+    with pytest.raises(objectstore.ObjectStoreError):
+        r.put_file(str(f), "f.txt")
