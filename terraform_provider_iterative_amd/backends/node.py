@@ -160,6 +160,44 @@ def shebang_python(script: str):
     # but brings its own site-packages (pyvenv.cfg next to the link)
     return words[0], flags
 
+
+_SHELLS = ("sh", "bash", "dash", "zsh")
+_SHELL_META = set("$`|&;<>*?(){}[]!~\\\"'")
+
+
+def shell_python_command(script: str):
+    """``(interpreter, flags, [file.py, args...])`` when ``script`` is a shell script whose
+    one command runs a Python file with this interpreter (``python3 train.py --lr 1e-4``,
+    optionally ``exec``, after ``set -e``-style lines): the common form of the reference's task
+    scripts, which a preloaded successor can run without the shell.  Anything else -- more
+    commands, variables, redirections, globs, quoting -- is None."""
+    import shlex
+
+    lines = (script or "").splitlines()
+    if not lines or not lines[0].startswith("#!"):
+        return None
+    words = lines[0][2:].split()
+    if not words:
+        return None
+    shell = os.path.basename(words[-1] if os.path.basename(words[0]) == "env" else words[0])
+    if shell not in _SHELLS:
+        return None
+    commands = [l.strip() for l in lines[1:]
+                if l.strip() and not l.strip().startswith("#")
+                and not l.strip().startswith("set ")]
+    if len(commands) != 1 or any(c in _SHELL_META for c in commands[0]):
+        return None
+    argv = shlex.split(commands[0])
+    if argv and argv[0] == "exec":
+        argv = argv[1:]
+    if len(argv) < 2 or not argv[1].endswith(".py"):
+        return None
+    found = shebang_python("#!%s\n" % argv[0]) if os.path.isabs(argv[0]) else \
+        shebang_python("#!/usr/bin/env %s\n" % argv[0])
+    if found is None:
+        return None
+    return found[0], found[1], argv[1:]
+
 class NodeTask(Task):
     """Task on this node; ``provider`` selects CPU-only or GPU placement."""
 
@@ -462,14 +500,19 @@ class NodeTask(Task):
             return []
         if knob("TPI_WARM_STANDBY", "1") == "hot":
             return []
-        interp = shebang_python(self.spec.environment.script)
+        script = self.spec.environment.script
+        interp = shebang_python(script)
+        target = None  # None: the task script itself (the supervisor appends its path)
         if interp is None:
-            return []
+            found = shell_python_command(script)
+            if found is None:
+                return []
+            interp, target = found[:2], found[2]
         path, flags = interp
         # TPI_PRELOAD=gpu: the parked process also initialises the GPU and prewarms an engine
         code = ("import sys; sys.path.insert(0, %r); "
-                "from terraform_provider_iterative_amd.runtime.preload import main; main(gpu=%r)"
-                % (ROOT, mode == "gpu"))
+                "from terraform_provider_iterative_amd.runtime.preload import main; "
+                "main(%r, gpu=%r)" % (ROOT, target, mode == "gpu"))
         return [path] + flags + ["-c", code]
 
     def _remote_sync(self, knob) -> Optional[Dict]:

@@ -55,7 +55,10 @@ def _warm_gpu() -> None:
 
 
 def main(argv=None, gpu: bool = False) -> None:
-    argv = list(sys.argv[1:] if argv is None else argv)
+    """``argv``: ``[file.py, args...]`` to run (a shell script's one ``python file.py ...``
+    command, :func:`backends.node.shell_python_command`); None: the script path the
+    supervisor appends to the command line."""
+    argv = list(sys.argv[1:2] if argv is None else argv)
     if not argv:
         raise SystemExit("usage: preload <script> [args...]")
     added = sys.path[0] if sys.path else None  # the package root the launcher put first

@@ -178,3 +178,55 @@ def test_a_preempted_gang_resumes_in_preloaded_successors_on_the_new_port(tmp_pa
         assert "torch-preloaded True" in line, line
         assert words[-1] != first[words[2]], (line, first)  # a fresh rendezvous port
     task.delete()
+
+
+def test_shell_scripts_that_run_one_python_file_are_preloaded():
+    from terraform_provider_iterative_amd.backends.node import shell_python_command
+
+    exe = sys.executable
+    assert shell_python_command("#!/bin/bash\nset -e\n%s train.py --lr 1e-4\n" % exe) == \
+        (exe, [], ["train.py", "--lr", "1e-4"])
+    assert shell_python_command("#!/bin/sh\n# run it\nexec %s -u x.py\n" % exe) is None  # -u
+    for script in ("#!/bin/bash\npip install -r r.txt\n%s train.py\n" % exe,  # two commands
+                   "#!/bin/bash\n%s train.py > log\n" % exe,                   # redirection
+                   "#!/bin/bash\n%s train.py $ARGS\n" % exe,                   # expansion
+                   "#!/bin/bash\n%s -m pkg.train\n" % exe,                     # a module
+                   "#!/bin/bash\n/nonexistent/python3 train.py\n",             # another python
+                   "#!/usr/bin/env python3\nprint(1)\n"):                      # not a shell
+        assert shell_python_command(script) is None, script
+
+
+WRAPPED = r'''import os, sys, time
+restart = int(os.environ["TPI_RESTART_COUNT"])
+print("incarnation %d torch-preloaded %s argv %s" % (restart, "torch" in sys.modules,
+                                                     " ".join(sys.argv[1:])), flush=True)
+if restart == 0:
+    while True:
+        time.sleep(0.05)
+'''
+
+
+def test_a_shell_wrapped_python_rank_resumes_in_a_preloaded_successor(tmp_path):
+    work = tmp_path / "work"
+    work.mkdir()
+    (work / "train.py").write_text(WRAPPED)
+    cloud = Cloud(provider="local",
+                  credentials=Credentials(node=NodeCredentials(state_root=str(tmp_path / "st"))))
+    spec = Task(environment=Environment(
+        script="#!/bin/bash\nset -e\nexec %s train.py --epochs 3\n" % sys.executable,
+        timeout=120, directory=str(work),
+        variables=Variables({"TPI_TASK": "true", "TPI_PRELOAD": "1", "TPI_MAX_RESTARTS": "1"})))
+    task = backends.new(cloud, new_deterministic_identifier("preload-sh"), spec)
+    task.create()
+    try:
+        _wait_event(task, lambda e: e.code == "standby-start" and "preloaded" in e.description,
+                    60)
+        time.sleep(4.0)
+        task.preempt()
+        status = task.wait(60)
+    finally:
+        logs = "\n".join(task.logs())
+    assert status["succeeded"] == 1, (status, logs)
+    assert "incarnation 0 torch-preloaded False argv --epochs 3" in logs, logs
+    assert "incarnation 1 torch-preloaded True argv --epochs 3" in logs, logs
+    task.delete()
