@@ -584,8 +584,15 @@ class S3Remote(ObjectRemote):
             body = "<CompleteMultipartUpload>%s</CompleteMultipartUpload>" % "".join(
                 "<Part><PartNumber>%d</PartNumber><ETag>%s</ETag></Part>" % (i + 1, e)
                 for i, e in enumerate(etags))
-            _, _, data = self._request("POST", key, {"uploadId": upload_id}, body=body.encode())
-            self._check_xml_error(data, "complete multipart upload")
+            try:
+                _, _, data = self._request("POST", key, {"uploadId": upload_id},
+                                           body=body.encode())
+                self._check_xml_error(data, "complete multipart upload")
+            except ObjectStoreError:
+                # a completion retried after a lost reply finds its upload gone (NoSuchUpload):
+                # the object is there if the first attempt went through
+                if self._head(key) != size:
+                    raise
         except BaseException:
             try:
                 self._request("DELETE", key, {"uploadId": upload_id})
