@@ -230,3 +230,21 @@ def test_a_shell_wrapped_python_rank_resumes_in_a_preloaded_successor(tmp_path):
     assert "incarnation 0 torch-preloaded False argv --epochs 3" in logs, logs
     assert "incarnation 1 torch-preloaded True argv --epochs 3" in logs, logs
     task.delete()
+
+
+def test_an_unused_preloaded_successor_leaves_no_log(tmp_path):
+    """The rank finishes normally: its parked successor is discarded without having run, and
+    `leo read` shows the rank's log only (no empty machine log)."""
+    cloud = Cloud(provider="local",
+                  credentials=Credentials(node=NodeCredentials(state_root=str(tmp_path / "st"))))
+    spec = Task(environment=Environment(
+        script="#!%s\nimport time\nprint('working', flush=True)\ntime.sleep(5)\n" % sys.executable,
+        timeout=60, variables=Variables({"TPI_TASK": "true", "TPI_PRELOAD": "1"})))
+    task = backends.new(cloud, new_deterministic_identifier("preload-unused"), spec)
+    task.create()
+    assert task.wait(60)["succeeded"] == 1
+    codes = [e.code for e in task.events()]
+    assert "standby-start" in codes and "standby-discarded" in codes, codes
+    logs = task.logs()
+    assert len(logs) == 1 and "working" in logs[0], logs
+    task.delete()
