@@ -153,6 +153,9 @@ def main():
     p.add_argument("--preload-gpu", action="store_true",
                    help="TPI_PRELOAD=gpu: the preloaded successor has also initialised the GPU "
                         "and prewarmed a checkpoint engine")
+    p.add_argument("--preload-gpu-lite", action="store_true",
+                   help="TPI_PRELOAD=gpu-lite: the preloaded successor has initialised the GPU "
+                        "(context, first queue) but made no engine")
     p.add_argument("--no-preload", action="store_true",
                    help="TPI_PRELOAD=0: the successor is a fresh process")
     p.add_argument("--no-stream", action="store_true",
@@ -200,10 +203,11 @@ def main():
                      "extra": [float(x) for x in args.extra_gib.split(",") if x.strip()]}
     # the ranks' runtime knobs travel as task variables (the rank environment is the task's)
     rank_env = {"TPI_TASK": "true", "TPI_STREAM_HANDOFF": "0" if args.no_stream else "1"}
-    if args.preload or args.no_preload or args.preload_gpu:
-        rank_env["TPI_PRELOAD"] = "0" if args.no_preload else ("gpu" if args.preload_gpu else "1")
+    if args.preload or args.no_preload or args.preload_gpu or args.preload_gpu_lite:
+        rank_env["TPI_PRELOAD"] = "0" if args.no_preload else (
+            "gpu" if args.preload_gpu else ("gpu-lite" if args.preload_gpu_lite else "1"))
     preload = (not args.no_preload and not args.hot and
-               (args.preload or args.preload_gpu or
+               (args.preload or args.preload_gpu or args.preload_gpu_lite or
                 os.environ.get("TPI_PRELOAD", "1") not in ("0", "false", "no")))
     for knob in ("TPI_D2H_ENGINE", "TPI_STREAM_TIMEOUT", "TPI_LINGER_SECONDS",
                  "TPI_HBM_HANDOFF", "TPI_RELEASE_HBM", "TPI_EXPLICIT_TEARDOWN",

@@ -26,7 +26,7 @@ import torch  # noqa: E402,F401
 from terraform_provider_iterative_amd.runtime.preload import _warm_gpu  # noqa: E402
 
 t = time.perf_counter()
-_warm_gpu()
+_warm_gpu(engine=os.environ.get("FOOTPRINT_LITE") is None)
 took = time.perf_counter() - t
 time.sleep(0.5)
 after = used()

@@ -496,7 +496,7 @@ class NodeTask(Task):
         interpreter flags are kept), since the successor runs it in-process; off with a hot
         standby (``TPI_WARM_STANDBY=hot``), whose parked successor has the GPU initialised."""
         mode = knob("TPI_PRELOAD", "1")
-        if mode not in ("1", "true", "yes", "gpu"):
+        if mode not in ("1", "true", "yes", "gpu", "gpu-lite"):
             return []
         if knob("TPI_WARM_STANDBY", "1") == "hot":
             return []
@@ -512,7 +512,7 @@ class NodeTask(Task):
         # TPI_PRELOAD=gpu: the parked process also initialises the GPU and prewarms an engine
         code = ("import sys; sys.path.insert(0, %r); "
                 "from terraform_provider_iterative_amd.runtime.preload import main; "
-                "main(%r, gpu=%r)" % (ROOT, target, mode == "gpu"))
+                "main(%r, gpu=%r)" % (ROOT, target, {"gpu": True, "gpu-lite": "lite"}.get(mode, False)))
         return [path] + flags + ["-c", code]
 
     def _remote_sync(self, knob) -> Optional[Dict]:

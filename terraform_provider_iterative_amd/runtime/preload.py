@@ -39,22 +39,25 @@ def _read_go(fd: int) -> str:
     return data.decode(errors="replace").strip()
 
 
-def _warm_gpu() -> None:
+def _warm_gpu(engine: bool = True) -> None:
     """``TPI_PRELOAD=gpu``: also initialise the GPU and prewarm a checkpoint engine, as a hot
-    standby does (the successor's Checkpointer takes the engine).  Costs the parked process a
-    GPU context and the engine's staging buffers for the life of the rank."""
+    standby does (the successor's Checkpointer takes the engine); 2.7 GB of HBM held for the
+    life of the rank (``profiles/round5/r5ah/``).  ``gpu-lite`` (``engine=False``): the GPU
+    context and the process's first hardware queue only (~137 ms of a successor's start,
+    ``profiles/round5/r5z/``); the engine is made after the activation."""
     import torch
 
-    from terraform_provider_iterative_amd.checkpoint import prewarm_engine
-
     torch.cuda.init()
-    device = torch.cuda.current_device()
     torch.empty(1 << 20, dtype=torch.uint8, device="cuda")  # context + caching allocator
-    prewarm_engine(device)
+    torch.ones(1, device="cuda").add_(1)  # a launch: the first hardware queue and code object
+    if engine:
+        from terraform_provider_iterative_amd.checkpoint import prewarm_engine
+
+        prewarm_engine(torch.cuda.current_device())
     torch.cuda.synchronize()
 
 
-def main(argv=None, gpu: bool = False) -> None:
+def main(argv=None, gpu=False) -> None:
     """``argv``: ``[file.py, args...]`` to run (a shell script's one ``python file.py ...``
     command, :func:`backends.node.shell_python_command`); None: the script path the
     supervisor appends to the command line."""
@@ -69,7 +72,7 @@ def main(argv=None, gpu: bool = False) -> None:
     from terraform_provider_iterative_amd.checkpoint import preemption  # noqa: F401
     if gpu:
         try:
-            _warm_gpu()
+            _warm_gpu(engine=gpu != "lite")
         except Exception as error:  # the successor initialises it itself
             print("tpi-preload: GPU warm-up failed: %s" % error, file=sys.stderr, flush=True)
     preloaded_s = time.time() - t0
