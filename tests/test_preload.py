@@ -119,6 +119,9 @@ def test_preload_is_on_by_default_and_off_on_request(tmp_path, monkeypatch):
     argv = argv_for(python_script)
     assert argv[0] == sys.executable and argv[1] == "-c" and "runtime.preload" in argv[2]
     assert argv_for(python_script, TPI_PRELOAD="0") == []
+    assert "gpu=True" in argv_for(python_script, TPI_PRELOAD="gpu")[2]
+    assert "gpu='lite'" in argv_for(python_script, TPI_PRELOAD="gpu-lite")[2]
+    assert "gpu=False" in argv[2]
     assert argv_for(python_script, TPI_WARM_STANDBY="hot") == []  # its own parked successor
     assert argv_for("#!/bin/sh\necho hi\n") == []
 
