@@ -359,3 +359,19 @@ def test_a_write_into_a_missing_bucket_fails(tmp_path, fake, backend, monkeypatc
     fake.store.missing_prefix = "missing"
     with pytest.raises(objectstore.ObjectStoreError):
         r.put_file(str(f), "f.txt")
+
+
+def test_aws_addressing_without_an_endpoint(monkeypatch):
+    """No endpoint: virtual-hosted AWS requests (bucket in the host name); a dotted bucket
+    name (which the wildcard certificate does not cover) goes path-style instead."""
+    for k in ("TPI_S3_ENDPOINT", "AWS_REGION", "AWS_DEFAULT_REGION"):
+        monkeypatch.delenv(k, raising=False)
+    r = remote.open_remote(remote.parse("s3://my-bucket/p", "", {"region": "eu-west-1"}))
+    assert (r.http.netloc, r.prefix_path, r.http.https) == \
+        ("my-bucket.s3.eu-west-1.amazonaws.com", "", True)
+    r = remote.open_remote(remote.parse("s3://my.dotted.bucket/p"))
+    assert (r.http.netloc, r.prefix_path) == ("s3.us-east-1.amazonaws.com", "/my.dotted.bucket")
+    az = remote.open_remote(remote.parse("az://ctr/p", "", {"account": "acct", "key": "a2V5"}))
+    assert (az.http.netloc, az.prefix_path) == ("acct.blob.core.windows.net", "/ctr")
+    gs = remote.open_remote(remote.parse("gs://gb/p", "", {"token": "t"}))
+    assert gs.http.netloc == "storage.googleapis.com" and gs.obj_path == "/storage/v1/b/gb/o"
