@@ -59,10 +59,7 @@ from ..ops import native
 
 log = logging.getLogger("tpi")
 
-# rclone backend name -> canonical name; URL scheme -> canonical name
-BACKENDS = {"s3": "s3", "googlecloudstorage": "googlecloudstorage", "gcs": "googlecloudstorage",
-            "azureblob": "azureblob"}
-SCHEMES = {"s3": "s3", "gs": "googlecloudstorage", "az": "azureblob"}
+from .objectnames import BACKENDS, SCHEMES, describe, is_object_store, parse  # noqa: F401
 
 
 class ObjectStoreError(OSError):
@@ -75,50 +72,6 @@ def _threads() -> int:
 
 def _part_bytes() -> int:
     return max(1, int(os.environ.get("TPI_OBJECT_PART_MB", "64"))) << 20
-
-
-# -- connection strings --------------------------------------------------------------------------
-
-def parse(container: str, path: str = "", opts: Optional[Dict[str, str]] = None
-          ) -> Optional[Connection]:
-    """The object-store :class:`Connection` named by a ``storage.container`` value (None: not
-    an object store).  ``container`` = bucket, ``path`` = key prefix (no leading ``/``)."""
-    conn = None
-    m = re.match(r"^(s3|gs|az)://([^/]+)(/.*)?$", container or "")
-    if m:
-        conn = Connection(SCHEMES[m.group(1)], m.group(2), (m.group(3) or "").strip("/"), {})
-    elif (container or "").startswith(":"):
-        parsed = Connection.parse(container)
-        if parsed.backend in BACKENDS:
-            bucket, _, prefix = parsed.container.strip("/").partition("/")
-            conn = Connection(BACKENDS[parsed.backend], bucket, prefix.strip("/"),
-                              dict(parsed.config))
-    if conn is None or not conn.container:
-        return None
-    for key, value in (opts or {}).items():
-        if key != "root" and value is not None and str(value) != "":
-            conn.config[str(key)] = str(value)
-    if path:
-        conn.path = posixpath.join(conn.path, path.strip("/")) if conn.path else path.strip("/")
-    conn.path = posixpath.normpath(conn.path).lstrip("/") if conn.path else ""
-    if conn.path == ".":
-        conn.path = ""
-    return conn
-
-
-def is_object_store(value: str) -> bool:
-    if not value:
-        return False
-    if re.match(r"^(s3|gs|az)://[^/]+", value):
-        return True
-    return value.startswith(tuple(":%s%s" % (b, sep) for b in BACKENDS for sep in (",", ":")))
-
-
-def describe(conn: Connection) -> str:
-    """``backend://bucket/prefix`` -- a connection without its secrets, for logs and events."""
-    scheme = {v: k for k, v in SCHEMES.items()}.get(conn.backend, conn.backend)
-    return "%s://%s/%s" % (scheme, conn.container, conn.path) if conn.path else \
-        "%s://%s" % (scheme, conn.container)
 
 
 def open_remote(conn: Connection) -> "ObjectRemote":

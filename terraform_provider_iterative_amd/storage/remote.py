@@ -39,7 +39,7 @@ import tempfile
 import threading
 from typing import Dict, Iterable, List, Optional, Tuple
 
-from . import objectstore
+from . import objectnames
 from .transfer import Connection, make_filter, transfer_rules
 from ..ops import native
 
@@ -59,7 +59,7 @@ def parse(container: str, path: str = "", opts: Optional[Dict[str, str]] = None
     and a ``root`` that a relative directory is taken under.  Object-store containers
     (``s3://``, ``gs://``, ``az://`` and rclone's forms) parse to their own connections
     (:mod:`storage.objectstore`)."""
-    obj = objectstore.parse(container, path, opts)
+    obj = objectnames.parse(container, path, opts)
     if obj is not None:
         return obj
     opts = dict(opts or {})
@@ -104,7 +104,7 @@ def is_remote(value: str) -> bool:
     """Does ``value`` (a container or a file path) name a location on another node?"""
     if not value:
         return False
-    if objectstore.is_object_store(value):
+    if objectnames.is_object_store(value):
         return True
     if value.startswith("ssh://"):
         return bool(_URL.match(value))
@@ -305,12 +305,14 @@ def open_remote(conn: Connection):
     (:func:`storage.objectstore.open_remote`) -- the same interface."""
     if conn.backend in BACKENDS:
         return SSHRemote(conn)
+    from . import objectstore  # the HTTP clients: only for a task that names an object store
+
     return objectstore.open_remote(conn)
 
 
 def describe(conn: Connection) -> str:
     """A container for logs and events (an object store's credentials left out)."""
-    return str(conn) if conn.backend in BACKENDS else objectstore.describe(conn)
+    return str(conn) if conn.backend in BACKENDS else objectnames.describe(conn)
 
 
 def split_file(location: str) -> Tuple[SSHRemote, str]:
@@ -350,7 +352,7 @@ def store(local: str, location: str) -> int:
 def object_source(location: str):
     """``(remote, key)`` of an object-store file location, read in place by ranged requests
     (:meth:`ObjectRemote.read_into`); None for other locations (fetched whole)."""
-    if not objectstore.is_object_store(location):
+    if not objectnames.is_object_store(location):
         return None
     return split_file(location)
 
