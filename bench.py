@@ -148,7 +148,8 @@ E2E_KEYS = ("ok", "verified", "status", "signal_to_restored_s", "save_s",
             "rank_start_to_restored_s", "saved_to_restored_s", "signal_to_durable_s", "streamed",
             "warm_standby_activated", "hot_standby", "preload", "preloaded_wait_s",
             "standby_pinned_wait_s", "restore_journal",
-            "extra_tensors_gib", "delete_s", "rank_exit_to_settled_s", "vram_before_start",
+            "extra_tensors_gib", "delete_s", "rank_exit_to_settled_s", "gpu_drain",
+            "successor_hbm_wait", "hbm_failed",
             "memory_guard",
             "released_exit_pending_at_settle")
 

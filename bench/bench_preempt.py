@@ -231,11 +231,9 @@ def main():
               "step_seconds": args.step_seconds, "materialize": args.materialize,
               "extra_tensors_gib": [float(x) for x in args.extra_gib.split(",") if x.strip()]}
     os.environ["TPI_WARM_STANDBY"] = "hot" if args.hot else ("1" if args.standby else "0")
-    # processes of an earlier run may still be giving back their HBM: start from an empty GPU
-    from terraform_provider_iterative_amd.parallel.placement import discover, wait_vram_drained
-
-    gpus = discover()
-    result["vram_before_start"] = wait_vram_drained(gpus[0].pci) if gpus else {}
+    # No drain of our own here: memory that earlier runs (or bench.py itself) gave back is
+    # waited for by the product -- the task's start (placement.settle_gpus, "gpu-drain") and
+    # the successor's allocation gate (preemption.wait_for_device_memory, "successor-hbm-wait")
     try:
         task.create()
         deadline = time.time() + args.timeout
@@ -318,6 +316,11 @@ def main():
         if t_settled and t_exit:  # the successor's exit -> final sync + final state
             result["rank_exit_to_settled_s"] = round(t_settled - t_exit, 3)
         result["released_exit_pending_at_settle"] = first("rank-released-exit")[0] is None
+        # the product's own memory gates (no bench-side drain): the task's start on a GPU
+        # whose memory was still coming back, and each successor's allocation gate
+        result["gpu_drain"] = [d for c, _, d in events if c == "gpu-drain"]
+        result["successor_hbm_wait"] = [d for c, _, d in events if c == "successor-hbm-wait"]
+        result["hbm_failed"] = [d for c, _, d in events if c == "checkpoint-hbm-failed"]
         result["ok"] = bool(status.get("succeeded") == 1 and result["verified"])
     finally:
         try:

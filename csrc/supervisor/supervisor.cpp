@@ -1464,7 +1464,17 @@ class Supervisor {
       }
     stop_stager();
     int unlinked = 0, exiting = 0;
-    for (auto& l : s_.leases) unlinked += unlink(l.c_str()) == 0;
+    // A GPU lease becomes its drain marker (gpu-N.lease -> gpu-N.drain, same JSON, with the
+    // driver's VRAM count at the reservation): the next task placed on that GPU waits until
+    // the driver has taken this task's HBM back (placement.settle_gpus) -- released processes
+    // may still be exiting, and the driver wipes freed VRAM for seconds after that.
+    for (auto& l : s_.leases) {
+      static const std::string kLease = ".lease";
+      bool gpu = l.size() > kLease.size() &&
+                 l.compare(l.size() - kLease.size(), kLease.size(), kLease) == 0;
+      std::string drain = gpu ? l.substr(0, l.size() - kLease.size()) + ".drain" : "";
+      unlinked += (gpu ? rename(l.c_str(), drain.c_str()) : unlink(l.c_str())) == 0;
+    }
     for (auto& d : detached_) exiting += d.pid > 0;
     event("resources-released", {std::to_string(unlinked) + " lease file(s)",
                                  std::to_string(exiting) + " released process(es) still exiting"});

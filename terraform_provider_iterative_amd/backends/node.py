@@ -796,6 +796,7 @@ class NodeTask(Task):
             return
         spec = self._spec_json()
         spec["restart_base"] = restart_base
+        self._settle_gpus(spec)
         spec_path = os.path.join(self.sup_dir, "spec.json")
         _write_json(spec_path, spec)
         # TPI_SUPERVISOR_BIN: an alternative build (e.g. the ASan/UBSan one of the tests)
@@ -815,6 +816,23 @@ class NodeTask(Task):
                 self.sup_dir, "supervisor.log"))
         pid = int(out.decode().strip() or 0)
         self._event("started", "supervisor pid %d" % pid)
+
+    def _settle_gpus(self, spec: Dict) -> None:
+        """A GPU handed over from another holder is used only once the driver has its memory
+        back (:meth:`Placement.settle_gpus`); each wait is journalled (``gpu-drain``)."""
+        gpus = [int(g) for g in str(spec["env"].get("TPI_VISIBLE_GPUS", "")).split(",") if g]
+        if not gpus:
+            return
+        for rec in self.placement.settle_gpus(gpus):
+            desc = ["gpu %d" % rec["gpu"], "waited %.3f s" % rec["waited_s"],
+                    "VRAM in use %.1f -> %.1f GB" % (rec["used_gb_at_start"], rec["used_gb"])]
+            if rec["previous"]:
+                desc.append("previous holder %s" % rec["previous"])
+            if rec["target_gb"] is not None:
+                desc.append("target %.1f GB" % rec["target_gb"])
+            if rec["timed_out"]:
+                desc.append("timed out (TPI_GPU_DRAIN_TIMEOUT): starting anyway")
+            self._event("gpu-drain", *desc)
 
     def stop(self, wait: float = 60.0) -> None:
         state = self._state()

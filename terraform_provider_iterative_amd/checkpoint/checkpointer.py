@@ -103,6 +103,17 @@ def streaming_writer(path: str) -> Optional[Dict[str, int]]:
     return None
 
 
+def region_total(path: str) -> Optional[int]:
+    """Bytes of device state the checkpoint region file ``path`` describes (its header's
+    ``total``), None when there is no readable header.  Reads the file only (no mapping)."""
+    try:
+        with open(path, "rb") as f:
+            head = f.read(PREAMBLE + Checkpointer.HEADER_RESERVE)
+        return int(Checkpointer.read_header(np.frombuffer(head, np.uint8))["total"])
+    except (OSError, ValueError, KeyError, CheckpointError):
+        return None
+
+
 def _local_scratch(remote_path: str) -> str:
     """Where a checkpoint bound for (or fetched from) another node is staged on this one:
     ``TPI_PERSIST_TMPDIR``, else the task directory, else the temp directory."""

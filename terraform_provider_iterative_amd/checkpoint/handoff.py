@@ -112,6 +112,20 @@ class HbmHandoff:
         pieces: Dict[str, List[List[int]]] = {}
         if big and route == "auto":
             pieces = self._relocate(raw_where, big)  # segment -> [[block base, 0, n], ...]
+        try:
+            return self._publish_hbm(manifest, lib, route, sizes, raw_where, big, pieces,
+                                     metadata)
+        except BaseException:
+            # nothing was published: the relocated copies would otherwise stay allocated
+            # through the whole save and the successor's allocation
+            self._free_relocated()
+            raise
+
+    def _publish_hbm(self, manifest: str, lib, route: str, sizes: Dict[int, int],
+                     raw_where: List[Optional[Tuple[int, int]]], big: set,
+                     pieces: Dict[str, List[List[int]]], metadata: Optional[Dict]) -> str:
+        """The second half of :meth:`export_hbm`: IPC handles (and dma-bufs) of every
+        allocation, then the manifest, written atomically."""
         # the allocations the successor maps, in order
         keys: List[int] = []
         index: Dict[int, int] = {}
@@ -140,7 +154,7 @@ class HbmHandoff:
                # the generation the save that follows this export will write
                "generation": self._target()[1]}
         handle = ctypes.create_string_buffer(64)
-        offset = ctypes.c_uint64(0)
+        offset, size = ctypes.c_uint64(0), ctypes.c_uint64(0)
         ipc: Dict[str, str] = {}
         dmabuf_set = set(as_dmabuf)
         for i, key in enumerate(keys):
@@ -436,11 +450,22 @@ class HbmHandoff:
         except ValueError:
             limit = 10.0
 
+        # Set (under ``gate``) once the hand-off has been given up or closed: an opener thread
+        # that returns from the driver after that closes its new mapping at once instead of
+        # recording it -- nothing would ever unmap it, and the predecessor has been told it may
+        # exit.
+        gate = threading.Lock()
+        given_up = [False]
+
         def open_ipc(i: int) -> None:
             base = ctypes.c_void_p()
             lib.check(lib.tpi_ipc_open(bytes.fromhex(ipc[i]), self.device_index,
                                        ctypes.byref(base)), "tpi_ipc_open")
-            bases[i] = mapped[i] = base.value
+            with gate:
+                if not given_up[0]:
+                    bases[i] = mapped[i] = base.value
+                    return
+            lib.tpi_ipc_close(base)
 
         def open_dmabufs() -> None:
             # the predecessor's server sends the descriptors in batches; each is checked
@@ -478,8 +503,14 @@ class HbmHandoff:
                                                             ctypes.byref(ptr),
                                                             ctypes.byref(size)),
                                       "tpi_dmabuf_import")
-                            mapped[i] = ptr.value
-                            via_dmabuf[i] = True
+                            with gate:
+                                late = given_up[0]
+                                if not late:
+                                    mapped[i] = ptr.value
+                                    via_dmabuf[i] = True
+                            if late:
+                                lib.tpi_dmabuf_unmap(ptr)
+                                raise CheckpointError("the hand-off was given up")
                             if int(size.value) < off + sizes[i]:
                                 # never let a kernel read past what was mapped
                                 raise CheckpointError(
@@ -513,6 +544,8 @@ class HbmHandoff:
 
         def close_all() -> None:
             t1 = time.perf_counter()
+            with gate:
+                given_up[0] = True  # from now on late openers close their own mappings
             each(close_one)
             self.hbm_close_s = time.perf_counter() - t1
             self.release_hbm_claim()  # nothing of the predecessor is mapped any more
@@ -618,7 +651,13 @@ class HbmHandoff:
             sig = torch.cuda.current_stream(self.device_index).cuda_stream
             t3 = time.perf_counter()
             phases["meminfo"] = t3 - t2
-            res = self.engine.copy_segments(src, self.plan, sig, dst)  # synchronous: copy done
+            try:
+                res = self.engine.copy_segments(src, self.plan, sig, dst)  # synchronous
+            except BaseException as error:
+                self.hbm_fault_dump = _dump_copy_plan(self._hbm_manifest_path(), src, dst,
+                                                      owner, bases, sizes, doc, error,
+                                                      self.device_index)
+                raise
             phases["copy"] = time.perf_counter() - t3
         except BaseException:
             close_all()
@@ -657,6 +696,36 @@ class HbmHandoff:
         if closer is not None:
             closer.join()
             self._hbm_closer = None
+
+
+def _dump_copy_plan(manifest: str, src: np.ndarray, dst: np.ndarray, owner: np.ndarray,
+                    bases: List[Optional[int]], sizes: List[int], doc: Dict,
+                    error: BaseException, device_index: int = 0) -> Optional[str]:
+    """Evidence of a failed hand-off copy (``<manifest>.fault.json``): every source and
+    destination descriptor the kernel was given, each source's mapped allocation
+    ``[base, base + size)``, the relocation pieces, and what the driver held on the device --
+    so a fault can be tied to an address instead of to timing."""
+    path = (manifest or "/tmp/tpi-hbm") + ".fault.%d.json" % os.getpid()
+    try:
+        from ..parallel.placement import device_vram_usage
+
+        def segs(a: np.ndarray) -> List[List[int]]:
+            return [[int(x["ptr"]), int(x["nbytes"]), int(x["kind"]), int(x["off"])] for x in a]
+
+        usage = None
+        try:
+            usage = device_vram_usage(device_index)
+        except Exception:
+            pass
+        with open(path, "w") as f:
+            json.dump({"error": str(error), "time": time.time(), "predecessor": doc.get("pid"),
+                       "src": segs(src), "dst": segs(dst), "owner": [int(o) for o in owner],
+                       "mapped": [[None if b is None else int(b), int(n)]
+                                  for b, n in zip(bases, sizes)],
+                       "pieces": doc.get("pieces"), "vram_used_total": usage}, f)
+        return path
+    except Exception:
+        return None
 
 
 def _seg_extent(seg) -> Tuple[int, int]:

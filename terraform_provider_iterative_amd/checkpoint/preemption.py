@@ -443,39 +443,54 @@ def standby(prefetch_path: Optional[str] = None, materialize: bool = False) -> b
 
 def wait_for_device_memory(spill: str, margin: float = 0.05,
                            timeout: Optional[float] = None) -> Optional[float]:
-    """A successor started while its predecessor on the same GPU still streams a state too big
-    for two copies (``spill`` is being written by a live process): block until the device has
-    room for the state (+ ``margin``, + 2 GiB for the engine and context) -- the predecessor
-    frees its tensors behind its spill (``Checkpointer.save(release_behind=True)``) -- or the
-    predecessor is gone / done.  Returns the seconds waited (None: nothing to wait for).
-    Called by :func:`standby` before the script allocates its state, so the restore can stream
-    behind the spill instead of starting after the predecessor's exit."""
-    from .checkpointer import streaming_writer
+    """A successor's gate before it allocates the state of ``spill`` (its predecessor's
+    checkpoint region): block until the device has room for the state (+ ``margin``, + 2 GiB
+    for the engine and context) by the *driver's* count as well as the HIP runtime's, or until
+    ``timeout`` (``TPI_STREAM_TIMEOUT``, default 30 s).  Returns the seconds waited (None:
+    nothing to wait for -- no state in ``spill``, or no GPU); every wait is journalled
+    (``successor-hbm-wait``).
 
-    peer = streaming_writer(spill)
+    * The predecessor still streams a state too big for two copies: it frees its tensors
+      behind its spill (``Checkpointer.save(release_behind=True)``), and the restore streams
+      behind the spill as room appears.
+    * The predecessor is gone: its HBM is not back yet -- the driver wipes freed VRAM and
+      releases it seconds after the exit, while the runtime already reports it free.
+      Allocating on top of it made the driver evict buffers under the hand-off copy (the
+      round-5 faults, ``profiles/round5/ipc_cause.md``), so the successor waits for that too.
+    Called by :func:`standby` before the script allocates its state."""
+    from .checkpointer import region_total, streaming_writer
+
     torch = sys.modules.get("torch")
-    if peer is None or torch is None or not torch.cuda.is_available():
+    if torch is None or not torch.cuda.is_available():
         return None
-    need = int(peer["total"] * (1 + margin)) + (2 << 30)
+    peer = streaming_writer(spill)
+    total = peer["total"] if peer is not None else region_total(spill)
+    if not total:
+        return None
+    need = int(total * (1 + margin)) + (2 << 30)
     if timeout is None:
         timeout = float(os.environ.get("TPI_STREAM_TIMEOUT", "30"))
     dev = torch.cuda.current_device()
     from ..parallel.placement import device_vram_usage
 
     t0 = time.monotonic()
-    while time.monotonic() - t0 < timeout:
+    free = driver_free = 0
+    fits = False
+    while True:
         free, _ = torch.cuda.mem_get_info(dev)
-        # The driver's own count too: memory an exiting process gave back can still be held
-        # (delayed frees) while the runtime already reports it free.  Filling the device on
-        # top of it made the hand-off copy fault in round 5 (profiles/round5/ipc_cause.md).
         usage = device_vram_usage(dev)
-        if usage is not None:
-            free = min(free, usage[1] - usage[0])
-        if free >= need or streaming_writer(spill) is None:
+        driver_free = free if usage is None else usage[1] - usage[0]
+        fits = min(free, driver_free) >= need
+        if fits or time.monotonic() - t0 >= timeout:
             break
+        if peer is not None and streaming_writer(spill) is None:
+            peer = None  # the spill is done: from now on only the driver's count matters
         time.sleep(0.005)
     waited = time.monotonic() - t0
-    journal("successor-hbm-wait", "%.1f GB needed" % (need / 1e9), "waited %.3f s" % waited)
+    journal("successor-hbm-wait", "%.1f GB needed" % (need / 1e9), "waited %.3f s" % waited,
+            "free %.1f GB (driver %.1f GB)" % (free / 1e9, driver_free / 1e9),
+            "predecessor streaming" if peer is not None else "predecessor done",
+            *([] if fits else ["timed out: allocating anyway"]))
     return waited
 
 
@@ -923,6 +938,53 @@ def materialize(spill: str, device: Any = None, **kwargs) -> Optional[Tuple[Chec
     return ck, tensors, dict(getattr(ck, "materialized_metadata", {}) or {})
 
 
+STICKY_HIP_ERRORS = ("illegal memory access", "illegal address", "illegal instruction",
+                     "launch failure", "hardware exception", "memory access fault", "ecc error")
+
+
+def _sticky_device_error(checkpointer: Checkpointer, error: BaseException) -> bool:
+    """Did ``error`` leave this process's GPU context unusable?  A kernel fault is sticky in
+    HIP: every later call on the device fails, so no restore -- from the host copy either --
+    can run in this process any more (round 5, r5g: the "fallback" after a faulting hand-off
+    copy died the same way).  Known messages, else one synchronisation probe."""
+    text = str(error).lower()
+    if any(word in text for word in STICKY_HIP_ERRORS):
+        return True
+    torch = sys.modules.get("torch")
+    if torch is None or not torch.cuda.is_initialized():
+        return False
+    try:
+        torch.cuda.synchronize(getattr(checkpointer, "device_index", None))
+        return False
+    except Exception as probe:
+        return any(word in str(probe).lower() for word in STICKY_HIP_ERRORS) or \
+            "hip" in str(probe).lower()
+
+
+def _hbm_fatal(checkpointer: Checkpointer, error: BaseException) -> None:
+    """A sticky device error during the HBM hand-off: fatal for this process.  The hand-off
+    is withdrawn (manifest removed: the predecessor may exit, and no successor imports it
+    again) and, under a supervisor, the rank exits as preempted -- its respawn is a new
+    process with a new GPU context, which restores from the host copy.  Without a supervisor
+    the caller re-raises."""
+    journal("checkpoint-hbm-fatal", str(error),
+            "sticky device error: this process's GPU context is unusable, so there is no "
+            "fallback in it", "dump %s" % getattr(checkpointer, "hbm_fault_dump", None),
+            "the respawn restores from the host copy" if os.environ.get("TPI_NOTIFY_FD")
+            else "no supervisor: raised to the script")
+    try:
+        os.remove(checkpointer._hbm_manifest_path())
+    except (OSError, TypeError):
+        pass
+    checkpointer.release_hbm_claim()
+    if not os.environ.get("TPI_NOTIFY_FD"):
+        return
+    print("tpi: FATAL: the HBM hand-off copy failed with a sticky device error (%s); exiting "
+          "%d so the supervisor respawns this rank from the host copy" % (
+              error, PREEMPTED_EXIT_CODE), file=sys.stderr, flush=True)
+    os._exit(PREEMPTED_EXIT_CODE)
+
+
 def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None,
            generation: Optional[int] = None) -> Optional[Dict]:
     """Restore from the host region (or ``persist_path``) if a complete checkpoint exists.
@@ -996,7 +1058,10 @@ def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None,
             # the exported state is the predecessor's last boundary: newer than a host copy
             # whose spill failed, and there even when no host copy completed at all
             return hbm["metadata"] or (header or {}).get("metadata", {})
-        except Exception as error:  # fall back to the host region
+        except Exception as error:  # fall back to the host region -- unless the GPU is gone
+            if _sticky_device_error(checkpointer, error):
+                _hbm_fatal(checkpointer, error)  # does not return under a supervisor
+                raise
             journal("checkpoint-hbm-failed", str(error), "%.1f GB free at the copy" % (
                 getattr(checkpointer, "hbm_free_before_copy", 0) / 1e9))
     if header is not None:

@@ -23,6 +23,9 @@ from typing import Dict, Iterator, List, Optional, Tuple
 from ..utils.record import field, record
 
 KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+DRAIN_MAX_AGE = 600.0     # s: an older drain marker is ignored
+DRAIN_QUIET_S = 0.25      # s without a falling VRAM count: nothing is being given back
+DRAIN_STEP = 64 << 20     # a fall of at least this much counts as memory coming back
 
 
 @record
@@ -77,8 +80,13 @@ def discover(environ=None) -> List[GPU]:
     """GPUs of this node (see module docstring)."""
     environ = os.environ if environ is None else environ
     override = environ.get("TPI_MI355X_GPUS")
-    if override is not None:
-        return [GPU(index=int(x), gfx="gfx950") for x in override.split(",") if x.strip()]
+    if override is not None:  # "0,1,..." or "0=<pci bus id>,..." (tests: a fake sysfs)
+        out = []
+        for item in (x.strip() for x in override.split(",")):
+            if item:
+                index, _, pci = item.partition("=")
+                out.append(GPU(index=int(index), gfx="gfx950", pci=pci))
+        return out
     gpus: List[GPU] = []
     try:
         nodes = sorted(os.listdir(KFD_NODES), key=lambda n: int(n) if n.isdigit() else 1 << 30)
@@ -191,6 +199,134 @@ class Placement:
     def lease_path(self, index: int) -> str:
         return os.path.join(self.root, "gpu-%d.lease" % index)
 
+    def drain_path(self, index: int) -> str:
+        """The released lease of the GPU's previous holder (renamed by its supervisor or by
+        :meth:`release`), until the next holder has seen the driver take its memory back."""
+        return os.path.join(self.root, "gpu-%d.drain" % index)
+
+    def _drain_marker(self, index: int) -> Optional[dict]:
+        raw = _read(self.drain_path(index))
+        if not raw:
+            return None
+        try:
+            marker = json.loads(raw)
+        except ValueError:
+            return None
+        try:  # a marker nobody consumed for this long says nothing about the GPU now
+            if time.time() - os.path.getmtime(self.drain_path(index)) > DRAIN_MAX_AGE:
+                return None
+        except OSError:
+            return None
+        return marker
+
+    def settle_gpus(self, indices: List[int], timeout: Optional[float] = None,
+                    poll: float = 0.02) -> List[dict]:
+        """Before a task's ranks start on GPUs ``indices``: wait until the amdgpu driver has
+        taken the previous holders' device memory back, bounded by ``timeout``
+        (``TPI_GPU_DRAIN_TIMEOUT``, default 30 s).  Returns one record per GPU that had
+        something to wait for (for the task's journal: ``gpu-drain``).
+
+        Why: a process's HBM is not free when it exits, nor when its supervisor hands the GPU
+        on -- the driver wipes freed VRAM and releases it seconds later (200 GB: ~5 s), while
+        the HIP runtime of the next process already reports it free.  A task that fills the
+        device on top of it makes the driver evict buffers under running kernels; the round-5
+        hand-off faults happened exactly there (``profiles/round5/ipc_cause.md``).
+
+        * A GPU with a drain marker (the previous holder's released lease): wait until the
+          driver's ``mem_info_vram_used`` is back to the count of the holder's reservation
+          (``vram_baseline``) + ``max(1 GiB, 1 %)``.
+        * Otherwise, a GPU using more than ``TPI_GPU_IDLE_FRACTION`` (3 %) of its memory: wait
+          while that count keeps falling (memory some other process freed, e.g. a benchmark's
+          own), until it has not fallen for 0.25 s.
+        The GPU's lease then records the settled count as its own baseline.  GPUs without a
+        readable counter (no sysfs, fake inventories) are not waited for."""
+        if timeout is None:
+            try:
+                timeout = float(os.environ.get("TPI_GPU_DRAIN_TIMEOUT", "30"))
+            except ValueError:
+                timeout = 30.0
+        try:
+            idle_fraction = float(os.environ.get("TPI_GPU_IDLE_FRACTION", "0.03"))
+        except ValueError:
+            idle_fraction = 0.03
+        by_index = {g.index: g for g in self.gpus}
+        todo = []
+        for index in indices:
+            gpu = by_index.get(index)
+            usage = vram_usage(gpu.pci) if gpu is not None and gpu.pci else None
+            if usage is None:
+                continue
+            used, total = usage
+            marker = self._drain_marker(index)
+            slack = max(1 << 30, total // 100)
+            baseline = None if marker is None else marker.get("vram_baseline")
+            item = {"gpu": index, "pci": gpu.pci, "used_at_start": used, "used": used,
+                    "total": total, "previous": (marker or {}).get("task"),
+                    "target": None if baseline is None else int(baseline) + slack,
+                    "idle": max(slack, int(idle_fraction * total)), "low": used,
+                    "last_drop": None, "done": False}
+            todo.append(item)
+        t0 = time.monotonic()
+        while todo:
+            now = time.monotonic()
+            pending = 0
+            for item in todo:
+                if item["done"]:
+                    continue
+                if item["target"] is not None:
+                    item["done"] = item["used"] <= item["target"]
+                else:
+                    quiet = now - (item["last_drop"] if item["last_drop"] is not None else t0)
+                    item["done"] = item["used"] <= item["idle"] or quiet >= DRAIN_QUIET_S
+                if item["done"]:
+                    item["waited"] = now - t0
+                pending += not item["done"]
+            if not pending or now - t0 >= timeout:
+                break
+            time.sleep(poll)
+            for item in todo:
+                if item["done"]:
+                    continue
+                usage = vram_usage(item["pci"])
+                if usage is None:
+                    item["done"], item["waited"] = True, time.monotonic() - t0
+                    continue
+                item["used"] = usage[0]
+                if usage[0] < item["low"] - DRAIN_STEP:
+                    item["low"] = usage[0]
+                    item["last_drop"] = time.monotonic()
+        waited = time.monotonic() - t0
+        out = []
+        for item in todo:
+            had_marker = item["previous"] is not None or item["target"] is not None
+            if had_marker or item["used_at_start"] > item["idle"]:
+                out.append({"gpu": item["gpu"], "previous": item["previous"],
+                            "waited_s": round(item.get("waited", waited), 3),
+                            "used_gb_at_start": round(item["used_at_start"] / 1e9, 2),
+                            "used_gb": round(item["used"] / 1e9, 2),
+                            "target_gb": None if item["target"] is None else
+                            round(item["target"] / 1e9, 2),
+                            "timed_out": not item["done"]})
+            try:
+                os.unlink(self.drain_path(item["gpu"]))
+            except FileNotFoundError:
+                pass
+            self._rebase_lease(item["gpu"], item["used"])
+        return out
+
+    def _rebase_lease(self, index: int, used: int) -> None:
+        """The settled driver count becomes the lease's baseline (nothing of its holder runs
+        on the GPU yet)."""
+        with self._locked():
+            lease = self._read_lease(index)
+            if not lease or lease.get("task") == "?":
+                return
+            lease["vram_baseline"] = int(used)
+            tmp = self.lease_path(index) + ".tmp"
+            with open(tmp, "w") as handle:
+                json.dump(lease, handle)
+            os.replace(tmp, self.lease_path(index))
+
     @contextmanager
     def _locked(self) -> Iterator[None]:
         fd = os.open(os.path.join(self.root, "placement.lock"), os.O_RDWR | os.O_CREAT, 0o644)
@@ -276,14 +412,27 @@ class Placement:
                 raise PlacementError("not enough free GPUs: need %d, free %d (held by %s)"
                                      % (need, len(free), ", ".join(busy) or "-"))
             chosen = self._choose(free, need, prefer_numa)
-            now = time.time()
             for gpu in chosen:
-                tmp = self.lease_path(gpu.index) + ".tmp"
-                with open(tmp, "w") as handle:
-                    json.dump({"task": task_id, "task_dir": task_dir, "created": now,
-                               "creator_pid": os.getpid(), "gpu": gpu.index}, handle)
-                os.replace(tmp, self.lease_path(gpu.index))
+                self._write_lease(gpu, {"task": task_id, "task_dir": task_dir})
             return sorted(held + chosen, key=lambda g: g.index)
+
+    def _write_lease(self, gpu: GPU, lease: dict) -> None:
+        """A GPU's lease, with the driver's VRAM count of a GPU nobody holds
+        (``vram_baseline``): what the driver must be back to before the next holder starts
+        (:meth:`settle_gpus`).  A drain marker still pending carries the baseline over (the
+        previous holder's memory is not back yet, so the count now would include it)."""
+        lease = dict(lease, created=time.time(), creator_pid=os.getpid(), gpu=gpu.index)
+        marker = self._drain_marker(gpu.index)
+        if marker is not None and marker.get("vram_baseline") is not None:
+            lease["vram_baseline"] = marker["vram_baseline"]
+        else:
+            usage = vram_usage(gpu.pci) if gpu.pci else None
+            if usage is not None:
+                lease["vram_baseline"] = usage[0]
+        tmp = self.lease_path(gpu.index) + ".tmp"
+        with open(tmp, "w") as handle:
+            json.dump(lease, handle)
+        os.replace(tmp, self.lease_path(gpu.index))
 
     @staticmethod
     def _choose(free: List[GPU], need: int, prefer_numa: bool) -> List[GPU]:
@@ -303,8 +452,8 @@ class Placement:
         with self._locked():
             n = 0
             for gpu in self.held_by(task_id):
-                try:
-                    os.unlink(self.lease_path(gpu.index))
+                try:  # the lease becomes the GPU's drain marker (see settle_gpus)
+                    os.replace(self.lease_path(gpu.index), self.drain_path(gpu.index))
                     n += 1
                 except FileNotFoundError:
                     pass
@@ -434,12 +583,8 @@ class Placement:
             self._reserve_memory(req, allocs, alloc)
             now = time.time()
             for gpu in chosen:
-                tmp = self.lease_path(gpu.index) + ".tmp"
-                with open(tmp, "w") as handle:
-                    json.dump({"task": req.task, "task_dir": req.task_dir, "created": now,
-                               "creator_pid": os.getpid(), "gpu": gpu.index,
-                               "spot": req.spot}, handle)
-                os.replace(tmp, self.lease_path(gpu.index))
+                self._write_lease(gpu, {"task": req.task, "task_dir": req.task_dir,
+                                        "spot": req.spot})
             record = dict(alloc.to_json(), task_dir=req.task_dir, created=now,
                           creator_pid=os.getpid())
             os.makedirs(os.path.dirname(self.alloc_path(req.task)), exist_ok=True)
@@ -640,7 +785,7 @@ def vram_usage(pci: str) -> Optional[Tuple[int, int]]:
     """``(used, total)`` bytes of a GPU's device memory from the amdgpu driver's sysfs
     counters (no GPU context needed: readable while other processes still hold the device),
     None when unreadable.  ``pci``: the GPU's bus id (:attr:`GPU.pci`)."""
-    base = "/sys/bus/pci/devices/%s" % pci
+    base = os.path.join(os.environ.get("TPI_SYSFS_PCI", "/sys/bus/pci/devices"), pci)
     used, total = _read(base + "/mem_info_vram_used").strip(), \
         _read(base + "/mem_info_vram_total").strip()
     if not (used.isdigit() and total.isdigit()):

@@ -249,11 +249,60 @@ def attach(manifest: Optional[str] = None, rank: Optional[int] = None,
 
     lib = hip()
     device = int(entry["device"])
-    ptr = ctypes.c_void_p()
-    handle_bytes = bytes.fromhex(entry["ipc"])
-    lib.check(lib.tpi_ipc_open(handle_bytes, device, ctypes.byref(ptr)), "hipIpcOpenMemHandle")
-    buffer = _device_tensor(ptr.value, int(data["total"]), device)
-    return HbmWorkdir(data, rank, buffer, mapping=ptr.value)
+    ptr = _ipc_open_bounded(lib, bytes.fromhex(entry["ipc"]), device, int(data["total"]))
+    buffer = _device_tensor(ptr, int(data["total"]), device)
+    return HbmWorkdir(data, rank, buffer, mapping=ptr)
+
+
+def _ipc_open_bounded(lib, handle: bytes, device: int, nbytes: int,
+                      timeout: Optional[float] = None) -> int:
+    """``hipIpcOpenMemHandle`` of the stager's image, bounded by ``TPI_IPC_OPEN_TIMEOUT``
+    (default 30 s here): an import that never returns (the HIP runtime's IPC import can spin
+    forever, ``profiles/round5/ipc_cause.md``) fails the rank with a ``workdir-attach-failed``
+    event instead of hanging it.  The opener is a daemon thread, so a stuck one cannot hold up
+    the process's exit; if it returns after the deadline it closes its own mapping."""
+    import threading
+    import time
+
+    if timeout is None:
+        try:
+            timeout = float(os.environ.get("TPI_IPC_OPEN_TIMEOUT", "30"))
+        except ValueError:
+            timeout = 30.0
+    result: Dict[str, object] = {}
+    lock = threading.Lock()
+
+    def opener() -> None:
+        ptr = ctypes.c_void_p()
+        rc = lib.tpi_ipc_open(handle, device, ctypes.byref(ptr))
+        with lock:
+            if "abandoned" not in result:
+                result["rc"], result["ptr"] = rc, ptr.value
+                return
+        if rc == 0:
+            lib.tpi_ipc_close(ptr)
+
+    t0 = time.monotonic()
+    thread = threading.Thread(target=opener, name="tpi-workdir-attach", daemon=True)
+    thread.start()
+    thread.join(timeout)
+    with lock:
+        if "rc" not in result:
+            result["abandoned"] = True
+    if "abandoned" in result:
+        from ..checkpoint.preemption import journal
+
+        message = ("workdir attach: hipIpcOpenMemHandle of the staged %.2f GB image on device "
+                   "%d did not return within %.1f s (TPI_IPC_OPEN_TIMEOUT)" % (
+                       nbytes / 1e9, device, timeout))
+        journal("workdir-attach-failed", message)
+        raise TimeoutError(message)
+    lib.check(int(result["rc"]), "hipIpcOpenMemHandle")
+    from ..checkpoint.preemption import journal
+
+    journal("workdir-attached", "%.2f GB" % (nbytes / 1e9),
+            "ipc open %.4f s" % (time.monotonic() - t0))
+    return int(result["ptr"])
 
 
 # ---- native loader (used by the stager binary; exposed for ranks, benches and tests) ----------

@@ -1010,3 +1010,83 @@ def test_streamed_restore_on_its_own_sdma_engine(codec, tmp_path):
     assert reader.engine.set_h2d_sdma(False) == 0
     reader.close()
     writer.close()
+
+
+STUCK_EXPORTER = r'''
+import sys, torch
+sys.path.insert(0, %(root)r)
+from terraform_provider_iterative_amd.checkpoint import Checkpointer
+g = torch.Generator(device="cuda").manual_seed(23)
+t = {"big": torch.empty(int(2.1 * 2 ** 30) // 4, device="cuda"),
+     "n": torch.randn(4096, device="cuda", generator=g)}
+t["big"].normal_(generator=g)
+ck = Checkpointer(t, path=%(path)r, tile_bytes=1 << 20, chunk_bytes=256 << 20)
+ck.save({"step": 7})  # the host copy the successor falls back to
+print("exported", ck.export_hbm({"step": 7}), flush=True)
+sys.stdin.readline()  # hold the memory (and the offer) until the successor is done
+'''
+
+STUCK_SUCCESSOR = r'''
+import os, sys, threading, time, torch
+sys.path.insert(0, %(root)r)
+from terraform_provider_iterative_amd.checkpoint import Checkpointer, preemption
+g = torch.Generator(device="cuda").manual_seed(23)
+want_big = torch.empty(int(2.1 * 2 ** 30) // 4, device="cuda")
+want_big.normal_(generator=g)
+want_n = torch.randn(4096, device="cuda", generator=g)
+dst = {"big": torch.zeros_like(want_big), "n": torch.zeros(4096, device="cuda")}
+ck = Checkpointer(dst, path=%(path)r, tile_bytes=1 << 20, chunk_bytes=256 << 20)
+assert ck.hbm_ready()
+t0 = time.monotonic()
+meta = preemption.resume(ck)
+took = time.monotonic() - t0
+torch.cuda.synchronize()
+ok = torch.equal(dst["big"], want_big) and torch.equal(dst["n"], want_n)
+stuck = [t.name for t in threading.enumerate() if t.name == "tpi-ipc-open" and t.is_alive()]
+print("resumed", meta.get("step"), "took %%.2f" %% took, "bitexact", ok, "stuck", len(stuck),
+      flush=True)
+ck.close()
+sys.exit(0 if ok else 3)
+'''
+
+
+def test_a_stuck_ipc_import_falls_back_to_the_host_copy_on_hardware(tmp_path):
+    """VERDICT r5 #6, on the real driver: an IPC import that never returns (a 2.1 GiB
+    allocation offered over HIP IPC with the size guard lifted, TPI_HBM_ROUTE=ipc and
+    TPI_IPC_MAX_ALLOC=3 GiB) makes the successor give up after TPI_IPC_OPEN_TIMEOUT, restore
+    bit-exactly from the host copy, and exit normally with the opener thread still stuck in
+    the driver.  The successor is a child process, so a stuck runtime cannot take the test
+    runner with it."""
+    import os
+    import subprocess
+    import sys
+    import time
+
+    root = os.path.dirname(os.path.dirname(__file__))
+    path = str(tmp_path / "spill")
+    env = dict(os.environ, TPI_HBM_ROUTE="ipc", TPI_IPC_MAX_ALLOC=str(3 << 30),
+               TPI_IPC_OPEN_TIMEOUT="4", TPI_EVENTS_FILE=str(tmp_path / "events.jsonl"))
+    child = subprocess.Popen([sys.executable, "-c", STUCK_EXPORTER % {"root": root, "path": path}],
+                             stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=env)
+    try:
+        line = child.stdout.readline()
+        assert line.startswith("exported"), line
+        t0 = time.monotonic()
+        succ = subprocess.run([sys.executable, "-c", STUCK_SUCCESSOR % {"root": root,
+                                                                        "path": path}],
+                              env=env, capture_output=True, text=True, timeout=100)
+        wall = time.monotonic() - t0
+    finally:
+        child.stdin.write("\n")
+        child.stdin.flush()
+        child.wait(60)
+    out = succ.stdout + succ.stderr
+    assert succ.returncode == 0, out[-3000:]
+    assert "resumed 7" in out and "bitexact True" in out, out[-3000:]
+    took = float(out.split("took ")[1].split()[0])
+    assert 3.5 <= took < 30, out[-2000:]  # gave up at the timeout, then the host restore
+    events = open(tmp_path / "events.jsonl").read()
+    assert "checkpoint-hbm-failed" in events and "TPI_IPC_OPEN_TIMEOUT" in events
+    assert '"checkpoint-restored", "description": ["rank 0", "host region"' in events
+    print("stuck-import fallback: resume %.2f s, successor wall %.2f s, %s" % (
+        took, wall, out.split("stuck ")[1].split()[0] + " opener(s) still stuck at exit"))

@@ -110,3 +110,68 @@ def test_task_workdir_staged_in_hbm_and_written_back(tmp_path, monkeypatch):
     assert data[:3] == b"XYZ" and data[3:] == (work / "a.bin").read_bytes()[3:]
     assert any(e.code == "workdir-sync" and "dirty_shards 1" in e.description for e in events)
     task.delete()
+
+
+
+ATTACH_BIG = """#!/bin/sh
+exec python3 - <<'EOF'
+import os, time, torch
+from terraform_provider_iterative_amd.runtime.stage import attach
+t0 = time.monotonic()
+w = attach()
+took = time.monotonic() - t0
+root = os.environ["TPI_DATA_DIRECTORY"]
+rel = "big.bin"
+view = w.tensor(rel)
+size = os.path.getsize(os.path.join(root, rel))
+assert view.numel() == size, (view.numel(), size)
+with open(os.path.join(root, rel), "rb") as f:
+    for k in range(17):  # 1 MiB windows across the whole image, the last one at its end
+        off = min(k * (size // 16), size - (1 << 20))
+        f.seek(off)
+        host = f.read(1 << 20)
+        assert bytes(view[off:off + (1 << 20)].cpu().numpy()) == host, off
+print("attached big %.3f GB in %.4f s" % (size / 1e9, took), w.stats["verified"])
+EOF
+"""
+
+
+def test_task_attaches_a_staged_workdir_beyond_2_gib(tmp_path, monkeypatch):
+    """a workdir of 2.6 GB goes through the real stager (its image is one
+    hipMalloc of the /opt/rocm runtime) and is mapped by the rank (PyTorch's HIP runtime)
+    through HIP IPC -- the import that never returns for a PyTorch exporter's allocations of
+    2 GiB or more (profiles/round5/ipc_cause.md).  The attach is bounded
+    (TPI_IPC_OPEN_TIMEOUT): it either maps in time or fails the rank with an event."""
+    monkeypatch.delenv("TPI_MI355X_GPUS", raising=False)
+    monkeypatch.setenv("PYTHONPATH", ROOT)
+    work = tmp_path / "work"
+    work.mkdir()
+    rng = np.random.default_rng(3)
+    size = int(2.6e9) + 12345
+    with open(work / "big.bin", "wb") as f:
+        left = size
+        while left:
+            n = min(left, 256 << 20)
+            f.write(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+            left -= n
+    cloud = Cloud(provider="mi355x",
+                  credentials=Credentials(node=NodeCredentials(state_root=str(tmp_path / "st"))))
+    spec = Task(size=Size(machine="m+mi355x"), parallelism=1,
+                environment=Environment(script=ATTACH_BIG, timeout=300, directory=str(work),
+                                        variables=Variables({"TPI_STAGE": "hbm",
+                                                             "TPI_IPC_OPEN_TIMEOUT": "20"})))
+    task = backends.new(cloud, new_deterministic_identifier("hbm-stage-big"), spec)
+    task.create()
+    status = task.wait(240)
+    logs = "\n".join(task.logs())
+    events = task.events()
+    stager_log = open(os.path.join(task.sup_dir, "stager.log")).read()
+    try:
+        assert status["succeeded"] == 1, (logs, stager_log, [(e.code, e.description)
+                                                             for e in events])
+        assert "attached big 2.600 GB" in logs and "True" in logs
+        attached = [e for e in events if e.code == "workdir-attached"]
+        assert attached and not any(e.code == "workdir-attach-failed" for e in events)
+        print("big attach:", attached[0].description, logs.strip().splitlines()[-1])
+    finally:
+        task.delete()

@@ -687,6 +687,8 @@ def test_dmabuf_route_hands_every_allocation_over_the_socket(tmp_path, monkeypat
         plan = Plan
         _entries_digest = "d"
         export_hbm = Checkpointer.export_hbm
+        _publish_hbm = Checkpointer._publish_hbm
+        _free_relocated = Checkpointer._free_relocated
         _serve_dmabufs = Checkpointer._serve_dmabufs
         _close_dmabuf_server = Checkpointer._close_dmabuf_server
 
@@ -754,6 +756,7 @@ def test_auto_route_relocates_tensors_of_big_allocations(tmp_path, monkeypatch):
                (0x2000_0000_0000, 0, 1 << 20), (0x3000_0000_0000, 0, 5 * G // 2)]
     alloc_size = {0x1000_0000_0000: 5 * G, 0x2000_0000_0000: 4 << 20, 0x3000_0000_0000: 5 * G // 2}
     blocks, copies, opened = [], [], {}
+    freed, fail_export = [], []
 
     class FakeLib:
         def tpi_mem_range(self, ptr, base, size):
@@ -771,12 +774,15 @@ def test_auto_route_relocates_tensors_of_big_allocations(tmp_path, monkeypatch):
             return 0
 
         def tpi_dev_free(self, ptr):
+            freed.append(ptr.value)
             return 0
 
         def tpi_dmabuf_available(self):
             return 1
 
         def tpi_ipc_export(self, ptr, handle, off, size):
+            if fail_export:
+                return 1
             handle.raw = ("%064x" % ptr.value).encode()[:64]
             return 0
 
@@ -820,10 +826,24 @@ def test_auto_route_relocates_tensors_of_big_allocations(tmp_path, monkeypatch):
         plan = Plan
         _entries_digest = "d"
         export_hbm = Checkpointer.export_hbm
+        _publish_hbm = Checkpointer._publish_hbm
+        _free_relocated = Checkpointer._free_relocated
         _relocate = Checkpointer._relocate
 
         def _target(self):
             return None, 1
+
+    # an export that fails after the relocation frees the relocated blocks at
+    # once (nothing was published), instead of holding them through the save
+    freed.clear()
+    fail_export.append(True)
+    failing = Exporter(str(tmp_path / "spill-failing"))
+    with pytest.raises(AssertionError, match="tpi_ipc_export"):
+        failing.export_hbm()
+    assert len(freed) == 8 and not failing._relocated
+    assert not os.path.exists(str(tmp_path / "spill-failing") + ".hbm")
+    fail_export.clear()
+    copies.clear()
 
     with open(Exporter(str(tmp_path / "spill")).export_hbm()) as f:
         doc = json.load(f)

@@ -67,9 +67,13 @@ def test_rank_env_and_gpu_assignment(cloud):
     task.delete()
 
 
-def test_four_concurrent_two_gpu_tasks(cloud):
-    tasks = [_task(cloud, "conc-%d" % i, "#!/bin/sh\nsleep 2\necho done\n",
-                   machine="16-64000+mi355x*2") for i in range(4)]
+def test_four_concurrent_two_gpu_tasks(cloud, tmp_path):
+    # the four tasks hold their GPUs until the test opens the gate (a fixed sleep could run
+    # out under a loaded `pytest -n 8` before the fifth task was applied)
+    gate = tmp_path / "gate"
+    hold = ("#!/bin/sh\ni=0\nwhile [ ! -e %s ] && [ $i -lt 600 ]; do sleep 0.05; i=$((i+1)); "
+            "done\necho done\n" % gate)
+    tasks = [_task(cloud, "conc-%d" % i, hold, machine="16-64000+mi355x*2") for i in range(4)]
     for t in tasks:
         t.create()
     sets = [set(t.gpus()) for t in tasks]
@@ -81,6 +85,7 @@ def test_four_concurrent_two_gpu_tasks(cloud):
     extra.create()
     assert extra.status() == {"running": 0, "succeeded": 0, "failed": 0}  # leo read: queued
     assert extra.supervisor_running() and not extra.gpus()
+    gate.write_text("go")
     for t in tasks:
         assert t.wait(30)["succeeded"] == 1
     assert extra.wait(30)["succeeded"] == 1

@@ -18,8 +18,11 @@ from terraform_provider_iterative_amd.utils.identifier import new_deterministic_
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
+# The task holds until the test opens GATE (after its second create): a fixed sleep raced the
+# second create under `pytest -n 8`, which then found the task finished and re-ran it.
 SCRIPT = """#!/bin/sh
-sleep 3
+i=0
+while [ ! -e "%(gate)s" ] && [ $i -lt 1200 ]; do sleep 0.05; i=$((i+1)); done
 echo "rank $RANK says $GREETING_FROM_CLIENT"
 cat input.txt
 test -e skip.log && echo "skip.log leaked"
@@ -55,10 +58,10 @@ def _workdir(tmp_path):
     return work
 
 
-def _spec(work):
+def _spec(work, gate):
     return Task(size=Size(machine="s"),
                 environment=Environment(
-                    script=SCRIPT, directory=str(work), directory_out="results",
+                    script=SCRIPT % {"gate": gate}, directory=str(work), directory_out="results",
                     exclude_list=["skip.log"],
                     variables=Variables({"GREETING_*": None})),
                 parallelism=1)
@@ -80,11 +83,13 @@ def test_remote_node_create_read_delete(tmp_path, remote):
     work = _workdir(tmp_path)
     cloud = Cloud(provider="local", region="host=gpu-node-7")
     ident = new_deterministic_identifier("remote-smoke")
-    spec = _spec(work)
+    gate = tmp_path / "gate"
+    spec = _spec(work, gate)
     task = backends.new(cloud, ident, spec)
     assert isinstance(task, RemoteNodeTask)
     task.create()
     backends.new(cloud, ident, spec).create()  # idempotent, like the reference's smoke test
+    gate.write_text("go")  # only now may the task finish
     status = _wait(task)
     assert status["succeeded"] == 1, task.logs()
     log = "".join(task.logs())
