@@ -1030,10 +1030,10 @@ STUCK_SUCCESSOR = r'''
 import os, sys, threading, time, torch
 sys.path.insert(0, %(root)r)
 from terraform_provider_iterative_amd.checkpoint import Checkpointer, preemption
-g = torch.Generator(device="cuda").manual_seed(23)
+g = torch.Generator(device="cuda").manual_seed(23)  # the exporter's draw order: n, then big
+want_n = torch.randn(4096, device="cuda", generator=g)
 want_big = torch.empty(int(2.1 * 2 ** 30) // 4, device="cuda")
 want_big.normal_(generator=g)
-want_n = torch.randn(4096, device="cuda", generator=g)
 dst = {"big": torch.zeros_like(want_big), "n": torch.zeros(4096, device="cuda")}
 ck = Checkpointer(dst, path=%(path)r, tile_bytes=1 << 20, chunk_bytes=256 << 20)
 assert ck.hbm_ready()
