@@ -85,6 +85,9 @@ def parse_args(argv=None):
                    help="auto (1 GPU): after everything else, untimed, preempt a real "
                         "iterative_task holding --total-gb of state twice (cold successor, hot "
                         "standby) and report signal -> restored (preempt_e2e)")
+    p.add_argument("--config2", choices=("auto", "none"), default="auto",
+                   help="untimed, 1 GPU: apply -> first log of BASELINE config 2 (10 GB "
+                        "workdir + train.py) through tpi apply (first_log_latency_config2)")
     p.add_argument("--e2e-timeout", type=float, default=420.0,
                    help="seconds each preempt_e2e run may take")
     p.add_argument("--device", choices=("cuda", "cpu"), default="cuda",
@@ -146,10 +149,10 @@ def first_log_latency(timeout: float = 60.0, parallelism: int = 1):
 
 E2E_KEYS = ("ok", "verified", "status", "signal_to_restored_s", "save_s",
             "rank_start_to_restored_s", "saved_to_restored_s", "signal_to_durable_s", "streamed",
-            "warm_standby_activated", "hot_standby", "preload", "preloaded_wait_s",
+            "warm_standby_activated", "hot_standby", "preload", "preloaded_wait_s", "preload_gpu",
             "standby_pinned_wait_s", "restore_journal",
             "extra_tensors_gib", "delete_s", "rank_exit_to_settled_s", "gpu_drain",
-            "successor_hbm_wait", "hbm_failed",
+            "successor_hbm_wait", "hbm_failed", "hbm_fault_dumps",
             "memory_guard",
             "released_exit_pending_at_settle")
 
@@ -193,6 +196,38 @@ def preempt_e2e(total_gb: float, codec: str, timeout: float) -> dict:
             "fresh_signal_to_restored_s": runs.get("fresh", {}).get("signal_to_restored_s"),
             "verified": all(r.get("ok") is True for r in runs.values()),
             "gb": total_gb, "runs": runs}
+
+
+def workdir_config2(gb: float, timeout: float) -> dict:
+    """BASELINE config 2 through the product, untimed: ``tpi apply`` of a
+    ``gb`` GB synthetic workdir + PyTorch-ROCm ``examples/train/train.py`` on ``mi355x``
+    (``bench/bench_workdir.py``, one child process).  ``first_log_s``: apply -> the task's
+    first log line; ``push_s`` / ``push_method``: the workdir's push into task storage as the
+    task journalled it (reflinked where the filesystem can, else copied); ``stage_s``: rank
+    start -> the stager's HBM image published (it runs beside the rank's start-up)."""
+    import subprocess
+
+    cmd = [sys.executable, os.path.join(ROOT, "bench", "bench_workdir.py"), "--gb", repr(gb),
+           "--steps", "2", "--files", "10"]
+    t0 = time.perf_counter()
+    try:
+        proc = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+        lines = [l for l in proc.stdout.splitlines() if l.startswith("{")]
+        if proc.returncode != 0 or not lines:
+            return {"error": "exit %d: %s" % (proc.returncode, proc.stderr[-600:])}
+        r = json.loads(lines[-1])
+    except Exception as error:  # never lose the headline to the side measurement
+        return {"error": repr(error)}
+    out = {"first_log_s": r.get("apply_to_first_log_s"), "push_s": r.get("push_s"),
+           "push_method": r.get("push_method"), "stage_s": r.get("stage_s"),
+           "apply_s": r.get("apply_s"), "stage_GBps": r.get("stage_GBps"),
+           "train_step_ms": r.get("train_step_ms"), "workdir_gb": gb,
+           "ok": bool(r.get("apply_ok") and r.get("stage_GBps")),
+           "wall_s": round(time.perf_counter() - t0, 1)}
+    print("bench: config2 apply -> first log %s s (push %s s, %s; stage %s s)" % (
+        out["first_log_s"], out["push_s"], out["push_method"], out["stage_s"]),
+        file=sys.stderr, flush=True)
+    return out
 
 
 def launch_ranks(args, argv) -> int:
@@ -746,9 +781,13 @@ def main(argv=None):
         tensors.clear()
         torch.cuda.empty_cache()
         e2e = preempt_e2e(args.total_gb, args.codec, args.e2e_timeout)
+    config2 = None
+    if args.config2 == "auto" and on_gpu and world == 1:
+        config2 = workdir_config2(10.0, args.e2e_timeout)
     if out is not None and side_to_stderr:
         side = {"save_async": async_stall, "raw_GBps": raw, "workdir_broadcast": fanout,
-                "sequential": sequential, "preempt_e2e": e2e}
+                "sequential": sequential, "preempt_e2e": e2e,
+                "first_log_latency_config2": config2}
         print("bench-side " + json.dumps(side), file=sys.stderr, flush=True)
     elif out is not None:
         out["save_async"] = async_stall
@@ -756,6 +795,7 @@ def main(argv=None):
         out["workdir_broadcast"] = fanout
         out["sequential"] = sequential
         out["preempt_e2e"] = e2e
+        out["first_log_latency_config2"] = config2
         if isinstance(sequential, dict) and "GBps" in sequential:
             out["value_sequential"] = sequential["GBps"]
     emit()

@@ -262,8 +262,19 @@ def main():
                     e.code == "standby-start" and "preloaded" in e.description
                     for e in task.events()):
                 time.sleep(0.1)
-            time.sleep(3.0)  # its imports (it parks on its activation pipe after them)
+            # its imports (it parks on its activation pipe after them) and -- by default, once
+            # the supervisor has seen the rank use the GPU from one process -- its GPU context
+            t_park = time.time()
+            while time.time() - t_park < 20 and not any(
+                    e.code == "preload-gpu-warmed" for e in task.events()):
+                if any(e.code == "preload-plain" for e in task.events()):
+                    break
+                time.sleep(0.1)
+            if not any(e.code == "preload-gpu-warmed" for e in task.events()):
+                time.sleep(max(0.0, 3.0 - (time.time() - t_park)))
             result["preloaded_wait_s"] = round(time.time() - t_wait, 3)
+            result["preload_gpu"] = next((e.description for e in task.events() if e.code in (
+                "preload-gpu-warmed", "preload-plain")), None)
         t_preempt = time.time()
         task.preempt()
         status = task.wait(args.timeout)
@@ -320,7 +331,21 @@ def main():
         # whose memory was still coming back, and each successor's allocation gate
         result["gpu_drain"] = [d for c, _, d in events if c == "gpu-drain"]
         result["successor_hbm_wait"] = [d for c, _, d in events if c == "successor-hbm-wait"]
-        result["hbm_failed"] = [d for c, _, d in events if c == "checkpoint-hbm-failed"]
+        result["hbm_failed"] = [d for c, _, d in events
+                                if c in ("checkpoint-hbm-failed", "checkpoint-hbm-fatal")]
+        # a failed hand-off copy leaves its descriptors next to the spill (handoff.py
+        # _dump_copy_plan): keep them with the result, the spill directory is removed below
+        import glob
+
+        dumps = []
+        for path in glob.glob(spill + ".hbm.fault.*.json"):
+            try:
+                with open(path) as f:
+                    dumps.append(json.load(f))
+            except (OSError, ValueError):
+                pass
+        if dumps:
+            result["hbm_fault_dumps"] = dumps
         result["ok"] = bool(status.get("succeeded") == 1 and result["verified"])
     finally:
         try:

@@ -109,6 +109,14 @@ def main():
         m = re.search(r"done (\{.*\})", logs)
         if m:
             stats = json.loads(m.group(1))
+        events = []
+        for path in glob.glob(os.path.join(base, "state", "*", "*", "supervisor",
+                                           "events.jsonl")):
+            with open(path) as handle:
+                events += [json.loads(line) for line in handle if line.strip()]
+        pushed = next((e["description"] for e in events if e["code"] == "pushed"), None)
+        staged = next((e for e in events if e["code"] == "workdir-staged"), None)
+        started = next((e for e in events if e["code"] == "started"), None)
         d = subprocess.run(tpi + ["destroy", "-auto-approve"], cwd=work, env=env,
                            capture_output=True, text=True)
         result = {
@@ -125,6 +133,12 @@ def main():
                                                        "read_s", "files")},
             "staging": "runtime (tpi-stager)" if args.stage == "auto" else "train.py",
             "end_to_end_s": round(wall, 2), "apply_ok": apply.returncode == 0,
+            # the product's own journal: the push (reflinked or copied), the stager's load
+            "push_s": float(pushed[2].split()[0]) if pushed else None,
+            "push_method": pushed[3] if pushed else None,
+            "stage_s": round(staged["time"] - started["time"], 3) if staged and started
+            else None,
+            "staged_event": staged["description"] if staged else None,
             "destroy_ok": d.returncode == 0,
         }
         if apply.returncode != 0 or not m:

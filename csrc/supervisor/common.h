@@ -153,6 +153,12 @@ struct Rank {
   bool unused_standby = false;   // a standby discarded before activation (empty log: removed)
   int gofd = -1;                 // standby only: write end of its activation pipe
   double hold_until = 0;  // a resuming incarnation: no new hot standby until it restored
+  // preloaded successor (runtime/preload.py) only: parked outside the rank's memory cgroup
+  // (it joins at activation), and whether its GPU context was warmed on evidence
+  // (+1 warmed, -1 kept plain, 0 undecided) after `gpu_evidence` agreeing samples
+  bool preloaded = false;
+  int preload_gpu = 0;
+  int gpu_evidence = 0;
   // restored from its predecessor's HBM ("restored hbm"): the predecessor must stay alive
   // until this incarnation has unmapped the IPC imports ("closed") or died
   bool awaiting_close = false;
@@ -213,6 +219,12 @@ struct Spec {
   std::vector<std::string> sync_argv;
   // preloaded successors (TPI_PRELOAD): the launcher; the script path is appended
   std::vector<std::string> preload_argv;
+  // TPI_PRELOAD=1/auto: warm the parked successor's GPU context ("warm" on its activation
+  // pipe) once the running rank shows it is safe -- exactly one of the rank's processes holds
+  // the GPU device (preload_gpu_device, /dev/kfd), over two samples
+  bool preload_gpu_auto = false;
+  std::string preload_gpu_device = "/dev/kfd";
+  double preload_evidence_interval = 1.0;
   double sync_interval = 10, sync_timeout = 600;
   int restart_base = 0;  // restarts of earlier supervisors of this task (requeued incarnations)
 };
@@ -284,6 +296,9 @@ Spec load_spec(const std::string& path) {
   for (auto& a : v["requeue_argv"].a) s.requeue_argv.push_back(a.str());
   for (auto& a : v["sync"]["argv"].a) s.sync_argv.push_back(a.str());
   for (auto& a : v["preload_argv"].a) s.preload_argv.push_back(a.str());
+  s.preload_gpu_auto = v["preload_gpu_auto"].boolean(false);
+  s.preload_gpu_device = v["preload_gpu_device"].str("/dev/kfd");
+  s.preload_evidence_interval = v["preload_evidence_interval"].num(1.0);
   s.sync_interval = v["sync"]["interval"].num(10);
   s.sync_timeout = v["sync"]["timeout"].num(600);
   s.restart_base = (int)v["restart_base"].num(0);

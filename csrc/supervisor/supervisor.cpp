@@ -170,6 +170,11 @@ class Supervisor {
           if (r.state == Rank::RUNNING && r.pid > 0 && r.term_at == 0 &&
               standby_[r.index].pid <= 0 && r.hot_spawns < 2)
             timeout = std::min(timeout, std::max(r.hold_until, r.started + kPreloadDelay) - t);
+      if (s_.preload_gpu_auto)
+        for (auto& r : ranks_)
+          if (standby_[r.index].pid > 0 && standby_[r.index].preloaded &&
+              standby_[r.index].preload_gpu == 0)
+            timeout = std::min(timeout, next_evidence_ - t);
       if (s_.disk_limit_bytes) timeout = std::min(timeout, next_disk_check_ - t);
       timeout = sync_.timeout(t, timeout);
       if (stager_fd_ >= 0) timeout = std::min(timeout, stager_deadline_ - t);
@@ -202,7 +207,10 @@ class Supervisor {
       }
       if (released) handoff_released();
       if (s_.standby_hot) keep_hot_standbys();
-      if (!s_.preload_argv.empty()) keep_preloaded();
+      if (!s_.preload_argv.empty()) {
+        keep_preloaded();
+        check_preload_evidence(now());
+      }
       if (pfds[0].revents & POLLIN) handle_signals();
       if (ctl_fd_ >= 0 && nrank_fds < pfds.size() && (pfds[nrank_fds].revents & POLLIN))
         handle_control();
@@ -596,7 +604,9 @@ class Supervisor {
       }
     }
     std::string exec_cmd = "exec \"$0\"";
-    const std::string cg_procs = memory_.cgroup_procs(r.index);
+    // a preloaded successor parks outside the rank's memory cgroup (its imported interpreter
+    // would eat into the running rank's limit); it joins the cgroup when it is activated
+    const std::string cg_procs = preload ? std::string() : memory_.cgroup_procs(r.index);
     pid_t parent = getpid();
     pid_t pid = fork();
     if (pid == 0) {
@@ -690,6 +700,9 @@ class Supervisor {
                                      "machine " + r.uuid, "gpus " + (r.gpus.empty() ? "-" : r.gpus),
                                      "restart " + std::to_string(r.restarts)};
     if (preload) desc.push_back("preloaded");
+    r.preloaded = preload;
+    r.preload_gpu = 0;
+    r.gpu_evidence = 0;
     event(standby ? "standby-start" : "rank-start", desc);
   }
 
@@ -780,6 +793,12 @@ class Supervisor {
       discard_standby(r.index, "activation failed");
       return false;
     }
+    std::vector<std::string> how = {"warm standby"};
+    if (sb.preloaded) {
+      how.push_back("preloaded");
+      if (sb.preload_gpu > 0) how.push_back("GPU warmed");
+      join_cgroup(r.index, sb.pid);
+    }
     const int restarts = r.restarts;
     r.uuid = sb.uuid;
     r.pid = sb.pid;
@@ -801,10 +820,102 @@ class Supervisor {
     r.state = Rank::RUNNING;
     r.hold_until = now() + kStandbyHold;
     sb = Rank();
-    event("rank-start", {"rank " + std::to_string(r.index), "pid " + std::to_string(r.pid),
-                         "machine " + r.uuid, "gpus " + (r.gpus.empty() ? "-" : r.gpus),
-                         "restart " + std::to_string(r.restarts), "warm standby"});
+    std::vector<std::string> desc = {"rank " + std::to_string(r.index),
+                                     "pid " + std::to_string(r.pid), "machine " + r.uuid,
+                                     "gpus " + (r.gpus.empty() ? "-" : r.gpus),
+                                     "restart " + std::to_string(r.restarts)};
+    desc.insert(desc.end(), how.begin(), how.end());
+    event("rank-start", desc);
     return true;
+  }
+
+  // Move a (preloaded) process into rank `index`'s memory cgroup, where the rank's own
+  // processes are placed at their spawn; memory it charged while parked stays where it was.
+  void join_cgroup(int index, pid_t pid) {
+    const std::string procs = memory_.cgroup_procs(index);
+    if (procs.empty() || pid <= 0) return;
+    const int cfd = open(procs.c_str(), O_WRONLY | O_APPEND | O_CLOEXEC);
+    if (cfd < 0) return;
+    const std::string num = std::to_string((int)pid) + "\n";
+    if (write(cfd, num.data(), num.size()) != (ssize_t)num.size()) {
+    }
+    close(cfd);
+  }
+
+  // Processes of process group `pgid` (a rank: the supervisor makes each rank a group leader)
+  // that hold `device` open.
+  static std::vector<pid_t> device_holders(pid_t pgid, const std::string& device) {
+    std::vector<pid_t> out;
+    DIR* proc = opendir("/proc");
+    if (!proc) return out;
+    char path[96], buf[512], link[256];
+    while (struct dirent* de = readdir(proc)) {
+      if (de->d_name[0] < '0' || de->d_name[0] > '9') continue;
+      snprintf(path, sizeof(path), "/proc/%s/stat", de->d_name);
+      if (!read_small(path, buf, sizeof(buf))) continue;
+      const char* rp = strrchr(buf, ')');
+      int ppid = 0, pgrp = 0;
+      char state = 0;
+      if (!rp || sscanf(rp + 1, " %c %d %d", &state, &ppid, &pgrp) != 3 || pgrp != pgid) continue;
+      snprintf(path, sizeof(path), "/proc/%s/fd", de->d_name);
+      DIR* fds = opendir(path);
+      if (!fds) continue;
+      bool holds = false;
+      while (struct dirent* fe = readdir(fds)) {
+        if (fe->d_name[0] == '.') continue;
+        char fpath[160];
+        snprintf(fpath, sizeof(fpath), "/proc/%s/fd/%s", de->d_name, fe->d_name);
+        const ssize_t n = readlink(fpath, link, sizeof(link) - 1);
+        if (n <= 0) continue;
+        link[n] = 0;
+        if (device == link) {
+          holds = true;
+          break;
+        }
+      }
+      closedir(fds);
+      if (holds) out.push_back((pid_t)atoi(de->d_name));
+    }
+    closedir(proc);
+    return out;
+  }
+
+  // Evidence for warming a parked preloaded successor's GPU (spec "preload_gpu_auto"): the
+  // successor runs the script in-process, so a context it creates before the script starts is
+  // one the script would otherwise create itself -- unless the script forks GPU-using workers
+  // before it touches the GPU (they cannot use a context inherited over fork()).  The running
+  // incarnation tells which kind the script is: one process of the rank holding the GPU device
+  // in two samples -> "warm" (the successor initialises the GPU now: ~0.13 s off a cold
+  // recovery, profiles/round5/r5ai); two or more -> the successor stays plain; none yet -> ask
+  // again later.
+  double next_evidence_ = 0;
+  void check_preload_evidence(double t) {
+    if (!s_.preload_gpu_auto || t < next_evidence_) return;
+    next_evidence_ = t + s_.preload_evidence_interval;
+    for (auto& r : ranks_) {
+      Rank& sb = standby_[r.index];
+      if (r.state != Rank::RUNNING || r.pid <= 0 || r.term_at > 0 || sb.pid <= 0 ||
+          !sb.preloaded || sb.preload_gpu != 0 || sb.gofd < 0)
+        continue;
+      const std::vector<pid_t> holders = device_holders(r.pid, s_.preload_gpu_device);
+      if (holders.empty()) continue;
+      if (holders.size() > 1) {
+        sb.preload_gpu = -1;
+        event("preload-plain", {"rank " + std::to_string(r.index),
+                                std::to_string(holders.size()) + " processes of the rank hold " +
+                                    s_.preload_gpu_device,
+                                "the preloaded successor leaves the GPU to the script"});
+        continue;
+      }
+      if (++sb.gpu_evidence < 2) continue;
+      static const char kWarm[] = "warm\n";
+      if (write(sb.gofd, kWarm, sizeof(kWarm) - 1) != (ssize_t)(sizeof(kWarm) - 1)) continue;
+      sb.preload_gpu = 1;
+      event("preload-gpu-warm", {"rank " + std::to_string(r.index),
+                                 "pid " + std::to_string(holders[0]) + " alone holds " +
+                                     s_.preload_gpu_device,
+                                 "the preloaded successor initialises its GPU context now"});
+    }
   }
 
   void emit_line(Rank& r, const std::string& line) {

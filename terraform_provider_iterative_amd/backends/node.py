@@ -487,6 +487,10 @@ class NodeTask(Task):
             "sync": self._remote_sync(knob),
             # a preloaded successor per Python rank (runtime/preload.py; TPI_PRELOAD=0: none)
             "preload_argv": self._preload_argv(knob),
+            # TPI_PRELOAD=1/auto (default): the parked successor creates its GPU context once
+            # the running rank shows it uses the GPU from one process ("plain": never)
+            "preload_gpu_auto": knob("TPI_PRELOAD", "1") in ("1", "true", "yes", "auto"),
+            "preload_gpu_device": knob("TPI_PRELOAD_GPU_DEVICE", "/dev/kfd"),
         }
 
     def _preload_argv(self, knob) -> List[str]:
@@ -496,7 +500,7 @@ class NodeTask(Task):
         interpreter flags are kept), since the successor runs it in-process; off with a hot
         standby (``TPI_WARM_STANDBY=hot``), whose parked successor has the GPU initialised."""
         mode = knob("TPI_PRELOAD", "1")
-        if mode not in ("1", "true", "yes", "gpu", "gpu-lite"):
+        if mode not in ("1", "true", "yes", "auto", "plain", "gpu", "gpu-lite"):
             return []
         if knob("TPI_WARM_STANDBY", "1") == "hot":
             return []
@@ -899,11 +903,20 @@ class NodeTask(Task):
             log.info("Uploaded %d files to %s", stats["files"],
                      remote_storage.describe(self.remote_conn))
             return
+        t0 = time.perf_counter()
         if os.environ.get("TPI_PUSH_LINK", "") in ("1", "true", "yes"):
-            # hard links instead of copies (no snapshot: see storage.link_tree)
-            storage.link_tree(directory, self.data_dir, self.spec.environment.exclude_list)
+            # hard links instead of copies (opt-in: no snapshot, see storage.link_tree)
+            st = storage.link_tree(directory, self.data_dir, self.spec.environment.exclude_list)
+            self._event("pushed", "%d files" % (st["linked"] + st["copied"]),
+                        "%d bytes" % st["bytes"], "%.3f s" % (time.perf_counter() - t0),
+                        "hard links %d" % st["linked"])
             return
-        storage.transfer(directory, self.data_dir, self.spec.environment.exclude_list)
+        # the default: a snapshot of the workdir -- each file reflinked (FICLONE: shared
+        # extents, copy-on-write) where the filesystem can, else copied by 16 threads
+        st = storage.transfer(directory, self.data_dir, self.spec.environment.exclude_list)
+        self._event("pushed", "%d files" % st.get("files", 0), "%d bytes" % st.get("bytes", 0),
+                    "%.3f s" % (time.perf_counter() - t0),
+                    "reflinked %d" % st.get("cloned", 0))
 
     def _restore_remote(self) -> None:
         stats = remote_storage.open_remote(self.remote_conn).get_tree("data", self.data_dir,

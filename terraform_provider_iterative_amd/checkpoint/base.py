@@ -3,7 +3,15 @@ process that publishes a streamed save is still alive."""
 from __future__ import annotations
 
 import os
+import struct
 from dataclasses import dataclass
+
+# The region / file format (``checkpointer`` module docstring): magic and preamble, and the
+# streamed save's progress block (magic, then state 1 streaming / 2 complete / 3 failed).
+MAGIC = b"TPICKPT2"
+PREAMBLE = 32
+PROGRESS_MAGIC = struct.unpack("<Q", b"TPIPROG1")[0]
+STREAM_RUNNING, STREAM_COMPLETE, STREAM_FAILED = 1, 2, 3
 
 
 class CheckpointError(RuntimeError):

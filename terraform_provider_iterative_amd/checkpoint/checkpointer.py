@@ -48,24 +48,18 @@ from ..ops import hip, native
 from ..ops.packing import PackPlan, TensorEntry, align_up
 from ..ops.packing import pack as host_pack, unpack as host_unpack
 from . import host
-from .base import CheckpointError, TransferResult, _writer_alive
+from .base import (MAGIC, PREAMBLE, PROGRESS_MAGIC, STREAM_COMPLETE,  # noqa: F401
+                   STREAM_FAILED, STREAM_RUNNING, CheckpointError, TransferResult,
+                   _writer_alive)
 from .handoff import (FDS_PER_MESSAGE, HBM_ROUTES, IPC_MAX_ALLOC, RELOCATE_CHUNK,
                       HbmHandoff)
 from .engine import (MODES, DeviceEngine, _engine_pool, _take_engine,  # noqa: F401
                      prewarm_engine)
 from .host import HostRegion
+from .materialize import ALLOC_HEADROOM, ALLOC_LOOKAHEAD, Materializer  # noqa: F401
+from .persist import FILE_THREADS, LOAD_CHUNK, Persistence, _local_scratch  # noqa: F401
 
-MAGIC = b"TPICKPT2"
-PREAMBLE = 32
-FILE_THREADS = 16        # persist / load: native pwrite/pread threads
-LOAD_CHUNK = 256 << 20   # load: bytes read (and published to the restore) per step
-PROGRESS_MAGIC = struct.unpack("<Q", b"TPIPROG1")[0]
-STREAM_RUNNING, STREAM_COMPLETE, STREAM_FAILED = 1, 2, 3
 CODECS = ("none", "tpz1")
-
-
-ALLOC_HEADROOM = 512 << 20  # materialize(): free HBM beyond a tensor's size before allocating it
-ALLOC_LOOKAHEAD = 3  # materialize(): groups allocated ahead of the restore once HBM runs short
 
 
 def _layout(header_cap: int, entries_len: int, ntiles: int, total: int, tile_bytes: int):
@@ -114,15 +108,6 @@ def region_total(path: str) -> Optional[int]:
         return None
 
 
-def _local_scratch(remote_path: str) -> str:
-    """Where a checkpoint bound for (or fetched from) another node is staged on this one:
-    ``TPI_PERSIST_TMPDIR``, else the task directory, else the temp directory."""
-    base = (os.environ.get("TPI_PERSIST_TMPDIR") or os.environ.get("TPI_TASK_DIRECTORY")
-            or tempfile.gettempdir())
-    return os.path.join(base, ".tpi-persist-%d-%s" % (os.getpid(),
-                                                     os.path.basename(remote_path) or "ckpt"))
-
-
 class PendingSave:
     """An asynchronous save in flight (:meth:`Checkpointer.save_async`)."""
 
@@ -162,7 +147,7 @@ class _Slot:
         self.digests_valid = False   # ... describes what the slot holds right now
 
 
-class Checkpointer(HbmHandoff):
+class Checkpointer(HbmHandoff, Materializer, Persistence):
     """Save/restore a fixed set of tensors through one host region.
 
     ``path=None`` keeps the spill in anonymous host DRAM (lives as long as this object);
@@ -811,480 +796,12 @@ class Checkpointer(HbmHandoff):
                                                                       res.first_bad))
         return res
 
-    # -- progressive materialisation: allocate the state while it streams in -----------------
-    @classmethod
-    def materialize(cls, path: str, device: Any = None, *, group_bytes: int = 4 << 30,
-                    stream_timeout: Optional[float] = None,
-                    memory_timeout: Optional[float] = None,
-                    **kwargs) -> Tuple["Checkpointer", Dict[str, Any], TransferResult]:
-        """Create the tensors a checkpoint region holds and restore them, group by group.
-
-        For a successor whose state does not fit next to its predecessor's on one GPU (a
-        170 GB rank on 288 GB of HBM): instead of allocating the whole state up front -- which
-        waits until the predecessor has spilled *and* freed all of it -- each group of about
-        ``group_bytes`` is allocated as soon as the device has room for it (a background
-        thread retries the allocation while the predecessor frees its tensors behind its
-        spill, ``save(release_behind=True)``) and restored at once, behind the predecessor's
-        streamed save when one is still running.  Allocation, the driver's clearing of the
-        freed HBM, the spill and the restore then overlap instead of running one after the
-        other.  Tensors come back contiguous, with the saved names, shapes and dtypes; the
-        returned checkpointer is bound to them (later saves go to the same region).
-        ``device`` may be ``"cpu"`` (host tensors, complete checkpoints only).
-        ``memory_timeout`` (default ``TPI_STREAM_TIMEOUT`` or 30 s): give up when no
-        allocation has succeeded for that long.  Returns ``(checkpointer, tensors, result)``.
-        """
-        import torch
-
-        t0 = time.perf_counter()
-        layout = _region_layout(path)
-        dev = torch.device(device if device is not None else "cuda")
-        if dev.type == "cuda" and dev.index is None:
-            dev = torch.device("cuda", torch.cuda.current_device())
-        entries = [TensorEntry.from_json(e) for e in layout["entries"]]
-        plan = PackPlan.from_entries(entries, layout["total"], layout["tile_bytes"])
-        plan.device = str(dev)
-        plan._bound = []
-        kwargs.setdefault("codec", layout["codec"])
-        t1 = time.perf_counter()
-        ck = cls(None, path, tile_bytes=layout["tile_bytes"], slots=layout["slots"], _plan=plan,
-                 **kwargs)
-        try:
-            if ck._entries_digest != layout["entries_sha256"] or ck.size != layout["size"]:
-                raise CheckpointError("%s: region layout not reproducible from its entries"
-                                      % path)
-            t2 = time.perf_counter()
-            if ck.engine is not None:  # before the predecessor's freeing makes hipMalloc slow
-                ck.engine.reserve(len(entries) + 1, plan.ntiles, layout["codec"] == "tpz1")
-                # TPI_MATERIALIZE_H2D=sdma: the restore's host-to-device copies on an SDMA
-                # engine of their own (profiles/round4/materialize_170g.md)
-                ck.h2d_engine = ck.engine.set_h2d_sdma(
-                    os.environ.get("TPI_MATERIALIZE_H2D", "hip") == "sdma")
-            ck._setup_times = {"layout": round(t1 - t0, 4), "checkpointer": round(t2 - t1, 4),
-                               "reserve": round(time.perf_counter() - t2, 4)}
-            tensors, res = ck._materialize(dev, group_bytes, stream_timeout, memory_timeout)
-        except BaseException:
-            ck.close()
-            raise
-        return ck, tensors, res
-
-    def _groups(self, group_bytes: int) -> List[Tuple[int, int]]:
-        """Entry index ranges ``[lo, hi)`` of about ``group_bytes`` each, in stream order."""
-        out, lo, acc = [], 0, 0
-        for i, e in enumerate(self.plan.entries):
-            acc += e.nbytes
-            if acc >= group_bytes or i == len(self.plan.entries) - 1:
-                out.append((lo, i + 1))
-                lo, acc = i + 1, 0
-        return out
-
-    def _sub_plan(self, lo: int, hi: int, tensors: Sequence[Any],
-                  lead: Any) -> Tuple[PackPlan, int, int]:
-        """(plan, first tile, end tile) of entries ``[lo, hi)``: the tiles that hold them, the
-        plan's offsets relative to the first tile.  Neighbouring groups may share a boundary
-        tile; each restore scatters only its own tensors from it.  The bytes of the first tile
-        before the group's first tensor (the previous group's tail) land in ``lead``, a
-        scratch buffer of one tile: the device kernels need a segment at offset 0."""
-        tile = self.plan.tile_bytes
-        group = self.plan.entries[lo:hi]
-        ta = group[0].offset // tile
-        tb = min(self.plan.ntiles, -(-(group[-1].offset + group[-1].nbytes) // tile))
-        base = ta * tile
-        entries = [TensorEntry(e.name, e.dtype, e.shape, e.nbytes, e.offset - base)
-                   for e in group]
-        named = {e.name: t for e, t in zip(group, tensors)}
-        gap = group[0].offset - base
-        if gap:
-            entries.insert(0, TensorEntry("\0lead", "uint8", (gap,), gap, 0))
-            named = dict([("\0lead", lead[:gap])] + list(named.items()))
-        sub = PackPlan.from_entries(entries, min(self.plan.total, tb * tile) - base, tile)
-        sub.bind(named)
-        return sub, ta, tb
-
-    def _materialize(self, dev, group_bytes: int, stream_timeout: Optional[float],
-                     memory_timeout: Optional[float]) -> Tuple[Dict[str, Any], TransferResult]:
-        import torch
-
-        t_start = time.perf_counter()
-        self.wait_pending()
-        found = self._streaming()
-        streaming = found is not None
-        if found is None:
-            found = self._active()
-        if found is None:
-            raise CheckpointError("no checkpoint to materialize in %s" % self.path)
-        slot, header = found
-        self._check_compatible(header)
-        early_fallback = None
-        if streaming and self.engine is None:
-            streaming = False  # host tensors: wait for the whole spill first
-            try:
-                self._restore_streaming_wait(slot, stream_timeout)
-                header = self._slot_header(slot) or header
-            except CheckpointError as error:  # a two-slot region's older copy, if any
-                older = self._active()
-                if older is None:
-                    raise
-                slot, header = older
-                early_fallback = str(error)
-        zipped = header.get("codec", "none") == "tpz1"
-        if stream_timeout is None:
-            stream_timeout = float(os.environ.get("TPI_STREAM_TIMEOUT", "30"))
-        if memory_timeout is None:
-            memory_timeout = float(os.environ.get("TPI_STREAM_TIMEOUT", "30"))
-        entries = self.plan.entries
-        groups = self._groups(max(1, int(group_bytes)))
-        ready: "queue.Queue[Any]" = queue.Queue()
-        stop = threading.Event()
-        waited = [0.0]
-        # per group, seconds from the start: [allocation start, allocated, restore start, end]
-        trace: List[List[float]] = []
-
-        # torch.empty() holds the GIL while the driver clears just-freed HBM (seconds behind a
-        # big spill), which would stall the restoring thread at its next Python step: allocate
-        # through _tpi_torch.empty (the same caching-allocator call, GIL released) when built
-        try:
-            from ..ops._loader import torch_ext
-
-            empty_nogil = torch_ext().empty
-        except Exception:  # not built: torch.empty (correct, restores may stall behind it)
-            empty_nogil = None
-        likes: Dict[str, Any] = {}
-
-        def empty(e: TensorEntry):
-            dtype = getattr(torch, e.dtype)
-            if empty_nogil is None:
-                return torch.empty(e.shape, dtype=dtype, device=dev)
-            like = likes.get(e.dtype)
-            if like is None:
-                like = likes[e.dtype] = torch.empty(0, dtype=dtype, device=dev)
-            return empty_nogil(list(e.shape), like)
-
-        restored = [0]  # groups restored so far (the main thread counts)
-        # groups that fit in the HBM free right now are allocated at once; the rest -- memory
-        # the predecessor has yet to free -- only ALLOC_LOOKAHEAD groups ahead of the restore:
-        # by then that memory has long been freed, and its hipMalloc does not block the
-        # restore's copies (see the gate below)
-        budget = (torch.cuda.mem_get_info(dev)[0] - ALLOC_HEADROOM) if dev.type == "cuda" \
-            else float("inf")
-        upfront = 0
-        for lo, hi in groups:
-            size = sum(e.nbytes for e in entries[lo:hi])
-            if size > budget:
-                break
-            budget -= size
-            upfront += 1
-
-        lookahead = int(os.environ.get("TPI_ALLOC_LOOKAHEAD", ALLOC_LOOKAHEAD))
-
-        def allocate():  # runs ahead of the restores, as far as the device has room
-            try:
-                if dev.type == "cuda":
-                    torch.cuda.set_device(dev)
-                for gi, (lo, hi) in enumerate(groups):
-                    while (gi >= upfront and restored[0] + lookahead < gi
-                           and not stop.is_set()):
-                        stop.wait(0.002)
-                    out = []
-                    t_group = time.perf_counter()
-                    for e in entries[lo:hi]:
-                        last = time.monotonic()
-                        while True:
-                            if stop.is_set():
-                                return
-                            # ask before allocating: a hipMalloc that has to wait for memory
-                            # the predecessor is still freeing blocks for up to a second
-                            # inside the HIP runtime, and holds up this process's
-                            # hipMemcpyAsync calls -- the restore's -- all that time (HIP API
-                            # trace, profiles/round4/materialize_170g.md)
-                            if (dev.type == "cuda" and time.monotonic() - last <= memory_timeout
-                                    and torch.cuda.mem_get_info(dev)[0]
-                                    < e.nbytes + ALLOC_HEADROOM):
-                                t = time.monotonic()
-                                stop.wait(0.002)
-                                waited[0] += time.monotonic() - t
-                                continue
-                            try:
-                                out.append(empty(e))
-                                break
-                            except RuntimeError as error:  # torch's OOM error included
-                                if "out of memory" not in str(error).lower():
-                                    raise
-                                # the predecessor is still freeing (behind its spill)
-                                if time.monotonic() - last > memory_timeout:
-                                    raise CheckpointError(
-                                        "no room for %s (%.1f GB) within %.0f s" % (
-                                            e.name, e.nbytes / 1e9, memory_timeout))
-                                t = time.monotonic()
-                                stop.wait(0.002)
-                                waited[0] += time.monotonic() - t
-                    trace.append([round(t_group - t_start, 4),
-                                  round(time.perf_counter() - t_start, 4)])
-                    ready.put(out)
-            except BaseException as error:  # surfaced by the restoring thread
-                ready.put(error)
-
-        t_lead = time.perf_counter()
-        lead = torch.empty(self.plan.tile_bytes, dtype=torch.uint8, device=dev)
-        setup = dict(getattr(self, "_setup_times", {}), lead=round(time.perf_counter() - t_lead, 4),
-                     find=round(t_lead - t_start, 4))
-        worker = threading.Thread(target=allocate, name="tpi-materialize-alloc", daemon=True)
-        worker.start()
-        tensors: Dict[str, Any] = {}
-        total = TransferResult(self.plan.total, 0.0, wire_bytes=0)
-        src = {"slot": slot, "header": header, "zipped": zipped, "streaming": streaming}
-        done: List[Tuple[int, int, List[Any]]] = []  # restored groups, for a fallback
-        fallback = early_fallback
-
-        def restore_group(lo: int, hi: int, item: List[Any]) -> TransferResult:
-            slot, zipped = src["slot"], src["zipped"]
-            sub, ta, tb = self._sub_plan(lo, hi, item, lead)
-            crcs = slot.crcs[ta:tb]
-            csizes = slot.csizes[ta:tb] if zipped else None
-            # earlier tiles are in host memory: the previous group waited for them
-            start = int(slot.csizes[:ta].sum(dtype=np.uint64)) if zipped \
-                else ta * self.plan.tile_bytes
-            stream_base = self.region.addr + slot.base + self.stream_offset
-            if self.engine is not None:
-                sig = torch.cuda.current_stream(dev).cuda_stream
-                if src["streaming"]:
-                    from ..ops._loader import HipError
-
-                    try:
-                        res = self.engine.restore_stream(
-                            sub, stream_base + start, crcs, csizes,
-                            slot.progress.ctypes.data + 16, stream_timeout, sig, tile_base=ta)
-                    except HipError as error:
-                        raise CheckpointError(str(error)) from error
-                elif zipped:
-                    res = self.engine.restore_z(sub, stream_base + start, crcs, csizes, sig)
-                else:
-                    res = self.engine.restore(sub, stream_base + start, crcs, self.mode, sig)
-            else:
-                t0 = time.perf_counter()
-                if zipped:
-                    nbytes = int(csizes.sum(dtype=np.uint64))
-                    stream, _ = tpz.decode(self.region.array(
-                        slot.base + self.stream_offset + start, nbytes),
-                        csizes, sub.total, self.plan.tile_bytes)
-                else:
-                    nbytes = sub.total
-                    stream = self.region.array(slot.base + self.stream_offset + start,
-                                               sub.total)
-                bad, first = host_unpack(sub, stream, crcs)
-                res = TransferResult(sub.total, time.perf_counter() - t0, 0, bad, first,
-                                     wire_bytes=nbytes)
-            if res.bad_tiles:
-                res.first_bad += ta
-            return res
-
-        try:
-            for gi, (lo, hi) in enumerate(groups):
-                item = ready.get()
-                if isinstance(item, BaseException):
-                    raise item
-                t_group = time.perf_counter()
-                try:
-                    res = restore_group(lo, hi, item)
-                except CheckpointError as error:
-                    # the predecessor's streamed save failed (or its writer died): fall back
-                    # to the complete copy a two-slot region still holds -- every group
-                    # again, so the state is one generation throughout
-                    older = self._active() if src["streaming"] else None
-                    if older is None:
-                        raise
-                    self._check_compatible(older[1])
-                    fallback = str(error)
-                    src.update(slot=older[0], header=older[1], streaming=False,
-                               zipped=older[1].get("codec", "none") == "tpz1")
-                    total = TransferResult(self.plan.total, 0.0, wire_bytes=0)
-                    for lo2, hi2, item2 in done:
-                        again = restore_group(lo2, hi2, item2)
-                        total.chunks += again.chunks
-                        total.wire_bytes += again.wire_bytes
-                        if again.bad_tiles:
-                            total.bad_tiles += again.bad_tiles
-                            total.first_bad = again.first_bad if total.first_bad < 0 \
-                                else total.first_bad
-                    res = restore_group(lo, hi, item)
-                total.chunks += res.chunks
-                total.wire_bytes += res.wire_bytes
-                if res.bad_tiles:
-                    total.bad_tiles += res.bad_tiles
-                    if total.first_bad < 0:
-                        total.first_bad = res.first_bad
-                done.append((lo, hi, item))
-                for e, t in zip(entries[lo:hi], item):
-                    tensors[e.name] = t
-                restored[0] = gi + 1
-                trace[gi] += [
-                    round(t_group - t_start, 4), round(time.perf_counter() - t_start, 4)]
-        finally:
-            stop.set()
-            worker.join()
-        slot, header, streaming = src["slot"], src["header"], src["streaming"]
-        self.plan.bind(tensors)
-        total.seconds = time.perf_counter() - t_start
-        total.crc = int(header.get("crc32c", 0)) if not streaming else \
-            native().crc32c_combine_tiles_ptr(slot.crcs.ctypes.data, self.plan.ntiles,
-                                              self.plan.tile_bytes, self.plan.total)
-        self.materialize_stats = {"groups": len(groups), "upfront_groups": upfront,
-                                  "alloc_wait_s": round(waited[0], 4),
-                                  "streamed": streaming, "trace": trace, "setup": setup,
-                                  "fallback": fallback,
-                                  "h2d_engine": getattr(self, "h2d_engine", None),
-                                  "alloc": "nogil" if empty_nogil is not None else "torch"}
-        self.materialized_metadata = header.get("metadata", {})
-        self.last_restore = total
-        if total.bad_tiles:
-            raise CheckpointError("%d corrupt tile(s), first at %d" % (total.bad_tiles,
-                                                                      total.first_bad))
-        return tensors, total
-
-    def _restore_streaming_wait(self, slot: _Slot, timeout: Optional[float]) -> None:
-        """Host path of a streamed checkpoint: wait until its writer completed it."""
-        if timeout is None:
-            timeout = float(os.environ.get("TPI_STREAM_TIMEOUT", "30"))
-        prog = slot.progress
-        last, seen = time.monotonic(), -1
-        while int(prog[4]) != STREAM_COMPLETE:
-            if int(prog[4]) == STREAM_FAILED:
-                raise CheckpointError("the streamed checkpoint failed in its writer")
-            if int(prog[2]) != seen:
-                seen, last = int(prog[2]), time.monotonic()
-            elif time.monotonic() - last > timeout:
-                raise CheckpointError("streamed checkpoint stalled (writer gone?)")
-            time.sleep(0.001)
-
     def _check_compatible(self, header: Dict) -> None:
         if (header["total"] != self.plan.total or header["tile_bytes"] != self.plan.tile_bytes
                 or header.get("stream_offset") != self.stream_offset
                 or header.get("crc_offset") != self.crc_offset
                 or header.get("entries_sha256") != self._entries_digest):
             raise CheckpointError("checkpoint layout does not match the bound tensors")
-
-    def persist(self, path: str) -> str:
-        """Write the current checkpoint (header, CRCs, stream: one slot) to ``path``
-        atomically.  ``path`` may name a file on another node or in a bucket (``ssh://host/dir/
-        file``, ``host:/dir/file``, ``s3://``/``gs://``/``az://bucket/key``: an off-node
-        ``storage.container``, :mod:`..storage.remote`); the slot then goes there straight
-        from the host region, with no local temporary file."""
-        from ..storage import remote
-
-        self.wait_pending()
-        active = self._active()
-        if active is None:
-            raise CheckpointError("nothing saved yet")
-        slot, header = active
-        if remote.is_remote(path):
-            nbytes = self.stream_offset + int(header["stream_bytes"])
-            view = memoryview((ctypes.c_char * nbytes).from_address(
-                self.region.addr + slot.base)).cast("B")
-            remote.store_bytes(view, path)
-            return path
-        tmp = path + ".tpi-partial"
-        # parallel pwrite of the slot (native, GIL released) + fsync, then an atomic rename
-        native().write_file_ptr(tmp, self.region.addr + slot.base,
-                                self.stream_offset + int(header["stream_bytes"]),
-                                FILE_THREADS, True)
-        os.replace(tmp, path)
-        return path
-
-    def load(self, path: str) -> TransferResult:
-        """Read a persisted checkpoint file into the region (the slot a save would write, so
-        a bad file leaves the current checkpoint intact with ``slots=2``) and restore it.
-
-        The stream section is read by parallel native readers in chunks that are published
-        like a streamed save's (progress block), so the device restore runs behind the file
-        read instead of after it.  ``path`` may name a file on another node (see
-        :meth:`persist`): an object in a bucket is read in place by ranged requests, streamed
-        the same way; a file on an SSH node is fetched first."""
-        from ..storage import remote
-
-        obj = None
-        if remote.is_remote(path):
-            obj = remote.object_source(path)
-            if obj is None:
-                tmp = remote.fetch(path, os.path.dirname(_local_scratch(path)))
-                try:
-                    return self.load(tmp)
-                finally:
-                    os.remove(tmp)
-        self.wait_pending()
-        self._wait_writers()
-        slot, generation = self._target()
-        if obj is None:
-            with open(path, "rb") as f:
-                head = np.frombuffer(f.read(PREAMBLE + self.header_cap), np.uint8)
-                size = os.fstat(f.fileno()).st_size
-        else:
-            size = obj[0].size(obj[1])
-            if size is None:
-                raise CheckpointError("no checkpoint at %s" % path)
-            head = np.frombuffer(obj[0].read(obj[1], 0, min(size, PREAMBLE + self.header_cap)),
-                                 np.uint8)
-        header = self.read_header(head)
-        self._check_compatible(header)
-        if not header.get("complete"):
-            raise CheckpointError("%s holds an incomplete checkpoint" % path)
-        stream_bytes = int(header["stream_bytes"])
-        end = self.stream_offset + stream_bytes
-        if size < end:
-            raise CheckpointError("%s is truncated (%d of %d bytes)" % (path, size, end))
-        self._invalidate(slot)
-        # entries + CRCs + blob sizes first (small), then the stream, streamed
-        if obj is None:
-            native().read_stream_ptr(path, self.region.addr + slot.base + self.entries_offset,
-                                     self.entries_offset,
-                                     self.stream_offset - self.entries_offset,
-                                     FILE_THREADS, 64 << 20, 0, 0, 0)
-        else:
-            obj[0].read_into(obj[1], self.region.addr + slot.base + self.entries_offset,
-                             self.entries_offset, self.stream_offset - self.entries_offset)
-        if header.get("codec", "none") == "tpz1":
-            tile_ends = np.cumsum(slot.csizes.astype(np.uint64), dtype=np.uint64)
-            if len(tile_ends) and int(tile_ends[-1]) != stream_bytes:
-                raise CheckpointError("%s: blob sizes do not add up to the stream" % path)
-        else:
-            tile_ends = np.minimum(np.arange(1, self.plan.ntiles + 1, dtype=np.uint64)
-                                   * np.uint64(self.plan.tile_bytes), np.uint64(self.plan.total))
-        header["generation"] = generation  # newest once complete; written last, like a save
-        prog = slot.progress
-        prog[1], prog[2], prog[3], prog[5] = generation, 0, 0, os.getpid()
-        prog[4] = STREAM_RUNNING
-        prog[0] = PROGRESS_MAGIC
-        self._write_header(slot, dict(header, complete=False, streaming=True))
-        failure: list = []
-
-        def publish(done: int) -> None:  # as read_stream's words: bytes, then whole tiles
-            prog[3] = done
-            prog[2] = int(np.searchsorted(tile_ends, np.uint64(done), side="right"))
-
-        def read():
-            try:
-                if obj is None:
-                    native().read_stream_ptr(path,
-                                             self.region.addr + slot.base + self.stream_offset,
-                                             self.stream_offset, stream_bytes, FILE_THREADS,
-                                             LOAD_CHUNK, prog.ctypes.data + 16,
-                                             tile_ends.ctypes.data, len(tile_ends))
-                else:
-                    obj[0].read_into(obj[1], self.region.addr + slot.base + self.stream_offset,
-                                     self.stream_offset, stream_bytes, publish)
-                self._write_header(slot, header)
-                prog[4] = STREAM_COMPLETE
-            except BaseException as error:  # the restore sees FAILED and raises
-                failure.append(error)
-                prog[4] = STREAM_FAILED
-
-        reader = threading.Thread(target=read, name="tpi-load", daemon=True)
-        reader.start()
-        try:
-            res = self.restore()
-        finally:
-            reader.join()
-        if failure:
-            raise CheckpointError("loading %s failed: %s" % (path, failure[0]))
-        return res
 
     def release_device(self) -> int:
         """A preempted rank after its save: free the HBM this checkpointer and its bound

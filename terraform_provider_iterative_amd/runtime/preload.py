@@ -10,8 +10,17 @@ environment once the rank has run a while, it imports and then blocks on its act
 ("go port=<rendezvous port>"); it then runs the script exactly as ``python script`` would:
 ``__main__``, ``sys.argv``, ``sys.path[0]`` the script's directory, exit status from
 ``SystemExit`` or an uncaught exception.  It never touches the GPU before activation (nothing
-here initialises HIP unless ``TPI_PRELOAD=gpu``), so the script's own ``HIP_VISIBLE_DEVICES``
-and device choices hold.
+here initialises HIP unless ``TPI_PRELOAD=gpu``/``gpu-lite``, or -- the default -- until the
+supervisor has seen the running incarnation use the GPU from its main process alone: then it
+writes "warm" and this process creates its GPU context while parked (``gpu-lite``, ~0.13 s off
+the cold recovery); a script whose other processes hold the GPU keeps a plain successor, since
+workers it forks before touching the GPU could not use an inherited context).  So the
+script's own ``HIP_VISIBLE_DEVICES`` and device choices hold.
+
+The parked process has imported PyTorch before the script runs: environment variables a script
+sets before ``import torch`` to configure it (``OMP_NUM_THREADS``, allocator settings) do not
+reach a preloaded successor -- set them in the task's ``environment`` block instead, or use
+``TPI_PRELOAD=0``.  It waits outside the rank's memory cgroup and joins it when activated.
 EOF on the pipe (the rank finished, the task stopped): it exits quietly.
 
 Reference: a spot VM's replacement boots and runs the machine script from the start
@@ -26,17 +35,27 @@ import sys
 import time
 
 
-def _read_go(fd: int) -> str:
+def _read_go(fd: int, on_warm=None) -> str:
+    """The activation line ("go port=N"; "" at EOF).  A "warm" line before it -- the
+    supervisor's evidence that the script uses the GPU from its main process only
+    (``supervisor.cpp`` ``check_preload_evidence``) -- calls ``on_warm`` and keeps waiting."""
     data = b""
-    while not data.endswith(b"\n"):
+    while True:
+        while b"\n" in data:
+            line, data = data.split(b"\n", 1)
+            text = line.decode(errors="replace").strip()
+            if text == "warm":
+                if on_warm is not None:
+                    on_warm()
+                continue
+            return text
         try:
             chunk = os.read(fd, 256)
         except InterruptedError:
             continue
         if not chunk:
-            break
+            return data.decode(errors="replace").strip()
         data += chunk
-    return data.decode(errors="replace").strip()
 
 
 def _warm_gpu(engine: bool = True) -> None:
@@ -69,7 +88,7 @@ def main(argv=None, gpu=False) -> None:
     import torch  # noqa: F401  -- the point: the import a successor would wait for
 
     import terraform_provider_iterative_amd.checkpoint  # noqa: F401
-    from terraform_provider_iterative_amd.checkpoint import preemption  # noqa: F401
+    from terraform_provider_iterative_amd.checkpoint import preemption
     if gpu:
         try:
             _warm_gpu(engine=gpu != "lite")
@@ -77,7 +96,21 @@ def main(argv=None, gpu=False) -> None:
             print("tpi-preload: GPU warm-up failed: %s" % error, file=sys.stderr, flush=True)
     preloaded_s = time.time() - t0
     fd = int(os.environ.get("TPI_STANDBY_FD", "4"))
-    line = _read_go(fd)
+    warmed = []
+
+    def warm() -> None:  # the supervisor saw the rank use the GPU from one process only
+        if gpu or warmed:
+            return
+        t1 = time.time()
+        try:
+            _warm_gpu(engine=False)
+            warmed.append(time.time() - t1)
+            preemption.journal("preload-gpu-warmed", "GPU context %.3f s" % warmed[0])
+        except Exception as error:  # the successor initialises it itself after activation
+            print("tpi-preload: GPU warm-up failed: %s" % error, file=sys.stderr, flush=True)
+            warmed.append(-1.0)
+
+    line = _read_go(fd, warm)
     try:
         os.close(fd)
     except OSError:
@@ -90,6 +123,8 @@ def main(argv=None, gpu=False) -> None:
     for name in ("TPI_STANDBY", "TPI_STANDBY_FD"):
         os.environ.pop(name, None)
     os.environ["TPI_PRELOADED"] = "%.3f" % preloaded_s
+    if warmed:
+        os.environ["TPI_PRELOAD_GPU_WARMED"] = "%.3f" % warmed[0]
     if os.environ.get("TPI_DEADLINE"):  # set at spawn; the time left is that of now
         try:
             os.environ["TPI_REMAINING_RUN_TIME"] = str(

@@ -124,7 +124,14 @@ def test_preempted_training_resumes_in_a_preloaded_successor_on_gpu(cloud, tmp_p
             e.code == "standby-start" and "preloaded" in e.description for e in task.events()):
         time.sleep(0.1)
     assert any(e.code == "standby-start" for e in task.events()), task.logs()
-    time.sleep(4.0)  # its imports; it then parks
+    # the default (TPI_PRELOAD=1 = auto): the rank's main process alone holds
+    # /dev/kfd, so the supervisor has the parked successor create its GPU context (gpu-lite)
+    while time.time() < deadline and not any(e.code == "preload-gpu-warm"
+                                             for e in task.events()):
+        time.sleep(0.1)
+    assert any(e.code == "preload-gpu-warm" for e in task.events()), [
+        (e.code, e.description) for e in task.events()]
+    time.sleep(4.0)  # its imports and its GPU context; it then parks
     task.preempt()
     status = task.wait(300)
     logs = task.logs()
@@ -134,8 +141,10 @@ def test_preempted_training_resumes_in_a_preloaded_successor_on_gpu(cloud, tmp_p
     resumed = [l for l in logs[1].splitlines() if "resumed from step" in l]
     assert resumed and int(resumed[0].rsplit(" ", 1)[1]) >= 1, logs[1]
     assert "done" in logs[1]
-    assert any(e.code == "rank-start" and "warm standby" in e.description
-               for e in task.events())
+    assert any(e.code == "rank-start" and "warm standby" in e.description and
+               "GPU warmed" in e.description for e in task.events()), [
+        (e.code, e.description) for e in task.events()]
+    assert not any(e.code == "preload-plain" for e in task.events())
     task.delete()
 
 

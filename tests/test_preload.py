@@ -251,3 +251,78 @@ def test_an_unused_preloaded_successor_leaves_no_log(tmp_path):
     logs = task.logs()
     assert len(logs) == 1 and "working" in logs[0], logs
     task.delete()
+
+
+EVIDENCE = r'''#!%(python)s
+import os, sys, time
+restart = int(os.environ["TPI_RESTART_COUNT"])
+if restart == 0:
+    dev = open(%(device)r, "rb")  # "initialises the GPU": the main process holds the device
+    if %(fork)r and os.fork() == 0:  # a worker forked after that holds it too
+        while True:
+            time.sleep(0.05)
+    print("incarnation 0 holds the device", flush=True)
+    while True:
+        time.sleep(0.05)
+print("incarnation %%d warmed %%s" %% (restart, os.environ.get("TPI_PRELOAD_GPU_WARMED")),
+      flush=True)
+'''
+
+
+def _evidence_task(tmp_path, fork, name):
+    device = tmp_path / "fake-kfd"
+    device.write_bytes(b"")
+    cloud = Cloud(provider="local",
+                  credentials=Credentials(node=NodeCredentials(state_root=str(tmp_path / "st"))))
+    spec = Task(environment=Environment(
+        script=EVIDENCE % {"python": sys.executable, "device": str(device), "fork": fork},
+        timeout=120, variables=Variables({"TPI_TASK": "true", "TPI_PRELOAD": "1",
+                                          "TPI_MAX_RESTARTS": "1",
+                                          "TPI_PRELOAD_GPU_DEVICE": str(device)})))
+    return backends.new(cloud, new_deterministic_identifier(name), spec)
+
+
+def test_the_preloaded_successor_warms_its_gpu_on_evidence(tmp_path):
+    """VERDICT r5 #4: the default cold successor gets its GPU context before the preemption
+    when the running rank shows it is safe -- its main process alone holds the GPU device
+    (faked here by a file, ``TPI_PRELOAD_GPU_DEVICE``) -- and the activation names it."""
+    task = _evidence_task(tmp_path, False, "preload-evidence")
+    task.create()
+    try:
+        warm = _wait_event(task, lambda e: e.code == "preload-gpu-warm", 60)
+        assert "alone holds" in " ".join(warm.description)
+        time.sleep(2.0)  # the parked successor finishes importing (and tries its warm-up)
+        task.preempt()
+        status = task.wait(60)
+    finally:
+        logs = "\n".join(task.logs())
+    assert status["succeeded"] == 1, (status, logs)
+    line = next(l for l in logs.splitlines() if "incarnation 1" in l)
+    assert "warmed None" not in line, line  # the successor did run its warm-up (no GPU: -1)
+    starts = [e for e in task.events() if e.code == "rank-start" and "restart 1" in e.description]
+    assert starts and "GPU warmed" in starts[0].description, starts
+    assert not any(e.code == "preload-plain" for e in task.events())
+    task.delete()
+
+
+def test_a_script_whose_workers_hold_the_gpu_keeps_a_plain_successor(tmp_path):
+    """A script with other processes on the GPU (forked workers, or a fork after the GPU was
+    initialised) gets a plain preloaded successor: no context inherited by what it forks."""
+    task = _evidence_task(tmp_path, True, "preload-plain")
+    task.create()
+    try:
+        plain = _wait_event(task, lambda e: e.code == "preload-plain", 60)
+        assert "2 processes of the rank hold" in " ".join(plain.description)
+        time.sleep(1.5)
+        assert not any(e.code == "preload-gpu-warm" for e in task.events())
+        task.preempt()
+        status = task.wait(60)
+    finally:
+        logs = "\n".join(task.logs())
+    assert status["succeeded"] == 1, (status, logs)
+    line = next(l for l in logs.splitlines() if "incarnation 1" in l)
+    assert "warmed None" in line, line
+    starts = [e for e in task.events() if e.code == "rank-start" and "restart 1" in e.description]
+    assert starts and "preloaded" in starts[0].description and \
+        "GPU warmed" not in starts[0].description, starts
+    task.delete()
