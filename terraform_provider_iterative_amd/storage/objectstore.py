@@ -764,6 +764,17 @@ def rs256_sign(pem: str, message: bytes) -> bytes:
     return s.to_bytes(k, "big")
 
 
+def _range_end(headers: Dict[str, str]) -> int:
+    """Last byte a GCS resumable session has kept, from a 308's ``Range: bytes=0-N`` (-1:
+    no ``Range``, nothing kept yet)."""
+    value = ""
+    for k, v in (headers or {}).items():
+        if k.lower() == "range":
+            value = v
+    m = re.match(r"^bytes=0-(\d+)$", value.strip())
+    return int(m.group(1)) if m else -1
+
+
 def _b64url(data: bytes) -> str:
     return base64.urlsafe_b64encode(data).rstrip(b"=").decode()
 
@@ -870,8 +881,17 @@ class GCSRemote(ObjectRemote):
                 return
 
     def _put(self, key: str, data: bytes, meta: Dict[str, str]) -> None:
-        self._request("POST", self.upload_path, {"uploadType": "media", "name": key},
-                      {"Content-Type": "application/octet-stream"}, data)
+        """One request: a multipart upload, so the object gets its metadata (mtime) as on
+        the S3 and Azure paths (``uploadType=media`` would drop it)."""
+        boundary = "tpi-" + os.urandom(12).hex()
+        head = json.dumps({"name": key, "metadata": meta}).encode()
+        body = b"".join([
+            b"--", boundary.encode(), b"\r\nContent-Type: application/json; charset=UTF-8\r\n\r\n",
+            head, b"\r\n--", boundary.encode(),
+            b"\r\nContent-Type: application/octet-stream\r\n\r\n", data,
+            b"\r\n--", boundary.encode(), b"--\r\n"])
+        self._request("POST", self.upload_path, {"uploadType": "multipart", "name": key},
+                      {"Content-Type": "multipart/related; boundary=" + boundary}, body)
 
     def _get(self, key: str, start: int, end: int) -> bytes:
         status, _, data = self._request("GET", self._object(key), {"alt": "media"},
@@ -891,18 +911,35 @@ class GCSRemote(ObjectRemote):
         path = location.path
         params = dict(urllib.parse.parse_qsl(location.query, keep_blank_values=True))
         part = max(256 << 10, self.part // (256 << 10) * (256 << 10))
-        for offset in range(0, size, part):
+        offset, stalls = 0, 0
+        while offset < size:
             n = min(part, size - offset)
             with self._slots:
                 body = self._read(local, offset, n)
-                status, _, _ = self._request(
+                status, rh, _ = self._request(
                     "PUT", path, params,
                     {"Content-Range": "bytes %d-%d/%d" % (offset, offset + n - 1, size)}, body,
                     ok=(200, 201, 308))
-            last = offset + n >= size
-            if (status in (200, 201)) != last:
-                raise ObjectStoreError("%s: resumable upload of %s answered %d at %d" % (
-                    self, key, status, offset))
+            if status in (200, 201):
+                if offset + n < size:
+                    raise ObjectStoreError("%s: resumable upload of %s finished early at %d"
+                                           % (self, key, offset + n))
+                return
+            # 308: the session kept bytes [0, N] -- possibly less than was sent (a retried or
+            # cut-off PUT); resume from N + 1, never from where this loop thought it was
+            got = _range_end(rh) + 1
+            if got <= offset:
+                stalls += 1
+                if stalls > _Http.RETRIES:
+                    raise ObjectStoreError("%s: resumable upload of %s stuck at %d" % (
+                        self, key, got))
+            else:
+                stalls = 0
+            if got > offset + n:
+                raise ObjectStoreError("%s: resumable upload of %s: server kept %d bytes, "
+                                       "%d were sent" % (self, key, got, offset + n))
+            offset = got
+        raise ObjectStoreError("%s: resumable upload of %s never completed" % (self, key))
 
     def _delete(self, keys: List[str]) -> None:
         def one(k: str) -> None:

@@ -44,6 +44,7 @@ class Store:
         self.missing_prefix = None  # writes into buckets with this name prefix: 404
         self.pubkey = None    # GCS: PEM of the service account's public key
         self.sa_email = ""
+        self.gcs_short = []   # GCS resumable PUTs: keep this many bytes fewer of the next ones
 
     def bucket(self, service, name):
         return self.objects.setdefault((service, name), {})
@@ -325,10 +326,29 @@ class Handler(BaseHTTPRequestHandler):
             if upload and q.get("uploadType") == "media":
                 objs[q["name"]] = body
                 return self._reply(200, json.dumps({"name": q["name"]}).encode())
+            if upload and q.get("uploadType") == "multipart":
+                ctype = self.headers.get("Content-Type", "")
+                bm = re.match(r"multipart/related; boundary=(\S+)$", ctype)
+                if not bm:
+                    return self._reply(400, b"not multipart/related")
+                sep = b"--" + bm.group(1).encode()
+                parts = [p for p in body.split(sep)[1:] if not p.startswith(b"--")]
+                if len(parts) != 2:
+                    return self._reply(400, b"expected metadata + media")
+                docs = []
+                for part in parts:
+                    head, _, payload = part.partition(b"\r\n\r\n")
+                    docs.append(payload[:-2] if payload.endswith(b"\r\n") else payload)
+                meta = json.loads(docs[0])
+                objs[meta["name"]] = docs[1]
+                st.meta[("gs", bucket, meta["name"])] = dict(meta.get("metadata") or {})
+                return self._reply(200, json.dumps({"name": meta["name"]}).encode())
             if upload and q.get("uploadType") == "resumable" and self.command == "POST":
                 uid = uuid.uuid4().hex
                 st.uploads[uid] = {"name": q["name"], "data": b"",
-                                   "size": int(self.headers["X-Upload-Content-Length"])}
+                                   "size": int(self.headers["X-Upload-Content-Length"]),
+                                   "metadata": dict(json.loads(body or b"{}").get("metadata")
+                                                    or {})}
                 loc = "http://%s:%d/upload/storage/v1/b/%s/o?uploadType=resumable&upload_id=%s" % (
                     self.server.server_address[0], self.server.server_address[1],
                     urllib.parse.quote(bucket), uid)
@@ -339,10 +359,15 @@ class Handler(BaseHTTPRequestHandler):
                 a, b, total = int(r.group(1)), int(r.group(2)), int(r.group(3))
                 if a != len(up["data"]) or total != up["size"] or b - a + 1 != len(body):
                     return self._reply(400, b"bad range")
+                if st.gcs_short:  # the session keeps only part of this chunk
+                    body = body[:max(0, len(body) - st.gcs_short.pop(0))]
                 up["data"] += body
                 if len(up["data"]) < total:
-                    return self._reply(308, headers={"Range": "bytes=0-%d" % b})
+                    kept = len(up["data"])
+                    return self._reply(308, headers={"Range": "bytes=0-%d" % (kept - 1)}
+                                       if kept else {})
                 objs[up["name"]] = up["data"]
+                st.meta[("gs", bucket, up["name"])] = up["metadata"]
                 del st.uploads[q["upload_id"]]
                 return self._reply(200, json.dumps({"name": up["name"]}).encode())
             if not name and self.command == "GET":

@@ -375,3 +375,23 @@ def test_aws_addressing_without_an_endpoint(monkeypatch):
     assert (az.http.netloc, az.prefix_path) == ("acct.blob.core.windows.net", "/ctr")
     gs = remote.open_remote(remote.parse("gs://gb/p", "", {"token": "t"}))
     assert gs.http.netloc == "storage.googleapis.com" and gs.obj_path == "/storage/v1/b/gb/o"
+
+
+def test_gcs_resumes_from_the_range_the_session_kept(tmp_path, fake):
+    """a resumable session may keep only part of a chunk (a retried or cut-off
+    PUT); the upload goes on from the ``Range`` of the 308, not from where it thought it was.
+    Small files go up as a multipart upload with their metadata, like S3 and Azure."""
+    r = remote.open_remote(remote.parse("gs://resume", "", fake.options("googlecloudstorage")))
+    r.part = 256 << 10
+    big = tmp_path / "big.bin"
+    big.write_bytes(os.urandom(5 * (256 << 10) + 1234))
+    fake.store.gcs_short = [1000, 0, 256 << 10]  # 2nd chunk short, 4th chunk kept nothing
+    assert r.put_file(str(big), "big.bin") == big.stat().st_size
+    assert fake.objects("googlecloudstorage", "resume")["big.bin"] == big.read_bytes()
+    assert not fake.store.gcs_short
+    assert "mtime" in " ".join(fake.store.meta[("gs", "resume", "big.bin")]).lower()
+    small = tmp_path / "small.txt"
+    small.write_text("tiny")
+    r.put_file(str(small), "small.txt")
+    assert fake.objects("googlecloudstorage", "resume")["small.txt"] == b"tiny"
+    assert "mtime" in " ".join(fake.store.meta[("gs", "resume", "small.txt")]).lower()
