@@ -37,6 +37,9 @@ from ..storage import transfer as storage
 from ..utils.identifier import Identifier, parse_identifier
 from ..utils.steps import Step, StepTiming, run_steps
 from .base import Task
+from .node_queue import NodeQueue, Queued  # noqa: F401
+from .node_storage import NodeStorage
+from .nodeio import _now, _read_json, _write_json, control_socket  # noqa: F401
 
 log = logging.getLogger("tpi")
 
@@ -51,59 +54,6 @@ PASSTHROUGH_PREFIXES = ("LC_", "HSA_", "HIP_", "ROCR_", "ROCM_", "NCCL_", "RCCL_
 DEFAULT_MASTER_PORT_BASE = 29500
 HBM_MB_PER_GPU = 288 * 1024  # MI355X: 288 GiB of HBM3E per GPU
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-
-
-class Queued(Exception):
-    """Placement could not reserve the machine now: the task waits in the node queue."""
-
-
-def control_socket(sup_dir: str, command: str, timeout: float = 2.0) -> Optional[Dict]:
-    """One request on a supervisor's control socket (``<sup_dir>/control.sock``); the reply as
-    a dict, or None when no supervisor is listening.  The path is reached through
-    ``/proc/self/fd`` because AF_UNIX paths are limited to 108 bytes (the supervisor binds
-    the same way)."""
-    try:
-        dfd = os.open(sup_dir, os.O_RDONLY | os.O_DIRECTORY)
-    except OSError:
-        return None
-    try:
-        with socket.socket(socket.AF_UNIX, socket.SOCK_STREAM) as sock:
-            sock.settimeout(timeout)
-            sock.connect("/proc/self/fd/%d/control.sock" % dfd)
-            sock.sendall(command.encode() + b"\n")
-            chunks = []
-            while True:
-                data = sock.recv(65536)
-                if not data:
-                    break
-                chunks.append(data)
-    except OSError:
-        return None
-    finally:
-        os.close(dfd)
-    try:
-        return json.loads(b"".join(chunks).decode() or "null")
-    except ValueError:
-        return None
-
-
-def _now() -> float:
-    return time.time()
-
-
-def _write_json(path: str, data) -> None:
-    tmp = path + ".tmp"
-    with open(tmp, "w") as handle:
-        json.dump(data, handle, indent=1, sort_keys=True)
-    os.replace(tmp, path)
-
-
-def _read_json(path: str):
-    try:
-        with open(path) as handle:
-            return json.load(handle)
-    except (OSError, ValueError):
-        return None
 
 
 def node_address() -> str:
@@ -124,7 +74,6 @@ def _free_port(start: int) -> int:
             except OSError:
                 continue
     return start
-
 
 
 def shebang_python(script: str):
@@ -198,7 +147,7 @@ def shell_python_command(script: str):
         return None
     return found[0], found[1], argv[1:]
 
-class NodeTask(Task):
+class NodeTask(NodeQueue, NodeStorage, Task):
     """Task on this node; ``provider`` selects CPU-only or GPU placement."""
 
     def __init__(self, cloud: Cloud, identifier: Identifier, task: TaskSpec):
@@ -316,18 +265,6 @@ class NodeTask(Task):
         if machine.gpus and self.provider != PROVIDER_MI355X:
             raise ValueError("GPU machine types need cloud = \"mi355x\"")
 
-    def _create_storage(self) -> None:
-        for d in (self.root, self.reports_dir, self.sup_dir):
-            os.makedirs(d, exist_ok=True)
-        try:
-            os.remove(self._stop_marker())
-        except FileNotFoundError:
-            pass
-        os.makedirs(self.data_dir, exist_ok=True)
-        if self._saved is None:
-            self._saved = self._definition()
-            _write_json(self.task_file, self._saved)
-            self._event("created", "task %s" % self.id)
 
     def _knob(self, name: str, default: str) -> str:
         """Runtime knob: the task's own environment block, else the provider's."""
@@ -351,76 +288,6 @@ class NodeTask(Task):
         except (TypeError, ValueError):
             return False
 
-    def _request(self) -> Optional[Request]:
-        d = self._definition()
-        machine = self._machine()
-        gpus = machine.gpus if self.provider == PROVIDER_MI355X else 0
-        reserve = self.resource_mode() == "reserve"
-        if not gpus and not reserve:
-            return None
-        selectors = parse_region_selectors(self.cloud.region)
-        return Request(task=self.id, parallelism=d["parallelism"], gpus_per_rank=gpus,
-                       cpus_per_rank=machine.cpus if reserve else 0,
-                       memory_mb_per_rank=machine.memory_mb if reserve else 0,
-                       spot=self.spot(), task_dir=self.root,
-                       gpu_filter=_index_list(selectors["gpus"]) if "gpus" in selectors else None,
-                       numa=int(selectors["numa"]) if "numa" in selectors else None)
-
-    def _place(self) -> None:
-        """Reserve the task's machine(s) on this node; raises :class:`Queued` when they are
-        busy (``TPI_PLACEMENT_QUEUE=0``: fail instead, the pre-queue behaviour)."""
-        definition = self._definition()
-        req = self._request()
-        if req is None:
-            definition["gpus"] = []
-            _write_json(self.task_file, definition)
-            return
-        placement = self.placement
-        try:
-            alloc = placement.reserve(req)
-        except PlacementBusy as busy:
-            if self._knob("TPI_PLACEMENT_QUEUE", "1") == "0":
-                raise PlacementError("%s: %s" % (self.id, busy)) from None
-            placement.enqueue(req, reason=str(busy))
-            self._event("queued", str(busy), "spot" if req.spot else "on-demand",
-                        "position %d" % placement.position(self.id))
-            self._reclaim(placement, req)
-            raise Queued(str(busy)) from None
-        except PlacementError as error:
-            raise PlacementError("%s: %s" % (self.id, error)) from None
-        self._apply(definition, alloc, placement)
-
-    def _apply(self, definition: Dict, alloc: Allocation, placement: Placement) -> None:
-        by_index = {g.index: g for g in placement.gpus}
-        definition["gpus"] = list(alloc.gpus)
-        definition["gpu_info"] = [by_index[g].to_json() for g in alloc.gpus if g in by_index]
-        definition["allocation"] = alloc.to_json()
-        _write_json(self.task_file, definition)
-        desc = ["gpus " + (",".join(str(g) for g in alloc.gpus) or "-")]
-        if any(alloc.rank_cpus):
-            desc.append("cpus " + " | ".join(_ranges(c) for c in alloc.rank_cpus))
-        if alloc.memory_mb:
-            desc.append("memory %d MB" % alloc.memory_mb)
-        if alloc.spot:
-            desc.append("spot")
-        self._event("placed", *(desc + alloc.notes))
-
-    def _reclaim(self, placement: Placement, req: Request) -> List[str]:
-        """On-demand task that does not fit: requeue the spot tasks whose resources make it
-        fit (they checkpoint, release and wait for capacity again)."""
-        if req.spot or placement.position(self.id) != 0:
-            return []
-        out = []
-        for victim in placement.victims(req):
-            task_dir = victim.get("task_dir") or ""
-            reply = control_socket(os.path.join(task_dir, "supervisor"),
-                                   "requeue reclaimed by %s" % self.id)
-            if reply and reply.get("ok"):
-                placement.mark_requeueing(victim["task"])
-                self._event("reclaim", "spot task %s" % victim["task"],
-                            "gpus " + ",".join(str(g) for g in victim.get("gpus") or []))
-                out.append(victim["task"])
-        return out
 
     def _spec_json(self) -> Dict:
         d = self._definition()
@@ -656,82 +523,6 @@ class NodeTask(Task):
         run_steps(steps, self.timings)
         log.info("Creation completed" + (" (queued: %s)" % queued[0] if queued else ""))
 
-    # -- the node queue -----------------------------------------------------------------------
-    def _waiter_argv(self) -> List[str]:
-        code = ("import sys; sys.path.insert(0, %r); "
-                "from terraform_provider_iterative_amd.parallel.scheduler import main; "
-                "sys.exit(main([%r]))" % (ROOT, self.root))
-        return [sys.executable, "-c", code]
-
-    def _spawn_waiter(self) -> int:
-        """Start the detached process that waits for this task's turn, then starts it."""
-        logfile = open(os.path.join(self.sup_dir, "queue.log"), "ab")
-        try:
-            proc = subprocess.Popen(self._waiter_argv(), stdin=subprocess.DEVNULL,
-                                    stdout=logfile, stderr=logfile, close_fds=True,
-                                    cwd=self.root, start_new_session=True)
-        finally:
-            logfile.close()
-        self._write_queue_state(proc.pid)
-        return proc.pid
-
-    def _write_queue_state(self, pid: int, phase: str = "queued") -> None:
-        state = self._state()
-        _write_json(os.path.join(self.sup_dir, "state.json"), {
-            "pid": pid, "task_id": self.id, "phase": phase, "running": 0, "ranks": [],
-            "restarts": int(state.get("restarts", 0) or 0), "heartbeat": _now()})
-
-    def run_queued(self, poll: float = 0.1) -> int:
-        """The waiter (:mod:`..parallel.scheduler`): hold this task's place in the queue until
-        its machine can be reserved, reclaiming spot capacity when it is the on-demand head,
-        then start the supervisor.  SIGTERM (``leo stop`` / ``delete``) leaves the queue."""
-        stopping: List[bool] = []
-        signal.signal(signal.SIGTERM, lambda *_: stopping.append(True))
-        if os.path.exists(self._stop_marker()):
-            stopping.append(True)
-        else:
-            self._write_queue_state(os.getpid())
-        placement = self.placement
-        req = self._request()
-        requeued = self._was_running()
-        if req is None:  # nothing to wait for
-            self.start(restart_base=self._restarts() + requeued, force=True)
-            return 0
-        placement.enqueue(req, waiter_pid=os.getpid(),
-                          reason="requeued" if requeued else "busy")
-        if requeued:  # a reclaimed spot task: back in the queue, resumes when placed again
-            self._event("queued", "requeued", "spot" if req.spot else "on-demand",
-                        "position %d" % placement.position(self.id))
-        t0 = _now()
-        while not stopping:
-            if os.path.exists(self._stop_marker()):
-                break
-            try:
-                alloc = placement.reserve(req)
-            except PlacementBusy:
-                if not req.spot:
-                    self._reclaim(placement, req)
-                time.sleep(poll)
-                continue
-            except PlacementError as error:
-                placement.dequeue(self.id)
-                self._event("placement-failed", str(error))
-                self._write_queue_state(0, "stopped")
-                return 1
-            self._event("dequeued", "waited %.3f s" % (_now() - t0))
-            self._apply(self._definition(), alloc, placement)
-            self.start(restart_base=self._restarts() + requeued, force=True)
-            return 0
-        placement.dequeue(self.id)
-        self._event("stop-requested", "queued task left the queue")
-        self._write_queue_state(0, "stopped")
-        return 0
-
-    def _restarts(self) -> int:
-        return int(self._state().get("restarts", 0) or 0)
-
-    def _was_running(self) -> bool:
-        return any(e.code == "rank-start" for e in self.events())
 
     def read(self) -> None:
         if not os.path.isdir(self.root):
@@ -789,11 +580,6 @@ class NodeTask(Task):
                                % (self.id, left))
         self._event("killed", "processes left after stop were killed")
 
-    def _delete_storage(self) -> None:
-        # With a pre-allocated container the data lives outside self.root and is kept
-        # (the reference only empties buckets it created, task/aws/task.go:245-299).
-        if os.path.isdir(self.root):
-            storage.native().remove_tree(self.root)
 
     def start(self, restart_base: int = 0, force: bool = False) -> None:
         if not force and self.supervisor_running():
@@ -821,22 +607,6 @@ class NodeTask(Task):
         pid = int(out.decode().strip() or 0)
         self._event("started", "supervisor pid %d" % pid)
 
-    def _settle_gpus(self, spec: Dict) -> None:
-        """A GPU handed over from another holder is used only once the driver has its memory
-        back (:meth:`Placement.settle_gpus`); each wait is journalled (``gpu-drain``)."""
-        gpus = [int(g) for g in str(spec["env"].get("TPI_VISIBLE_GPUS", "")).split(",") if g]
-        if not gpus:
-            return
-        for rec in self.placement.settle_gpus(gpus):
-            desc = ["gpu %d" % rec["gpu"], "waited %.3f s" % rec["waited_s"],
-                    "VRAM in use %.1f -> %.1f GB" % (rec["used_gb_at_start"], rec["used_gb"])]
-            if rec["previous"]:
-                desc.append("previous holder %s" % rec["previous"])
-            if rec["target_gb"] is not None:
-                desc.append("target %.1f GB" % rec["target_gb"])
-            if rec["timed_out"]:
-                desc.append("timed out (TPI_GPU_DRAIN_TIMEOUT): starting anyway")
-            self._event("gpu-drain", *desc)
 
     def stop(self, wait: float = 60.0) -> None:
         state = self._state()
@@ -893,47 +663,6 @@ class NodeTask(Task):
         if not reply.get("ok"):
             raise NotFoundError("task %s: %s" % (self.id, reply.get("error")))
 
-    def push(self) -> None:
-        directory = self.spec.environment.directory
-        if not directory:
-            return
-        if self.remote_conn is not None:  # into the container; the node restores from it
-            stats = remote_storage.open_remote(self.remote_conn).put_tree(
-                directory, "data", storage.transfer_rules(self.spec.environment.exclude_list))
-            log.info("Uploaded %d files to %s", stats["files"],
-                     remote_storage.describe(self.remote_conn))
-            return
-        t0 = time.perf_counter()
-        if os.environ.get("TPI_PUSH_LINK", "") in ("1", "true", "yes"):
-            # hard links instead of copies (opt-in: no snapshot, see storage.link_tree)
-            st = storage.link_tree(directory, self.data_dir, self.spec.environment.exclude_list)
-            self._event("pushed", "%d files" % (st["linked"] + st["copied"]),
-                        "%d bytes" % st["bytes"], "%.3f s" % (time.perf_counter() - t0),
-                        "hard links %d" % st["linked"])
-            return
-        # the default: a snapshot of the workdir -- each file reflinked (FICLONE: shared
-        # extents, copy-on-write) where the filesystem can, else copied by 16 threads
-        st = storage.transfer(directory, self.data_dir, self.spec.environment.exclude_list)
-        self._event("pushed", "%d files" % st.get("files", 0), "%d bytes" % st.get("bytes", 0),
-                    "%.3f s" % (time.perf_counter() - t0),
-                    "reflinked %d" % st.get("cloned", 0))
-
-    def _restore_remote(self) -> None:
-        stats = remote_storage.open_remote(self.remote_conn).get_tree("data", self.data_dir,
-                                                                    ["+ **"])
-        self._event("container-restored", remote_storage.describe(self.remote_conn),
-                    "%d files" % stats["files"], "%d bytes" % stats["bytes"])
-
-    def pull(self) -> None:
-        saved = self._saved or {}
-        directory = self.spec.environment.directory or saved.get("directory") or "."
-        out = self.spec.environment.directory_out or saved.get("directory_out") or ""
-        excludes = self.spec.environment.exclude_list or saved.get("exclude") or []
-        rules = storage.limit_transfer(out, storage.transfer_rules(excludes))
-        if self.remote_conn is not None:  # the container holds the task's final data
-            remote_storage.open_remote(self.remote_conn).get_tree("data", directory, rules)
-            return
-        storage.transfer(self.data_dir, directory, rules=rules)
 
     def status(self) -> Dict[str, int]:
         initial = new_status()
@@ -1004,32 +733,6 @@ class NodeTask(Task):
                 break
             time.sleep(poll)
         return self.status()
-
-
-def _ranges(cpus: List[int]) -> str:
-    """``[0,1,2,5]`` -> ``"0-2,5"``."""
-    out, start, prev = [], None, None
-    for c in sorted(cpus):
-        if start is None:
-            start = prev = c
-        elif c == prev + 1:
-            prev = c
-        else:
-            out.append(str(start) if start == prev else "%d-%d" % (start, prev))
-            start = prev = c
-    if start is not None:
-        out.append(str(start) if start == prev else "%d-%d" % (start, prev))
-    return ",".join(out) or "-"
-
-
-def _index_list(spec: str) -> List[int]:
-    out: List[int] = []
-    for part in spec.replace("|", ":").replace(";", ":").split(":"):
-        if not part:
-            continue
-        lo, _, hi = part.partition("-")
-        out.extend(range(int(lo), int(hi or lo) + 1))
-    return out
 
 
 def list_tasks(cloud: Cloud) -> List[Identifier]:
