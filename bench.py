@@ -152,7 +152,8 @@ E2E_KEYS = ("ok", "verified", "status", "signal_to_restored_s", "save_s",
             "warm_standby_activated", "hot_standby", "preload", "preloaded_wait_s", "preload_gpu",
             "standby_pinned_wait_s", "restore_journal",
             "extra_tensors_gib", "delete_s", "rank_exit_to_settled_s", "gpu_drain",
-            "successor_hbm_wait", "hbm_failed", "hbm_fault_dumps",
+            "successor_hbm_wait", "hbm_failed", "hbm_fault_dumps", "hbm_skipped",
+            "timeline_on_failure",
             "memory_guard",
             "released_exit_pending_at_settle")
 

@@ -346,7 +346,10 @@ def main():
                 pass
         if dumps:
             result["hbm_fault_dumps"] = dumps
+        result["hbm_skipped"] = [d for c, _, d in events if c == "checkpoint-hbm-skipped"]
         result["ok"] = bool(status.get("succeeded") == 1 and result["verified"])
+        if result["hbm_failed"] or not result["ok"]:  # the whole journal, for the record
+            result["timeline_on_failure"] = result.get("timeline")
     finally:
         try:
             # the task is over for its users once the supervisor settled; a released

@@ -190,6 +190,11 @@ class NodeQueue:
         for rec in self.placement.settle_gpus(gpus):
             desc = ["gpu %d" % rec["gpu"], "waited %.3f s" % rec["waited_s"],
                     "VRAM in use %.1f -> %.1f GB" % (rec["used_gb_at_start"], rec["used_gb"])]
+            if rec["orphaned_gb_at_start"] is not None:
+                desc.append("held by no process %.1f -> %.1f GB" % (
+                    rec["orphaned_gb_at_start"], rec["orphaned_gb"]))
+            if rec["floor"]:
+                desc.append("stopped falling: taken as the GPU's idle level")
             if rec["previous"]:
                 desc.append("previous holder %s" % rec["previous"])
             if rec["target_gb"] is not None:

@@ -656,7 +656,8 @@ class HbmHandoff:
             except BaseException as error:
                 self.hbm_fault_dump = _dump_copy_plan(self._hbm_manifest_path(), src, dst,
                                                       owner, bases, sizes, doc, error,
-                                                      self.device_index)
+                                                      self.device_index,
+                                                      getattr(self, "hbm_device_state", None))
                 raise
             phases["copy"] = time.perf_counter() - t3
         except BaseException:
@@ -700,7 +701,8 @@ class HbmHandoff:
 
 def _dump_copy_plan(manifest: str, src: np.ndarray, dst: np.ndarray, owner: np.ndarray,
                     bases: List[Optional[int]], sizes: List[int], doc: Dict,
-                    error: BaseException, device_index: int = 0) -> Optional[str]:
+                    error: BaseException, device_index: int = 0,
+                    device_state: Optional[Dict] = None) -> Optional[str]:
     """Evidence of a failed hand-off copy (``<manifest>.fault.json``): every source and
     destination descriptor the kernel was given, each source's mapped allocation
     ``[base, base + size)``, the relocation pieces, and what the driver held on the device --
@@ -717,12 +719,18 @@ def _dump_copy_plan(manifest: str, src: np.ndarray, dst: np.ndarray, owner: np.n
             usage = device_vram_usage(device_index)
         except Exception:
             pass
+        at_fault = None
+        if device_state and device_state.get("pci"):  # sysfs: readable after the fault too
+            from ..parallel.placement import orphaned_vram
+
+            at_fault = orphaned_vram(device_state["pci"])
         with open(path, "w") as f:
             json.dump({"error": str(error), "time": time.time(), "predecessor": doc.get("pid"),
                        "src": segs(src), "dst": segs(dst), "owner": [int(o) for o in owner],
                        "mapped": [[None if b is None else int(b), int(n)]
                                   for b, n in zip(bases, sizes)],
-                       "pieces": doc.get("pieces"), "vram_used_total": usage}, f)
+                       "pieces": doc.get("pieces"), "vram_used_total": usage,
+                       "device_before_copy": device_state, "device_at_fault": at_fault}, f)
         return path
     except Exception:
         return None

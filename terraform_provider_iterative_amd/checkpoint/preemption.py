@@ -938,6 +938,61 @@ def materialize(spill: str, device: Any = None, **kwargs) -> Optional[Tuple[Chec
     return ck, tensors, dict(getattr(ck, "materialized_metadata", {}) or {})
 
 
+HANDOFF_HEADROOM = 1 << 30  # free device memory (driver's count) an HBM hand-off copy needs
+
+
+def _device_settled_for_handoff(checkpointer: Checkpointer) -> bool:
+    """May the HBM hand-off copy run now?  Only on a device that is not over-committed: the
+    driver's count leaves ``HANDOFF_HEADROOM`` free and holds no more orphaned memory (exited
+    processes, frees still being wiped) than a GPU carries idle.  Over-committed VRAM makes the
+    driver evict buffers -- the predecessor's, which this process maps over HIP IPC, among
+    them -- and the round-5/6 hand-off faults happened on such devices
+    (``profiles/round6/handoff_fault.md``).  Waits up to ``TPI_HANDOFF_DRAIN_TIMEOUT``
+    (default 10 s) for the drain; False sends the restore to the host copy.  The state seen is
+    kept on the checkpointer (``hbm_device_state``: the fault dump's context) and journalled
+    whenever it waited or refused."""
+    from ..parallel.placement import ORPHAN_LIMIT, kfd_gpu_id, orphaned_vram
+    import ctypes
+
+    from ..ops import hip
+
+    lib = hip(required=False)
+    if lib is None:
+        return True
+    bus = ctypes.create_string_buffer(64)
+    if lib.tpi_device_pci_bus_id(getattr(checkpointer, "device_index", 0) or 0, bus, 64) != 0:
+        return True
+    pci = bus.value.decode().lower()
+    gid = kfd_gpu_id(pci)
+    try:
+        timeout = float(os.environ.get("TPI_HANDOFF_DRAIN_TIMEOUT", "10"))
+    except ValueError:
+        timeout = 10.0
+    t0 = time.monotonic()
+    while True:
+        st = orphaned_vram(pci, gid)
+        if st is None:
+            return True
+        checkpointer.hbm_device_state = dict(st, pci=pci)
+        room = st["total"] - st["used"] >= HANDOFF_HEADROOM
+        settled = st["orphaned"] is None or st["orphaned"] <= ORPHAN_LIMIT
+        waited = time.monotonic() - t0
+        if (room and settled) or waited >= timeout:
+            break
+        time.sleep(0.005)
+    desc = ["VRAM in use %.1f of %.1f GB" % (st["used"] / 1e9, st["total"] / 1e9),
+            "held by no process %s" % ("?" if st["orphaned"] is None else
+                                       "%.1f GB" % (st["orphaned"] / 1e9)),
+            "waited %.3f s" % waited]
+    if not (room and settled):
+        journal("checkpoint-hbm-skipped", "device over-committed: restoring from the host copy",
+                *desc)
+        return False
+    if waited > 0.001:
+        journal("handoff-device-settled", *desc)
+    return True
+
+
 STICKY_HIP_ERRORS = ("illegal memory access", "illegal address", "illegal instruction",
                      "launch failure", "hardware exception", "memory access fault", "ecc error")
 
@@ -1015,6 +1070,8 @@ def resume(checkpointer: Checkpointer, persist_path: Optional[str] = None,
     hbm = checkpointer.hbm_metadata()
     if hbm is not None and generation is not None and hbm["generation"] != generation:
         hbm = None
+    if hbm is not None and not _device_settled_for_handoff(checkpointer):
+        hbm = None  # over-committed device: its buffers may move under the copy -- host route
     if hbm is not None:
         try:  # the predecessor on this GPU is alive and exported its tensors: copy from HBM
             res = checkpointer.restore_hbm()

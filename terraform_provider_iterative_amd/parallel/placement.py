@@ -23,8 +23,14 @@ from typing import Dict, Iterator, List, Optional, Tuple
 from ..utils.record import field, record
 
 KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def _kfd(sub: str) -> str:
+    """A path under KFD's sysfs tree (``TPI_SYSFS_KFD`` replaces ``/sys/class/kfd/kfd``: tests
+    fake the topology and the per-process accounting)."""
+    root = os.environ.get("TPI_SYSFS_KFD")
+    return os.path.join(root, sub) if root else os.path.join("/sys/class/kfd/kfd", sub)
 DRAIN_MAX_AGE = 600.0     # s: an older drain marker is ignored
-DRAIN_QUIET_S = 0.25      # s without a falling VRAM count: nothing is being given back
 DRAIN_STEP = 64 << 20     # a fall of at least this much counts as memory coming back
 
 
@@ -226,45 +232,51 @@ class Placement:
         (``TPI_GPU_DRAIN_TIMEOUT``, default 30 s).  Returns one record per GPU that had
         something to wait for (for the task's journal: ``gpu-drain``).
 
-        Why: a process's HBM is not free when it exits, nor when its supervisor hands the GPU
-        on -- the driver wipes freed VRAM and releases it seconds later (200 GB: ~5 s), while
-        the HIP runtime of the next process already reports it free.  A task that fills the
-        device on top of it makes the driver evict buffers under running kernels; the round-5
-        hand-off faults happened exactly there (``profiles/round5/ipc_cause.md``).
+        Why: a process's HBM is not free when it exits, nor when it frees it -- the driver
+        wipes freed VRAM and releases it seconds later (200 GB: ~5 s; a 100 GB buffer as one
+        step at the end of its wipe), while the HIP runtime of the next process already
+        reports it free.  A task that fills the device on top of it over-commits VRAM, and the
+        driver then evicts buffers -- including ones another process maps over HIP IPC --
+        under running kernels; the round-5/6 hand-off faults came on exactly such runs
+        (``profiles/round5/ipc_cause.md``, ``profiles/round6/``).
 
-        * A GPU with a drain marker (the previous holder's released lease): wait until the
-          driver's ``mem_info_vram_used`` is back to the count of the holder's reservation
-          (``vram_baseline``) + ``max(1 GiB, 1 %)``.
-        * Otherwise, a GPU using more than ``TPI_GPU_IDLE_FRACTION`` (3 %) of its memory: wait
-          while that count keeps falling (memory some other process freed, e.g. a benchmark's
-          own), until it has not fallen for 0.25 s.
-        The GPU's lease then records the settled count as its own baseline.  GPUs without a
-        readable counter (no sysfs, fake inventories) are not waited for."""
+        A GPU is settled when both hold:
+        * orphaned memory -- the driver's ``mem_info_vram_used`` minus what live processes
+          hold by KFD's per-process accounting -- is at most ``ORPHAN_LIMIT`` (or this GPU's
+          learned idle floor + 2 GiB), or has stopped falling for ``ORPHAN_FLAT_S`` (then it
+          is no drain: the level is remembered as the GPU's floor);
+        * with a drain marker (the previous holder's released lease): the driver's count is
+          back to that holder's reservation count (``vram_baseline``) + ``max(1 GiB, 1 %)``.
+        Without KFD's accounting, a count that keeps falling is waited for until it has not
+        fallen for ``ORPHAN_FLAT_S``.  The GPU's lease then records the settled count as its
+        own baseline.  GPUs without a readable counter (no sysfs, fake inventories) are not
+        waited for."""
         if timeout is None:
             try:
                 timeout = float(os.environ.get("TPI_GPU_DRAIN_TIMEOUT", "30"))
             except ValueError:
                 timeout = 30.0
-        try:
-            idle_fraction = float(os.environ.get("TPI_GPU_IDLE_FRACTION", "0.03"))
-        except ValueError:
-            idle_fraction = 0.03
         by_index = {g.index: g for g in self.gpus}
         todo = []
         for index in indices:
             gpu = by_index.get(index)
-            usage = vram_usage(gpu.pci) if gpu is not None and gpu.pci else None
-            if usage is None:
+            if gpu is None or not gpu.pci:
                 continue
-            used, total = usage
+            gid = kfd_gpu_id(gpu.pci)
+            state = orphaned_vram(gpu.pci, gid)
+            if state is None:
+                continue
             marker = self._drain_marker(index)
-            slack = max(1 << 30, total // 100)
+            total = state["total"]
             baseline = None if marker is None else marker.get("vram_baseline")
-            item = {"gpu": index, "pci": gpu.pci, "used_at_start": used, "used": used,
-                    "total": total, "previous": (marker or {}).get("task"),
-                    "target": None if baseline is None else int(baseline) + slack,
-                    "idle": max(slack, int(idle_fraction * total)), "low": used,
-                    "last_drop": None, "done": False}
+            floor = self._orphan_floor(index)
+            item = {"gpu": index, "pci": gpu.pci, "gid": gid, "start": state, "now": state,
+                    "previous": (marker or {}).get("task"),
+                    "target": None if baseline is None else
+                    int(baseline) + max(1 << 30, total // 100),
+                    "limit": max(ORPHAN_LIMIT, (floor or 0) + (2 << 30)),
+                    "low": state["orphaned"] if state["orphaned"] is not None else state["used"],
+                    "last_drop": None, "done": False, "flat": False}
             todo.append(item)
         t0 = time.monotonic()
         while todo:
@@ -273,13 +285,19 @@ class Placement:
             for item in todo:
                 if item["done"]:
                     continue
-                if item["target"] is not None:
-                    item["done"] = item["used"] <= item["target"]
-                else:
-                    quiet = now - (item["last_drop"] if item["last_drop"] is not None else t0)
-                    item["done"] = item["used"] <= item["idle"] or quiet >= DRAIN_QUIET_S
-                if item["done"]:
-                    item["waited"] = now - t0
+                st = item["now"]
+                level = st["orphaned"] if st["orphaned"] is not None else None
+                quiet = now - (item["last_drop"] if item["last_drop"] is not None else t0)
+                flat = quiet >= ORPHAN_FLAT_S
+                if level is not None:
+                    drained = level <= item["limit"] or flat
+                else:  # no per-process accounting: a falling count is a drain
+                    drained = flat or (item["target"] is None and
+                                       st["used"] <= max(ORPHAN_LIMIT, st["total"] // 33))
+                back = item["target"] is None or st["used"] <= item["target"]
+                if drained and (back or flat):
+                    item["done"], item["waited"] = True, now - t0
+                    item["flat"] = flat and not (level is not None and level <= item["limit"])
                 pending += not item["done"]
             if not pending or now - t0 >= timeout:
                 break
@@ -287,32 +305,55 @@ class Placement:
             for item in todo:
                 if item["done"]:
                     continue
-                usage = vram_usage(item["pci"])
-                if usage is None:
+                st = orphaned_vram(item["pci"], item["gid"])
+                if st is None:
                     item["done"], item["waited"] = True, time.monotonic() - t0
                     continue
-                item["used"] = usage[0]
-                if usage[0] < item["low"] - DRAIN_STEP:
-                    item["low"] = usage[0]
+                item["now"] = st
+                level = st["orphaned"] if st["orphaned"] is not None else st["used"]
+                if level < item["low"] - DRAIN_STEP:
+                    item["low"] = level
                     item["last_drop"] = time.monotonic()
         waited = time.monotonic() - t0
         out = []
         for item in todo:
-            had_marker = item["previous"] is not None or item["target"] is not None
-            if had_marker or item["used_at_start"] > item["idle"]:
+            start, now = item["start"], item["now"]
+            orphan0 = start["orphaned"]
+            busy = (orphan0 is not None and orphan0 > item["limit"]) or (
+                orphan0 is None and start["used"] > max(ORPHAN_LIMIT, start["total"] // 33))
+            if item["previous"] is not None or item["target"] is not None or busy:
                 out.append({"gpu": item["gpu"], "previous": item["previous"],
                             "waited_s": round(item.get("waited", waited), 3),
-                            "used_gb_at_start": round(item["used_at_start"] / 1e9, 2),
-                            "used_gb": round(item["used"] / 1e9, 2),
+                            "used_gb_at_start": round(start["used"] / 1e9, 2),
+                            "used_gb": round(now["used"] / 1e9, 2),
+                            "orphaned_gb_at_start": None if orphan0 is None else
+                            round(orphan0 / 1e9, 2),
+                            "orphaned_gb": None if now["orphaned"] is None else
+                            round(now["orphaned"] / 1e9, 2),
                             "target_gb": None if item["target"] is None else
                             round(item["target"] / 1e9, 2),
+                            "floor": item["flat"],
                             "timed_out": not item["done"]})
+            if item["flat"] and now["orphaned"] is not None:
+                self._set_orphan_floor(item["gpu"], now["orphaned"])
             try:
                 os.unlink(self.drain_path(item["gpu"]))
             except FileNotFoundError:
                 pass
-            self._rebase_lease(item["gpu"], item["used"])
+            self._rebase_lease(item["gpu"], now["used"])
         return out
+
+    def _orphan_floor(self, index: int) -> Optional[int]:
+        """Orphaned VRAM this GPU was seen to carry without draining (its idle level)."""
+        raw = _read(os.path.join(self.root, "gpu-%d.floor" % index)).strip()
+        return int(raw) if raw.isdigit() else None
+
+    def _set_orphan_floor(self, index: int, value: int) -> None:
+        path = os.path.join(self.root, "gpu-%d.floor" % index)
+        tmp = path + ".tmp"
+        with open(tmp, "w") as handle:
+            handle.write(str(int(value)))
+        os.replace(tmp, path)
 
     def _rebase_lease(self, index: int, used: int) -> None:
         """The settled driver count becomes the lease's baseline (nothing of its holder runs
@@ -791,6 +832,64 @@ def vram_usage(pci: str) -> Optional[Tuple[int, int]]:
     if not (used.isdigit() and total.isdigit()):
         return None
     return int(used), int(total)
+
+
+ORPHAN_LIMIT = 4 << 30  # orphaned VRAM (held by no live process) a GPU may carry when idle
+ORPHAN_FLAT_S = 3.0     # an orphan count that has not fallen for this long is no drain
+
+
+def kfd_gpu_id(pci: str) -> Optional[int]:
+    """KFD's ``gpu_id`` of the GPU at PCI bus id ``pci`` (``0000:d9:00.0``): the topology node
+    whose ``domain``/``location_id`` match it.  None when the topology is unreadable."""
+    try:
+        dom, bus, devfn = pci.split(":")
+        dev, fn = devfn.split(".")
+        loc = (int(bus, 16) << 8) | (int(dev, 16) << 3) | int(fn, 16)
+        domain = int(dom, 16)
+        nodes = os.listdir(_kfd("topology/nodes"))
+    except (ValueError, OSError):
+        return None
+    for node in nodes:
+        props = {}
+        for line in _read(os.path.join(_kfd("topology/nodes"), node, "properties")).splitlines():
+            key, _, value = line.partition(" ")
+            props[key] = value.strip()
+        if props.get("location_id") == str(loc) and props.get("domain", "0") == str(domain):
+            gid = _read(os.path.join(_kfd("topology/nodes"), node, "gpu_id")).strip()
+            return int(gid) if gid.isdigit() and int(gid) else None
+    return None
+
+
+def live_vram(gpu_id: Optional[int]) -> Optional[int]:
+    """Bytes of a GPU's memory that live processes hold, by KFD's per-process accounting
+    (``/sys/class/kfd/kfd/proc/<pid>/vram_<gpu_id>``; a process's count drops when it frees,
+    before the driver has wiped and released the memory).  None when unreadable."""
+    if gpu_id is None:
+        return None
+    try:
+        pids = os.listdir(_kfd("proc"))
+    except OSError:
+        return None
+    total, seen = 0, False
+    for pid in pids:
+        raw = _read(os.path.join(_kfd("proc"), pid, "vram_%d" % gpu_id)).strip()
+        if raw.isdigit():
+            total += int(raw)
+            seen = True
+    return total if seen or not pids else None
+
+
+def orphaned_vram(pci: str, gpu_id: Optional[int] = None) -> Optional[Dict[str, int]]:
+    """``{"used", "total", "live", "orphaned"}`` of a GPU: device memory the driver counts as
+    used that no live process holds -- memory of exited processes and frees the driver is still
+    wiping (plus the driver's own few GB).  ``live``/``orphaned`` are None without KFD's
+    per-process accounting."""
+    usage = vram_usage(pci) if pci else None
+    if usage is None:
+        return None
+    live = live_vram(gpu_id if gpu_id is not None else kfd_gpu_id(pci))
+    return {"used": usage[0], "total": usage[1], "live": live,
+            "orphaned": None if live is None else max(0, usage[0] - live)}
 
 
 def device_vram_usage(device_index: int) -> Optional[Tuple[int, int]]:

@@ -37,10 +37,43 @@ class FakeVram:
         os.replace(tmp, self.dir / "mem_info_vram_used")
 
 
+class FakeKfd:
+    """KFD's topology node of the fake GPU (gpu_id 4242 at PCI_LOC) and its per-process VRAM
+    accounting (``proc/<pid>/vram_<gpu_id>``)."""
+
+    GPU_ID = 4242
+
+    def __init__(self, root):
+        self.root = root
+        node = root / "topology" / "nodes" / "3"
+        node.mkdir(parents=True)
+        (node / "properties").write_text("gfx_target_version 90500\ndomain 0\nlocation_id %d\n"
+                                         % (0xfa << 8))
+        (node / "gpu_id").write_text("%d\n" % self.GPU_ID)
+        (root / "proc").mkdir()
+
+    def live(self, pid: int, used: int) -> None:
+        d = self.root / "proc" / str(pid)
+        d.mkdir(exist_ok=True)
+        (d / ("vram_%d" % self.GPU_ID)).write_text("%d\n" % used)
+
+    def exit(self, pid: int) -> None:
+        import shutil
+
+        shutil.rmtree(self.root / "proc" / str(pid))
+
+
 @pytest.fixture()
 def vram(tmp_path, monkeypatch):
     monkeypatch.setenv("TPI_SYSFS_PCI", str(tmp_path / "pci"))
+    monkeypatch.setenv("TPI_SYSFS_KFD", str(tmp_path / "no-kfd"))  # no accounting by default
     return FakeVram(tmp_path / "pci")
+
+
+@pytest.fixture()
+def kfd(tmp_path, monkeypatch):
+    monkeypatch.setenv("TPI_SYSFS_KFD", str(tmp_path / "kfd"))
+    return FakeKfd(tmp_path / "kfd")
 
 
 def _placement(tmp_path):
@@ -103,11 +136,41 @@ def test_memory_freed_by_a_process_that_held_no_lease_is_waited_for(tmp_path, vr
     thread.join()
     assert recs and recs[0]["previous"] is None and recs[0]["used_gb"] == 3.0
     assert recs[0]["waited_s"] >= 0.35
-    # a GPU busy with something that does not go away costs one quiet period, not the bound
+    # a GPU busy with something that does not go away costs one flat period, not the bound
     vram.set(100 * GB)
     t0 = time.monotonic()
     recs = placement.settle_gpus([0], timeout=10)
-    assert time.monotonic() - t0 < 1.5 and not recs[0]["timed_out"]
+    assert time.monotonic() - t0 < 3 + 1.5 and not recs[0]["timed_out"] and recs[0]["floor"]
+
+
+def test_orphaned_memory_is_what_the_start_waits_for(tmp_path, vram, kfd):
+    """With KFD's per-process accounting the gate waits for memory no live process holds
+    (exited processes, frees being wiped) -- never for what live processes use -- and learns
+    a GPU's idle level when orphaned memory stops falling above the limit."""
+    from terraform_provider_iterative_amd.parallel.placement import orphaned_vram
+
+    placement = _placement(tmp_path)
+    placement.allocate("task-b", 1)
+    kfd.live(111, 100 * GB)  # another user's live process: 100 GB, not ours to wait for
+    vram.set(101 * GB)
+    assert orphaned_vram(PCI)["orphaned"] == 1 * GB
+    t0 = time.monotonic()
+    assert placement.settle_gpus([0], timeout=10) == []
+    assert time.monotonic() - t0 < 0.5
+    vram.set(250 * GB)  # ... plus 150 GB that a process freed and the driver still wipes
+    timer = threading.Timer(0.6, vram.set, (102 * GB,))
+    timer.start()
+    recs = placement.settle_gpus([0], timeout=10)
+    timer.join()
+    assert recs[0]["orphaned_gb_at_start"] == 150.0 and recs[0]["orphaned_gb"] == 2.0
+    assert 0.5 < recs[0]["waited_s"] < 3 and not recs[0]["floor"]
+    # 10 GB the driver never gives back (its own): waited for once, then remembered
+    vram.set(110 * GB)
+    recs = placement.settle_gpus([0], timeout=10)
+    assert recs[0]["floor"] and 2.9 < recs[0]["waited_s"] < 4.5
+    t0 = time.monotonic()
+    assert placement.settle_gpus([0], timeout=10) == []
+    assert time.monotonic() - t0 < 0.5
 
 
 def test_unreadable_counters_are_not_waited_for(tmp_path, monkeypatch):
