@@ -772,8 +772,11 @@ class Supervisor {
     sb.exit_requested_at = sb.term_at;
     sb.state = Rank::DONE;
     sb.unused_standby = true;
-    struct stat st;  // nothing printed yet (a parked preloaded successor): no machine log
-    if (sb.logfd >= 0 && fstat(sb.logfd, &st) == 0 && st.st_size == 0)
+    // A standby that never ran the script leaves no machine log: nothing printed yet, or a
+    // preloaded successor (it never runs the script before activation; what it printed while
+    // parked is start-up noise, e.g. libdrm's when it warmed its GPU context).
+    struct stat st;
+    if (sb.logfd >= 0 && (sb.preloaded || (fstat(sb.logfd, &st) == 0 && st.st_size == 0)))
       unlink((s_.reports_dir + "/task-" + sb.uuid).c_str());
     event("standby-discarded", {"rank " + std::to_string(index), "machine " + sb.uuid, why});
     detached_.push_back(sb);

@@ -3,10 +3,14 @@
 * ``_lib/_tpi_native*.so``  host C++ (pybind11): filters, walker/transfer, CRC32C, XXH64,
   CPU pack/unpack.
 * ``_lib/libtpi_hip.so``    HIP/CDNA4 kernels, checkpoint/staging engine and the RCCL task
-  communicator, ``--offload-arch=gfx950``, linked against the libamdhip64 that ships with
-  torch so one HIP runtime is loaded.
-* ``_lib/tpi-supervisor``   the on-node rank supervisor (C++ executable).
-* ``_lib/tpi-stager``       the per-task workdir stager (C++/HIP executable on libtpi_hip).
+  communicator, ``--offload-arch=gfx950``.  It needs ``libamdhip64.so.7`` / ``librccl.so.1``
+  by soname: in a PyTorch process (``ops._loader`` always imports torch first) those sonames
+  are torch's bundled runtime (HIP 7.0), so one HIP runtime is loaded there.
+* ``_lib/tpi-supervisor``   the on-node rank supervisor (C++ executable, no HIP).
+* ``_lib/tpi-stager``       the per-task workdir stager (C++/HIP executable on libtpi_hip).  No
+  torch in it: its sonames resolve to /opt/rocm's runtime (HIP 7.2).  Its HBM images are
+  therefore exported by 7.2 and imported by the ranks' 7.0 runtime -- the pairing that opens
+  allocations of 2 GiB and more (``profiles/round6/ipc_runtime.md``).
 
 Nothing built is tracked by git.  A target is rebuilt when its ``.stamp`` (SHA-256 of the
 compile command and of every source/header it depends on) no longer matches -- content, not
