@@ -31,15 +31,15 @@
 #include <vector>
 #include "json.h"
 
-namespace {
+namespace tpi_sup {
 
-double now() {
+inline double now() {
   struct timespec ts;
   clock_gettime(CLOCK_REALTIME, &ts);
   return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
 
-std::string read_file(const std::string& path) {
+inline std::string read_file(const std::string& path) {
   std::ifstream in(path, std::ios::binary);
   if (!in) throw std::runtime_error("cannot read " + path);
   std::stringstream ss;
@@ -47,7 +47,7 @@ std::string read_file(const std::string& path) {
   return ss.str();
 }
 
-void write_all(int fd, const std::string& s) {
+inline void write_all(int fd, const std::string& s) {
   const char* p = s.data();
   size_t left = s.size();
   while (left) {
@@ -61,7 +61,7 @@ void write_all(int fd, const std::string& s) {
   }
 }
 
-bool atomic_write(const std::string& path, const std::string& data) {
+inline bool atomic_write(const std::string& path, const std::string& data) {
   std::string tmp = path + ".tmp";
   int fd = open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
   if (fd < 0) return false;
@@ -70,7 +70,7 @@ bool atomic_write(const std::string& path, const std::string& data) {
   return rename(tmp.c_str(), path.c_str()) == 0;
 }
 
-std::string uuid4() {
+inline std::string uuid4() {
   unsigned char b[16];
   int fd = open("/dev/urandom", O_RDONLY | O_CLOEXEC);
   if (fd < 0 || read(fd, b, 16) != 16) {
@@ -87,7 +87,7 @@ std::string uuid4() {
   return out;
 }
 
-std::string utc_stamp(double t) {
+inline std::string utc_stamp(double t) {
   time_t s = (time_t)t;
   struct tm tm;
   gmtime_r(&s, &tm);
@@ -96,7 +96,7 @@ std::string utc_stamp(double t) {
   return buf;
 }
 
-const char* signame(int sig) {
+inline const char* signame(int sig) {
   switch (sig) {
     case SIGTERM: return "TERM";
     case SIGKILL: return "KILL";
@@ -119,9 +119,9 @@ enum class TermReason { NONE, STOP, PREEMPT, TIMEOUT, FAILFAST, REQUEUE, OOM, DI
 
 // --daemon: the launching parent blocks on this pipe until the ranks are spawned and the
 // first state.json is on disk, so "create returned" implies "supervisor visible".
-int g_ready_fd = -1;
+inline int g_ready_fd = -1;
 
-void signal_ready() {
+inline void signal_ready() {
   if (g_ready_fd >= 0) {
     write_all(g_ready_fd, "1");
     close(g_ready_fd);
@@ -229,7 +229,7 @@ struct Spec {
   int restart_base = 0;  // restarts of earlier supervisors of this task (requeued incarnations)
 };
 
-Spec load_spec(const std::string& path) {
+inline Spec load_spec(const std::string& path) {
   Value v = tpi::json::parse(read_file(path));
   Spec s;
   s.task_id = v["task_id"].str();
@@ -307,7 +307,7 @@ Spec load_spec(const std::string& path) {
 }
 
 // Small /proc file into buf (NUL-terminated); false when unreadable or empty.
-bool read_small(const char* path, char* buf, size_t cap) {
+inline bool read_small(const char* path, char* buf, size_t cap) {
   int fd = open(path, O_RDONLY | O_CLOEXEC);
   if (fd < 0) return false;
   ssize_t n = read(fd, buf, cap - 1);
@@ -317,4 +317,4 @@ bool read_small(const char* path, char* buf, size_t cap) {
   return true;
 }
 
-}  // namespace
+}  // namespace tpi_sup

@@ -22,7 +22,7 @@
 
 #include "common.h"
 
-namespace {
+namespace tpi_sup {
 
 class ContainerSync {
  public:
@@ -125,4 +125,4 @@ class ContainerSync {
   int failures_ = 0;
 };
 
-}  // namespace
+}  // namespace tpi_sup

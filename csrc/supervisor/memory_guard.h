@@ -27,7 +27,7 @@
 
 #include "common.h"
 
-namespace {
+namespace tpi_sup {
 
 class MemoryGuard {
  public:
@@ -453,4 +453,4 @@ class MemoryGuard {
   std::vector<MemTrack> mem_;
 };
 
-}  // namespace
+}  // namespace tpi_sup

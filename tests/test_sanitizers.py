@@ -1,6 +1,7 @@
 """ASan/UBSan builds of the host C++: the native data-plane sources plus a
 self-checking harness (tests/native/sanitize_main.cpp), and the rank supervisor driving a
 real two-rank task through the node backend."""
+import glob
 import os
 import shutil
 import subprocess
@@ -64,7 +65,7 @@ def test_step_boundary_agreement_under_tsan(tmp_path):
 
 def test_supervisor_under_asan_ubsan(tmp_path, monkeypatch):
     exe = str(tmp_path / "tpi-supervisor-asan")
-    _compile(exe, [os.path.join(ROOT, "csrc", "supervisor", "supervisor.cpp")])
+    _compile(exe, sorted(glob.glob(os.path.join(ROOT, "csrc", "supervisor", "*.cpp"))))
     monkeypatch.setenv("TPI_SUPERVISOR_BIN", exe)
     monkeypatch.setenv("TPI_MI355X_GPUS", "0,1,2,3")
     monkeypatch.setenv("ASAN_OPTIONS", ENV["ASAN_OPTIONS"])
@@ -106,7 +107,7 @@ def test_supervisor_preemption_paths_under_asan_ubsan(tmp_path, monkeypatch):
     from test_preemption import ROOT as _root, STANDBY
 
     exe = str(tmp_path / "tpi-supervisor-asan")
-    _compile(exe, [os.path.join(ROOT, "csrc", "supervisor", "supervisor.cpp")])
+    _compile(exe, sorted(glob.glob(os.path.join(ROOT, "csrc", "supervisor", "*.cpp"))))
     monkeypatch.setenv("TPI_SUPERVISOR_BIN", exe)
     monkeypatch.setenv("TPI_WARM_STANDBY", "1")
     monkeypatch.setenv("ASAN_OPTIONS", ENV["ASAN_OPTIONS"])
@@ -207,7 +208,7 @@ def test_supervisor_hand_off_protocol_under_asan_ubsan(tmp_path, monkeypatch):
     from test_handoff_protocol import test_predecessor_released_only_after_closed
 
     exe = str(tmp_path / "tpi-supervisor-asan")
-    _compile(exe, [os.path.join(ROOT, "csrc", "supervisor", "supervisor.cpp")])
+    _compile(exe, sorted(glob.glob(os.path.join(ROOT, "csrc", "supervisor", "*.cpp"))))
     monkeypatch.setenv("ASAN_OPTIONS", ENV["ASAN_OPTIONS"])
     monkeypatch.setenv("UBSAN_OPTIONS", ENV["UBSAN_OPTIONS"])
     for die in (False, True):
