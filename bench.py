@@ -221,6 +221,7 @@ def workdir_config2(gb: float, timeout: float) -> dict:
         return {"error": repr(error)}
     out = {"first_log_s": r.get("apply_to_first_log_s"), "push_s": r.get("push_s"),
            "push_method": r.get("push_method"), "stage_s": r.get("stage_s"),
+           "gpu_drain": r.get("gpu_drain"),
            "apply_s": r.get("apply_s"), "stage_GBps": r.get("stage_GBps"),
            "train_step_ms": r.get("train_step_ms"), "workdir_gb": gb,
            "ok": bool(r.get("apply_ok") and r.get("stage_GBps")),
@@ -375,6 +376,12 @@ def main(argv=None):
         # state spawns the probe's `tpi apply` ~17 ms slower (profiles/hw_queues_round3.md).
         gpus = torch.cuda.device_count() if on_gpu else world
         latency = first_log_latency(parallelism=max(1, min(world, gpus)))
+    config2 = None
+    if rank == 0 and world == 1 and on_gpu and args.config2 == "auto":
+        # config 2 as a user meets it: on an idle GPU, before this process fills the device
+        # (after the timed loop the driver is still taking back its 200 GB, and the task's
+        # start would rightly wait for that: gpu-drain)
+        config2 = workdir_config2(10.0, args.e2e_timeout)
 
     from terraform_provider_iterative_amd.checkpoint import Checkpointer
 
@@ -782,9 +789,6 @@ def main(argv=None):
         tensors.clear()
         torch.cuda.empty_cache()
         e2e = preempt_e2e(args.total_gb, args.codec, args.e2e_timeout)
-    config2 = None
-    if args.config2 == "auto" and on_gpu and world == 1:
-        config2 = workdir_config2(10.0, args.e2e_timeout)
     if out is not None and side_to_stderr:
         side = {"save_async": async_stall, "raw_GBps": raw, "workdir_broadcast": fanout,
                 "sequential": sequential, "preempt_e2e": e2e,

@@ -139,6 +139,7 @@ def main():
             "stage_s": round(staged["time"] - started["time"], 3) if staged and started
             else None,
             "staged_event": staged["description"] if staged else None,
+            "gpu_drain": [e["description"] for e in events if e["code"] == "gpu-drain"],
             "destroy_ok": d.returncode == 0,
         }
         if apply.returncode != 0 or not m:

@@ -309,11 +309,19 @@ class Placement:
                 if st is None:
                     item["done"], item["waited"] = True, time.monotonic() - t0
                     continue
-                item["now"] = st
+                prev, item["now"] = item["now"], st
                 level = st["orphaned"] if st["orphaned"] is not None else st["used"]
                 if level < item["low"] - DRAIN_STEP:
                     item["low"] = level
                     item["last_drop"] = time.monotonic()
+                # memory still moving -- exiting processes' memory turning orphaned (the
+                # orphaned count rises), or the driver's count falling -- is no idle level
+                moved = abs(st["used"] - prev["used"]) > DRAIN_STEP or (
+                    st["orphaned"] is not None and prev["orphaned"] is not None
+                    and st["orphaned"] > prev["orphaned"] + DRAIN_STEP)
+                if moved:
+                    item["last_drop"] = time.monotonic()
+                    item["low"] = min(item["low"], level)
         waited = time.monotonic() - t0
         out = []
         for item in todo:
@@ -334,7 +342,9 @@ class Placement:
                             round(item["target"] / 1e9, 2),
                             "floor": item["flat"],
                             "timed_out": not item["done"]})
-            if item["flat"] and now["orphaned"] is not None:
+            if item["flat"] and now["orphaned"] is not None and now["orphaned"] <= ORPHAN_FLOOR_MAX:
+                # a level above ORPHAN_FLOOR_MAX is no driver's own memory (a stuck or leaked
+                # buffer): not learned, so the next start looks again
                 self._set_orphan_floor(item["gpu"], now["orphaned"])
             try:
                 os.unlink(self.drain_path(item["gpu"]))
@@ -836,6 +846,7 @@ def vram_usage(pci: str) -> Optional[Tuple[int, int]]:
 
 ORPHAN_LIMIT = 4 << 30  # orphaned VRAM (held by no live process) a GPU may carry when idle
 ORPHAN_FLAT_S = 3.0     # an orphan count that has not fallen for this long is no drain
+ORPHAN_FLOOR_MAX = 16 << 30  # the most a learned idle level may be
 
 
 def kfd_gpu_id(pci: str) -> Optional[int]:

@@ -157,6 +157,34 @@ def test_orphaned_memory_is_what_the_start_waits_for(tmp_path, vram, kfd):
     t0 = time.monotonic()
     assert placement.settle_gpus([0], timeout=10) == []
     assert time.monotonic() - t0 < 0.5
+
+
+def test_memory_turning_orphaned_is_no_idle_level(tmp_path, vram, kfd):
+    """Processes still exiting move their memory from "live" to "orphaned" (the orphaned
+    count rises while the driver's total stays): that is a drain in progress, never the GPU's
+    idle level (round 6, r6c: 62 -> 80 GB was taken for a floor)."""
+    placement = _placement(tmp_path)
+    placement.allocate("task-b", 1)
+    vram.set(170 * GB)
+    kfd.live(222, 110 * GB)  # an exiting predecessor still holds 110 GB; 60 GB orphaned
+
+    def exit_then_wipe():
+        time.sleep(1.0)
+        kfd.live(222, 40 * GB)   # tearing down: orphaned rises to 130 GB
+        time.sleep(1.0)
+        kfd.exit(222)            # gone: 170 GB orphaned
+        time.sleep(1.5)
+        vram.set(90 * GB)        # the wipe frees it in steps
+        time.sleep(1.0)
+        vram.set(3 * GB)
+
+    thread = threading.Thread(target=exit_then_wipe)
+    thread.start()
+    recs = placement.settle_gpus([0], timeout=20)
+    thread.join()
+    assert recs[0]["orphaned_gb"] == 3.0 and not recs[0]["floor"], recs
+    assert recs[0]["waited_s"] > 4.0
+    assert placement._orphan_floor(0) is None
     vram.set(250 * GB)  # ... plus 150 GB that a process freed and the driver still wipes
     timer = threading.Timer(0.6, vram.set, (102 * GB,))
     timer.start()
@@ -171,6 +199,34 @@ def test_orphaned_memory_is_what_the_start_waits_for(tmp_path, vram, kfd):
     t0 = time.monotonic()
     assert placement.settle_gpus([0], timeout=10) == []
     assert time.monotonic() - t0 < 0.5
+
+
+def test_memory_turning_orphaned_is_no_idle_level(tmp_path, vram, kfd):
+    """Processes still exiting move their memory from "live" to "orphaned" (the orphaned
+    count rises while the driver's total stays): that is a drain in progress, never the GPU's
+    idle level (round 6, r6c: 62 -> 80 GB was taken for a floor)."""
+    placement = _placement(tmp_path)
+    placement.allocate("task-b", 1)
+    vram.set(170 * GB)
+    kfd.live(222, 110 * GB)  # an exiting predecessor still holds 110 GB; 60 GB orphaned
+
+    def exit_then_wipe():
+        time.sleep(1.0)
+        kfd.live(222, 40 * GB)   # tearing down: orphaned rises to 130 GB
+        time.sleep(1.0)
+        kfd.exit(222)            # gone: 170 GB orphaned
+        time.sleep(1.5)
+        vram.set(90 * GB)        # the wipe frees it in steps
+        time.sleep(1.0)
+        vram.set(3 * GB)
+
+    thread = threading.Thread(target=exit_then_wipe)
+    thread.start()
+    recs = placement.settle_gpus([0], timeout=20)
+    thread.join()
+    assert recs[0]["orphaned_gb"] == 3.0 and not recs[0]["floor"], recs
+    assert recs[0]["waited_s"] > 4.0
+    assert placement._orphan_floor(0) is None
 
 
 def test_unreadable_counters_are_not_waited_for(tmp_path, monkeypatch):
