@@ -48,7 +48,6 @@ namespace tpi_sup {
 class Supervisor {
  public:
   explicit Supervisor(Spec spec);
-
   int run();
 
  private:
@@ -77,7 +76,6 @@ class Supervisor {
   static thread_local uint64_t du_total_;
   static int du_visit(const char*, const struct stat* st, int type, struct FTW*);
   uint64_t workdir_bytes();
-
   void check_limits(double t);
   bool disk_exceeded_ = false;
 
@@ -92,34 +90,20 @@ class Supervisor {
   std::string stager_out_;
 
   void stage();
-
   void read_stager();
-
   void stage_failed(const std::string& why);
-
   bool start_stager();
-
   void stop_stager();
-
   void stager_exited(int st);
-
   void event(const std::string& code, const std::vector<std::string>& desc);
-
   static const char* state_name(Rank::State st);
-
   int running() const;
-
   void write_state(const char* phase = nullptr);
-
   std::string state_json(const char* phase = nullptr);
-
   void write_status(Rank& r, const std::string& result, const std::string& code,
                     const std::string& status);
-
   std::vector<std::string> rank_env(const Rank& r);
-
   void spawn(Rank& r, bool standby = false, bool preload = false);
-
   void spawn_standby(Rank& r, bool preload = false);
 
   // Preloaded successors (spec "preload_argv", TPI_PRELOAD=1): every running Python rank keeps
@@ -141,13 +125,9 @@ class Supervisor {
   // and GPU.  It comes after the successor reports "restored", or kStandbyHold seconds.
   static constexpr double kStandbyHold = 10.0;
   void keep_hot_standbys();
-
   void discard_standby(int index, const char* why);
-
   bool activate_standby(Rank& r);
-
   void join_cgroup(int index, pid_t pid);
-
   static std::vector<pid_t> device_holders(pid_t pgid, const std::string& device);
 
   // Evidence for warming a parked preloaded successor's GPU (spec "preload_gpu_auto"): the
@@ -160,19 +140,12 @@ class Supervisor {
   // again later.
   double next_evidence_ = 0;
   void check_preload_evidence(double t);
-
   void emit_line(Rank& r, const std::string& line);
-
   void pump(Rank& r);
-
   bool notified(Rank& r);
-
   void release_predecessors(int index, const char* why);
-
   void handoff_released();
-
   void close_log(Rank& r);
-
   void terminate(Rank& r, TermReason why);
 
   // Exit trace: a released or discarded process should be gone within ~1-2 s (its kernel
@@ -184,47 +157,27 @@ class Supervisor {
   static constexpr int kTraceMax = 64;  // events per process
 
   static std::string thread_waits(pid_t pid);
-
   void trace_exits(double t);
-
   void check_grace(double t);
-
   void check_deadline(double t);
-
   void check_respawn(double t);
-
   void next_master_port();
-
   void handle_signals();
-
   void request_stop(const std::string& source);
-
   bool request_preempt(const std::string& source, int rank = -1);
-
   bool request_requeue(const std::string& source);
-
   void open_control();
-
   void close_control();
-
   void handle_control();
-
   void reap();
-
   void on_exit(Rank& r, int st);
-
   bool ranks_settled();
-
   bool all_finished() { return ranks_settled() && detached_.empty(); }
 
   void release_resources();
-
   void settle();
-
   void drain_rank_logs();
-
   int finish();
-
   bool spawn_requeue();
 };
 
