@@ -313,9 +313,16 @@ int wait_published(const uint64_t* words, uint64_t tiles, double timeout_s) {
 }
 
 
-int prepare(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total) {
+int ensure_staging(tpi_engine* e) {
+  for (auto& buf : e->staging)
+    if (!buf) HIP_OK(hipMalloc(&buf, e->staging_bytes));
+  return 0;
+}
+
+int prepare(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, bool staging) {
   if (check_segments(segs, n, total)) return -1;
   HIP_OK(hipSetDevice(e->device));
+  if (staging && ensure_staging(e)) return -1;
   // a previous call that failed half-way may have left copies out of a staging buffer
   if (e->sdma && tpi_sdma_wait_all(e->sdma)) return -1;
   if ((size_t)n > e->seg_cap) {
@@ -485,7 +492,8 @@ tpi_engine* tpi_engine_create(int device, uint64_t chunk_bytes, int nbuf, uint64
   }
   // staging chunks also hold TPZ1 blobs: worst case tpz_bound() per tile
   const uint64_t staging_bytes = chunk_bytes + (chunk_bytes / tile_bytes) * (TPZ_HDR + 128);
-  e->staging.assign(nbuf, nullptr);
+  e->staging.assign(nbuf, nullptr);  // allocated by the first pipeline (ensure_staging)
+  e->staging_bytes = staging_bytes;
   e->ev_a.assign(nbuf, nullptr);
   e->ev_b.assign(nbuf, nullptr);
   e->ev_c.assign(nbuf, nullptr);
@@ -495,14 +503,12 @@ tpi_engine* tpi_engine_create(int device, uint64_t chunk_bytes, int nbuf, uint64
       return bail("hipEventCreate", err);
     if ((err = hipEventCreateWithFlags(&e->ev_d[i], hipEventDisableTiming)) != hipSuccess)
       return bail("hipEventCreate", err);
-    if ((err = hipMalloc(&e->staging[i], staging_bytes)) != hipSuccess)
-      return bail("hipMalloc(staging)", err);
     if ((err = hipEventCreateWithFlags(&e->ev_a[i], hipEventDisableTiming)) != hipSuccess)
       return bail("hipEventCreate", err);
     if ((err = hipEventCreateWithFlags(&e->ev_b[i], hipEventDisableTiming)) != hipSuccess)
       return bail("hipEventCreate", err);
   }
-  step("staging + events");
+  step("events");
   if ((err = hipEventCreateWithFlags(&e->ev_wait, hipEventDisableTiming)) != hipSuccess)
     return bail("hipEventCreate", err);
   if ((err = hipEventCreateWithFlags(&e->ev_done, hipEventDisableTiming)) != hipSuccess)

@@ -130,7 +130,11 @@ int tpi_copy_segments(tpi_engine* e, const tpi_seg* src, const tpi_seg* dst, int
   std::lock_guard<std::mutex> lk(e->mu);
   auto t0 = std::chrono::steady_clock::now();
   if (check_segments(src, n, total)) return -1;
-  if (prepare(e, dst, n, total)) return -1;  // dst -> d_segs
+  bool fused = true;
+  for (int i = 0; i < n && fused; ++i)
+    fused = src[i].off == dst[i].off && src[i].nbytes == dst[i].nbytes;
+  if (const char* m = getenv("TPI_HANDOFF_COPY")) fused = fused && strcmp(m, "staged") != 0;
+  if (prepare(e, dst, n, total, !fused)) return -1;  // dst -> d_segs (+ staging if staged)
   hipStream_t cs = e->compute;  // the stream of this copy (TPI_HANDOFF_PRIORITY)
   if (e->urgent) {  // after the descriptor upload prepare() queued on `compute`
     HIP_OK(hipEventRecord(e->ev_prio, e->compute));
@@ -167,10 +171,6 @@ int tpi_copy_segments(tpi_engine* e, const tpi_seg* src, const tpi_seg* dst, int
   // device time of the kernels alone (stats->pack_ms): what the hand-off spends beside them
   // (descriptor uploads, host checks, synchronisation) is copy_ms - pack_ms
   if (good) good = ok(hipEventRecord(e->ev_t0, cs), "hipEventRecord");
-  bool fused = true;
-  for (int i = 0; i < n && fused; ++i)
-    fused = src[i].off == dst[i].off && src[i].nbytes == dst[i].nbytes;
-  if (const char* m = getenv("TPI_HANDOFF_COPY")) fused = fused && strcmp(m, "staged") != 0;
   // The fused route's tile digest: the XXH64-class stream hash (no table lookups, reads at
   // ~6 TB/s) by default; TPI_HANDOFF_HASH=crc32c keeps the CRC32C tile kernels (~4.3 TB/s
   // read-back, LDS-lookup bound).

@@ -167,9 +167,16 @@ int tpi_engine_set_host_region(tpi_engine* e, void* base, uint64_t bytes, uint64
 // Allocate now what the pipelines would allocate on first use (segment descriptors, tile
 // CRCs, the codec's decode buffers): a successor that restores while its predecessor frees
 // HBM must not meet a hipMalloc that waits for the driver to clear that memory.
+int tpi_engine_alloc_staging(tpi_engine* e) {
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_OK(hipSetDevice(e->device));
+  return ensure_staging(e);
+}
+
 int tpi_engine_reserve(tpi_engine* e, int nsegs, uint64_t ntiles, int codec) {
   std::lock_guard<std::mutex> lk(e->mu);
   HIP_OK(hipSetDevice(e->device));
+  if (ensure_staging(e)) return -1;  // a restore through the host needs the ring
   if ((size_t)nsegs > e->seg_cap) {
     if (e->d_segs) HIP_OK(hipFree(e->d_segs));
     e->d_segs = nullptr;

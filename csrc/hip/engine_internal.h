@@ -122,7 +122,11 @@ struct tpi_engine {
   std::vector<hipEvent_t> ev_d;  // second half of staging slot b copied
   uint64_t split_lead = 2;       // split once the restore trails the writer by this many chunks
   uint64_t split_chunks = 0;     // chunks split by the last streamed restore
+  // staging ring: allocated at the first pipeline that needs it (ensure_staging), so an
+  // engine that only runs the HBM hand-off copy -- a parked successor's prewarmed one --
+  // holds no staging HBM
   std::vector<void*> staging;
+  uint64_t staging_bytes = 0;
   std::vector<hipEvent_t> ev_a, ev_b;  // save: packed/copied; restore: copied/unpacked
   hipEvent_t ev_wait = nullptr, ev_done = nullptr;
   hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;  // timing: the hand-off kernels' device time
@@ -205,7 +209,9 @@ int publish_chunk(tpi_engine* e, const std::vector<ChunkMark>& marks, uint64_t j
                   uint64_t* tiles_published, uint32_t* crcs_out);
 bool writer_alive(uint64_t pid);
 int wait_published(const uint64_t* words, uint64_t tiles, double timeout_s);
-int prepare(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total);
+// `staging`: the caller's pipeline moves data through the staging ring (ensure_staging)
+int prepare(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, bool staging = true);
+int ensure_staging(tpi_engine* e);
 void* device_view(void* host);
 void* meta_view(tpi_engine* e, const void* host, uint64_t bytes, bool restore_side);
 int prepare_codec(tpi_engine* e, uint64_t ntiles);

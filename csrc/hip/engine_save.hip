@@ -259,7 +259,7 @@ int tpi_snapshot(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total, void
                  uint32_t* dev_crcs, uint64_t wait_stream) {
   TpiRange range("tpi_snapshot");
   std::lock_guard<std::mutex> lk(e->mu);
-  if (prepare(e, segs, n, total)) return -1;
+  if (prepare(e, segs, n, total, false)) return -1;
   e->hash_valid = false;
   if (wait_stream != TPI_NO_STREAM) {
     HIP_OK(hipEventRecord(e->ev_wait, (hipStream_t)wait_stream));
@@ -286,6 +286,7 @@ int tpi_spill(tpi_engine* e, const void* dev_src, const uint32_t* dev_crcs, uint
   auto t0 = std::chrono::steady_clock::now();
   HIP_OK(hipSetDevice(e->device));
   if (e->sdma && tpi_sdma_wait_all(e->sdma)) return -1;
+  if (ensure_staging(e)) return -1;
   const uint64_t tile = e->tile;
   const uint64_t ntiles = (total + tile - 1) / tile;
   // the snapshot was packed on `compute`; everything below is ordered after it

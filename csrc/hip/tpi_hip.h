@@ -184,6 +184,9 @@ int tpi_engine_set_h2d_sdma(tpi_engine* e, int on);
 // Allocate the buffers the pipelines would otherwise allocate on first use, for up to
 // `nsegs` segments and `ntiles` tiles (and the codec's decode buffers when `codec`).
 int tpi_engine_reserve(tpi_engine* e, int nsegs, uint64_t ntiles, int codec);
+// Allocate the engine's HBM staging ring now (engines allocate it at their first pipeline
+// that moves data through it; the HBM hand-off copy never does).
+int tpi_engine_alloc_staging(tpi_engine* e);
 // Restore while another process is still writing the region: chunk k is copied once words[0]
 // covers its tiles; `timeout_s` without progress fails the call.  csizes == NULL: raw stream.
 int tpi_restore_stream(tpi_engine* e, const tpi_seg* segs, int n, uint64_t total,

@@ -35,13 +35,21 @@ class _Stats(ctypes.Structure):
 class DeviceEngine:
     """Per-device pipeline: compute + copy streams, ``nbuf`` staging chunks in HBM."""
 
-    def __init__(self, device_index: int, chunk_bytes: int, nbuf: int, tile_bytes: int):
+    def __init__(self, device_index: int, chunk_bytes: int, nbuf: int, tile_bytes: int,
+                 lite: bool = False):
+        """``lite``: leave the HBM staging ring to the first pipeline that needs it (the HBM
+        hand-off copy never does): a parked successor's prewarmed engine then holds no
+        staging memory.  Otherwise it is allocated now, off any later restore's path."""
         self.lib = hip()
         self.device_index = device_index
         handle = self.lib.tpi_engine_create(device_index, chunk_bytes, nbuf, tile_bytes)
         if not handle:
             raise CheckpointError("engine creation failed: %s" % self.lib.error())
         self.handle = handle
+        if not lite and self.lib.tpi_engine_alloc_staging(handle) != 0:
+            error = self.lib.error()
+            self.lib.tpi_engine_destroy(handle)
+            raise CheckpointError("engine staging allocation failed: %s" % error)
         self.chunk_bytes = int(self.lib.tpi_engine_chunk_bytes(handle))
         # which engine moves device -> host bytes: an SDMA copy engine ("sdma<i>") or, with
         # TPI_D2H_ENGINE=blit / no engine, HIP's blit kernels on the CUs ("blit")
@@ -208,7 +216,7 @@ _engine_pool_lock = threading.Lock()
 
 
 def prewarm_engine(device_index: Optional[int] = None, chunk_bytes: int = 256 << 20,
-                   nbuf: int = 3, tile_bytes: int = 1 << 20) -> bool:
+                   nbuf: int = 3, tile_bytes: int = 1 << 20, lite: bool = False) -> bool:
     """Create a device engine now for the next :class:`Checkpointer` with these parameters.
 
     Engine creation (streams, HBM staging chunks, pinned bounce buffers, SDMA binding) takes
@@ -220,12 +228,15 @@ def prewarm_engine(device_index: Optional[int] = None, chunk_bytes: int = 256 <<
             import torch
 
             device_index = torch.cuda.current_device()
-        engine = DeviceEngine(device_index, chunk_bytes, nbuf, tile_bytes)
-        # a successor's first restore then allocates nothing (PREWARM_TILES: 256 GB of 1 MiB
-        # tiles, a few MB of descriptors); allocating under its predecessor's release of HBM
-        # waits for the driver's clearing (profiles/round4/materialize_170g.md)
-        engine.reserve(PREWARM_SEGS, PREWARM_TILES, True)
-        _warm_engine(engine, device_index, tile_bytes)
+        engine = DeviceEngine(device_index, chunk_bytes, nbuf, tile_bytes, lite=lite)
+        if lite:  # streams, events and the hand-off kernels' code: what the HBM copy needs
+            _warm_handoff(engine, device_index, tile_bytes)
+        else:
+            # a successor's first restore then allocates nothing (PREWARM_TILES: 256 GB of
+            # 1 MiB tiles, a few MB of descriptors); allocating under its predecessor's release
+            # of HBM waits for the driver's clearing (profiles/round4/materialize_170g.md)
+            engine.reserve(PREWARM_SEGS, PREWARM_TILES, True)
+            _warm_engine(engine, device_index, tile_bytes)
     except Exception:
         return False
     with _engine_pool_lock:
@@ -259,6 +270,20 @@ def _warm_engine(engine: DeviceEngine, device_index: int, tile_bytes: int) -> No
         torch.cuda.synchronize(dev)
     finally:
         region.close()
+
+
+def _warm_handoff(engine: DeviceEngine, device_index: int, tile_bytes: int) -> None:
+    """One tiny HBM hand-off copy + read-back (contiguous and transposed): loads the code
+    object of the copy kernels and sizes the descriptor buffers, nothing else."""
+    import torch
+
+    dev = torch.device("cuda", device_index)
+    src = {"a": torch.ones(4096, device=dev), "t": torch.ones(64, 48, device=dev).t()}
+    dst = {"a": torch.zeros(4096, device=dev), "t": torch.zeros(64, 48, device=dev).t()}
+    plan = PackPlan.from_tensors(src, tile_bytes)
+    sig = torch.cuda.current_stream(dev).cuda_stream
+    engine.copy_segments(plan.segs.copy(), PackPlan.from_tensors(dst, tile_bytes), sig)
+    torch.cuda.synchronize(dev)
 
 
 def _take_engine(device_index: int, chunk_bytes: int, nbuf: int,

@@ -97,6 +97,7 @@ class HipLib:
             "tpi_engine_split_chunks": (u64, [vp]),
             "tpi_engine_set_progress": (i32, [vp, vp]),
             "tpi_engine_reserve": (i32, [vp, i32, u64, i32]),
+            "tpi_engine_alloc_staging": (i32, [vp]),
             "tpi_engine_set_h2d_sdma": (i32, [vp, i32]),
             "tpi_ipc_export": (i32, [vp, vp, c.POINTER(u64), c.POINTER(u64)]),
             "tpi_mem_range": (i32, [vp, c.POINTER(u64), c.POINTER(u64)]),

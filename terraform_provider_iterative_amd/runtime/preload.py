@@ -61,18 +61,20 @@ def _read_go(fd: int, on_warm=None) -> str:
 def _warm_gpu(engine: bool = True) -> None:
     """``TPI_PRELOAD=gpu``: also initialise the GPU and prewarm a checkpoint engine, as a hot
     standby does (the successor's Checkpointer takes the engine); 2.7 GB of HBM held for the
-    life of the rank (``profiles/round5/r5ah/``).  ``gpu-lite`` (``engine=False``): the GPU
-    context and the process's first hardware queue only (~137 ms of a successor's start,
-    ``profiles/round5/r5z/``); the engine is made after the activation."""
+    life of the rank (``profiles/round5/r5ah/``).  ``gpu-lite`` (``engine=False``, also the
+    default's warm-up on evidence): the GPU context, the process's first hardware queue (~137 ms
+    of a successor's start, ``profiles/round5/r5z/``) and an engine without its HBM staging
+    ring, its hand-off kernels loaded -- all the HBM copy from a live predecessor needs."""
     import torch
 
     torch.cuda.init()
     torch.empty(1 << 20, dtype=torch.uint8, device="cuda")  # context + caching allocator
     torch.ones(1, device="cuda").add_(1)  # a launch: the first hardware queue and code object
-    if engine:
-        from terraform_provider_iterative_amd.checkpoint import prewarm_engine
+    from terraform_provider_iterative_amd.checkpoint import prewarm_engine
 
-        prewarm_engine(torch.cuda.current_device())
+    # gpu-lite: an engine without its staging ring, its hand-off kernels loaded (the HBM copy
+    # needs nothing else; a host-path restore allocates the ring at its start)
+    prewarm_engine(torch.cuda.current_device(), lite=not engine)
     torch.cuda.synchronize()
 
 

@@ -1090,3 +1090,48 @@ def test_a_stuck_ipc_import_falls_back_to_the_host_copy_on_hardware(tmp_path):
     assert '"checkpoint-restored", "description": ["rank 0", "host region"' in events
     print("stuck-import fallback: resume %.2f s, successor wall %.2f s, %s" % (
         took, wall, out.split("stuck ")[1].split()[0] + " opener(s) still stuck at exit"))
+
+
+def test_a_lite_engine_holds_no_staging_until_a_pipeline_needs_it(tmp_path):
+    """A parked successor's prewarmed engine (``DeviceEngine(lite=True)``, the default
+    preload's warm-up) leaves its HBM staging ring to the first pipeline that moves data
+    through it: the hand-off copy runs without it, a host save allocates it then and is exact."""
+    import numpy as np
+
+    from terraform_provider_iterative_amd.checkpoint import Checkpointer
+    from terraform_provider_iterative_amd.checkpoint.engine import MODES, DeviceEngine
+    from terraform_provider_iterative_amd.checkpoint.host import HostRegion
+    from terraform_provider_iterative_amd.ops.packing import PackPlan
+
+    torch.cuda.synchronize()
+    chunk, nbuf = 256 << 20, 3
+    free0 = torch.cuda.mem_get_info()[0]
+    full = DeviceEngine(0, chunk, nbuf, 1 << 20)
+    free1 = torch.cuda.mem_get_info()[0]
+    lite = DeviceEngine(0, chunk, nbuf, 1 << 20, lite=True)
+    free2 = torch.cuda.mem_get_info()[0]
+    assert free0 - free1 >= nbuf * chunk  # the full engine's ring
+    assert free1 - free2 < chunk  # the lite one: streams, events, tables
+    g = torch.Generator(device="cuda").manual_seed(3)
+    src = {"a": torch.randn(3 << 20, device="cuda", generator=g),
+           "t": torch.randn(300, 700, device="cuda", generator=g).t()}
+    dst = {"a": torch.zeros(3 << 20, device="cuda"), "t": torch.zeros(300, 700, device="cuda").t()}
+    plan = PackPlan.from_tensors(src, 1 << 20)
+    sig = torch.cuda.current_stream().cuda_stream
+    res = lite.copy_segments(plan.segs.copy(), PackPlan.from_tensors(dst, 1 << 20), sig)
+    torch.cuda.synchronize()
+    assert res.bad_tiles == 0 and all(torch.equal(dst[k], src[k]) for k in src)
+    assert torch.cuda.mem_get_info()[0] > free2 - chunk  # still no ring
+    region = HostRegion((plan.total + (2 << 20)) // 4096 * 4096, device=True, populate=True)
+    try:
+        crcs = np.zeros(plan.ntiles, np.uint32)
+        lite.save(plan, region.addr, crcs, MODES["sdma"], sig)  # allocates the ring now
+        for v in dst.values():
+            v.zero_()
+        lite.restore(PackPlan.from_tensors(dst, 1 << 20), region.addr, crcs, MODES["sdma"], sig)
+        torch.cuda.synchronize()
+        assert all(torch.equal(dst[k], src[k]) for k in src)
+    finally:
+        region.close()
+        lite.close()
+        full.close()
