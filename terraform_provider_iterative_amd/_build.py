@@ -23,13 +23,17 @@ native component as ``TPI_VERSION_STRING``.
 from __future__ import annotations
 
 import glob
-import hashlib
 import os
 import shutil
 import subprocess
 import sys
 import sysconfig
 from typing import List, Sequence
+
+try:  # the builtin module: hashlib would load OpenSSL on every CLI start (~4 ms)
+    from _sha256 import sha256 as _sha256
+except ImportError:  # pragma: no cover
+    from hashlib import sha256 as _sha256
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
@@ -62,7 +66,7 @@ def _digest(cmd: Sequence[str], deps: Sequence[str]) -> str:
     # Paths inside the tree are hashed relative to it: a copy of the tree elsewhere (a GPU
     # box runs a snapshot from a scratch directory) keeps its stamps valid instead of
     # recompiling everything on first use.
-    h = hashlib.sha256()
+    h = _sha256()
     h.update("\0".join(c.replace(ROOT, "@ROOT@") for c in cmd if ".tmp." not in c).encode())
     for dep in sorted(set(deps)):
         # outside the tree (torch's version file): the absolute path, the same on every box

@@ -22,7 +22,6 @@ import datetime as _dt
 import json
 import os
 import sys
-import tarfile
 from typing import Any, Dict
 
 MARKER = "TPI-AGENT "
@@ -100,7 +99,7 @@ def _describe(task) -> Dict[str, Any]:
             "addresses": task.get_addresses(), "gpus": task.gpus()}
 
 
-def _safe_members(tar: tarfile.TarFile):
+def _safe_members(tar: "tarfile.TarFile"):
     """Regular files and directories with relative, non-escaping names only."""
     for member in tar:
         name = os.path.normpath(member.name)
@@ -113,6 +112,8 @@ def _safe_members(tar: tarfile.TarFile):
 def _push(task) -> Dict[str, Any]:
     os.makedirs(task.data_dir, exist_ok=True)
     count = size = 0
+    import tarfile
+
     with tarfile.open(fileobj=sys.stdin.buffer, mode="r|") as tar:
         for member in _safe_members(tar):
             if member.isdir():
@@ -149,6 +150,8 @@ def write_tar(root: str, flt, stream) -> Dict[str, int]:
     from ..ops import native
 
     count = size = 0
+    import tarfile
+
     with tarfile.open(fileobj=stream, mode="w|") as tar:
         if os.path.isdir(root):
             for rel, nbytes, _mtime, _mode, is_dir in native().walk(root, flt):

@@ -33,7 +33,6 @@ import os
 import re
 import shlex
 import subprocess
-import tarfile
 import threading
 from typing import Any, Dict, List, Optional
 
@@ -230,6 +229,8 @@ class RemoteNodeTask(Task):
 
     def pull(self) -> None:
         """The node's task storage, limited to ``directory_out``, into the local workdir."""
+        import tarfile  # remote-node pulls only
+
         env = self.spec.environment
         local = storage.Connection.parse(env.directory or ".").local_path()
         proc = self.transport.popen("pull", self._request(directory_out=env.directory_out,

@@ -7,7 +7,6 @@ a visible GPU a missing or broken HIP library is an error, never a silent CPU fa
 """
 from __future__ import annotations
 
-import ctypes
 import importlib.util
 import os
 import threading
@@ -79,6 +78,8 @@ class HipLib:
 
     def __init__(self, path: str):
         self.path = path
+        import ctypes  # the HIP bindings only: `tpi apply` never loads them
+
         lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
         c = ctypes
         u64, i64, i32, vp = c.c_uint64, c.c_int64, c.c_int, c.c_void_p

@@ -34,7 +34,6 @@ import posixpath
 import re
 import shlex
 import subprocess
-import tarfile
 import tempfile
 import threading
 from typing import Dict, Iterable, List, Optional, Tuple
@@ -158,6 +157,8 @@ class SSHRemote:
                  only: Optional[Iterable[str]] = None) -> Dict[str, int]:
         """Copy ``local_dir`` (filter ``rules``; ``only``: just these relative paths) into
         ``<root>/<rel>`` -- rclone copy semantics: nothing there is deleted."""
+        import tarfile  # SSH containers only: not on every apply's import path
+
         flt = make_filter(transfer_rules([]) if rules is None else rules)
         entries = [e for e in native().walk(local_dir, flt) if not e[4]]
         if only is not None:
@@ -194,6 +195,8 @@ class SSHRemote:
                  ) -> Dict[str, int]:
         """Copy ``<root>/<rel>`` into ``local_dir`` through filter ``rules`` (a missing remote
         directory copies nothing)."""
+        import tarfile
+
         src = self.path(rel)
         command = "if [ -d %s ]; then tar -c -f - -C %s .; fi" % (shlex.quote(src),
                                                                  shlex.quote(src))

@@ -9,7 +9,6 @@ appends the payloads to a local JSONL file instead (auditable telemetry).
 """
 from __future__ import annotations
 
-import hashlib
 import json
 import logging
 import os
@@ -38,6 +37,8 @@ def deterministic(data: str) -> str:
     import uuid
 
     ns = uuid.uuid5(uuid.NAMESPACE_DNS, "iterative.ai")
+    import hashlib  # scrypt (OpenSSL): only when a CI identity is hashed, not on every start
+
     dk = hashlib.scrypt(data.encode(), salt=ns.bytes, n=1 << 16, r=8, p=1, dklen=8,
                         maxmem=256 << 20)
     return str(uuid.uuid5(ns, dk.hex()))

@@ -7,9 +7,13 @@ vectors of ``identifier_test.go:41-74`` are pinned in ``tests/test_common.py``.
 """
 from __future__ import annotations
 
-import hashlib
+import os
 import re
-import secrets
+
+try:  # the builtin module: hashlib would load OpenSSL (~4 ms of every CLI start)
+    from _sha256 import sha256 as _sha256
+except ImportError:  # pragma: no cover
+    from hashlib import sha256 as _sha256
 
 from .record import record
 from .petname import generate as _petname
@@ -44,7 +48,7 @@ def _base36(number: int) -> str:
 
 def _hash(seed: str, size: int) -> str:
     """Deterministic base36 digest (``identifier.go:88-101``)."""
-    digest = hashlib.sha256(seed.encode("utf-8")).digest()
+    digest = _sha256(seed.encode("utf-8")).digest()
     result = _base36(int.from_bytes(digest, "big"))
     if len(result) < size:  # pragma: no cover - 2**256 has 50 base36 digits
         raise ValueError("not enough bytes to satisfy requested size")
@@ -94,7 +98,7 @@ def new_deterministic_identifier(name: str, prefix: str = DEFAULT_PREFIX) -> Ide
 
 
 def new_random_identifier(name: str = "", prefix: str = DEFAULT_PREFIX) -> Identifier:
-    seed = _base36(int.from_bytes(secrets.token_bytes(8), "big"))
+    seed = _base36(int.from_bytes(os.urandom(8), "big"))
     if not name:
         name = _petname(3, "-")
     return Identifier(prefix=prefix[:3], name=name, salt=_hash(seed, SHORT_LENGTH // 2))

@@ -6,7 +6,19 @@ for compatibility because random identifiers are never re-derived.
 """
 from __future__ import annotations
 
-import secrets
+import os
+
+
+def _choice(seq):
+    """``secrets.choice`` without importing ``secrets`` (it pulls in hmac/OpenSSL: ~4 ms of
+    every CLI start); the same OS randomness."""
+    n = len(seq)
+    limit = (1 << 32) - (1 << 32) % n  # rejection sampling: no modulo bias
+    while True:
+        x = int.from_bytes(os.urandom(4), "little")
+        if x < limit:
+            return seq[x % n]
+
 
 ADVERBS = (
     "ably", "aptly", "boldly", "briskly", "calmly", "deftly", "eagerly", "evenly",
@@ -35,9 +47,9 @@ NAMES = (
 def generate(words: int = 3, separator: str = "-") -> str:
     if words <= 0:
         return ""
-    parts = [secrets.choice(NAMES)]
+    parts = [_choice(NAMES)]
     if words >= 2:
-        parts.insert(0, secrets.choice(ADJECTIVES))
+        parts.insert(0, _choice(ADJECTIVES))
     for _ in range(words - 2):
-        parts.insert(0, secrets.choice(ADVERBS))
+        parts.insert(0, _choice(ADVERBS))
     return separator.join(parts)

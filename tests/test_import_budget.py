@@ -10,7 +10,9 @@ import sys
 import textwrap
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEAVY = ("http.client", "ssl", "xml.etree", "xml.etree.ElementTree", "email.utils")
+HEAVY = ("http.client", "ssl", "xml.etree", "xml.etree.ElementTree", "email.utils",
+         # OpenSSL's hash module, tar and ctypes: ~9 ms more of every start (round 6)
+         "_hashlib", "tarfile", "ctypes", "secrets")
 
 MAIN_TF = '''
 resource "iterative_task" "imports" {
