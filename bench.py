@@ -21,10 +21,19 @@ trained AdamW state (an untrained one would be all-zero moments, which compress 
 
     python bench.py --gpus N --steps K --warmup W
 
-Rank 0 prints one JSON line.  ``value`` = checkpoint bytes moved (save + restore) by all
-ranks per second of wall time (max over ranks of the timed region).  Before the timed
-region rank 0 also measures task apply -> first-log latency of an ``iterative_task`` on the
-node-local runtime (reported as ``first_log_latency_s``; not part of ``value``).
+Rank 0 prints one JSON line.  ``value`` = checkpoint bytes moved (save + restore, both
+directions counted together: they run at once on the two directions of the PCIe link) by all
+ranks per second of wall time (max over ranks of the timed region).  Untimed side
+measurements, none of them part of ``value``:
+
+* before the timed region: task apply -> first-log latency of an ``iterative_task`` on the
+  node-local runtime (``first_log_latency_s``), and on one GPU BASELINE config 2 -- ``tpi
+  apply`` of a 10 GB workdir + ``train.py`` on an idle GPU (``first_log_latency_config2``:
+  first log, push, staging);
+* after it: async-save stall, raw (codec-free) rates, the workdir fan-out, the sequential
+  rate, and on one GPU config 4 end to end through the product (``preempt_e2e``: cold =
+  the default preloaded successor, hot standby, fresh process; each run's own memory gates --
+  ``gpu_drain``, ``successor_hbm_wait`` -- are reported, the bench adds no wait of its own).
 """
 from __future__ import annotations
 
