@@ -847,3 +847,33 @@ def _split_relocated(src: np.ndarray, dst: np.ndarray, pieces: Dict[str, List[Li
     out_owner.append(owner[prev:])
     return (np.concatenate(out_src), np.concatenate(out_dst),
             np.concatenate(out_owner).astype(np.int64))
+
+
+class _SpillOffer(HbmHandoff):
+    """The claim protocol of the HBM offer next to a spill file, without a checkpointer (a
+    successor deciding before it has allocated anything)."""
+
+    def __init__(self, spill: str):
+        self._spill = spill
+
+    def _hbm_manifest_path(self) -> Optional[str]:
+        return self._spill + ".hbm"
+
+
+def decline_hbm_handoff(spill: str) -> bool:
+    """Successor side: withdraw the predecessor's HBM offer next to ``spill`` -- claim it, then
+    remove the manifest and the claim -- because this process cannot make room for its own copy
+    of the state next to the exported one.  The predecessor, waiting for a claimer
+    (``preemption._await_successor``), sees "successor closed" at once and exits, which gives
+    its HBM back; the successor restores from the host copy.  False: no offer, or another
+    process holds it."""
+    offer = _SpillOffer(spill)
+    manifest = offer._hbm_manifest_path()
+    if not os.path.exists(manifest) or not offer.claim_hbm():
+        return False
+    try:
+        os.remove(manifest)  # first: the claim's removal then reads as "closed"
+    except OSError:
+        pass
+    offer.release_hbm_claim()
+    return True

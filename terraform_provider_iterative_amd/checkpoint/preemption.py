@@ -299,20 +299,39 @@ def tick(metadata: Optional[Dict] = None, force: bool = False) -> bool:
 def _handoff_safe() -> bool:
     """May the successor start while this process is still exiting?  Its teardown (unpinning
     the host region) takes ~1.4 s per 100 GB but holds this process's HBM until the end, so
-    hand off early only when a second copy of the current HBM footprint fits next to it."""
+    hand off early only when a second copy of the current HBM footprint fits next to it --
+    by the successor's own measure (:func:`successor_need`, the room
+    :func:`wait_for_device_memory` waits for) and the driver's count as well as the runtime's.
+    A looser test here (footprint <= free) let a 150 GB state export its HBM that its
+    successor then could not make room for: both waited for the other until the 20 s linger
+    ran out (profiles/round6/r6f)."""
     if os.environ.get("TPI_EARLY_HANDOFF", "1") in ("0", "false", "no"):
         return False
     torch = sys.modules.get("torch")
     if torch is None or not torch.cuda.is_initialized():
         return True
+    from ..parallel.placement import device_vram_usage
+
     try:
         for dev in range(torch.cuda.device_count()):
             free, total = torch.cuda.mem_get_info(dev)
-            if total - free > free:
+            used = total - free
+            usage = device_vram_usage(dev)
+            if usage is not None:
+                free = min(free, usage[1] - usage[0])
+            if free < successor_need(used):
                 return False
     except Exception:
         return False
     return True
+
+
+def successor_need(state_bytes: int, margin: float = 0.01) -> int:
+    """Device memory a successor needs free before it allocates a state of ``state_bytes``:
+    the state + ``margin`` (the caching allocator's rounding), + 2 GiB for its engine and GPU
+    context.  A 150 GB state (152 GB in use with the context) still hands off device to device
+    on a 288 GiB MI355X: 155.7 GB needed, 157.2 GB free."""
+    return int(state_bytes * (1 + margin)) + (2 << 30)
 
 
 _phase: Dict[str, float] = {}  # handler phase durations (s), for the journal
@@ -441,11 +460,11 @@ def standby(prefetch_path: Optional[str] = None, materialize: bool = False) -> b
     return True
 
 
-def wait_for_device_memory(spill: str, margin: float = 0.05,
+def wait_for_device_memory(spill: str, margin: float = 0.01,
                            timeout: Optional[float] = None) -> Optional[float]:
     """A successor's gate before it allocates the state of ``spill`` (its predecessor's
-    checkpoint region): block until the device has room for the state (+ ``margin``, + 2 GiB
-    for the engine and context) by the *driver's* count as well as the HIP runtime's, or until
+    checkpoint region): block until the device has room for the state
+    (:func:`successor_need`) by the *driver's* count as well as the HIP runtime's, or until
     ``timeout`` (``TPI_STREAM_TIMEOUT``, default 30 s).  Returns the seconds waited (None:
     nothing to wait for -- no state in ``spill``, or no GPU); every wait is journalled
     (``successor-hbm-wait``).
@@ -467,7 +486,7 @@ def wait_for_device_memory(spill: str, margin: float = 0.05,
     total = peer["total"] if peer is not None else region_total(spill)
     if not total:
         return None
-    need = int(total * (1 + margin)) + (2 << 30)
+    need = successor_need(total, margin)
     if timeout is None:
         timeout = float(os.environ.get("TPI_STREAM_TIMEOUT", "30"))
     dev = torch.cuda.current_device()
@@ -475,7 +494,7 @@ def wait_for_device_memory(spill: str, margin: float = 0.05,
 
     t0 = time.monotonic()
     free = driver_free = 0
-    fits = False
+    fits = declined = False
     while True:
         free, _ = torch.cuda.mem_get_info(dev)
         usage = device_vram_usage(dev)
@@ -485,6 +504,16 @@ def wait_for_device_memory(spill: str, margin: float = 0.05,
             break
         if peer is not None and streaming_writer(spill) is None:
             peer = None  # the spill is done: from now on only the driver's count matters
+        if peer is None and not declined:
+            # a predecessor that exported its HBM keeps it until a successor claims it: with
+            # no room for our copy next to it, withdraw the offer so it exits now (restore
+            # from the host copy) instead of both waiting out its linger
+            from .handoff import decline_hbm_handoff
+
+            declined = True
+            if decline_hbm_handoff(spill):
+                journal("successor-hbm-declined", "%.1f GB needed" % (need / 1e9),
+                        "free %.1f GB (driver %.1f GB)" % (free / 1e9, driver_free / 1e9))
         time.sleep(0.005)
     waited = time.monotonic() - t0
     journal("successor-hbm-wait", "%.1f GB needed" % (need / 1e9), "waited %.3f s" % waited,

@@ -243,12 +243,13 @@ class Placement:
         A GPU is settled when both hold:
         * orphaned memory -- the driver's ``mem_info_vram_used`` minus what live processes
           hold by KFD's per-process accounting -- is at most ``ORPHAN_LIMIT`` (or this GPU's
-          learned idle floor + 2 GiB), or has stopped falling for ``ORPHAN_FLAT_S`` (then it
-          is no drain: the level is remembered as the GPU's floor);
+          learned idle floor + 2 GiB), or has stopped falling for ``ORPHAN_FLAT_S`` -- longer
+          for a big count, :func:`flat_window` -- (then it is no drain: a level up to
+          ``ORPHAN_FLOOR_MAX`` is remembered as the GPU's floor);
         * with a drain marker (the previous holder's released lease): the driver's count is
           back to that holder's reservation count (``vram_baseline``) + ``max(1 GiB, 1 %)``.
         Without KFD's accounting, a count that keeps falling is waited for until it has not
-        fallen for ``ORPHAN_FLAT_S``.  The GPU's lease then records the settled count as its
+        fallen for :func:`flat_window`.  The GPU's lease then records the settled count as its
         own baseline.  GPUs without a readable counter (no sysfs, fake inventories) are not
         waited for."""
         if timeout is None:
@@ -288,7 +289,8 @@ class Placement:
                 st = item["now"]
                 level = st["orphaned"] if st["orphaned"] is not None else None
                 quiet = now - (item["last_drop"] if item["last_drop"] is not None else t0)
-                flat = quiet >= ORPHAN_FLAT_S
+                flat = quiet >= flat_window(st["orphaned"] if st["orphaned"] is not None
+                                            else st["used"])
                 if level is not None:
                     drained = level <= item["limit"] or flat
                 else:  # no per-process accounting: a falling count is a drain
@@ -845,7 +847,17 @@ def vram_usage(pci: str) -> Optional[Tuple[int, int]]:
 
 
 ORPHAN_LIMIT = 4 << 30  # orphaned VRAM (held by no live process) a GPU may carry when idle
-ORPHAN_FLAT_S = 3.0     # an orphan count that has not fallen for this long is no drain
+ORPHAN_FLAT_S = 3.0     # an orphan count that has not fallen for this long is no drain ...
+WIPE_RATE_MIN = 20e9    # ... unless it is big: the driver wipes freed VRAM at ~35 GB/s and
+#                         gives a buffer back in one step at the end of its wipe, so a 150 GB
+#                         buffer shows no fall for ~4.3 s (profiles/round6/r6f: a 3 s window
+#                         took it for an idle level)
+
+
+def flat_window(level: int) -> float:
+    """Seconds without a fall after which ``level`` bytes of orphaned VRAM are taken for no
+    drain: ``ORPHAN_FLAT_S``, or as long as the driver's wipe of that much memory can take."""
+    return max(ORPHAN_FLAT_S, level / WIPE_RATE_MIN)
 ORPHAN_FLOOR_MAX = 16 << 30  # the most a learned idle level may be
 
 

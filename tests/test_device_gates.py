@@ -179,3 +179,93 @@ def test_workdir_attach_is_bounded_and_journalled(tmp_path, monkeypatch):
     lib2.release.set()
     assert stage._ipc_open_bounded(lib2, b"\0" * 64, 0, 3 * GB, timeout=5) == 0x1000
     assert _events(events)[-1]["code"] == "workdir-attached" and not lib2.closed
+
+
+class FakeCudaDevices(FakeCuda):
+    TOTAL = 288 * 2 ** 30  # an MI355X: 288 GiB = 309.2 GB
+
+    def device_count(self):
+        return 1
+
+    def mem_get_info(self, dev):
+        return self.free, self.TOTAL
+
+
+def test_early_hand_off_needs_the_successors_room_by_both_counts(monkeypatch):
+    """The predecessor offers its HBM only when the successor's own measure (state + 1 % +
+    2 GiB) fits next to it -- "footprint <= free" offered states the successor then could not
+    make room for, and both waited out the linger (r6f)."""
+    from terraform_provider_iterative_amd.parallel import placement
+
+    cuda = FakeCudaDevices(0)
+    monkeypatch.setitem(sys.modules, "torch", types.SimpleNamespace(cuda=cuda))
+    monkeypatch.delenv("TPI_EARLY_HANDOFF", raising=False)
+    driver = {"used": None}
+    monkeypatch.setattr(placement, "device_vram_usage",
+                        lambda dev: None if driver["used"] is None
+                        else (driver["used"], cuda.TOTAL))
+    cuda.free = cuda.TOTAL - 154 * GB  # footprint 154 <= free 155.2, but the need is 157.7
+    assert not preemption._handoff_safe()
+    cuda.free = cuda.TOTAL - 152 * GB  # a 150 GB state + context: still two copies
+    assert preemption._handoff_safe()
+    cuda.free = cuda.TOTAL - 102 * GB  # 100 GB state
+    assert preemption._handoff_safe()
+    driver["used"] = 210 * GB  # ... unless the driver still holds an exited process's memory
+    assert not preemption._handoff_safe()
+    assert preemption.successor_need(100 * GB) == 101 * GB + 2 * 2 ** 30
+
+
+PREDECESSOR = textwrap.dedent('''
+    import os, sys, time
+    sys.path.insert(0, %(root)r)
+    from terraform_provider_iterative_amd.checkpoint import preemption
+    from terraform_provider_iterative_amd.checkpoint.handoff import _SpillOffer
+
+    open(%(spill)r + ".hbm", "w").write("{}")  # the exported offer
+    print("offered", flush=True)
+    t0 = time.monotonic()
+    how = preemption._await_successor(_SpillOffer(%(spill)r))
+    print("exit: %%s after %%.2f s" %% (how, time.monotonic() - t0), flush=True)
+''')
+
+
+def test_successor_withdraws_an_offer_it_cannot_make_room_for(tmp_path, monkeypatch):
+    from terraform_provider_iterative_amd.checkpoint import checkpointer as ckmod
+    from terraform_provider_iterative_amd.parallel import placement
+
+    spill = str(tmp_path / "spill")
+    events = tmp_path / "events.jsonl"
+    env = dict(os.environ, TPI_EVENTS_FILE=str(events), TPI_LINGER_SECONDS="60")
+    pred = subprocess.Popen([sys.executable, "-c", PREDECESSOR % {"root": ROOT, "spill": spill}],
+                            env=env, stdout=subprocess.PIPE, text=True)
+    try:
+        assert pred.stdout.readline().strip() == "offered"
+        monkeypatch.setenv("TPI_EVENTS_FILE", str(events))
+        # the predecessor holds its 150 GB state, and memory an earlier process left is still
+        # being wiped by the driver: no room for a second copy
+        cuda = FakeCudaDevices(140 * GB)
+        monkeypatch.setitem(sys.modules, "torch", types.SimpleNamespace(cuda=cuda))
+        monkeypatch.setattr(ckmod, "streaming_writer", lambda path: None)  # spill complete
+        monkeypatch.setattr(ckmod, "region_total", lambda path: 150 * GB)
+        monkeypatch.setattr(placement, "device_vram_usage",
+                            lambda dev: (cuda.TOTAL - cuda.free, cuda.TOTAL))
+
+        def predecessor_exits():  # its memory comes back once it has gone
+            pred.wait(30)
+            cuda.free = cuda.TOTAL - 2 * GB
+
+        threading.Thread(target=predecessor_exits, daemon=True).start()
+        t0 = time.monotonic()
+        preemption.wait_for_device_memory(spill, timeout=20)
+        assert time.monotonic() - t0 < 10  # not the predecessor's 60 s linger
+        out = pred.stdout.read()
+        assert "exit: successor closed" in out, out
+        codes = [e["code"] for e in _events(events)]
+        assert "successor-hbm-declined" in codes
+        rec = [e for e in _events(events) if e["code"] == "successor-hbm-wait"][-1]
+        assert not any("timed out" in d for d in rec["description"])
+        assert not os.path.exists(spill + ".hbm") and not os.path.exists(spill + ".hbm.claim")
+    finally:
+        if pred.poll() is None:
+            pred.kill()
+        pred.wait()
