@@ -313,17 +313,35 @@ def _handoff_safe() -> bool:
     from ..parallel.placement import device_vram_usage
 
     try:
+        states = _registered_state_bytes()
         for dev in range(torch.cuda.device_count()):
             free, total = torch.cuda.mem_get_info(dev)
-            used = total - free
+            # the successor's copy is the registered state (a hot standby's own context is
+            # already in use next to it); without a registered plan, all memory in use
+            state = states.get(dev, 0) if states else total - free
+            if not state:
+                continue
             usage = device_vram_usage(dev)
             if usage is not None:
                 free = min(free, usage[1] - usage[0])
-            if free < successor_need(used):
+            if free < successor_need(state):
                 return False
     except Exception:
         return False
     return True
+
+
+def _registered_state_bytes() -> Dict[int, int]:
+    """Bytes of the registered checkpointers' states per device index ({} when none is
+    bound yet)."""
+    out: Dict[int, int] = {}
+    for ck in _registered:
+        plan = getattr(ck, "plan", None)
+        total = getattr(plan, "total", None) if plan is not None else None
+        if total:
+            dev = int(getattr(ck, "device_index", 0) or 0)
+            out[dev] = out.get(dev, 0) + int(total)
+    return out
 
 
 def successor_need(state_bytes: int, margin: float = 0.01) -> int:

@@ -213,6 +213,15 @@ def test_early_hand_off_needs_the_successors_room_by_both_counts(monkeypatch):
     driver["used"] = 210 * GB  # ... unless the driver still holds an exited process's memory
     assert not preemption._handoff_safe()
     assert preemption.successor_need(100 * GB) == 101 * GB + 2 * 2 ** 30
+    # with a registered state the measure is that state, not everything in use: a hot
+    # standby's context (here 2 GB) sits next to a 150 GB state, and a second copy still fits
+    driver["used"] = None
+    ck = types.SimpleNamespace(plan=types.SimpleNamespace(total=150 * GB), device_index=0)
+    monkeypatch.setattr(preemption, "_registered", [ck])
+    cuda.free = cuda.TOTAL - 154 * GB
+    assert preemption._handoff_safe()
+    ck.plan.total = 153 * GB
+    assert not preemption._handoff_safe()
 
 
 PREDECESSOR = textwrap.dedent('''
