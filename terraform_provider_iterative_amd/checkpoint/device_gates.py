@@ -56,7 +56,7 @@ def wait_for_device_memory(spill: str, margin: float = 0.01,
       releases it seconds after the exit, while the runtime already reports it free.
       Allocating on top of it made the driver evict buffers under the hand-off copy (the
       round-5 faults, ``profiles/round5/ipc_cause.md``), so the successor waits for that too.
-    Called by :func:`standby` before the script allocates its state."""
+    Called by ``preemption.standby`` before the script allocates its state."""
     from .checkpointer import region_total, streaming_writer
 
     torch = sys.modules.get("torch")
@@ -93,13 +93,13 @@ def wait_for_device_memory(spill: str, margin: float = 0.01,
             declined = True
             if decline_hbm_handoff(spill):
                 _journal("successor-hbm-declined", "%.1f GB needed" % (need / 1e9),
-                        "free %.1f GB (driver %.1f GB)" % (free / 1e9, driver_free / 1e9))
+                         "free %.1f GB (driver %.1f GB)" % (free / 1e9, driver_free / 1e9))
         time.sleep(0.005)
     waited = time.monotonic() - t0
     _journal("successor-hbm-wait", "%.1f GB needed" % (need / 1e9), "waited %.3f s" % waited,
-            "free %.1f GB (driver %.1f GB)" % (free / 1e9, driver_free / 1e9),
-            "predecessor streaming" if peer is not None else "predecessor done",
-            *([] if fits else ["timed out: allocating anyway"]))
+             "free %.1f GB (driver %.1f GB)" % (free / 1e9, driver_free / 1e9),
+             "predecessor streaming" if peer is not None else "predecessor done",
+             *([] if fits else ["timed out: allocating anyway"]))
     return waited
 
 
@@ -151,7 +151,7 @@ def _device_settled_for_handoff(checkpointer: Checkpointer) -> bool:
             "waited %.3f s" % waited]
     if not (room and settled):
         _journal("checkpoint-hbm-skipped", "device over-committed: restoring from the host copy",
-                *desc)
+                 *desc)
         return False
     if waited > 0.001:
         _journal("handoff-device-settled", *desc)
@@ -188,10 +188,10 @@ def _hbm_fatal(checkpointer: Checkpointer, error: BaseException) -> None:
     process with a new GPU context, which restores from the host copy.  Without a supervisor
     the caller re-raises."""
     _journal("checkpoint-hbm-fatal", str(error),
-            "sticky device error: this process's GPU context is unusable, so there is no "
-            "fallback in it", "dump %s" % getattr(checkpointer, "hbm_fault_dump", None),
-            "the respawn restores from the host copy" if os.environ.get("TPI_NOTIFY_FD")
-            else "no supervisor: raised to the script")
+             "sticky device error: this process's GPU context is unusable, so there is no "
+             "fallback in it", "dump %s" % getattr(checkpointer, "hbm_fault_dump", None),
+             "the respawn restores from the host copy" if os.environ.get("TPI_NOTIFY_FD")
+             else "no supervisor: raised to the script")
     try:
         os.remove(checkpointer._hbm_manifest_path())
     except (OSError, TypeError):
