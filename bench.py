@@ -391,6 +391,11 @@ def main(argv=None):
         # (after the timed loop the driver is still taking back its 200 GB, and the task's
         # start would rightly wait for that: gpu-drain)
         config2 = workdir_config2(10.0, args.e2e_timeout)
+    if world > 1:
+        # the other ranks start their setup (filling and pinning their share of the state)
+        # only after rank 0's probes: N-1 setups beside it inflated the measured first log
+        # (rehearsal with 4 ranks on one GPU: 0.217 s against 0.073 s, profiles/round6/r6j)
+        barrier()
 
     from terraform_provider_iterative_amd.checkpoint import Checkpointer
 
