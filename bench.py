@@ -385,6 +385,10 @@ def main(argv=None):
         # state spawns the probe's `tpi apply` ~17 ms slower (profiles/hw_queues_round3.md).
         gpus = torch.cuda.device_count() if on_gpu else world
         latency = first_log_latency(parallelism=max(1, min(world, gpus)))
+        if latency:
+            print("bench: apply -> first log %s s (CLI), %s s (API); GPU memory gate waited "
+                  "up to %s s" % (latency.get("cli_s"), latency.get("api_s"),
+                                  latency.get("gpu_drain_max_s")), file=sys.stderr, flush=True)
     config2 = None
     if rank == 0 and world == 1 and on_gpu and args.config2 == "auto":
         # config 2 as a user meets it: on an idle GPU, before this process fills the device

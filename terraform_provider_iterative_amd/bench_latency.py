@@ -61,6 +61,25 @@ def _first_log(state_root: str, timeout: float, t0: float, poll: float = 0.0005,
     return None
 
 
+def _gate_wait(state_root: str) -> float:
+    """Seconds the task's start waited for its GPUs' memory (``gpu-drain`` events: the driver
+    still wiping memory an earlier process freed), summed over the task's journals -- part of
+    the measured latency, reported beside it."""
+    waited = 0.0
+    for path in glob.glob(os.path.join(state_root, "*", "*", "supervisor", "events.jsonl")):
+        try:
+            with open(path) as handle:
+                for line in handle:
+                    if '"gpu-drain"' not in line:
+                        continue
+                    for item in json.loads(line).get("description", []):
+                        if isinstance(item, str) and item.startswith("waited "):
+                            waited += float(item.split()[1])
+        except (OSError, ValueError):
+            continue
+    return waited
+
+
 def _cleanup(workdir: str, env: Dict[str, str]) -> None:
     subprocess.run([sys.executable, os.path.join(ROOT, "bin", "tpi"), "destroy", "-auto-approve"],
                    cwd=workdir, env=env, capture_output=True, timeout=120)
@@ -68,8 +87,9 @@ def _cleanup(workdir: str, env: Dict[str, str]) -> None:
 
 def measure_first_log_latency(timeout: float = 60.0, cloud: Optional[str] = None,
                               repeats: int = 3, parallelism: int = 1) -> Dict[str, float]:
-    """Returns ``{"cli_s": .., "api_s": .., "cloud": ..}`` (medians over ``repeats``): the
-    first log line of any rank; with ``parallelism`` N > 1 also ``cli_all_s`` / ``api_all_s``,
+    """Returns ``{"cli_s": .., "api_s": .., "cloud": .., "gpu_drain_max_s": ..}`` (medians over
+    ``repeats``; the last: the longest wait of any sample's start for its GPUs' memory, included
+    in its latency): the first log line of any rank; with ``parallelism`` N > 1 also ``cli_all_s`` / ``api_all_s``,
     until every one of the N ranks (one GPU each on ``mi355x``) has logged."""
     gpu = False
     try:
@@ -80,7 +100,7 @@ def measure_first_log_latency(timeout: float = 60.0, cloud: Optional[str] = None
         pass
     cloud = cloud or ("mi355x" if gpu else "local")
     machine = "m+mi355x" if cloud == "mi355x" else "s"
-    cli, api, cli_all, api_all = [], [], [], []
+    cli, api, cli_all, api_all, gate = [], [], [], [], []
     for i in range(repeats):
         base = tempfile.mkdtemp(prefix="tpi-latency-")
         try:
@@ -99,6 +119,7 @@ def measure_first_log_latency(timeout: float = 60.0, cloud: Optional[str] = None
             latency = _first_log(env["TPI_STATE_ROOT"], timeout, t0, proc=proc)
             every = _first_log(env["TPI_STATE_ROOT"], timeout, t0, count=parallelism, proc=proc)
             proc.wait(timeout=timeout)
+            gate.append(_gate_wait(env["TPI_STATE_ROOT"]))
             if latency is not None:
                 cli.append(latency)
             if every is not None:
@@ -125,6 +146,7 @@ def measure_first_log_latency(timeout: float = 60.0, cloud: Optional[str] = None
                 wait = timeout if created else 0.0  # a refused create logs nothing
                 lat = _first_log(os.environ["TPI_STATE_ROOT"], wait, t1)
                 every = _first_log(os.environ["TPI_STATE_ROOT"], wait, t1, count=parallelism)
+                gate.append(_gate_wait(os.environ["TPI_STATE_ROOT"]))
                 if lat is not None:
                     api.append(lat)
                 if every is not None:
@@ -146,7 +168,10 @@ def measure_first_log_latency(timeout: float = 60.0, cloud: Optional[str] = None
         return round(xs[len(xs) // 2], 4) if xs else None
 
     out = {"cli_s": median(cli), "api_s": median(api), "cloud": cloud, "samples": len(cli),
-           "parallelism": parallelism}
+           "parallelism": parallelism,
+           # the most any sample's start waited for the driver to give its GPUs' memory back
+           # (0 on an idle node; after a job that freed 100+ GB, seconds: gpu-drain)
+           "gpu_drain_max_s": round(max(gate), 4) if gate else None}
     if parallelism > 1:
         out.update(cli_all_s=median(cli_all), api_all_s=median(api_all))
     return out
