@@ -10,7 +10,11 @@
 * :func:`_sticky_device_error` / :func:`_hbm_fatal`: a sticky HIP error in the copy is fatal
   for the process -- the hand-off is withdrawn and the respawn restores from the host copy.
 
-Why (the round-5/6 faults): ``profiles/round6/handoff_fault.md``.
+Why (the round-5/6 faults): ``profiles/round6/handoff_fault.md``.  Reference: a replacement
+for a reclaimed spot VM is a fresh machine from the group's launch template
+(``task/aws/resources/resource_auto_scaling_group.go:51-106``) and never inherits its
+predecessor's memory; on one node the same GPU changes hands instead, and these gates (with
+``parallel/placement.py`` ``settle_gpus`` for a task's start) stand in for that guarantee.
 """
 from __future__ import annotations
 

@@ -230,7 +230,10 @@ class Placement:
         """Before a task's ranks start on GPUs ``indices``: wait until the amdgpu driver has
         taken the previous holders' device memory back, bounded by ``timeout``
         (``TPI_GPU_DRAIN_TIMEOUT``, default 30 s).  Returns one record per GPU that had
-        something to wait for (for the task's journal: ``gpu-drain``).
+        something to wait for (for the task's journal: ``gpu-drain``).  Reference: the
+        reference's replacement machine is a fresh VM (``task/aws/resources/
+        resource_auto_scaling_group.go:51-106``) that inherits nothing of its predecessor;
+        here a GPU changes hands on one node, so its start waits for what the last holder left.
 
         Why: a process's HBM is not free when it exits, nor when it frees it -- the driver
         wipes freed VRAM and releases it seconds later (200 GB: ~5 s; a 100 GB buffer as one
