@@ -179,6 +179,7 @@ struct Spec {
   std::vector<std::vector<int>> rank_cpus;   // NUMA-local cores of the rank's GPUs (affinity)
   std::string master_addr = "127.0.0.1";
   int master_port = 29500;
+  bool master_port_probe = false;  // master_port is a base: take the first free port from it
   bool gang = true, fail_fast = true, respawn_on_sigterm = true, login_shell = false;
   bool standby = false;
   bool standby_hot = false;  // keep the standby running before any preemption
@@ -252,6 +253,7 @@ inline Spec load_spec(const std::string& path) {
   s.rank_cpus.resize(s.parallelism);
   s.master_addr = v["master_addr"].str("127.0.0.1");
   s.master_port = (int)v["master_port"].num(29500);
+  s.master_port_probe = v["master_port_probe"].boolean(false);
   s.gang = v["gang"].boolean(true);
   s.fail_fast = v["fail_fast"].boolean(s.parallelism > 1);
   s.respawn_on_sigterm = v["respawn_on_sigterm"].boolean(true);

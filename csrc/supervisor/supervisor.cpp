@@ -67,6 +67,7 @@ int Supervisor::run() {
   memory_.start();
   event("supervisor-start", {"pid " + std::to_string(getpid()),
                              "parallelism " + std::to_string(s_.parallelism)});
+  if (s_.master_port_probe) pick_master_port(0);
   if (s_.deadline > 0 && now() >= s_.deadline) {
     // Past the deadline before running (tpl:38-41): nothing may run any more.
     for (auto& r : ranks_) {

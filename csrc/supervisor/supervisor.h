@@ -162,6 +162,7 @@ class Supervisor {
   void check_deadline(double t);
   void check_respawn(double t);
   void next_master_port();
+  void pick_master_port(int from);
   void handle_signals();
   void request_stop(const std::string& source);
   bool request_preempt(const std::string& source, int rank = -1);

@@ -314,8 +314,13 @@ void Supervisor::check_respawn(double t) {
 
 // A fresh rendezvous port for every gang incarnation: a predecessor that lingers after its
 // spill (early hand-off) may still hold the old one -- rank 0's TCPStore listens on it.
-void Supervisor::next_master_port() {
-  for (int i = 1; i <= 256; ++i) {
+void Supervisor::next_master_port() { pick_master_port(1); }
+
+// The first port at master_port + from, ... that binds on the loopback (spec
+// "master_port_probe": the task's first incarnation, so `tpi apply` does not probe ports
+// itself -- its Python side then needs no socket module).
+void Supervisor::pick_master_port(int from) {
+  for (int i = from; i <= from + 255; ++i) {
     int port = s_.master_port + i;
     if (port > 65000) port = 20000 + port % 1000;
     int fd = socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
@@ -327,6 +332,7 @@ void Supervisor::next_master_port() {
     const bool free_port = fd >= 0 && bind(fd, (struct sockaddr*)&a, sizeof(a)) == 0;
     if (fd >= 0) close(fd);
     if (free_port) {
+      if (port == s_.master_port && from == 0) return;  // the base itself: nothing to say
       s_.master_port = port;
       event("rendezvous", {"master port " + std::to_string(port)});
       return;

@@ -19,7 +19,6 @@ import json
 import logging
 import os
 import signal
-import socket
 import subprocess
 import sys
 import time
@@ -57,23 +56,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 
 
 def node_address() -> str:
+    import socket
+
     try:
         with socket.socket(socket.AF_INET, socket.SOCK_DGRAM) as s:
             s.connect(("10.255.255.255", 1))
             return s.getsockname()[0]
     except OSError:
         return "127.0.0.1"
-
-
-def _free_port(start: int) -> int:
-    for port in range(start, start + 2000):
-        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-            try:
-                s.bind(("127.0.0.1", port))
-                return port
-            except OSError:
-                continue
-    return start
 
 
 def shebang_python(script: str):
@@ -331,7 +321,9 @@ class NodeTask(NodeQueue, NodeStorage, Task):
             "script": script_path, "env": env, "deadline": d.get("deadline", 0),
             "parallelism": parallelism, "ranks": ranks,
             "master_addr": "127.0.0.1",
-            "master_port": _free_port(DEFAULT_MASTER_PORT_BASE + (hash(self.id) % 1000) * 7),
+            # a base: the supervisor takes the first free port from it (no probing here)
+            "master_port": DEFAULT_MASTER_PORT_BASE + (hash(self.id) % 1000) * 7,
+            "master_port_probe": True,
             "gang": True, "fail_fast": parallelism > 1, "respawn_on_sigterm": True,
             "max_restarts": int(knob("TPI_MAX_RESTARTS", "-1")),
             "grace_seconds": float(knob("TPI_GRACE_SECONDS", "30")),

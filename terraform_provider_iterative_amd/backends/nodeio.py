@@ -4,7 +4,6 @@ from __future__ import annotations
 
 import json
 import os
-import socket
 import time
 from typing import Dict, Optional
 
@@ -14,6 +13,8 @@ def control_socket(sup_dir: str, command: str, timeout: float = 2.0) -> Optional
     a dict, or None when no supervisor is listening.  The path is reached through
     ``/proc/self/fd`` because AF_UNIX paths are limited to 108 bytes (the supervisor binds
     the same way)."""
+    import socket  # not on `tpi apply`'s path (tests/test_import_budget.py)
+
     try:
         dfd = os.open(sup_dir, os.O_RDONLY | os.O_DIRECTORY)
     except OSError:

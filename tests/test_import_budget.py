@@ -13,6 +13,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEAVY = ("http.client", "ssl", "xml.etree", "xml.etree.ElementTree", "email.utils",
          # OpenSSL's hash module, tar and ctypes: ~9 ms more of every start (round 6)
          "_hashlib", "tarfile", "ctypes", "secrets")
+# imported only once the task has started (its `addresses` attribute), not before: the
+# rendezvous port is probed by the supervisor, not by `tpi apply` (round 6)
+BEFORE_START = ("socket",)
 
 MAIN_TF = '''
 resource "iterative_task" "imports" {
@@ -38,6 +41,15 @@ PROBE = textwrap.dedent('''
             json.dump(sorted(sys.modules), f)
 
     atexit.register(dump)
+    from terraform_provider_iterative_amd.backends import node
+    real_start = node.NodeTask.start
+
+    def start(self, *a, **kw):  # what the CLI had loaded when it started the supervisor
+        with open(out + ".start", "w") as f:
+            json.dump(sorted(sys.modules), f)
+        return real_start(self, *a, **kw)
+
+    node.NodeTask.start = start
     sys.argv = ["tpi", "apply", "-auto-approve"]
     from terraform_provider_iterative_amd.cli.tf import main
     code = main()
@@ -56,16 +68,18 @@ def _apply_modules(tmp_path):
         proc = subprocess.run([sys.executable, "-c", PROBE % {"root": ROOT, "out": str(out)}],
                               cwd=work, env=env, capture_output=True, text=True, timeout=120)
         assert proc.returncode == 0, proc.stderr[-2000:]
-        return set(json.loads(out.read_text()))
+        at_start = tmp_path / "modules.json.start"
+        return set(json.loads(out.read_text())), set(json.loads(at_start.read_text()))
     finally:
         subprocess.run([sys.executable, os.path.join(ROOT, "bin", "tpi"), "destroy",
                         "-auto-approve"], cwd=work, env=env, capture_output=True, timeout=120)
 
 
 def test_local_apply_does_not_import_the_object_store_clients(tmp_path):
-    loaded = _apply_modules(tmp_path)
+    loaded, at_start = _apply_modules(tmp_path)
     assert "terraform_provider_iterative_amd.backends.node" in loaded  # the apply really ran
     assert not (loaded & set(HEAVY)), sorted(loaded & set(HEAVY))
+    assert not (at_start & set(BEFORE_START)), sorted(at_start & set(BEFORE_START))
     assert "terraform_provider_iterative_amd.storage.objectstore" not in loaded
 
 

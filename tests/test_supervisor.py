@@ -176,3 +176,27 @@ def test_rank_cpu_affinity_from_spec(binary, tmp_path):
     full = ",".join(map(str, allowed))
     assert str(want[0]) in lines
     assert len(lines) == 2 and any(l != str(want[0]) or full == str(want[0]) for l in lines)
+
+
+def test_supervisor_takes_the_first_free_rendezvous_port(binary, tmp_path):
+    """``master_port_probe``: the spec's port is a base, and the supervisor (not ``tpi
+    apply``) takes the first port from it that binds -- journalled when it is not the base."""
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as busy:
+        busy.bind(("127.0.0.1", 0))
+        base = busy.getsockname()[1]
+        busy.listen(1)
+        task, spec = _spec(tmp_path, "#!/bin/sh\necho port=$MASTER_PORT\n", master_port=base,
+                           master_port_probe=True)
+        _run(binary, spec)
+    port = int(_logs(task)[0].split("port=")[1].split()[0])
+    assert base < port <= base + 255
+    assert any(e["code"] == "rendezvous" and "master port %d" % port in e["description"]
+               for e in _events(task))
+    # a free base is used as it is, without a journal line
+    task2, spec2 = _spec(tmp_path / "again", "#!/bin/sh\necho port=$MASTER_PORT\n",
+                         master_port=port, master_port_probe=True)
+    _run(binary, spec2)
+    assert "port=%d" % port in _logs(task2)[0]
+    assert not any(e["code"] == "rendezvous" for e in _events(task2))
