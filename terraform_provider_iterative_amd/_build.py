@@ -15,7 +15,11 @@
 Nothing built is tracked by git.  A target is rebuilt when its ``.stamp`` (SHA-256 of the
 compile command and of every source/header it depends on) no longer matches -- content, not
 mtimes, so a fresh checkout (where every file has the checkout's mtime) always compiles from
-source.  ``python -m terraform_provider_iterative_amd._build`` builds everything;
+source.  The content check costs a few ms (reading and hashing every source, importing
+pybind11 for the command), which ``tpi apply`` would pay before every task start; a ``.fast``
+file next to the stamp records the size and mtime of every dependency, of the target and of
+this file as they were when the content last matched, and while all of them are unchanged the
+content check is skipped (any change, a fresh checkout included, goes back to it).  ``python -m terraform_provider_iterative_amd._build`` builds everything;
 ``__graft_entry__.build()`` calls :func:`build_all`.  The release version
 (``_version.py``, the reference's ``-X utils.Version``, ``Makefile:10``) is compiled into every
 native component as ``TPI_VERSION_STRING``.
@@ -91,6 +95,40 @@ def _stale(target: str, cmd: Sequence[str], deps: Sequence[str]) -> bool:
 def _stamp(target: str, cmd: Sequence[str], deps: Sequence[str]) -> None:
     with open(target + ".stamp", "w") as handle:
         handle.write(_digest(cmd, deps) + "\n")
+    _write_fast(target, deps)
+
+
+_FAST_ENV = ("CXX", "ROCM_PATH", "PYTORCH_ROCM_ARCH", "TPI_VERSION")
+
+
+def _fast_signature(target: str, deps: Sequence[str]) -> str:
+    """Sizes and mtimes of ``target``, its dependencies and this file, plus the environment
+    the command depends on (its compiler, ROCm, architecture, version)."""
+    parts = ["%s=%s" % (k, os.environ.get(k, "")) for k in _FAST_ENV]
+    for path in [target, os.path.abspath(__file__), *sorted(set(deps))]:
+        st = os.stat(path)
+        name = os.path.relpath(path, ROOT) if path.startswith(ROOT + os.sep) else path
+        parts.append("%s:%d:%d" % (name, st.st_size, st.st_mtime_ns))
+    return "\n".join(parts)
+
+
+def _fast_fresh(target: str, deps: Sequence[str]) -> bool:
+    """True when nothing :func:`_fast_signature` covers changed since the content last matched."""
+    try:
+        with open(target + ".fast") as handle:
+            return handle.read() == _fast_signature(target, deps)
+    except OSError:
+        return False
+
+
+def _write_fast(target: str, deps: Sequence[str]) -> None:
+    try:
+        tmp = target + ".fast.tmp.%d" % os.getpid()
+        with open(tmp, "w") as handle:
+            handle.write(_fast_signature(target, deps))
+        os.replace(tmp, target + ".fast")
+    except OSError:
+        pass
 
 
 def _run(cmd: List[str], verbose: bool) -> None:
@@ -110,6 +148,7 @@ def _build(target: str, cmd: List[str], deps: Sequence[str], force: bool,
            verbose: bool) -> str:
     """Compile ``cmd`` (whose output is the placeholder ``@OUT@``) into ``target`` when stale."""
     if not force and not _stale(target, cmd, deps):
+        _write_fast(target, deps)  # the content matched: skip the hashing next time
         return target
     tmp = _atomic_output(target)
     _run([tmp if c == "@OUT@" else c for c in cmd], verbose)
@@ -125,6 +164,8 @@ def _define_version() -> str:
 def build_native(force: bool = False, verbose: bool = False) -> str:
     srcs = _sources("native/*.cpp")
     deps = srcs + _sources("native/*.h", "common/*.h", "hip/tpi_hip.h")
+    if not force and _fast_fresh(NATIVE_SO, deps):
+        return NATIVE_SO
     import pybind11
 
     cxx = os.environ.get("CXX", "g++")
@@ -184,6 +225,8 @@ def build_supervisor(force: bool = False, verbose: bool = False) -> str:
     if not srcs:
         return ""
     deps = srcs + _sources("supervisor/*.h")
+    if not force and _fast_fresh(SUPERVISOR, deps):
+        return SUPERVISOR
     cxx = os.environ.get("CXX", "g++")
     cmd = [cxx, "-O2", "-std=c++17", "-Wall", "-pthread", _define_version(), *srcs,
            "-o", "@OUT@"]

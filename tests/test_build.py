@@ -77,3 +77,28 @@ def test_stamps_survive_moving_the_tree(tmp_path):
     res = subprocess.run([sys.executable, "-c", code], cwd=str(copy), capture_output=True,
                          text=True, timeout=120)
     assert res.returncode == 0, res.stderr
+
+
+def test_fast_path_skips_the_content_check_only_while_nothing_changed(tmp_path, monkeypatch):
+    """``tpi apply`` checks the supervisor's and the native module's stamps before every task
+    start: while no dependency's size or mtime moved, the ``.fast`` signature answers without
+    reading and hashing the sources; any change goes back to the content check."""
+    src = tmp_path / "a.cpp"
+    src.write_text("int x = 1;\n")
+    target = tmp_path / "out.bin"
+    target.write_bytes(b"built")
+    cmd = ["g++", "-O2", str(src), "-o", "@OUT@"]
+    assert not _build._fast_fresh(str(target), [str(src)])
+    _build._stamp(str(target), cmd, [str(src)])  # a build writes both
+    assert _build._fast_fresh(str(target), [str(src)])
+    os.utime(src, (1, 1))  # a checkout with other mtimes: back to the content check ...
+    assert not _build._fast_fresh(str(target), [str(src)])
+    assert not _build._stale(str(target), cmd, [str(src)])  # ... which still matches
+    _build._write_fast(str(target), [str(src)])
+    assert _build._fast_fresh(str(target), [str(src)])
+    src.write_text("int x = 22;\n")  # an edit changes size and mtime
+    assert not _build._fast_fresh(str(target), [str(src)])
+    assert _build._stale(str(target), cmd, [str(src)])
+    _build._write_fast(str(target), [str(src)])
+    monkeypatch.setenv("CXX", "clang++")  # the compiler is part of the signature
+    assert not _build._fast_fresh(str(target), [str(src)])
