@@ -362,7 +362,24 @@ def _confirm(prompt: str, auto: bool) -> bool:
     return sys.stdin.readline().strip() == "yes"
 
 
-def build_parser() -> argparse.ArgumentParser:
+COMMANDS = ("init", "validate", "plan", "apply", "destroy", "refresh", "show", "output",
+            "state", "version")
+
+
+def _command_in(argv: List[str]) -> Optional[str]:
+    """The subcommand ``argv`` names (the first word that is no option or ``-chdir``'s value)."""
+    it = iter(argv)
+    for tok in it:
+        if tok == "-chdir":
+            next(it, None)
+        elif not tok.startswith("-"):
+            return tok
+    return None
+
+
+def build_parser(only: Optional[str] = None) -> argparse.ArgumentParser:
+    """The CLI's parser; ``only``: just that subcommand's parser (argparse spends ~10 ms on
+    the ten of them -- gettext lookups per string -- on every ``tpi apply``)."""
     p = argparse.ArgumentParser(prog="tpi", description="Terraform-compatible engine for "
                                 "iterative_* resources on the MI355X node runtime")
     p.add_argument("-chdir", dest="chdir", default=None)
@@ -381,23 +398,36 @@ def build_parser() -> argparse.ArgumentParser:
         sp.add_argument("-no-color", dest="no_color", action="store_true")
         return sp
 
-    common(sub.add_parser("init"), state=False)
-    common(sub.add_parser("validate"), state=False)
-    common(sub.add_parser("plan"), plan_opts=True).add_argument("-destroy", action="store_true")
+    def want(name: str) -> bool:
+        return only is None or only == name
+
+    if want("init"):
+        common(sub.add_parser("init"), state=False)
+    if want("validate"):
+        common(sub.add_parser("validate"), state=False)
+    if want("plan"):
+        common(sub.add_parser("plan"), plan_opts=True).add_argument("-destroy",
+                                                                    action="store_true")
     for name in ("apply", "destroy"):
-        sp = common(sub.add_parser(name), plan_opts=True)
-        sp.add_argument("-auto-approve", dest="auto_approve", action="store_true")
-    common(sub.add_parser("refresh"), plan_opts=True)
-    sp = common(sub.add_parser("show"))
-    sp.add_argument("-json", dest="json", action="store_true")
-    sp = common(sub.add_parser("output"))
-    sp.add_argument("-json", dest="json", action="store_true")
-    sp.add_argument("-raw", dest="raw", action="store_true")
-    sp.add_argument("name", nargs="?")
-    sp = common(sub.add_parser("state"))
-    sp.add_argument("subcommand", choices=("list", "show", "rm"))
-    sp.add_argument("addresses", nargs="*")
-    sub.add_parser("version")
+        if want(name):
+            sp = common(sub.add_parser(name), plan_opts=True)
+            sp.add_argument("-auto-approve", dest="auto_approve", action="store_true")
+    if want("refresh"):
+        common(sub.add_parser("refresh"), plan_opts=True)
+    if want("show"):
+        sp = common(sub.add_parser("show"))
+        sp.add_argument("-json", dest="json", action="store_true")
+    if want("output"):
+        sp = common(sub.add_parser("output"))
+        sp.add_argument("-json", dest="json", action="store_true")
+        sp.add_argument("-raw", dest="raw", action="store_true")
+        sp.add_argument("name", nargs="?")
+    if want("state"):
+        sp = common(sub.add_parser("state"))
+        sp.add_argument("subcommand", choices=("list", "show", "rm"))
+        sp.add_argument("addresses", nargs="*")
+    if want("version"):
+        sub.add_parser("version")
     return p
 
 
@@ -409,7 +439,9 @@ def _version_text() -> str:
 
 
 def main(argv: Optional[List[str]] = None) -> int:
-    args = build_parser().parse_args(argv)
+    words = sys.argv[1:] if argv is None else argv
+    command = _command_in(words)
+    args = build_parser(command if command in COMMANDS else None).parse_args(words)
     if args.chdir:
         os.chdir(args.chdir)
     verbose = bool(os.environ.get("TF_LOG_PROVIDER") or os.environ.get("TF_LOG"))
