@@ -27,11 +27,11 @@ native component as ``TPI_VERSION_STRING``.
 from __future__ import annotations
 
 import glob
+import importlib.machinery
 import os
 import shutil
 import subprocess
 import sys
-import sysconfig
 from typing import List, Sequence
 
 try:  # the builtin module: hashlib would load OpenSSL on every CLI start (~4 ms)
@@ -46,11 +46,14 @@ LIB = os.path.join(PKG, "_lib")
 ROCM_LIB = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0] or "gfx950"
 
-NATIVE_SO = os.path.join(LIB, "_tpi_native" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
+# the interpreter's extension suffix (sysconfig's EXT_SUFFIX) without importing sysconfig,
+# which costs `tpi apply` ~3 ms per start; sysconfig is imported where a build needs it
+_EXT_SUFFIX = importlib.machinery.EXTENSION_SUFFIXES[0]
+NATIVE_SO = os.path.join(LIB, "_tpi_native" + _EXT_SUFFIX)
 HIP_SO = os.path.join(LIB, "libtpi_hip.so")
 SUPERVISOR = os.path.join(LIB, "tpi-supervisor")
 STAGER = os.path.join(LIB, "tpi-stager")
-TORCH_EXT = os.path.join(LIB, "_tpi_torch" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
+TORCH_EXT = os.path.join(LIB, "_tpi_torch" + _EXT_SUFFIX)
 
 
 def _sources(*patterns: str) -> List[str]:
@@ -166,6 +169,8 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
     deps = srcs + _sources("native/*.h", "common/*.h", "hip/tpi_hip.h")
     if not force and _fast_fresh(NATIVE_SO, deps):
         return NATIVE_SO
+    import sysconfig
+
     import pybind11
 
     cxx = os.environ.get("CXX", "g++")
@@ -254,6 +259,8 @@ def build_torch_ext(force: bool = False, verbose: bool = False) -> str:
     if not srcs:
         return ""
     import torch
+
+    import sysconfig
 
     inc = os.path.join(os.path.dirname(torch.__file__), "include")
     tl = torch_lib_dir()

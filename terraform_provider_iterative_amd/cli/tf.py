@@ -23,7 +23,6 @@ import os
 import sys
 import threading
 import time
-from concurrent.futures import ThreadPoolExecutor
 from typing import Any, Dict, List, Optional, Tuple
 
 from ..utils.record import field, record
@@ -223,6 +222,12 @@ class Engine:
     def _run_parallel(self, fn, changes: List[Change], state: State) -> List[bool]:
         if not changes:
             return []
+        if len(changes) == 1 or self.parallelism <= 1:
+            # one resource (the usual apply): no pool -- and no concurrent.futures import,
+            # ~3 ms of every `tpi apply` start
+            return [fn(c, state) for c in changes]
+        from concurrent.futures import ThreadPoolExecutor
+
         with ThreadPoolExecutor(max_workers=self.parallelism) as pool:
             return list(pool.map(lambda c: fn(c, state), changes))
 

@@ -12,7 +12,9 @@ import textwrap
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEAVY = ("http.client", "ssl", "xml.etree", "xml.etree.ElementTree", "email.utils",
          # OpenSSL's hash module, tar and ctypes: ~9 ms more of every start (round 6)
-         "_hashlib", "tarfile", "ctypes", "secrets")
+         "_hashlib", "tarfile", "ctypes", "secrets",
+         # sysconfig (the extension suffix) and a thread pool for one resource: ~6 ms (round 6)
+         "sysconfig", "concurrent.futures")
 # imported only once the task has started (its `addresses` attribute), not before: the
 # rendezvous port is probed by the supervisor, not by `tpi apply` (round 6)
 BEFORE_START = ("socket",)
@@ -59,6 +61,12 @@ PROBE = textwrap.dedent('''
 
 
 def _apply_modules(tmp_path):
+    from terraform_provider_iterative_amd import _build
+
+    # the stamps' stat signatures current (a content check -- right after a checkout or an
+    # edit of the sources -- imports the build's own modules once; not what is measured here)
+    _build.build_native()
+    _build.build_supervisor()
     work = tmp_path / "work"
     work.mkdir()
     (work / "main.tf").write_text(MAIN_TF)
