@@ -25,12 +25,11 @@ import time
 from typing import Dict, List, Optional
 
 from .. import _build
-from ..models.cloud import PROVIDER_LOCAL, PROVIDER_MI355X, Cloud, parse_region_selectors
+from ..models.cloud import PROVIDER_LOCAL, PROVIDER_MI355X, Cloud
 from ..models.machine_types import MachineType, parse_node_machine
 from ..models.values import (STATUS_RUNNING, Event, NotFoundError, NotImplementedErr,
                              RemoteStorage, Task as TaskSpec, new_status)
-from ..parallel.placement import (Allocation, Placement, PlacementBusy, PlacementError,
-                                  Request, node_cpus, pid_alive)
+from ..parallel.placement import Placement, node_cpus, pid_alive
 from ..storage import remote as remote_storage
 from ..storage import transfer as storage
 from ..utils.identifier import Identifier, parse_identifier

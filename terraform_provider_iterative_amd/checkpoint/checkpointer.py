@@ -34,9 +34,7 @@ import ctypes
 import hashlib
 import json
 import os
-import queue
 import struct
-import tempfile
 import threading
 import time
 from typing import Any, Dict, List, Mapping, Optional, Sequence, Tuple, Union
@@ -45,14 +43,14 @@ import numpy as np
 
 from ..ops import codec as tpz
 from ..ops import hip, native
-from ..ops.packing import PackPlan, TensorEntry, align_up
+from ..ops.packing import PackPlan, align_up
 from ..ops.packing import pack as host_pack, unpack as host_unpack
 from . import host
 from .base import (MAGIC, PREAMBLE, PROGRESS_MAGIC, STREAM_COMPLETE,  # noqa: F401
                    STREAM_FAILED, STREAM_RUNNING, CheckpointError, TransferResult,
                    _writer_alive)
-from .handoff import (FDS_PER_MESSAGE, HBM_ROUTES, IPC_MAX_ALLOC, RELOCATE_CHUNK,
-                      HbmHandoff)
+from .handoff import (FDS_PER_MESSAGE, HBM_ROUTES, IPC_MAX_ALLOC, RELOCATE_CHUNK,  # noqa: F401
+                      HbmHandoff)  # (the constants: re-exported, tests read them here)
 from .engine import (MODES, DeviceEngine, _engine_pool, _take_engine,  # noqa: F401
                      prewarm_engine)
 from .host import HostRegion

@@ -10,7 +10,6 @@ bucket's ``data/`` before the task runs again (``task/common/machine/machine-scr
 """
 from __future__ import annotations
 
-import ctypes
 import os
 import queue
 import threading
@@ -20,10 +19,9 @@ from typing import Any, Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from ..ops import codec as tpz
-from ..ops import hip, native
+from ..ops import native
 from ..ops.packing import PackPlan, TensorEntry
 from ..ops.packing import unpack as host_unpack
-from . import host
 from .base import STREAM_COMPLETE, STREAM_FAILED, CheckpointError, TransferResult
 
 ALLOC_HEADROOM = 512 << 20  # materialize(): free HBM beyond a tensor's size before allocating it

@@ -11,12 +11,10 @@ import ctypes
 import os
 import tempfile
 import threading
-from typing import Dict
 
 import numpy as np
 
 from ..ops import native
-from . import host
 from .base import (PREAMBLE, PROGRESS_MAGIC, STREAM_COMPLETE, STREAM_FAILED, STREAM_RUNNING,
                    CheckpointError, TransferResult)
 
