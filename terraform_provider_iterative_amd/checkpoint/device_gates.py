@@ -34,18 +34,25 @@ def _journal(code: str, *description: str) -> None:
     journal(code, *description)
 
 
-def successor_need(state_bytes: int, margin: float = 0.01) -> int:
+SUCCESSOR_OVERHEAD = 2 << 30  # a successor's GPU context and checkpoint engine, still to come
+PARKED_OVERHEAD = 256 << 20   # ... when it already holds them (a parked hot standby): the
+#                               hand-off's descriptors and digests only
+
+
+def successor_need(state_bytes: int, margin: float = 0.01,
+                   overhead: int = SUCCESSOR_OVERHEAD) -> int:
     """Device memory a successor needs free before it allocates a state of ``state_bytes``:
-    the state + ``margin`` (the caching allocator's rounding), + 2 GiB for its engine and GPU
-    context.  A 150 GB state needs 153.7 GB free next to it, which a 288 GiB MI355X (309.2 GB)
-    has only while the predecessor, a hot standby and memory the driver still wipes hold less
-    than 5.6 GB besides the state (``profiles/round6/r6h``: they held more, so 150 GB took the
-    big-state path)."""
-    return int(state_bytes * (1 + margin)) + (2 << 30)
+    the state + ``margin`` (the caching allocator's rounding), + ``overhead`` for what it has
+    not allocated yet -- its GPU context and engine (2 GiB), or, for a hot standby parked with
+    both, ``PARKED_OVERHEAD`` (its memory is already in the device's count).  A 150 GB state
+    next to a parked hot standby needs 151.8 GB free (the 2 GiB measure, 153.7 GB, sent it to the
+    big-state path in ``profiles/round6/r6g``, ``r6h``: 153.2-153.7 GB were free)."""
+    return int(state_bytes * (1 + margin)) + int(overhead)
 
 
 def wait_for_device_memory(spill: str, margin: float = 0.01,
-                           timeout: Optional[float] = None) -> Optional[float]:
+                           timeout: Optional[float] = None,
+                           overhead: int = SUCCESSOR_OVERHEAD) -> Optional[float]:
     """A successor's gate before it allocates the state of ``spill`` (its predecessor's
     checkpoint region): block until the device has room for the state
     (:func:`successor_need`) by the *driver's* count as well as the HIP runtime's, or until
@@ -70,7 +77,7 @@ def wait_for_device_memory(spill: str, margin: float = 0.01,
     total = peer["total"] if peer is not None else region_total(spill)
     if not total:
         return None
-    need = successor_need(total, margin)
+    need = successor_need(total, margin, overhead)
     if timeout is None:
         timeout = float(os.environ.get("TPI_STREAM_TIMEOUT", "30"))
     dev = torch.cuda.current_device()

@@ -43,9 +43,10 @@ from .checkpointer import Checkpointer, CheckpointError
 
 log = logging.getLogger("tpi.preemption")
 
-from .device_gates import (HANDOFF_HEADROOM, PREEMPTED_EXIT_CODE, STICKY_HIP_ERRORS,  # noqa: F401
-                           _device_settled_for_handoff, _hbm_fatal, _sticky_device_error,
-                           successor_need, wait_for_device_memory)
+from .device_gates import (HANDOFF_HEADROOM, PARKED_OVERHEAD, PREEMPTED_EXIT_CODE,  # noqa: F401
+                           STICKY_HIP_ERRORS, SUCCESSOR_OVERHEAD, _device_settled_for_handoff,
+                           _hbm_fatal, _sticky_device_error, successor_need,
+                           wait_for_device_memory)
 
 _registered: List[Checkpointer] = []
 _persist_paths: Dict[int, str] = {}
@@ -316,6 +317,8 @@ def _handoff_safe() -> bool:
 
     try:
         states = _registered_state_bytes()
+        # a hot standby parked with its context and engine: that memory is in the count already
+        overhead = PARKED_OVERHEAD if _standby_parked() else SUCCESSOR_OVERHEAD
         for dev in range(torch.cuda.device_count()):
             free, total = torch.cuda.mem_get_info(dev)
             # the successor's copy is the registered state (a hot standby's own context is
@@ -326,11 +329,47 @@ def _handoff_safe() -> bool:
             usage = device_vram_usage(dev)
             if usage is not None:
                 free = min(free, usage[1] - usage[0])
-            if free < successor_need(state):
+            if free < successor_need(state, overhead=overhead):
                 return False
     except Exception:
         return False
     return True
+
+
+def _standby_marker(spill: str) -> str:
+    return spill + ".standby"
+
+
+def _mark_parked(spill: str) -> None:
+    """A hot standby with its GPU context and engine made: say so next to the spill (its pid),
+    so the predecessor counts its memory as already allocated (:func:`_handoff_safe`)."""
+    path = _standby_marker(spill)
+    tmp = "%s.%d.tmp" % (path, os.getpid())
+    try:
+        with open(tmp, "w") as handle:
+            handle.write(str(os.getpid()))
+        os.replace(tmp, path)
+    except OSError:
+        pass
+
+
+def _standby_parked() -> bool:
+    """Is a hot standby of a registered checkpointer's spill parked now (its marker names a
+    live process other than this one)?"""
+    from .base import _writer_alive
+
+    for ck in _registered:
+        spill = getattr(ck, "path", None)
+        if not spill:
+            continue
+        try:
+            with open(_standby_marker(spill)) as handle:
+                pid = int(handle.read().strip() or 0)
+        except (OSError, ValueError):
+            continue
+        if pid > 0 and pid != os.getpid() and _writer_alive(pid):
+            return True
+    return False
 
 
 def _registered_state_bytes() -> Dict[int, int]:
@@ -430,6 +469,8 @@ def standby(prefetch_path: Optional[str] = None, materialize: bool = False) -> b
         from .checkpointer import prewarm_engine
 
         prewarm_engine(torch.cuda.current_device())
+        if prefetch_path:
+            _mark_parked(prefetch_path)
     if prefetch_path:
         from .host import prefetch, wait_pinned, watch_prefetch
 
@@ -467,7 +508,10 @@ def standby(prefetch_path: Optional[str] = None, materialize: bool = False) -> b
     os.environ.pop("TPI_STANDBY", None)
     journal("standby-activated")
     if wait_memory:
-        wait_for_device_memory(prefetch_path)
+        # parked with a context and engine: only the state (and descriptors) are still to come
+        parked = torch is not None and torch.cuda.is_initialized()
+        wait_for_device_memory(prefetch_path,
+                               overhead=PARKED_OVERHEAD if parked else SUCCESSOR_OVERHEAD)
     _notify(b"standby\n")  # the activated process can itself be succeeded by a standby
     return True
 

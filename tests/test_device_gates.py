@@ -278,3 +278,39 @@ def test_successor_withdraws_an_offer_it_cannot_make_room_for(tmp_path, monkeypa
         if pred.poll() is None:
             pred.kill()
         pred.wait()
+
+
+def test_a_parked_hot_standby_needs_no_room_for_its_context_again(tmp_path, monkeypatch):
+    """A hot standby parks with its GPU context and engine made, so that memory is in the
+    device's count already: the offer then needs the state + 1 % + 256 MiB next to it, not
+    + 2 GiB (a 150 GB state on a 288 GiB MI355X: r6g/r6h took the host path for want of
+    ~0.1 GB).  The marker of a dead process, or of this one, does not count."""
+    import subprocess as sp
+
+    from terraform_provider_iterative_amd.parallel import placement
+
+    cuda = FakeCudaDevices(FakeCudaDevices.TOTAL - 156 * GB)  # 150 GB state + contexts + rest
+    monkeypatch.setitem(sys.modules, "torch", types.SimpleNamespace(cuda=cuda))
+    monkeypatch.delenv("TPI_EARLY_HANDOFF", raising=False)
+    monkeypatch.setattr(placement, "device_vram_usage", lambda dev: None)
+    spill = str(tmp_path / "spill")
+    ck = types.SimpleNamespace(plan=types.SimpleNamespace(total=150 * GB), device_index=0,
+                               path=spill)
+    monkeypatch.setattr(preemption, "_registered", [ck])
+    assert not preemption._handoff_safe()  # 153.2 GB free < 153.65 GB needed
+    standby = sp.Popen([sys.executable, "-c", "import time; time.sleep(60)"])
+    try:
+        with open(spill + ".standby", "w") as handle:
+            handle.write(str(standby.pid))
+        assert preemption._standby_parked()
+        assert preemption._handoff_safe()  # 153.2 GB free >= 151.8 GB needed
+    finally:
+        standby.kill()
+        standby.wait()
+    assert not preemption._standby_parked() and not preemption._handoff_safe()
+    with open(spill + ".standby", "w") as handle:
+        handle.write(str(os.getpid()))  # our own marker (a standby that became the rank)
+    assert not preemption._standby_parked()
+    preemption._mark_parked(spill)  # what a parked standby writes
+    with open(spill + ".standby") as handle:
+        assert int(handle.read()) == os.getpid()
