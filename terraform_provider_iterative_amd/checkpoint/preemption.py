@@ -353,6 +353,17 @@ def _mark_parked(spill: str) -> None:
         pass
 
 
+def _unmark_parked(spill: str) -> None:
+    path = _standby_marker(spill)
+    try:
+        with open(path) as handle:
+            mine = handle.read().strip() == str(os.getpid())
+        if mine:
+            os.remove(path)
+    except (OSError, ValueError):
+        pass
+
+
 def _standby_parked() -> bool:
     """Is a hot standby of a registered checkpointer's spill parked now (its marker names a
     live process other than this one)?"""
@@ -499,6 +510,8 @@ def standby(prefetch_path: Optional[str] = None, materialize: bool = False) -> b
         except InterruptedError:
             continue
     cancel.set()
+    if prefetch_path:  # parked no more: activated (the offer was decided) or discarded
+        _unmark_parked(prefetch_path)
     if not msg.startswith(b"go"):
         os._exit(0)  # discarded before activation
     os.close(fd)

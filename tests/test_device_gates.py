@@ -311,6 +311,8 @@ def test_a_parked_hot_standby_needs_no_room_for_its_context_again(tmp_path, monk
     with open(spill + ".standby", "w") as handle:
         handle.write(str(os.getpid()))  # our own marker (a standby that became the rank)
     assert not preemption._standby_parked()
-    preemption._mark_parked(spill)  # what a parked standby writes
+    preemption._mark_parked(spill)  # what a parked standby writes ...
     with open(spill + ".standby") as handle:
         assert int(handle.read()) == os.getpid()
+    preemption._unmark_parked(spill)  # ... and removes when it is activated or discarded
+    assert not os.path.exists(spill + ".standby")
