@@ -130,10 +130,12 @@ def transfer(source: str, destination: str, exclude: Optional[Iterable[str]] = N
     entries = native().walk(src, flt)
     files = [e for e in entries if not e[4]]
     log.info("Transferring %s (%d files)...", human_size(sum(e[1] for e in files)), len(files))
-    # 256 MiB copy_file_range pieces, handed out round-robin over files (writers of one file
+    # 64 MiB copy_file_range pieces, handed out round-robin over files (writers of one file
     # serialise on its inode lock).  A copy into tmpfs / the page cache is bound per thread by
     # page allocation + memcpy (~2-3 GB/s), so it scales with the threads the task may use.
-    stats = native().copy_dir(src, dst, flt, threads or _copy_threads(), 256 << 20)
+    # 10 x 1 GB on the MI355X box's /tmp, 16 threads, median of 5: 63.7 GB/s with 64 MiB
+    # pieces (61.7-65.6), 58.7 with 256 MiB (50.8-59.2) (profiles/round6/r6v/summary.txt)
+    stats = native().copy_dir(src, dst, flt, threads or _copy_threads(), 64 << 20)
     log.debug("transfer %s -> %s: %s", src, dst, stats)
     return stats
 
